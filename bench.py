@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""Benchmark: audio samples/s (22.05 kHz) + real-time factor of the m2-tts
+mel-synthesis + vocoder path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vocoder|pipeline]
+
+One process per GPU (torchrun for N>1, RCCL backend); every rank processes
+its own batch of B utterances (weak scaling: utterances are independent, no
+collective in the data path).  Timed region: barrier + synchronize, K steps,
+synchronize + barrier; the max elapsed over ranks is the job time.
+
+Workloads:
+  vocoder  (default, BASELINE.json configs[1]) stage1_poc SimpleVocoder, B=32,
+           mel [32, 64, 500] ~ N(0,1) resident in HBM -> audio [32, 1, 32000]
+  pipeline (configs[2]) stage1_poc M2TTSModel.inference, B=32, 100 phonemes,
+           fixture weights with durations pinned to 5 frames -> T=500
+
+Extra fields: ``roofline`` for the dominant kernel (HIP events on its launch
+stream, around every launch of the timed region), ``cpu_baseline`` (the CPU
+oracle = the reference's op sequence, timed on this host, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "m2-tts_amd" / "src"))
+
+SAMPLE_RATE = 22050
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 vector = f32 MFMA peak
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec
+METRIC = "audio samples/sec (22.05 kHz) + RTF, stage1_poc batch=32 @1/2/4/8 MI355X"
+
+STAGE1 = dict(vocab_size=256, hidden_dim=64, mel_channels=64, text_encoder_layers=2, decoder_layers=2,
+              num_heads=2, dropout=0.1, vocoder_channels=128)
+
+
+def vocoder_flops_per_sample(C: int, M: int) -> float:
+    """Algorithmic FLOPs per output audio sample of SimpleVocoder.
+
+    Per mel frame: input conv 2*M*C*3; stage k (rate r, c -> c/2, L -> rL):
+    ConvT 2*2*c*(c/2) per output, resblock 2*(2*(c/2)^2*3) per output;
+    output conv 2*c_last*3 per sample.  Divided by 64 samples per frame."""
+    f = 2 * M * C * 3
+    c, n = C, 1
+    for r in (4, 4, 2, 2):
+        n *= r
+        co = c // 2
+        f += n * (2 * 2 * c * co + 2 * 2 * co * co * 3)
+        c = co
+    f += n * 2 * c * 3
+    return f / n
+
+
+def fixture_model(dev):
+    """Random-init stage1 weights (seed 1234) with durations pinned
+    to 5 frames/phoneme: projection weight * 0.01, bias 5.5."""
+    from models.tts_model import M2TTSModel
+    torch.manual_seed(1234)
+    m = M2TTSModel(**STAGE1)
+    with torch.no_grad():
+        p = m.duration_predictor.predictor.projection
+        p.weight.mul_(0.01)
+        p.bias.fill_(5.5)
+    return m.to(dev).eval()
+
+
+def cpu_baseline(workload: str, B: int, S: int, T: int, budget_s: float):
+    """Time the CPU oracle (reference op order) on a bounded sample of the workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import m2tts_oracle as orc
+    threads = torch.get_num_threads()
+    torch.manual_seed(1234)
+    from models.tts_model import M2TTSModel  # only for the seeded init (module construction on CPU)
+    m = M2TTSModel(**STAGE1)
+    sd = orc.pin_durations({k: v.detach().clone() for k, v in m.state_dict().items()})
+    cfg = orc.STAGE1
+    g = torch.Generator().manual_seed(0)
+    if workload == "vocoder":
+        mel = torch.randn(B, cfg.mel_channels, T, generator=g)
+        run = lambda: orc.vocoder(sd, mel)  # noqa: E731
+        desc = f"oracle SimpleVocoder single pass, B={B} mel [{B},{cfg.mel_channels},{T}]"
+    else:
+        ids = torch.randint(0, 42, (B, S), generator=g)
+        lens = torch.full((B,), S, dtype=torch.long)
+        run = lambda: orc.inference(sd, cfg, ids, lens, as_written=True)  # noqa: E731
+        desc = f"oracle M2TTSModel.inference as written (2 vocoder passes), B={B} S={S}"
+    with torch.no_grad():
+        run()  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            run()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or n >= 200:
+                break
+    samples = n * B * 64 * T
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": samples / el, "unit": "audio samples/s", "cores": threads, "kind": "port",
+            "sample": f"{desc}; {n} runs in {el:.1f} s; torch {torch.__version__} CPU, {threads} threads, {cpu_model}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", choices=["vocoder", "pipeline"], default="vocoder")
+    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
+    ap.add_argument("--phonemes", type=int, default=100)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline-extra", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as td
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from m2amd import _lib
+    lib = _lib.load()
+    model = fixture_model(dev)
+    B, S, T = args.batch, args.phonemes, 5 * args.phonemes
+    g = torch.Generator().manual_seed(1000 + rank)
+    mel = torch.randn(B, STAGE1["mel_channels"], T, generator=g).to(dev)
+    ids = torch.randint(0, 42, (B, S), generator=g).to(dev)
+    lens = torch.full((B,), S, dtype=torch.long, device=dev)
+    hm = model._hip(dev)
+
+    def step_vocoder():
+        return model.vocoder(mel)
+
+    def step_pipeline():
+        return model.inference(ids, lens)
+
+    step = step_vocoder if args.workload == "vocoder" else step_pipeline
+
+    def timed(fn, steps, warmup, profile=False):
+        for _ in range(warmup):
+            fn()
+        if profile:
+            _lib.check(lib.m2_profile_enable(hm.handle, steps), "m2_profile_enable")
+        torch.cuda.synchronize(dev)
+        if dist:
+            td.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        if dist:
+            td.barrier()
+        el = time.perf_counter() - t0
+        ms = []
+        if profile:
+            import ctypes
+            buf = (ctypes.c_float * steps)()
+            n = ctypes.c_int32(0)
+            _lib.check(lib.m2_profile_read(hm.handle, buf, steps, ctypes.byref(n)), "m2_profile_read")
+            ms = list(buf[: n.value])
+            lib.m2_profile_disable(hm.handle)
+        if dist:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            td.all_reduce(t, op=td.ReduceOp.MAX)
+            el = float(t.item())
+        return el, ms
+
+    elapsed, kern_ms = timed(step, args.steps, args.warmup, profile=True)
+    samples_per_step = B * 64 * T
+    total_samples = samples_per_step * args.steps * world
+    value = total_samples / elapsed
+
+    # Roofline of the dominant kernel (bracketed by HIP events inside m2_vocoder).
+    kname = lib.m2_profile_kernel_name().decode()
+    roofline = None
+    if kern_ms:
+        avg_ms = sum(kern_ms) / len(kern_ms)
+        # current dominant launch: resblock-0 conv1, 2*c*c*3 FLOP per (c, position), c = C/2, L = 4T
+        c, L = STAGE1["vocoder_channels"] // 2, 4 * T
+        flops = 2.0 * c * c * 3 * L * B
+        achieved = flops / (avg_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": kname,
+                    "avg_kernel_ms": round(avg_ms, 5), "launches": len(kern_ms),
+                    "algorithmic_flop_per_launch": flops}
+        tf = ROOT / "profiles" / "traffic.json"
+        if tf.exists():
+            try:
+                roofline["traffic"] = json.loads(tf.read_text()).get(kname)
+            except ValueError:
+                pass
+
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "audio samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded N(0,1) mel / U{0..41} phoneme ids; random-init stage1 weights, seed 1234)",
+        "config": {"workload": "stage1_poc SimpleVocoder B=32 (configs[1])" if args.workload == "vocoder"
+                   else "stage1_poc M2TTSModel.inference B=32 S=100 (configs[2])",
+                   "stage": "stage1_poc", "per_gpu_batch": B, "global_batch": B * world, "mel_frames": T,
+                   "audio_samples_per_utt": 64 * T, "parallelism": f"utterance-sharded x{world} (dp{world})"},
+        "rtf_x_realtime": round(value / SAMPLE_RATE, 1),
+        "rtf_x_realtime_per_gpu": round(value / SAMPLE_RATE / world, 1),
+        "roofline": roofline,
+    }
+    if args.workload == "vocoder":
+        out["vocoder_flop_per_sample"] = vocoder_flops_per_sample(STAGE1["vocoder_channels"], STAGE1["mel_channels"])
+        out["vocoder_tflops"] = round(value * out["vocoder_flop_per_sample"] / 1e12, 3)
+
+    if not args.no_pipeline_extra:
+        other = step_pipeline if args.workload == "vocoder" else step_vocoder
+        el2, _ = timed(other, max(5, args.steps // 2), 3)
+        n2 = max(5, args.steps // 2)
+        out["other_workload"] = {"workload": "pipeline" if args.workload == "vocoder" else "vocoder",
+                                 "value": round(samples_per_step * n2 * world / el2, 1),
+                                 "ms_per_step": round(el2 / n2 * 1e3, 4)}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.workload, B, S, T, args.cpu_budget)
+        out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        if not args.no_pipeline_extra:
+            other = "pipeline" if args.workload == "vocoder" else "vocoder"
+            out["cpu_baseline_other"] = cpu_baseline(other, B, S, T, args.cpu_budget / 2)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        td.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+/*
+ * m2tts_hip.h - C ABI of the MI355X (gfx950) implementation of the m2-tts
+ * mel-synthesis + vocoder forward path.
+ *
+ * The reference (Ryannasr11/m2-tts) has no FFI layer: its boundary is the
+ * Python nn.Module API of src/models/tts_model.py and components.py.  Each
+ * entry point below replaces the PyTorch op sequence of one reference
+ * module's forward; the citation is given per function.  The Python drop-in
+ * (m2-tts_amd/src/models/) binds these with ctypes - see INTEGRATION.md.
+ *
+ * Conventions
+ *  - All tensors are caller-owned DEVICE pointers (torch tensor.data_ptr()),
+ *    contiguous, fp32 unless stated; ids/lengths are int64.
+ *  - `stream` is a hipStream_t passed as void* (torch current stream's
+ *    cuda_stream); every call is stream-ordered and asynchronous.  No call
+ *    allocates or synchronises, except m2_model_create (one-time weight
+ *    packing) and m2_model_destroy.
+ *  - Scratch memory is the caller's: size it with m2_workspace_bytes().
+ *  - Return 0 on success; M2_E_* (<0) for argument/shape errors; a positive
+ *    value is a hipError_t passed through.  m2_last_error() returns a
+ *    thread-local message for the last failure on the calling thread.
+ */
+#ifndef M2TTS_HIP_H
+#define M2TTS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define M2_ABI_VERSION 1
+
+#define M2_OK 0
+#define M2_E_ARG (-1)         /* null pointer / bad enum / bad size           */
+#define M2_E_SHAPE (-2)       /* shape outside what the kernels support       */
+#define M2_E_WORKSPACE (-3)   /* workspace smaller than m2_workspace_bytes()  */
+#define M2_E_WEIGHTS (-4)     /* weight table incomplete                      */
+
+/* M2TTSModel.__init__ hyper-parameters (tts_model.py:303-313), plus the
+ * positional-encoding table length (TextEncoder max_seq_len, tts_model.py:29). */
+typedef struct m2_config {
+    int32_t vocab_size;          /* 256 */
+    int32_t hidden_dim;          /* H: 64 stage1, 96 stage2 */
+    int32_t mel_channels;        /* M: 64 / 80 */
+    int32_t text_encoder_layers; /* 2 / 3 */
+    int32_t decoder_layers;      /* 2 / 3 */
+    int32_t num_heads;           /* 2 */
+    int32_t vocoder_channels;    /* C: 128 / 256 */
+    int32_t max_positions;       /* 1000 */
+} m2_config;
+
+typedef struct m2_model m2_model;
+
+int32_t m2_abi_version(void);
+const char* m2_last_error(void);
+
+/* ---- weight table ---------------------------------------------------------
+ * The weights are addressed by their reference state_dict key
+ * (M2TTSModel.state_dict(), tts_model.py:303-343).  m2_weight_count/name/numel
+ * enumerate the keys in the order m2_model_create expects. */
+int32_t m2_weight_count(const m2_config* cfg);
+int32_t m2_weight_name(const m2_config* cfg, int32_t index, char* buf, int32_t buflen);
+int64_t m2_weight_numel(const m2_config* cfg, int32_t index);
+
+/* Packs and uploads the weights once (BatchNorm folded into the duration
+ * convs, conv weights re-laid out for the kernels).  `weights[i]` is a device
+ * pointer to the tensor named by m2_weight_name(cfg, i) (fp32; the BatchNorm
+ * num_batches_tracked entries are int64 and ignored).  Synchronises `stream`. */
+int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_t n_weights,
+                        void* stream, m2_model** out);
+int32_t m2_model_destroy(m2_model* model);
+int32_t m2_model_config(const m2_model* model, m2_config* out);
+
+/* Scratch bytes needed by the stage calls for a batch of B utterances of S
+ * phonemes and T mel frames (T = 0: encoder/duration only). */
+size_t m2_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T);
+
+/* ---- stage entry points ---------------------------------------------------*/
+
+/* TextEncoder.forward (tts_model.py:57-89): embedding*sqrt(H) + pe, L_enc pre-LN
+ * transformer layers with key-padding mask (components.py:131-140, 59-90,
+ * 226-241), final LayerNorm.  lengths may be NULL (no mask).
+ * out_enc [B,S,H]; out_mask [B,S] uint8 (may be NULL). */
+int32_t m2_text_encoder(const m2_model* model, const int64_t* ids, const int64_t* lengths,
+                        int32_t B, int32_t S, float* out_enc, uint8_t* out_mask,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* DurationPredictor.forward (tts_model.py:99-117): 2x[Conv1d k3 + BN(eval) +
+ * ReLU] -> Conv1d k1 -> softplus.  enc [B,S,H] -> out_dur [B,S]. */
+int32_t m2_duration_predictor(const m2_model* model, const float* enc, int32_t B, int32_t S,
+                              float* out_dur, void* workspace, size_t workspace_bytes, void* stream);
+
+/* LengthRegulator.forward, counting half (tts_model.py:146-162): per phoneme
+ * n = int(trunc(dur*scale)) (fp32 product, truncation toward zero, n<=0 -> 0);
+ * per utterance exclusive prefix sums out_cum [B,S+1] (int32), totals
+ * out_T [B] and the batch maximum out_Tmax [1] (int32).  `dur` is fp32, or
+ * int32 when dur_is_int != 0 (scale then ignored). */
+int32_t m2_length_regulator_count(const void* dur, int32_t dur_is_int, float scale,
+                                  int32_t B, int32_t S, int32_t* out_cum, int32_t* out_T,
+                                  int32_t* out_Tmax, void* stream);
+
+/* LengthRegulator.forward, expanding half (tts_model.py:146-178): frame t of
+ * utterance b copies enc[b, s] for cum[b,s] <= t < cum[b,s+1]; frames past
+ * the utterance's total are zero; the output has exactly T_out frames
+ * (padding or truncation, tts_model.py:165-176).  out [B,T_out,H]. */
+int32_t m2_length_regulator_expand(const float* enc, const int32_t* cum, int32_t B, int32_t S,
+                                   int32_t H, int32_t T_out, float* out, void* stream);
+
+/* MelDecoder.forward (tts_model.py:211-228): L_dec pre-LN transformer layers
+ * WITHOUT mask over the frames, LayerNorm, Linear(H->M).
+ * x [B,T,H] -> out_mel [B,T,M].  x is not modified. */
+int32_t m2_mel_decoder(const m2_model* model, const float* x, int32_t B, int32_t T, float* out_mel,
+                       void* workspace, size_t workspace_bytes, void* stream);
+
+/* SimpleVocoder.forward (tts_model.py:279-297): input_conv, 4x[ConvT(k=2r,s=r,
+ * p=r/2) + leaky(0.1) + LightweightResBlock], output_conv + tanh.
+ * mel_layout 0: mel [B,M,T] (the module's own input); 1: mel [B,T,M] (the
+ * decoder output, read transposed in place).  out_audio [B,1,64T]. */
+int32_t m2_vocoder(const m2_model* model, const float* mel, int32_t mel_layout, int32_t B,
+                   int32_t T, float* out_audio, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
+/* ---- kernel-level entry points (for the components API and tests) ---------*/
+
+/* LightweightResBlock.forward (components.py:196-200) of vocoder stage k
+ * (0..3): y = conv2(leaky(conv1(x))) + x.  x,y [B,c_k,L]; tmp: B*c_k*L floats. */
+int32_t m2_vocoder_resblock(const m2_model* model, int32_t k, const float* x, int32_t B, int32_t L,
+                            float* y, float* tmp, void* stream);
+
+/* leaky(ConvTranspose1d) of vocoder stage k (tts_model.py:255-263, 291):
+ * x [B,c,L] -> y [B,c/2,r*L]. */
+int32_t m2_vocoder_upsample(const m2_model* model, int32_t k, const float* x, int32_t B, int32_t L,
+                            float* y, void* stream);
+
+/* Standalone kernels with caller-supplied weights in PyTorch layout (used by
+ * the components API for modules that live outside an M2TTSModel). */
+
+/* y = act((conv1d(x; w [Cout,Cin,ksize], b [Cout], padding ksize/2) [* alpha + beta]))
+ * (+ res).  ksize 1 or 3; alpha/beta per output channel (the BatchNorm1d eval
+ * form, components.py:170-171) or NULL; act 0 none, 1 leaky(0.1), 2 tanh,
+ * 3 relu, 4 softplus(beta=1, threshold=20).  x [B,Cin,L], y/res [B,Cout,L].
+ * Serves Conv1d in ConvBlock, VariancePredictor.projection, the vocoder's
+ * input/output convs and LightweightResBlock convs used outside a model. */
+int32_t m2_conv1d(const float* x, const float* w, const float* b, const float* alpha,
+                  const float* beta, const float* res, int32_t ksize, int32_t act, int32_t B,
+                  int32_t Cin, int32_t Cout, int32_t L, float* y, void* stream);
+
+/* y = act(convT1d(x; w [Cin,Cout,2r], b, stride r, padding r/2)), r in {2,4};
+ * x [B,Cin,L] -> y [B,Cout,r*L] (tts_model.py:255-263, 291). */
+int32_t m2_conv_transpose1d(const float* x, const float* w, const float* b, int32_t rate,
+                            int32_t act, int32_t B, int32_t Cin, int32_t Cout, int32_t L, float* y,
+                            void* stream);
+
+/* y[R,N] = act(LN?(x)[R,K] . w[N,K]^T + b) (+ res[R,N]).  gamma/beta NULL:
+ * no LayerNorm (eps 1e-5); b may be NULL; act 0 none, 3 relu. */
+int32_t m2_linear(const float* x, const float* gamma, const float* beta, const float* w,
+                  const float* b, const float* res, int32_t act, int32_t R, int32_t K, int32_t N,
+                  float* y, void* stream);
+
+/* y[R,K] = LN(x) with affine gamma/beta, eps 1e-5. */
+int32_t m2_layer_norm(const float* x, const float* gamma, const float* beta, int32_t R, int32_t K,
+                      float* y, void* stream);
+
+/* Attention core of MultiHeadAttention.forward (components.py:72-86):
+ * qkv [B,N,3H] laid out (3, heads, hd) per row as the reference's reshape
+ * implies; key_mask [B,N] uint8 or NULL (masked keys score -1e9);
+ * out [B,N,H] (heads re-interleaved, before out_proj). */
+int32_t m2_attention(const float* qkv, const uint8_t* key_mask, int32_t B, int32_t N, int32_t H,
+                     int32_t heads, float* out, void* stream);
+
+/* TextEncoder embedding (tts_model.py:78-80): y[b,s,:] = emb[ids[b,s],:] *
+ * scale + pe[s,:] (scale = sqrt(H) as fp32); ids outside [0,vocab) read zeros. */
+int32_t m2_embed_positional(const int64_t* ids, const float* emb, const float* pe, int32_t B,
+                            int32_t S, int32_t H, int32_t vocab, float scale, float* y,
+                            void* stream);
+
+/* PositionalEncoding.forward (components.py:30-39): y = x + pe[:S] (x [B,S,H]). */
+int32_t m2_add_positional(const float* x, const float* pe, int32_t B, int32_t S, int32_t H,
+                          float* y, void* stream);
+
+/* ---- measurement ----------------------------------------------------------
+ * Kernel timing with HIP events recorded on the launch stream around the
+ * vocoder's dominant kernel (bench.py's roofline).  enable: allocate
+ * `capacity` event pairs (not in a timed region); each m2_vocoder call then
+ * records one pair while capacity lasts; read: synchronise the recorded
+ * events and return their durations in ms (n_out = count) and reset.
+ * m2_profile_kernel_name names the bracketed kernel. */
+int32_t m2_profile_enable(m2_model* model, int32_t capacity);
+int32_t m2_profile_read(m2_model* model, float* ms_out, int32_t capacity, int32_t* n_out);
+int32_t m2_profile_disable(m2_model* model);
+const char* m2_profile_kernel_name(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* M2TTS_HIP_H */

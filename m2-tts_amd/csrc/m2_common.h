@@ -1,0 +1,88 @@
+// Shared helpers for the m2-tts gfx950 kernels and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/m2tts_hip.h"
+
+namespace m2 {
+
+constexpr int kWave = 64;            // CDNA wavefront
+constexpr float kLnEps = 1e-5f;      // nn.LayerNorm / BatchNorm1d default eps
+constexpr float kLeaky = 0.1f;       // F.leaky_relu slope used by the vocoder
+constexpr float kMaskFill = -1e9f;   // components.py:539
+
+enum Act : int { ACT_NONE = 0, ACT_LEAKY = 1, ACT_TANH = 2, ACT_RELU = 3, ACT_SOFTPLUS = 4 };
+
+void set_error(const std::string& msg);
+
+// Status helpers: every C entry point returns through these.
+int32_t fail(int32_t code, const char* what);
+int32_t hip_status(hipError_t e, const char* where);
+
+#define M2_CHECK_ARG(cond, msg)                      \
+    do {                                             \
+        if (!(cond)) return ::m2::fail(M2_E_ARG, msg); \
+    } while (0)
+#define M2_CHECK_SHAPE(cond, msg)                      \
+    do {                                               \
+        if (!(cond)) return ::m2::fail(M2_E_SHAPE, msg); \
+    } while (0)
+#define M2_HIP(expr)                                                   \
+    do {                                                               \
+        hipError_t _e = (expr);                                        \
+        if (_e != hipSuccess) return ::m2::hip_status(_e, #expr);      \
+    } while (0)
+// After a kernel launch: surface launch-configuration errors immediately.
+#define M2_LAUNCHED(name)                                              \
+    do {                                                               \
+        hipError_t _e = hipGetLastError();                             \
+        if (_e != hipSuccess) return ::m2::hip_status(_e, name);       \
+    } while (0)
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+    if (act == ACT_LEAKY) return v > 0.f ? v : v * kLeaky;
+    if (act == ACT_TANH) return tanhf(v);
+    if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == ACT_SOFTPLUS) return v > 20.f ? v : log1pf(expf(v));  // F.softplus(beta=1, threshold=20)
+    return v;
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_t(float v) {
+    if constexpr (ACT == ACT_LEAKY) return v > 0.f ? v : v * kLeaky;
+    else if constexpr (ACT == ACT_TANH) return tanhf(v);
+    else if constexpr (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
+    else return v;
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Bump allocator over a caller-provided workspace (256-B aligned carves).
+struct Carve {
+    char* base;
+    size_t cap;
+    size_t off = 0;
+    bool ok = true;
+    Carve(void* p, size_t n) : base(static_cast<char*>(p)), cap(n) {}
+    template <typename T>
+    T* take(size_t count) {
+        size_t o = align_up(off, 256);
+        size_t n = count * sizeof(T);
+        if (o + n > cap || base == nullptr) { ok = false; off = o + n; return nullptr; }
+        off = o + n;
+        return reinterpret_cast<T*>(base + o);
+    }
+};
+
+// Byte counter with the same carve rule (for m2_workspace_bytes).
+struct Sizer {
+    size_t off = 0;
+    template <typename T>
+    T* take(size_t count) { off = align_up(off, 256) + count * sizeof(T); return nullptr; }
+};
+
+}  // namespace m2

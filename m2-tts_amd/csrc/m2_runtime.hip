@@ -1,0 +1,602 @@
+// C-ABI runtime: weight table, model handle, stage orchestration.
+// See include/m2tts_hip.h for the contract of every entry point.
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "m2_common.h"
+
+namespace m2 {
+
+// ---- launchers defined in the kernel translation units ---------------------
+int32_t launch_embed_pe(const int64_t*, const float*, const float*, int, int, int, int, float*, hipStream_t);
+int32_t launch_layer_norm(const float*, const float*, const float*, int, int, float*, hipStream_t);
+int32_t launch_linear(const float*, const float*, const float*, const float*, const float*,
+                      const float*, int, int, int, int, float*, hipStream_t);
+int32_t launch_attention(const float*, const uint8_t*, int, int, int, int, float*, hipStream_t);
+int32_t launch_duration(const float*, int, int, int, const float* const*, float*, hipStream_t);
+int32_t launch_lr_count(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
+int32_t launch_lr_expand(const float*, const int32_t*, int, int, int, int, float*, hipStream_t);
+int32_t launch_conv(const float*, const float*, const float*, const float*, const float*,
+                    const float*, int, int, bool, int, int, int, int, float*, hipStream_t);
+int32_t launch_add_pe(const float*, const float*, int, int, int, float*, hipStream_t);
+int32_t launch_embed_pe_scaled(const int64_t*, const float*, const float*, int, int, int, int, float, float*, hipStream_t);
+int32_t launch_convT(const float*, const float*, const float*, int, int, int, int, int, int,
+                     float*, hipStream_t);
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int32_t fail(int32_t code, const char* what) {
+    set_error(what);
+    return code;
+}
+
+int32_t hip_status(hipError_t e, const char* where) {
+    set_error(std::string(where) + ": " + hipGetErrorString(e));
+    return static_cast<int32_t>(e);
+}
+
+static constexpr int kRates[4] = {4, 4, 2, 2};  // tts_model.py:244
+// The launch bench.py times with events: per-layer path, stage-0 resblock conv1.
+static constexpr int kProfStage = 0;
+static constexpr const char* kProfKernel = "conv_kernel<3,8,4,0,0> (vocoder resblock 0 conv1)";
+
+// ---------------------------------------------------------------------------
+// Weight table in M2TTSModel.state_dict() order (tts_model.py:303-343).
+struct WSpec {
+    std::string name;
+    int64_t numel;
+    bool is_int64;
+};
+
+static void add_layer(std::vector<WSpec>& t, const std::string& p, int64_t H) {
+    t.push_back({p + ".self_attn.qkv.weight", 3 * H * H, false});
+    t.push_back({p + ".self_attn.out_proj.weight", H * H, false});
+    t.push_back({p + ".self_attn.out_proj.bias", H, false});
+    t.push_back({p + ".ffn.linear1.weight", 2 * H * H, false});
+    t.push_back({p + ".ffn.linear1.bias", 2 * H, false});
+    t.push_back({p + ".ffn.linear2.weight", 2 * H * H, false});
+    t.push_back({p + ".ffn.linear2.bias", H, false});
+    t.push_back({p + ".norm1.weight", H, false});
+    t.push_back({p + ".norm1.bias", H, false});
+    t.push_back({p + ".norm2.weight", H, false});
+    t.push_back({p + ".norm2.bias", H, false});
+}
+
+static std::vector<WSpec> weight_table(const m2_config& c) {
+    std::vector<WSpec> t;
+    const int64_t H = c.hidden_dim, M = c.mel_channels, C = c.vocoder_channels;
+    t.push_back({"text_encoder.embedding.weight", (int64_t)c.vocab_size * H, false});
+    t.push_back({"text_encoder.pos_encoding.pe", (int64_t)c.max_positions * H, false});
+    for (int i = 0; i < c.text_encoder_layers; ++i) add_layer(t, "text_encoder.layers." + std::to_string(i), H);
+    t.push_back({"text_encoder.norm.weight", H, false});
+    t.push_back({"text_encoder.norm.bias", H, false});
+    for (int j = 0; j < 2; ++j) {
+        const std::string p = "duration_predictor.predictor.conv_layers." + std::to_string(j);
+        t.push_back({p + ".conv.weight", H * H * 3, false});
+        t.push_back({p + ".conv.bias", H, false});
+        t.push_back({p + ".norm.weight", H, false});
+        t.push_back({p + ".norm.bias", H, false});
+        t.push_back({p + ".norm.running_mean", H, false});
+        t.push_back({p + ".norm.running_var", H, false});
+        t.push_back({p + ".norm.num_batches_tracked", 1, true});
+    }
+    t.push_back({"duration_predictor.predictor.projection.weight", H, false});
+    t.push_back({"duration_predictor.predictor.projection.bias", 1, false});
+    for (int i = 0; i < c.decoder_layers; ++i) add_layer(t, "decoder.layers." + std::to_string(i), H);
+    t.push_back({"decoder.norm.weight", H, false});
+    t.push_back({"decoder.norm.bias", H, false});
+    t.push_back({"decoder.mel_projection.weight", M * H, false});
+    t.push_back({"decoder.mel_projection.bias", M, false});
+    t.push_back({"vocoder.input_conv.weight", C * M * 3, false});
+    t.push_back({"vocoder.input_conv.bias", C, false});
+    int64_t ch = C;
+    for (int k = 0; k < 4; ++k) {
+        const std::string p = "vocoder.upsamples." + std::to_string(k);
+        t.push_back({p + ".weight", ch * (ch / 2) * 2 * kRates[k], false});
+        t.push_back({p + ".bias", ch / 2, false});
+        ch /= 2;
+    }
+    ch = C;
+    for (int k = 0; k < 4; ++k) {
+        ch /= 2;
+        const std::string p = "vocoder.resblocks." + std::to_string(k);
+        t.push_back({p + ".conv1.weight", ch * ch * 3, false});
+        t.push_back({p + ".conv1.bias", ch, false});
+        t.push_back({p + ".conv2.weight", ch * ch * 3, false});
+        t.push_back({p + ".conv2.bias", ch, false});
+    }
+    t.push_back({"vocoder.output_conv.weight", ch * 3, false});
+    t.push_back({"vocoder.output_conv.bias", 1, false});
+    return t;
+}
+
+static bool config_ok(const m2_config* c) {
+    if (!c) return false;
+    const bool pos = c->vocab_size > 0 && c->hidden_dim > 0 && c->mel_channels > 0 &&
+                     c->text_encoder_layers >= 0 && c->decoder_layers >= 0 && c->num_heads > 0 &&
+                     c->vocoder_channels >= 16 && c->max_positions > 0;
+    return pos && c->hidden_dim % c->num_heads == 0 && c->vocoder_channels % 16 == 0;
+}
+
+}  // namespace m2
+
+// ---------------------------------------------------------------------------
+struct m2_layer_w {
+    const float *qkv_w, *out_w, *out_b, *ff1_w, *ff1_b, *ff2_w, *ff2_b, *n1_w, *n1_b, *n2_w, *n2_b;
+};
+
+struct m2_model {
+    m2_config cfg{};
+    float* buf = nullptr;
+    std::vector<const float*> ptr;  // per weight-table entry (nullptr for int64 entries)
+    std::vector<m2_layer_w> enc, dec;
+    const float *emb = nullptr, *pe = nullptr, *enc_nw = nullptr, *enc_nb = nullptr;
+    const float* dur[10] = {};  // w1,b1,alpha1,beta1, w2,b2,alpha2,beta2, proj_w, proj_b
+    const float *dec_nw = nullptr, *dec_nb = nullptr, *mel_w = nullptr, *mel_b = nullptr;
+    const float *vin_w = nullptr, *vin_b = nullptr, *vout_w = nullptr, *vout_b = nullptr;
+    const float *up_w[4] = {}, *up_b[4] = {};
+    const float *rb_w1[4] = {}, *rb_b1[4] = {}, *rb_w2[4] = {}, *rb_b2[4] = {};
+    // measurement: event pairs recorded around the vocoder's dominant kernel
+    mutable std::vector<hipEvent_t> prof_begin, prof_end;
+    mutable int prof_next = 0;
+};
+
+namespace {
+// Record the begin/end event of the next free pair (no-op when profiling is off).
+struct ProfScope {
+    const m2_model* m;
+    hipStream_t st;
+    int slot = -1;
+    ProfScope(const m2_model* mm, hipStream_t s) : m(mm), st(s) {
+        if (m->prof_next < (int)m->prof_begin.size()) {
+            slot = m->prof_next++;
+            (void)hipEventRecord(m->prof_begin[slot], st);
+        }
+    }
+    ~ProfScope() {
+        if (slot >= 0) (void)hipEventRecord(m->prof_end[slot], st);
+    }
+};
+}  // namespace
+
+using namespace m2;
+
+namespace {
+
+int32_t mask_kernel_launch(const int64_t* lengths, int B, int S, uint8_t* mask, hipStream_t st);
+
+__global__ void padding_mask_kernel(const int64_t* __restrict__ lengths, int B, int S,
+                                    uint8_t* __restrict__ mask) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * S) return;
+    const int b = i / S, s = i - b * S;
+    mask[i] = (int64_t)s < lengths[b] ? 1 : 0;  // components.py:236-240
+}
+
+int32_t mask_kernel_launch(const int64_t* lengths, int B, int S, uint8_t* mask, hipStream_t st) {
+    if (B * S == 0) return M2_OK;
+    hipLaunchKernelGGL(padding_mask_kernel, dim3(cdiv(B * S, 256)), dim3(256), 0, st, lengths, B, S, mask);
+    M2_LAUNCHED("padding_mask_kernel");
+    return M2_OK;
+}
+
+struct TfBufs {
+    float *x, *qkv, *att, *hid;
+    uint8_t* mask;
+};
+
+template <typename A>
+void carve_tf(A& a, int B, int N, int H, TfBufs* out) {
+    const size_t R = (size_t)B * N;
+    float* x = a.template take<float>(R * H);
+    float* qkv = a.template take<float>(R * 3 * H);
+    float* att = a.template take<float>(R * H);
+    float* hid = a.template take<float>(R * 2 * H);
+    uint8_t* mask = a.template take<uint8_t>(R);
+    if (out) *out = TfBufs{x, qkv, att, hid, mask};
+}
+
+size_t vocoder_max_cl(const m2_config& c, int T) {
+    size_t best = (size_t)c.vocoder_channels * T;
+    size_t ch = c.vocoder_channels, L = T;
+    for (int k = 0; k < 4; ++k) {
+        ch /= 2;
+        L *= kRates[k];
+        best = std::max(best, ch * L);
+    }
+    return best;
+}
+
+template <typename A>
+void carve_voc(A& a, const m2_config& c, int B, int T, float** bufs) {
+    const size_t n = (size_t)B * vocoder_max_cl(c, T);
+    for (int i = 0; i < 3; ++i) {
+        float* p = a.template take<float>(n);
+        if (bufs) bufs[i] = p;
+    }
+}
+
+// One pre-LN transformer layer (components.py:131-140), x updated in place;
+// for the first decoder layer the residual source is the caller's input.
+int32_t run_layer(const m2_model* m, const m2_layer_w& L, const float* x_in, float* x, TfBufs& wb,
+                  const uint8_t* mask, int B, int N, hipStream_t st) {
+    const int H = m->cfg.hidden_dim, R = B * N;
+    int32_t rc;
+    if ((rc = launch_linear(x_in, L.n1_w, L.n1_b, L.qkv_w, nullptr, nullptr, ACT_NONE, R, H, 3 * H, wb.qkv, st))) return rc;
+    if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st))) return rc;
+    if ((rc = launch_linear(wb.att, nullptr, nullptr, L.out_w, L.out_b, x_in, ACT_NONE, R, H, H, x, st))) return rc;
+    if ((rc = launch_linear(x, L.n2_w, L.n2_b, L.ff1_w, L.ff1_b, nullptr, ACT_RELU, R, H, 2 * H, wb.hid, st))) return rc;
+    if ((rc = launch_linear(wb.hid, nullptr, nullptr, L.ff2_w, L.ff2_b, x, ACT_NONE, R, 2 * H, H, x, st))) return rc;
+    return M2_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t m2_abi_version(void) { return M2_ABI_VERSION; }
+
+const char* m2_last_error(void) { return g_last_error.c_str(); }
+
+int32_t m2_weight_count(const m2_config* cfg) {
+    if (!config_ok(cfg)) return fail(M2_E_ARG, "m2_weight_count: invalid config");
+    return (int32_t)weight_table(*cfg).size();
+}
+
+int32_t m2_weight_name(const m2_config* cfg, int32_t index, char* buf, int32_t buflen) {
+    if (!config_ok(cfg) || !buf || buflen <= 0) return fail(M2_E_ARG, "m2_weight_name: bad argument");
+    const auto t = weight_table(*cfg);
+    if (index < 0 || index >= (int32_t)t.size()) return fail(M2_E_ARG, "m2_weight_name: index out of range");
+    const std::string& n = t[index].name;
+    if ((int32_t)n.size() + 1 > buflen) return fail(M2_E_ARG, "m2_weight_name: buffer too small");
+    std::memcpy(buf, n.c_str(), n.size() + 1);
+    return M2_OK;
+}
+
+int64_t m2_weight_numel(const m2_config* cfg, int32_t index) {
+    if (!config_ok(cfg)) return fail(M2_E_ARG, "m2_weight_numel: invalid config");
+    const auto t = weight_table(*cfg);
+    if (index < 0 || index >= (int32_t)t.size()) return fail(M2_E_ARG, "m2_weight_numel: index out of range");
+    return t[index].numel;
+}
+
+int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_t n_weights,
+                        void* stream, m2_model** out) {
+    M2_CHECK_ARG(config_ok(cfg), "m2_model_create: invalid config");
+    M2_CHECK_ARG(weights && out, "m2_model_create: null argument");
+    const auto table = weight_table(*cfg);
+    if (n_weights != (int32_t)table.size()) return fail(M2_E_WEIGHTS, "m2_model_create: weight count mismatch");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int H = cfg->hidden_dim;
+
+    // Layout: every fp32 weight copied verbatim, then 2x(alpha,beta) for the
+    // BatchNorm inference form; 64-float aligned carves.
+    std::vector<size_t> off(table.size(), 0);
+    size_t total = 0;
+    for (size_t i = 0; i < table.size(); ++i) {
+        if (table[i].is_int64) continue;
+        total = align_up(total, 64);
+        off[i] = total;
+        total += (size_t)table[i].numel;
+        M2_CHECK_ARG(weights[i] != nullptr, "m2_model_create: null weight pointer");
+    }
+    total = align_up(total, 64);
+    const size_t bn_off = total;
+    total += 4 * (size_t)H;
+
+    auto* m = new m2_model();
+    m->cfg = *cfg;
+    hipError_t e = hipMalloc(&m->buf, total * sizeof(float));
+    if (e != hipSuccess) { delete m; return hip_status(e, "hipMalloc(model)"); }
+    auto bail = [&](hipError_t err, const char* w) { (void)hipFree(m->buf); delete m; return hip_status(err, w); };
+    for (size_t i = 0; i < table.size(); ++i) {
+        if (table[i].is_int64) continue;
+        e = hipMemcpyAsync(m->buf + off[i], weights[i], table[i].numel * sizeof(float), hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return bail(e, "hipMemcpyAsync(weight)");
+    }
+
+    // name -> index
+    auto idx = [&](const std::string& n) {
+        for (size_t i = 0; i < table.size(); ++i) if (table[i].name == n) return (int)i;
+        return -1;
+    };
+    m->ptr.resize(table.size(), nullptr);
+    for (size_t i = 0; i < table.size(); ++i) if (!table[i].is_int64) m->ptr[i] = m->buf + off[i];
+    auto P = [&](const std::string& n) { return m->ptr[idx(n)]; };
+
+    // BatchNorm1d eval: alpha = gamma / sqrt(var + eps), beta' = beta - mean * alpha
+    // (ATen batch_norm_cpu_collect_linear_and_constant_terms, fp32).
+    std::vector<float> host(4 * (size_t)H), bnw(H), bnb(H), bnm(H), bnv(H);
+    for (int j = 0; j < 2; ++j) {
+        const std::string p = "duration_predictor.predictor.conv_layers." + std::to_string(j) + ".norm.";
+        const float* src[4] = {static_cast<const float*>(weights[idx(p + "weight")]), static_cast<const float*>(weights[idx(p + "bias")]),
+                               static_cast<const float*>(weights[idx(p + "running_mean")]), static_cast<const float*>(weights[idx(p + "running_var")])};
+        float* dst[4] = {bnw.data(), bnb.data(), bnm.data(), bnv.data()};
+        for (int q = 0; q < 4; ++q) {
+            e = hipMemcpyAsync(dst[q], src[q], H * sizeof(float), hipMemcpyDeviceToHost, st);
+            if (e != hipSuccess) return bail(e, "hipMemcpyAsync(bn)");
+        }
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return bail(e, "hipStreamSynchronize");
+        for (int c = 0; c < H; ++c) {
+            const float invstd = 1.0f / std::sqrt(bnv[c] + 1e-5f);
+            const float a = invstd * bnw[c];
+            host[(2 * j) * H + c] = a;
+            host[(2 * j + 1) * H + c] = bnb[c] - bnm[c] * a;
+        }
+    }
+    e = hipMemcpyAsync(m->buf + bn_off, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return bail(e, "hipMemcpyAsync(bn up)");
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return bail(e, "hipStreamSynchronize");
+
+    m->emb = P("text_encoder.embedding.weight");
+    m->pe = P("text_encoder.pos_encoding.pe");
+    auto layer = [&](const std::string& p) {
+        return m2_layer_w{P(p + ".self_attn.qkv.weight"), P(p + ".self_attn.out_proj.weight"), P(p + ".self_attn.out_proj.bias"),
+                          P(p + ".ffn.linear1.weight"), P(p + ".ffn.linear1.bias"), P(p + ".ffn.linear2.weight"),
+                          P(p + ".ffn.linear2.bias"), P(p + ".norm1.weight"), P(p + ".norm1.bias"),
+                          P(p + ".norm2.weight"), P(p + ".norm2.bias")};
+    };
+    for (int i = 0; i < cfg->text_encoder_layers; ++i) m->enc.push_back(layer("text_encoder.layers." + std::to_string(i)));
+    for (int i = 0; i < cfg->decoder_layers; ++i) m->dec.push_back(layer("decoder.layers." + std::to_string(i)));
+    m->enc_nw = P("text_encoder.norm.weight");
+    m->enc_nb = P("text_encoder.norm.bias");
+    for (int j = 0; j < 2; ++j) {
+        const std::string p = "duration_predictor.predictor.conv_layers." + std::to_string(j) + ".conv.";
+        m->dur[4 * j + 0] = P(p + "weight");
+        m->dur[4 * j + 1] = P(p + "bias");
+        m->dur[4 * j + 2] = m->buf + bn_off + (2 * j) * H;
+        m->dur[4 * j + 3] = m->buf + bn_off + (2 * j + 1) * H;
+    }
+    m->dur[8] = P("duration_predictor.predictor.projection.weight");
+    m->dur[9] = P("duration_predictor.predictor.projection.bias");
+    m->dec_nw = P("decoder.norm.weight");
+    m->dec_nb = P("decoder.norm.bias");
+    m->mel_w = P("decoder.mel_projection.weight");
+    m->mel_b = P("decoder.mel_projection.bias");
+    m->vin_w = P("vocoder.input_conv.weight");
+    m->vin_b = P("vocoder.input_conv.bias");
+    for (int k = 0; k < 4; ++k) {
+        const std::string u = "vocoder.upsamples." + std::to_string(k);
+        const std::string r = "vocoder.resblocks." + std::to_string(k);
+        m->up_w[k] = P(u + ".weight");
+        m->up_b[k] = P(u + ".bias");
+        m->rb_w1[k] = P(r + ".conv1.weight");
+        m->rb_b1[k] = P(r + ".conv1.bias");
+        m->rb_w2[k] = P(r + ".conv2.weight");
+        m->rb_b2[k] = P(r + ".conv2.bias");
+    }
+    m->vout_w = P("vocoder.output_conv.weight");
+    m->vout_b = P("vocoder.output_conv.bias");
+    *out = m;
+    return M2_OK;
+}
+
+int32_t m2_profile_disable(m2_model* model);
+
+int32_t m2_model_destroy(m2_model* model) {
+    if (!model) return M2_OK;
+    m2_profile_disable(model);
+    hipError_t e = hipFree(model->buf);
+    delete model;
+    if (e != hipSuccess) return hip_status(e, "hipFree(model)");
+    return M2_OK;
+}
+
+int32_t m2_model_config(const m2_model* model, m2_config* out) {
+    M2_CHECK_ARG(model && out, "m2_model_config: null argument");
+    *out = model->cfg;
+    return M2_OK;
+}
+
+size_t m2_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T) {
+    if (!model || B < 0 || S < 0 || T < 0) return 0;
+    const int H = model->cfg.hidden_dim;
+    Sizer a, b, c;
+    carve_tf(a, B, S, H, nullptr);
+    carve_tf(b, B, T, H, nullptr);
+    carve_voc(c, model->cfg, B, T, nullptr);
+    return std::max(a.off, std::max(b.off, c.off)) + 256;
+}
+
+int32_t m2_text_encoder(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B,
+                        int32_t S, float* out_enc, uint8_t* out_mask, void* workspace,
+                        size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && ids && out_enc && B >= 0 && S >= 0, "m2_text_encoder: bad argument");
+    M2_CHECK_SHAPE(S <= m->cfg.max_positions, "m2_text_encoder: sequence longer than the positional table");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int H = m->cfg.hidden_dim;
+    Carve a(workspace, workspace_bytes);
+    TfBufs wb;
+    carve_tf(a, B, S, H, &wb);
+    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_text_encoder: workspace too small");
+    if (B == 0 || S == 0) return M2_OK;
+    int32_t rc;
+    const uint8_t* mask = nullptr;
+    if (lengths) {
+        uint8_t* mk = out_mask ? out_mask : wb.mask;
+        if ((rc = mask_kernel_launch(lengths, B, S, mk, st))) return rc;
+        mask = mk;
+    }
+    if ((rc = launch_embed_pe(ids, m->emb, m->pe, B, S, H, m->cfg.vocab_size, wb.x, st))) return rc;
+    for (const auto& L : m->enc)
+        if ((rc = run_layer(m, L, wb.x, wb.x, wb, mask, B, S, st))) return rc;
+    return launch_layer_norm(wb.x, m->enc_nw, m->enc_nb, B * S, H, out_enc, st);
+}
+
+int32_t m2_duration_predictor(const m2_model* m, const float* enc, int32_t B, int32_t S,
+                              float* out_dur, void* workspace, size_t workspace_bytes, void* stream) {
+    (void)workspace;
+    (void)workspace_bytes;
+    M2_CHECK_ARG(m && enc && out_dur && B >= 0 && S >= 0, "m2_duration_predictor: bad argument");
+    return launch_duration(enc, B, S, m->cfg.hidden_dim, m->dur, out_dur, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_length_regulator_count(const void* dur, int32_t dur_is_int, float scale, int32_t B,
+                                  int32_t S, int32_t* out_cum, int32_t* out_T, int32_t* out_Tmax,
+                                  void* stream) {
+    M2_CHECK_ARG(dur && out_cum && out_T && out_Tmax && B >= 0 && S >= 0, "m2_length_regulator_count: bad argument");
+    return launch_lr_count(dur, dur_is_int, scale, B, S, out_cum, out_T, out_Tmax, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_length_regulator_expand(const float* enc, const int32_t* cum, int32_t B, int32_t S,
+                                   int32_t H, int32_t T_out, float* out, void* stream) {
+    M2_CHECK_ARG(enc && cum && out && B >= 0 && S >= 0 && H > 0 && T_out >= 0, "m2_length_regulator_expand: bad argument");
+    return launch_lr_expand(enc, cum, B, S, H, T_out, out, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, float* out_mel,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && x && out_mel && B >= 0 && T >= 0, "m2_mel_decoder: bad argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int H = m->cfg.hidden_dim;
+    Carve a(workspace, workspace_bytes);
+    TfBufs wb;
+    carve_tf(a, B, T, H, &wb);
+    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_mel_decoder: workspace too small");
+    if (B == 0 || T == 0) return M2_OK;
+    int32_t rc;
+    const float* cur = x;
+    for (const auto& L : m->dec) {
+        if ((rc = run_layer(m, L, cur, wb.x, wb, nullptr, B, T, st))) return rc;
+        cur = wb.x;
+    }
+    return launch_linear(cur, m->dec_nw, m->dec_nb, m->mel_w, m->mel_b, nullptr, ACT_NONE, B * T, H,
+                         m->cfg.mel_channels, out_mel, st);
+}
+
+int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T,
+                   float* out_audio, void* workspace, size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && mel && out_audio && B >= 0 && T >= 0, "m2_vocoder: bad argument");
+    M2_CHECK_ARG(mel_layout == 0 || mel_layout == 1, "m2_vocoder: mel_layout must be 0 or 1");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    Carve a(workspace, workspace_bytes);
+    float* buf[3];
+    carve_voc(a, m->cfg, B, T, buf);
+    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
+    if (B == 0 || T == 0) return M2_OK;
+    int32_t rc;
+    int ch = m->cfg.vocoder_channels, L = T;
+    float *cur = buf[0], *up = buf[1], *tmp = buf[2];
+    if ((rc = launch_conv(mel, m->vin_w, m->vin_b, nullptr, nullptr, nullptr, 3, ACT_NONE, mel_layout == 1, B, m->cfg.mel_channels, ch, L, cur, st))) return rc;
+    for (int k = 0; k < 4; ++k) {
+        if ((rc = launch_convT(cur, m->up_w[k], m->up_b[k], kRates[k], ACT_LEAKY, B, ch, ch / 2, L, up, st))) return rc;
+        ch /= 2;
+        L *= kRates[k];
+        if (k == kProfStage) {
+            ProfScope ps(m, st);
+            if ((rc = launch_conv(up, m->rb_w1[k], m->rb_b1[k], nullptr, nullptr, nullptr, 3, ACT_LEAKY, false, B, ch, ch, L, tmp, st))) return rc;
+        } else if ((rc = launch_conv(up, m->rb_w1[k], m->rb_b1[k], nullptr, nullptr, nullptr, 3, ACT_LEAKY, false, B, ch, ch, L, tmp, st))) return rc;
+        if ((rc = launch_conv(tmp, m->rb_w2[k], m->rb_b2[k], nullptr, nullptr, up, 3, ACT_NONE, false, B, ch, ch, L, cur, st))) return rc;
+    }
+    return launch_conv(cur, m->vout_w, m->vout_b, nullptr, nullptr, nullptr, 3, ACT_TANH, false, B, ch, 1, L, out_audio, st);
+}
+
+int32_t m2_vocoder_resblock(const m2_model* m, int32_t k, const float* x, int32_t B, int32_t L,
+                            float* y, float* tmp, void* stream) {
+    M2_CHECK_ARG(m && x && y && tmp && k >= 0 && k < 4 && B >= 0 && L >= 0, "m2_vocoder_resblock: bad argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int ch = m->cfg.vocoder_channels >> (k + 1);
+    int32_t rc;
+    if ((rc = launch_conv(x, m->rb_w1[k], m->rb_b1[k], nullptr, nullptr, nullptr, 3, ACT_LEAKY, false, B, ch, ch, L, tmp, st))) return rc;
+    return launch_conv(tmp, m->rb_w2[k], m->rb_b2[k], nullptr, nullptr, x, 3, ACT_NONE, false, B, ch, ch, L, y, st);
+}
+
+int32_t m2_vocoder_upsample(const m2_model* m, int32_t k, const float* x, int32_t B, int32_t L,
+                            float* y, void* stream) {
+    M2_CHECK_ARG(m && x && y && k >= 0 && k < 4 && B >= 0 && L >= 0, "m2_vocoder_upsample: bad argument");
+    const int ch = m->cfg.vocoder_channels >> k;
+    return launch_convT(x, m->up_w[k], m->up_b[k], kRates[k], ACT_LEAKY, B, ch, ch / 2, L, y, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_conv1d(const float* x, const float* w, const float* b, const float* alpha,
+                  const float* beta, const float* res, int32_t ksize, int32_t act, int32_t B,
+                  int32_t Cin, int32_t Cout, int32_t L, float* y, void* stream) {
+    M2_CHECK_ARG(x && w && b && y && B >= 0 && L >= 0 && act >= 0 && act <= 4, "m2_conv1d: bad argument");
+    return launch_conv(x, w, b, alpha, beta, res, ksize, act, false, B, Cin, Cout, L, y, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_conv_transpose1d(const float* x, const float* w, const float* b, int32_t rate,
+                            int32_t act, int32_t B, int32_t Cin, int32_t Cout, int32_t L, float* y,
+                            void* stream) {
+    M2_CHECK_ARG(x && w && b && y && B >= 0 && L >= 0 && act >= 0 && act <= 3, "m2_conv_transpose1d: bad argument");
+    return launch_convT(x, w, b, rate, act, B, Cin, Cout, L, y, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_linear(const float* x, const float* gamma, const float* beta, const float* w,
+                  const float* b, const float* res, int32_t act, int32_t R, int32_t K, int32_t N,
+                  float* y, void* stream) {
+    M2_CHECK_ARG(x && w && y && R >= 0 && (act == ACT_NONE || act == ACT_RELU), "m2_linear: bad argument");
+    M2_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "m2_linear: gamma and beta go together");
+    return launch_linear(x, gamma, beta, w, b, res, act, R, K, N, y, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_layer_norm(const float* x, const float* gamma, const float* beta, int32_t R, int32_t K,
+                      float* y, void* stream) {
+    M2_CHECK_ARG(x && gamma && beta && y && R >= 0 && K > 0, "m2_layer_norm: bad argument");
+    return launch_layer_norm(x, gamma, beta, R, K, y, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_attention(const float* qkv, const uint8_t* key_mask, int32_t B, int32_t N, int32_t H,
+                     int32_t heads, float* out, void* stream) {
+    M2_CHECK_ARG(qkv && out && B >= 0 && N >= 0 && H > 0 && heads > 0, "m2_attention: bad argument");
+    return launch_attention(qkv, key_mask, B, N, H, heads, out, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_embed_positional(const int64_t* ids, const float* emb, const float* pe, int32_t B,
+                            int32_t S, int32_t H, int32_t vocab, float scale, float* y,
+                            void* stream) {
+    M2_CHECK_ARG(ids && emb && pe && y && B >= 0 && S >= 0 && H > 0 && vocab > 0, "m2_embed_positional: bad argument");
+    return launch_embed_pe_scaled(ids, emb, pe, B, S, H, vocab, scale, y, static_cast<hipStream_t>(stream));
+}
+
+int32_t m2_add_positional(const float* x, const float* pe, int32_t B, int32_t S, int32_t H,
+                          float* y, void* stream) {
+    M2_CHECK_ARG(x && pe && y && B >= 0 && S >= 0 && H > 0, "m2_add_positional: bad argument");
+    return launch_add_pe(x, pe, B, S, H, y, static_cast<hipStream_t>(stream));
+}
+
+const char* m2_profile_kernel_name(void) { return kProfKernel; }
+
+int32_t m2_profile_enable(m2_model* m, int32_t capacity) {
+    M2_CHECK_ARG(m && capacity >= 0, "m2_profile_enable: bad argument");
+    m2_profile_disable(m);
+    for (int i = 0; i < capacity; ++i) {
+        hipEvent_t a, b;
+        M2_HIP(hipEventCreate(&a));
+        M2_HIP(hipEventCreate(&b));
+        m->prof_begin.push_back(a);
+        m->prof_end.push_back(b);
+    }
+    m->prof_next = 0;
+    return M2_OK;
+}
+
+int32_t m2_profile_read(m2_model* m, float* ms_out, int32_t capacity, int32_t* n_out) {
+    M2_CHECK_ARG(m && ms_out && n_out, "m2_profile_read: bad argument");
+    const int n = std::min<int>(capacity, m->prof_next);
+    for (int i = 0; i < n; ++i) {
+        M2_HIP(hipEventSynchronize(m->prof_end[i]));
+        M2_HIP(hipEventElapsedTime(&ms_out[i], m->prof_begin[i], m->prof_end[i]));
+    }
+    *n_out = n;
+    m->prof_next = 0;
+    return M2_OK;
+}
+
+int32_t m2_profile_disable(m2_model* m) {
+    if (!m) return M2_OK;
+    for (auto e : m->prof_begin) (void)hipEventDestroy(e);
+    for (auto e : m->prof_end) (void)hipEventDestroy(e);
+    m->prof_begin.clear();
+    m->prof_end.clear();
+    m->prof_next = 0;
+    return M2_OK;
+}
+
+}  // extern "C"

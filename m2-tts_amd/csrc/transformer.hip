@@ -1,0 +1,318 @@
+// Transformer kernels for the text encoder and the mel decoder (gfx950).
+//
+//   embed_pe_kernel    TextEncoder embed*sqrt(H) + pe           tts_model.py:78-80
+//   layer_norm_kernel  nn.LayerNorm(eps 1e-5)                   tts_model.py:87,223
+//   linear_kernel      [LN ->] x.W^T + b [-> relu] [+ residual] components.py:55-56,98-103,131-140
+//   attention_kernel   softmax(QK^T*scale, -1e9 key mask).V     components.py:72-86
+//
+// All fp32.  The GEMMs run on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32,
+// 64 FLOP/clk/SIMD = the fp32 vector peak, one rounding per product).
+#include "m2_common.h"
+
+namespace m2 {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// x[b,s,:] = E[ids[b,s],:] * sqrt(H) + pe[s,:]
+// Out-of-range ids read a zero row (the reference would raise in nn.Embedding).
+__global__ void embed_pe_kernel(const int64_t* __restrict__ ids, const float* __restrict__ emb,
+                                const float* __restrict__ pe, int R, int S, int H, int vocab,
+                                float emb_scale, float* __restrict__ out) {
+    const int total = R * H;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int r = i / H, h = i - r * H;
+        const int64_t id = ids[r];
+        const float e = (id >= 0 && id < vocab) ? emb[id * H + h] : 0.f;
+        out[i] = e * emb_scale + pe[(r % S) * H + h];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// One wave per row; two-pass mean / biased variance, as nn.LayerNorm.
+__global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ g,
+                                                         const float* __restrict__ b, int R,
+                                                         int K, float* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= R) return;
+    const float* xr = x + (size_t)row * K;
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s += xr[k];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)K;
+    float v = 0.f;
+    for (int k = lane; k < K; k += 64) { float d = xr[k] - mean; v += d * d; }
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const float rstd = 1.0f / sqrtf(v / (float)K + kLnEps);
+    float* yr = y + (size_t)row * K;
+    for (int k = lane; k < K; k += 64) yr[k] = (xr[k] - mean) * rstd * g[k] + b[k];
+}
+
+// ---------------------------------------------------------------------------
+// y[R,N] = act(LN?(x)[R,K] . W[N,K]^T + bias) (+ res[R,N])
+//
+// Workgroup = 4 waves, output tile 64 rows x 64 cols; wave (wr,wc) owns a
+// 32x32 sub-tile accumulated by K/2 v_mfma_f32_32x32x2_f32.  X and W tiles
+// are staged in LDS with rows padded by 4 floats (16 B), so the per-lane
+// float4 operand reads of 32 different rows hit distinct bank quads.
+// k-order: at step s, lane half h supplies k = h*K/2 + s for BOTH operands,
+// so each lane streams its k range with float4 reads (any consistent k
+// permutation is a valid order for the sum).  Needs K % 8 == 0, K <= 256.
+constexpr int LIN_TILE = 64;
+
+__global__ __launch_bounds__(256) void linear_kernel(
+    const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ w, const float* __restrict__ bias, const float* res, int act, int R,
+    int K, int N, float* y) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int KP = K + 4;
+    float* Xs = lds;                    // [64][KP]
+    float* Ws = lds + LIN_TILE * KP;    // [64][KP]
+    float* stats = Ws + LIN_TILE * KP;  // [64][2] mean, rstd
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * LIN_TILE, c0 = blockIdx.y * LIN_TILE;
+    const int K4 = K >> 2;
+
+    for (int i = tid; i < LIN_TILE * K4; i += 256) {
+        const int row = i / K4, c4 = i - row * K4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r0 + row < R) v = *reinterpret_cast<const float4*>(x + (size_t)(r0 + row) * K + 4 * c4);
+        *reinterpret_cast<float4*>(Xs + row * KP + 4 * c4) = v;
+        float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c0 + row < N) u = *reinterpret_cast<const float4*>(w + (size_t)(c0 + row) * K + 4 * c4);
+        *reinterpret_cast<float4*>(Ws + row * KP + 4 * c4) = u;
+    }
+    __syncthreads();
+
+    if (gamma != nullptr) {
+        // 4 lanes per row: partial sums then a 4-lane butterfly.
+        const int row = tid >> 2, part = tid & 3;
+        const float* xr = Xs + row * KP;
+        float s = 0.f;
+        for (int k = part; k < K; k += 4) s += xr[k];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        const float mean = s / (float)K;
+        float v = 0.f;
+        for (int k = part; k < K; k += 4) { float d = xr[k] - mean; v += d * d; }
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        if (part == 0) { stats[2 * row] = mean; stats[2 * row + 1] = 1.0f / sqrtf(v / (float)K + kLnEps); }
+        __syncthreads();
+        for (int i = tid; i < LIN_TILE * K; i += 256) {
+            const int rr = i / K, k = i - rr * K;
+            float* p = Xs + rr * KP + k;
+            *p = (*p - stats[2 * rr]) * stats[2 * rr + 1] * gamma[k] + beta[k];
+        }
+        __syncthreads();
+    }
+
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wr = wave >> 1, wc = wave & 1;
+    if (c0 + wc * 32 >= N) return;  // whole sub-tile past the last column
+    const int li = lane & 31, h = lane >> 5;
+    const float* ap = Xs + (wr * 32 + li) * KP + h * (K >> 1);
+    const float* bp = Ws + (wc * 32 + li) * KP + h * (K >> 1);
+    f32x16 acc = {};
+    for (int s = 0; s < (K >> 1); s += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(ap + s);
+        const float4 bb = *reinterpret_cast<const float4*>(bp + s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bb.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bb.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bb.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bb.w, acc, 0, 0, 0);
+    }
+    const int col = c0 + wc * 32 + li;
+    if (col >= N) return;
+    const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = r0 + wr * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < R) {
+            float v = acc[reg] + bv;
+            if (act == ACT_RELU) v = v > 0.f ? v : 0.f;
+            const size_t o = (size_t)row * N + col;
+            if (res) v = res[o] + v;
+            y[o] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Attention core, one query per lane, keys streamed through LDS in chunks of
+// 64 with an online (running max / running sum) softmax.  Scores are
+// (q.k) * scale with the scale applied after the dot product and masked keys
+// set to exactly -1e9, as the reference does, so a fully masked row is a
+// uniform average - the same as the reference's softmax over -1e9s.
+template <int HD>
+__global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__ qkv,
+                                                       const uint8_t* __restrict__ key_mask,
+                                                       int N, int H, float scale,
+                                                       float* __restrict__ out) {
+    constexpr int KC = 64;
+    __shared__ __attribute__((aligned(16))) float Ks[KC * HD];
+    __shared__ __attribute__((aligned(16))) float Vs[KC * HD];
+    __shared__ float Mk[KC];
+    const int b = blockIdx.z, hh = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int qi = blockIdx.x * 64 + tid;
+    const size_t row3 = (size_t)3 * H;
+    const float* base = qkv + (size_t)b * N * row3;
+    const bool valid = qi < N;
+
+    float q[HD], o[HD];
+#pragma unroll
+    for (int d = 0; d < HD; ++d) { q[d] = valid ? base[qi * row3 + hh * HD + d] : 0.f; o[d] = 0.f; }
+    float m = -INFINITY, l = 0.f;
+
+    for (int j0 = 0; j0 < N; j0 += KC) {
+        __syncthreads();
+        for (int i = tid; i < KC * HD; i += 64) {
+            const int key = i / HD, d = i - key * HD;
+            const int j = j0 + key;
+            Ks[i] = j < N ? base[j * row3 + H + hh * HD + d] : 0.f;
+            Vs[i] = j < N ? base[j * row3 + 2 * H + hh * HD + d] : 0.f;
+        }
+        {
+            const int j = j0 + tid;
+            // 0: live key, 1: masked (score -1e9), 2: past the end (weight 0)
+            Mk[tid] = j >= N ? 2.f : ((key_mask && key_mask[(size_t)b * N + j] == 0) ? 1.f : 0.f);
+        }
+        __syncthreads();
+        float sc[KC];
+        float cmax = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            float dot = 0.f;
+            const float4* kr = reinterpret_cast<const float4*>(Ks + j * HD);
+#pragma unroll
+            for (int d4 = 0; d4 < HD / 4; ++d4) {
+                const float4 kv = kr[d4];
+                dot = fmaf(q[4 * d4 + 0], kv.x, dot);
+                dot = fmaf(q[4 * d4 + 1], kv.y, dot);
+                dot = fmaf(q[4 * d4 + 2], kv.z, dot);
+                dot = fmaf(q[4 * d4 + 3], kv.w, dot);
+            }
+            float s = dot * scale;
+            const float mk = Mk[j];
+            s = mk == 0.f ? s : (mk == 1.f ? kMaskFill : -INFINITY);
+            sc[j] = s;
+            cmax = fmaxf(cmax, s);
+        }
+        const float mn = fmaxf(m, cmax);
+        const float corr = expf(m - mn);  // m=-inf on the first chunk -> 0
+        l *= corr;
+#pragma unroll
+        for (int d = 0; d < HD; ++d) o[d] *= corr;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            const float p = expf(sc[j] - mn);
+            l += p;
+            const float4* vr = reinterpret_cast<const float4*>(Vs + j * HD);
+#pragma unroll
+            for (int d4 = 0; d4 < HD / 4; ++d4) {
+                const float4 vv = vr[d4];
+                o[4 * d4 + 0] = fmaf(p, vv.x, o[4 * d4 + 0]);
+                o[4 * d4 + 1] = fmaf(p, vv.y, o[4 * d4 + 1]);
+                o[4 * d4 + 2] = fmaf(p, vv.z, o[4 * d4 + 2]);
+                o[4 * d4 + 3] = fmaf(p, vv.w, o[4 * d4 + 3]);
+            }
+        }
+        m = mn;
+    }
+    if (!valid) return;
+    const float inv = 1.0f / l;
+    float* orow = out + ((size_t)b * N + qi) * H + hh * HD;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) orow[d] = o[d] * inv;
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers (used by the runtime and by the standalone C entry points).
+int32_t launch_embed_pe(const int64_t* ids, const float* emb, const float* pe, int B, int S, int H,
+                        int vocab, float* out, hipStream_t st) {
+    const int total = B * S * H;
+    const int grid = std::min(cdiv(total, 256), 4096);
+    const float scale = (float)std::sqrt((double)H);  // python float H**0.5, cast to fp32 by the mul
+    hipLaunchKernelGGL(embed_pe_kernel, dim3(grid), dim3(256), 0, st, ids, emb, pe, B * S, S, H,
+                       vocab, scale, out);
+    M2_LAUNCHED("embed_pe_kernel");
+    return M2_OK;
+}
+
+int32_t launch_embed_pe_scaled(const int64_t* ids, const float* emb, const float* pe, int B, int S,
+                               int H, int vocab, float scale, float* out, hipStream_t st) {
+    const int total = B * S * H;
+    if (total == 0) return M2_OK;
+    const int grid = std::min(cdiv(total, 256), 4096);
+    hipLaunchKernelGGL(embed_pe_kernel, dim3(grid), dim3(256), 0, st, ids, emb, pe, B * S, S, H,
+                       vocab, scale, out);
+    M2_LAUNCHED("embed_pe_kernel");
+    return M2_OK;
+}
+
+__global__ void add_pe_kernel(const float* __restrict__ x, const float* __restrict__ pe, int R,
+                              int S, int H, float* __restrict__ y) {
+    const int total = R * H;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int r = i / H, h = i - r * H;
+        y[i] = x[i] + pe[(r % S) * H + h];
+    }
+}
+
+int32_t launch_add_pe(const float* x, const float* pe, int B, int S, int H, float* y, hipStream_t st) {
+    const int total = B * S * H;
+    if (total == 0) return M2_OK;
+    hipLaunchKernelGGL(add_pe_kernel, dim3(std::min(cdiv(total, 256), 4096)), dim3(256), 0, st, x,
+                       pe, B * S, S, H, y);
+    M2_LAUNCHED("add_pe_kernel");
+    return M2_OK;
+}
+
+int32_t launch_layer_norm(const float* x, const float* g, const float* b, int R, int K, float* y,
+                          hipStream_t st) {
+    if (R == 0) return M2_OK;
+    hipLaunchKernelGGL(layer_norm_kernel, dim3(cdiv(R, 4)), dim3(256), 0, st, x, g, b, R, K, y);
+    M2_LAUNCHED("layer_norm_kernel");
+    return M2_OK;
+}
+
+int32_t launch_linear(const float* x, const float* gamma, const float* beta, const float* w,
+                      const float* bias, const float* res, int act, int R, int K, int N, float* y,
+                      hipStream_t st) {
+    M2_CHECK_SHAPE(K % 8 == 0 && K <= 256 && K > 0, "linear: K must be a multiple of 8 and <= 256");
+    if (R == 0 || N == 0) return M2_OK;
+    const size_t lds = sizeof(float) * (2 * LIN_TILE * (K + 4) + 2 * LIN_TILE);
+    static bool attr_set = false;
+    if (!attr_set) {
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(linear_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(linear_kernel, dim3(cdiv(R, LIN_TILE), cdiv(N, LIN_TILE)), dim3(256), lds,
+                       st, x, gamma, beta, w, bias, res, act, R, K, N, y);
+    M2_LAUNCHED("linear_kernel");
+    return M2_OK;
+}
+
+int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, int H, int heads,
+                         float* out, hipStream_t st) {
+    M2_CHECK_SHAPE(heads > 0 && H % heads == 0, "attention: H % heads != 0");
+    const int hd = H / heads;
+    if (B == 0 || N == 0) return M2_OK;
+    const float scale = (float)(1.0 / std::sqrt((double)hd));  // components.py:510, fp32 at the mul
+    dim3 grid(cdiv(N, 64), heads, B);
+    switch (hd) {
+        case 16: hipLaunchKernelGGL(attention_kernel<16>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
+        case 32: hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
+        case 48: hipLaunchKernelGGL(attention_kernel<48>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
+        case 64: hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
+        default: return fail(M2_E_SHAPE, "attention: head_dim must be 16, 32, 48 or 64");
+    }
+    M2_LAUNCHED("attention_kernel");
+    return M2_OK;
+}
+
+}  // namespace m2

@@ -1,0 +1,161 @@
+"""Model-level runtime: one packed ``m2_model`` handle per (model, device).
+
+``HipModel`` uploads the weights of an ``M2TTSModel`` once
+(``m2_model_create``) and exposes the stage entry points of the C ABI with
+torch tensors.  ``M2TTSModel`` (models/tts_model.py) keeps one HipModel per
+device in a side table and rebuilds it when any parameter/buffer changes
+storage or version (``load_state_dict``, ``.to()``, in-place edits).
+"""
+from __future__ import annotations
+
+import ctypes
+import weakref
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+from .ops import f32c, require_device, stream_handle
+
+Tensor = torch.Tensor
+
+
+def make_config(vocab_size: int, hidden_dim: int, mel_channels: int, text_encoder_layers: int,
+                decoder_layers: int, num_heads: int, vocoder_channels: int, max_positions: int) -> _lib.M2Config:
+    return _lib.M2Config(vocab_size, hidden_dim, mel_channels, text_encoder_layers, decoder_layers,
+                         num_heads, vocoder_channels, max_positions)
+
+
+def weight_names(cfg: _lib.M2Config):
+    lib = _lib.load()
+    n = lib.m2_weight_count(ctypes.byref(cfg))
+    _lib.check(0 if n >= 0 else n, "m2_weight_count")
+    buf = ctypes.create_string_buffer(256)
+    names = []
+    for i in range(n):
+        _lib.check(lib.m2_weight_name(ctypes.byref(cfg), i, buf, 256), "m2_weight_name")
+        names.append((buf.value.decode(), int(lib.m2_weight_numel(ctypes.byref(cfg), i))))
+    return names
+
+
+def state_key(module: torch.nn.Module) -> Tuple:
+    """Identity of the weights as stored right now (storage + version counters)."""
+    return tuple((t.data_ptr(), t._version) for t in module.state_dict(keep_vars=True).values())
+
+
+class HipModel:
+    def __init__(self, state: Dict[str, Tensor], cfg: _lib.M2Config, device: torch.device):
+        lib = _lib.load()
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.H = cfg.hidden_dim
+        self.M = cfg.mel_channels
+        names = weight_names(cfg)
+        ptrs = (ctypes.c_void_p * len(names))()
+        keep = []
+        for i, (name, numel) in enumerate(names):
+            if name not in state:
+                raise KeyError(f"m2-tts_amd: state_dict is missing {name!r}")
+            t = state[name]
+            if t.dtype == torch.int64:  # num_batches_tracked: not used by the forward path
+                ptrs[i] = t.data_ptr() if t.is_cuda else None
+                continue
+            require_device(t, what=f"weight {name}")
+            t = f32c(t.detach())
+            if t.numel() != numel:
+                raise ValueError(f"m2-tts_amd: {name} has {t.numel()} elements, expected {numel}")
+            keep.append(t)
+            ptrs[i] = t.data_ptr()
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(lib.m2_model_create(ctypes.byref(cfg), ptrs, len(names), stream_handle(self.device),
+                                           ctypes.byref(handle)), "m2_model_create")
+        self.handle = handle
+        self._ws: Optional[Tensor] = None
+        self._finalizer = weakref.finalize(self, lib.m2_model_destroy, handle)
+
+    # ------------------------------------------------------------------ scratch
+    def workspace(self, B: int, S: int, T: int) -> Tensor:
+        need = int(_lib.load().m2_workspace_bytes(self.handle, B, S, T))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    # ------------------------------------------------------------------ stages
+    def text_encoder(self, ids: Tensor, lengths: Optional[Tensor]):
+        require_device(ids, lengths, what="TextEncoder")
+        ids = ids.to(torch.int64).contiguous()
+        B, S = ids.shape
+        if S > self.cfg.max_positions:
+            raise RuntimeError(f"sequence length {S} exceeds the positional table ({self.cfg.max_positions})")
+        lens = lengths.to(torch.int64).contiguous() if lengths is not None else None
+        enc = torch.empty(B, S, self.H, device=self.device, dtype=torch.float32)
+        mask = torch.empty(B, S, device=self.device, dtype=torch.bool) if lens is not None else None
+        ws = self.workspace(B, S, 0)
+        _lib.call("m2_text_encoder", self.handle, ids.data_ptr(), None if lens is None else lens.data_ptr(), B, S,
+                  enc.data_ptr(), None if mask is None else mask.data_ptr(), ws.data_ptr(), ws.numel(),
+                  stream_handle(self.device))
+        return enc, mask
+
+    def duration(self, enc: Tensor) -> Tensor:
+        enc = f32c(enc)
+        B, S, _ = enc.shape
+        dur = torch.empty(B, S, device=self.device, dtype=torch.float32)
+        _lib.call("m2_duration_predictor", self.handle, enc.data_ptr(), B, S, dur.data_ptr(), None, 0,
+                  stream_handle(self.device))
+        return dur
+
+    def decoder(self, x: Tensor) -> Tensor:
+        x = f32c(x)
+        B, T, _ = x.shape
+        mel = torch.empty(B, T, self.M, device=self.device, dtype=torch.float32)
+        ws = self.workspace(B, 0, T)
+        _lib.call("m2_mel_decoder", self.handle, x.data_ptr(), B, T, mel.data_ptr(), ws.data_ptr(), ws.numel(),
+                  stream_handle(self.device))
+        return mel
+
+    def vocoder(self, mel: Tensor, layout_btm: bool) -> Tensor:
+        """mel [B,M,T] (layout_btm False) or [B,T,M] (True) -> audio [B,1,64T]."""
+        mel = f32c(mel)
+        B = mel.shape[0]
+        T = mel.shape[1] if layout_btm else mel.shape[2]
+        audio = torch.empty(B, 1, 64 * T, device=self.device, dtype=torch.float32)
+        ws = self.workspace(B, 0, T)
+        _lib.call("m2_vocoder", self.handle, mel.data_ptr(), 1 if layout_btm else 0, B, T, audio.data_ptr(),
+                  ws.data_ptr(), ws.numel(), stream_handle(self.device))
+        return audio
+
+    def resblock(self, k: int, x: Tensor) -> Tensor:
+        x = f32c(x)
+        B, _, L = x.shape
+        y = torch.empty_like(x)
+        tmp = torch.empty_like(x)
+        _lib.call("m2_vocoder_resblock", self.handle, k, x.data_ptr(), B, L, y.data_ptr(), tmp.data_ptr(),
+                  stream_handle(self.device))
+        return y
+
+    def upsample(self, k: int, x: Tensor, rate: int) -> Tensor:
+        x = f32c(x)
+        B, C, L = x.shape
+        y = torch.empty(B, C // 2, L * rate, device=self.device, dtype=torch.float32)
+        _lib.call("m2_vocoder_upsample", self.handle, k, x.data_ptr(), B, L, y.data_ptr(), stream_handle(self.device))
+        return y
+
+
+class HandleCache:
+    """Per-device HipModel for one nn.Module, rebuilt when its weights change."""
+
+    def __init__(self):
+        self._entries: Dict[torch.device, Tuple[Tuple, HipModel]] = {}
+
+    def get(self, module: torch.nn.Module, cfg: _lib.M2Config, device: torch.device) -> HipModel:
+        key = state_key(module)
+        ent = self._entries.get(device)
+        if ent is not None and ent[0] == key:
+            return ent[1]
+        hm = HipModel(module.state_dict(), cfg, device)
+        self._entries[device] = (key, hm)
+        return hm
+
+    def clear(self):
+        self._entries.clear()

@@ -1,0 +1,236 @@
+"""Drop-in ``models.tts_model`` for MI355X.
+
+Same classes, constructor signatures, submodule/parameter names (so
+reference checkpoints load unchanged), return types and shapes as the
+reference ``src/models/tts_model.py``; the forward path runs on gfx950 HIP
+kernels through the C ABI in ``include/m2tts_hip.h``:
+
+* ``M2TTSModel.forward`` / ``inference`` use one packed model handle
+  (``m2amd.runtime.HipModel``): one C call per stage, the length regulator as
+  a GPU scan + gather with a single device->host read of the frame count.
+* The stage modules (``text_encoder``, ``duration_predictor``,
+  ``length_regulator``, ``decoder``, ``vocoder``) may be called directly, as
+  the reference's callers do; inside an M2TTSModel they use the owner's
+  handle, standalone they compose the per-op kernels of ``m2amd.ops``.
+
+Differences from the reference that do not change results:
+* ``inference`` runs the vocoder once (the reference runs it inside
+  ``forward`` and again afterwards, tts_model.py:388-391 vs 435-436, on the
+  same mel) and skips the unscaled decoder pass when duration_scale != 1.
+* Eval-mode math only; see models/components.py.
+"""
+from __future__ import annotations
+
+import logging
+import weakref
+from typing import Any, Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from m2amd import ops
+from m2amd.runtime import HandleCache, make_config
+
+from .components import (LightweightResBlock, PositionalEncoding, TransformerEncoderLayer, VariancePredictor,
+                         count_parameters, create_padding_mask, initialize_weights)
+
+logger = logging.getLogger(__name__)
+Tensor = torch.Tensor
+
+UPSAMPLE_RATES = (4, 4, 2, 2)   # reference tts_model.py:244
+_HANDLES: "weakref.WeakKeyDictionary[nn.Module, HandleCache]" = weakref.WeakKeyDictionary()
+
+
+def _owner_handle(stage: nn.Module, attr: str, device: torch.device):
+    """The owning M2TTSModel's packed handle if `stage` is still its `attr`."""
+    ref = getattr(stage, "_m2_owner", None)
+    owner = ref() if ref is not None else None
+    if owner is None or getattr(owner, attr, None) is not stage:
+        return None
+    return owner._hip(device)
+
+
+class TextEncoder(nn.Module):
+    """Embedding*sqrt(H) + positional table, pre-LN transformer layers with a
+    key-padding mask, final LayerNorm (reference tts_model.py:19-89)."""
+
+    def __init__(self, vocab_size: int = 256, hidden_dim: int = 64, num_layers: int = 2, num_heads: int = 2,
+                 dropout: float = 0.1, max_seq_len: int = 1000):
+        super().__init__()
+        self.hidden_dim = hidden_dim
+        self.embedding = nn.Embedding(vocab_size, hidden_dim)
+        self.pos_encoding = PositionalEncoding(hidden_dim, max_seq_len)
+        self.layers = nn.ModuleList(
+            [TransformerEncoderLayer(hidden_dim=hidden_dim, num_heads=num_heads, ffn_dim=hidden_dim * 2, dropout=dropout)
+             for _ in range(num_layers)])
+        self.norm = nn.LayerNorm(hidden_dim)
+        self.dropout = nn.Dropout(dropout)
+        self.apply(initialize_weights)
+
+    def forward(self, phoneme_ids: Tensor, lengths: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+        hm = _owner_handle(self, "text_encoder", phoneme_ids.device)
+        if hm is not None:
+            return hm.text_encoder(phoneme_ids, lengths)
+        ops.require_device(phoneme_ids, self.embedding.weight, what="TextEncoder")
+        _, s = phoneme_ids.shape
+        mask = create_padding_mask(lengths, s) if lengths is not None else None
+        x = ops.embed_positional(phoneme_ids, self.embedding.weight, self.pos_encoding.pe[0, :s],
+                                 ops.sqrt_hidden(self.hidden_dim))
+        for layer in self.layers:
+            x = layer(x, mask)
+        return ops.layer_norm(x, self.norm.weight, self.norm.bias), mask
+
+
+class DurationPredictor(nn.Module):
+    """softplus(VariancePredictor(enc^T)) -> [B, S] (reference tts_model.py:92-117)."""
+
+    def __init__(self, hidden_dim: int = 64, kernel_size: int = 3, dropout: float = 0.1):
+        super().__init__()
+        self.predictor = VariancePredictor(hidden_dim, kernel_size, dropout)
+
+    def forward(self, encoder_output: Tensor) -> Tensor:
+        hm = _owner_handle(self, "duration_predictor", encoder_output.device)
+        if hm is not None:
+            return hm.duration(encoder_output)
+        x = encoder_output.transpose(1, 2).contiguous()
+        return self.predictor(x, _act=ops.ACT_SOFTPLUS).squeeze(1)
+
+
+class LengthRegulator(nn.Module):
+    """Repeat each phoneme row int(duration) times, pad/truncate to the batch
+    maximum or ``max_length`` (reference tts_model.py:120-178).  GPU scan +
+    gather; truncation toward zero and the all-zero-durations case (one zero
+    frame) follow the reference."""
+
+    def forward(self, encoder_output: Tensor, durations: Tensor, max_length: Optional[int] = None) -> Tensor:
+        return ops.regulate(encoder_output, durations, max_length)
+
+
+class MelDecoder(nn.Module):
+    """Unmasked pre-LN transformer over frames -> LayerNorm -> Linear(H, M)
+    (reference tts_model.py:181-228)."""
+
+    def __init__(self, hidden_dim: int = 64, mel_channels: int = 64, num_layers: int = 2, num_heads: int = 2,
+                 dropout: float = 0.1):
+        super().__init__()
+        self.layers = nn.ModuleList(
+            [TransformerEncoderLayer(hidden_dim=hidden_dim, num_heads=num_heads, ffn_dim=hidden_dim * 2, dropout=dropout)
+             for _ in range(num_layers)])
+        self.norm = nn.LayerNorm(hidden_dim)
+        self.mel_projection = nn.Linear(hidden_dim, mel_channels)
+        self.apply(initialize_weights)
+
+    def forward(self, x: Tensor) -> Tensor:
+        hm = _owner_handle(self, "decoder", x.device)
+        if hm is not None:
+            return hm.decoder(x)
+        for layer in self.layers:
+            x = layer(x)
+        return ops.linear(x, self.mel_projection.weight, self.mel_projection.bias,
+                          ln=(self.norm.weight, self.norm.bias))
+
+
+class SimpleVocoder(nn.Module):
+    """input_conv -> 4 x [ConvT(k=2r, s=r, p=r/2) -> leaky(0.1) -> resblock]
+    -> output_conv -> tanh; 64 samples per mel frame (reference
+    tts_model.py:231-297).  ``kernel_size``/``n_layers`` are accepted and, as
+    in the reference, do not change the upsampling schedule."""
+
+    def __init__(self, mel_channels: int = 64, hidden_channels: int = 128, kernel_size: int = 3, n_layers: int = 4):
+        super().__init__()
+        self.input_conv = nn.Conv1d(mel_channels, hidden_channels, kernel_size, padding=kernel_size // 2)
+        self.upsamples = nn.ModuleList()
+        self.resblocks = nn.ModuleList()
+        ch = hidden_channels
+        for r in UPSAMPLE_RATES:
+            self.upsamples.append(nn.ConvTranspose1d(ch, ch // 2, kernel_size=2 * r, stride=r, padding=r // 2))
+            ch //= 2
+            self.resblocks.append(LightweightResBlock(ch, kernel_size))
+        self.output_conv = nn.Conv1d(ch, 1, kernel_size, padding=kernel_size // 2)
+        self.apply(initialize_weights)
+
+    def forward(self, mel: Tensor) -> Tensor:
+        hm = _owner_handle(self, "vocoder", mel.device)
+        if hm is not None:
+            return hm.vocoder(mel, layout_btm=False)
+        if self.input_conv.kernel_size[0] != 3:
+            raise NotImplementedError("m2-tts_amd SimpleVocoder: kernel_size 3 only")
+        x = ops.conv1d(mel, self.input_conv.weight, self.input_conv.bias)
+        for r, up, rb in zip(UPSAMPLE_RATES, self.upsamples, self.resblocks):
+            x = ops.conv_transpose1d(x, up.weight, up.bias, r, act=ops.ACT_LEAKY)
+            x = rb(x)
+        return ops.conv1d(x, self.output_conv.weight, self.output_conv.bias, act=ops.ACT_TANH)
+
+
+class M2TTSModel(nn.Module):
+    """Text encoder -> duration predictor -> length regulator -> mel decoder ->
+    vocoder (reference tts_model.py:300-459)."""
+
+    def __init__(self, vocab_size: int = 256, hidden_dim: int = 64, mel_channels: int = 64,
+                 text_encoder_layers: int = 2, decoder_layers: int = 2, num_heads: int = 2, dropout: float = 0.1,
+                 vocoder_channels: int = 128):
+        super().__init__()
+        self.text_encoder = TextEncoder(vocab_size=vocab_size, hidden_dim=hidden_dim, num_layers=text_encoder_layers,
+                                        num_heads=num_heads, dropout=dropout)
+        self.duration_predictor = DurationPredictor(hidden_dim=hidden_dim, dropout=dropout)
+        self.length_regulator = LengthRegulator()
+        self.decoder = MelDecoder(hidden_dim=hidden_dim, mel_channels=mel_channels, num_layers=decoder_layers,
+                                  num_heads=num_heads, dropout=dropout)
+        self.vocoder = SimpleVocoder(mel_channels=mel_channels, hidden_channels=vocoder_channels)
+        self._m2_cfg = make_config(vocab_size, hidden_dim, mel_channels, text_encoder_layers, decoder_layers,
+                                   num_heads, vocoder_channels, self.text_encoder.pos_encoding.pe.shape[1])
+        me = weakref.ref(self)
+        for stage in (self.text_encoder, self.duration_predictor, self.decoder, self.vocoder):
+            object.__setattr__(stage, "_m2_owner", me)
+        total, trainable = count_parameters(self)
+        logger.info(f"M2TTSModel: {total:,} parameters ({trainable:,} trainable), "
+                    f"{total * 4 / (1024 * 1024):.1f} MB fp32")
+
+    # -------------------------------------------------------------- handle
+    def _hip(self, device: torch.device):
+        cache = _HANDLES.get(self)
+        if cache is None:
+            cache = HandleCache()
+            _HANDLES[self] = cache
+        return cache.get(self, self._m2_cfg, device)
+
+    # -------------------------------------------------------------- forward
+    def forward(self, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor] = None,
+                target_durations: Optional[Tensor] = None,
+                max_target_length: Optional[int] = None) -> Dict[str, Optional[Tensor]]:
+        """Reference tts_model.py:350-400: audio only when not training."""
+        ops.require_device(phoneme_ids, what="M2TTSModel")
+        with torch.no_grad():
+            hm = self._hip(phoneme_ids.device)
+            enc, mask = hm.text_encoder(phoneme_ids, phoneme_lengths)
+            dur = hm.duration(enc)
+            durations = target_durations if target_durations is not None else dur
+            reg = ops.regulate(enc, durations, max_target_length)
+            mel = hm.decoder(reg)
+            audio = None if self.training else hm.vocoder(mel, layout_btm=True)
+        return {"encoder_output": enc, "duration_pred": dur, "regulated_output": reg,
+                "mel_output": mel, "audio_output": audio, "padding_mask": mask}
+
+    def inference(self, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor] = None,
+                  duration_scale: float = 1.0) -> Tuple[Tensor, Tensor]:
+        """(mel [B,T,M], audio [B,1,64T]) - reference tts_model.py:402-438."""
+        self.eval()
+        ops.require_device(phoneme_ids, what="M2TTSModel")
+        with torch.no_grad():
+            hm = self._hip(phoneme_ids.device)
+            enc, _ = hm.text_encoder(phoneme_ids, phoneme_lengths)
+            dur = hm.duration(enc)
+            reg = ops.regulate(enc, dur, None, scale=duration_scale)
+            mel = hm.decoder(reg)
+            audio = hm.vocoder(mel, layout_btm=True)
+        return mel, audio
+
+    def get_model_size(self) -> Dict[str, Any]:
+        """Parameter counts per component (reference tts_model.py:440-459)."""
+        comps = {}
+        for name, module in self.named_children():
+            total, trainable = count_parameters(module)
+            comps[name] = {"total": total, "trainable": trainable, "size_mb": total * 4 / (1024 * 1024)}
+        total, trainable = count_parameters(self)
+        return {"total_params": total, "trainable_params": trainable,
+                "total_size_mb": total * 4 / (1024 * 1024), "components": comps}

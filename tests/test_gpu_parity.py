@@ -1,0 +1,310 @@
+"""GPU parity: the HIP path vs the reference's outputs (golden fixtures made
+by importing the reference, tests/golden/make_golden.py) and vs the CPU
+oracle (oracle/m2tts_oracle.py, bit-identical to the reference on CPU).
+
+Tolerances (BASELINE.json north_star): mel max-abs <= 1e-3, waveform RMS
+<= 1e-4.  Integer outputs (frame counts, masks) must match exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+import m2tts_oracle as orc
+from conftest import (AUDIO_RMS_TOL, MEL_MAXABS_TOL, golden, golden_state, maxabs, rms, stage_config)
+
+pytestmark = pytest.mark.gpu
+STAGES = ["s1", "s2"]
+# Intermediate fp32 tensors: reordering noise only.
+ENC_TOL = 1e-4
+
+
+def build_model(stage, dev, pinned=True):
+    from models.tts_model import M2TTSModel
+    m = M2TTSModel(**stage_config(stage).as_dict())
+    m.load_state_dict(golden_state(stage, pinned))
+    return m.to(dev).eval()
+
+
+def _ids(g, dev):
+    return torch.from_numpy(g["ids"]).to(dev), torch.from_numpy(g["lengths"]).to(dev)
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_forward_small(gpu, stage):
+    g = golden(f"{stage}_small")
+    m = build_model(stage, gpu)
+    ids, lens = _ids(g, gpu)
+    out = m(ids, lens)
+    assert maxabs(out["encoder_output"], g["encoder_output"]) <= ENC_TOL
+    assert maxabs(out["duration_pred"], g["duration_pred"]) <= ENC_TOL
+    assert torch.equal(out["padding_mask"].cpu(), torch.from_numpy(g["padding_mask"]))
+    assert out["regulated_output"].shape == tuple(g["regulated_output"].shape)
+    assert maxabs(out["regulated_output"], g["regulated_output"]) <= ENC_TOL
+    assert out["mel_output"].shape == tuple(g["mel"].shape)
+    assert maxabs(out["mel_output"], g["mel"]) <= MEL_MAXABS_TOL
+    assert out["audio_output"].shape == tuple(g["audio"].shape)
+    assert rms(out["audio_output"], g["audio"]) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_inference_small(gpu, stage):
+    g = golden(f"{stage}_small")
+    m = build_model(stage, gpu)
+    ids, lens = _ids(g, gpu)
+    mel, audio = m.inference(ids, lens)
+    assert mel.shape == tuple(g["mel"].shape) and audio.shape == tuple(g["audio"].shape)
+    assert maxabs(mel, g["mel"]) <= MEL_MAXABS_TOL
+    assert rms(audio, g["audio"]) <= AUDIO_RMS_TOL
+    assert maxabs(audio, g["audio"]) <= 1e-3
+
+
+@pytest.mark.parametrize("stage", STAGES)
+@pytest.mark.parametrize("sub", ["free", "pad", "trunc"])
+def test_teacher_forced(gpu, stage, sub):
+    g = golden(f"{stage}_target_{sub}")
+    m = build_model(stage, gpu)
+    ids, lens = _ids(g, gpu)
+    mtl = int(g["max_target_length"])
+    out = m(ids, lens, target_durations=torch.from_numpy(g["target_durations"]).to(gpu),
+            max_target_length=None if mtl < 0 else mtl)
+    assert out["regulated_output"].shape == tuple(g["regulated_output"].shape)
+    assert maxabs(out["regulated_output"], g["regulated_output"]) <= ENC_TOL
+    assert maxabs(out["mel_output"], g["mel"]) <= MEL_MAXABS_TOL
+    assert rms(out["audio_output"], g["audio"]) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_duration_scale(gpu, stage):
+    g = golden(f"{stage}_scale")
+    m = build_model(stage, gpu)
+    ids, lens = _ids(g, gpu)
+    mel, audio = m.inference(ids, lens, duration_scale=float(g["duration_scale"]))
+    assert mel.shape == tuple(g["mel"].shape)
+    assert maxabs(mel, g["mel"]) <= MEL_MAXABS_TOL
+    assert rms(audio, g["audio"]) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_untrained_durations_give_one_zero_frame(gpu, stage):
+    g = golden(f"{stage}_untrained")
+    m = build_model(stage, gpu, pinned=False)
+    ids, lens = _ids(g, gpu)
+    mel, audio = m.inference(ids, lens)
+    assert mel.shape == tuple(g["mel"].shape) == (2, 1, stage_config(stage).mel_channels)
+    assert maxabs(mel, g["mel"]) <= MEL_MAXABS_TOL
+    assert rms(audio, g["audio"]) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_vocoder_layers(gpu, stage):
+    """Every vocoder layer, through the model handle and the standalone kernels."""
+    m = build_model(stage, gpu)
+    voc = m.vocoder
+    hm = m._hip(gpu)
+    g = golden(f"{stage}_input_conv")
+    from m2amd import ops
+    y = ops.conv1d(torch.from_numpy(g["x"]).to(gpu), voc.input_conv.weight, voc.input_conv.bias)
+    assert maxabs(y, g["y"]) <= 1e-4
+    for k in range(4):
+        g = golden(f"{stage}_convT{k}")
+        x = torch.from_numpy(g["x"]).to(gpu)
+        assert maxabs(hm.upsample(k, x, int(g["rate"])), g["y"]) <= 1e-4
+        assert maxabs(ops.conv_transpose1d(x, voc.upsamples[k].weight, voc.upsamples[k].bias, int(g["rate"]),
+                                           act=ops.ACT_LEAKY), g["y"]) <= 1e-4
+        g = golden(f"{stage}_resblock{k}")
+        x = torch.from_numpy(g["x"]).to(gpu)
+        assert maxabs(hm.resblock(k, x), g["y"]) <= 1e-4
+        assert maxabs(voc.resblocks[k](x), g["y"]) <= 1e-4
+    g = golden(f"{stage}_output_conv")
+    y = ops.conv1d(torch.from_numpy(g["x"]).to(gpu), voc.output_conv.weight, voc.output_conv.bias, act=ops.ACT_TANH)
+    assert maxabs(y, g["y"]) <= 1e-5
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_stage_modules_called_directly(gpu, stage):
+    """Callers use model.text_encoder / duration_predictor / length_regulator /
+    decoder / vocoder directly (train_stage2.py:258); standalone copies of the
+    stage modules take the per-op path.  Both must agree with the reference."""
+    from models.tts_model import DurationPredictor, MelDecoder, SimpleVocoder, TextEncoder
+    cfg = stage_config(stage)
+    g = golden(f"{stage}_small")
+    m = build_model(stage, gpu)
+    ids, lens = _ids(g, gpu)
+    sd = golden_state(stage)
+    standalone = {
+        "text_encoder": TextEncoder(cfg.vocab_size, cfg.hidden_dim, cfg.text_encoder_layers, cfg.num_heads),
+        "duration_predictor": DurationPredictor(cfg.hidden_dim),
+        "decoder": MelDecoder(cfg.hidden_dim, cfg.mel_channels, cfg.decoder_layers, cfg.num_heads),
+        "vocoder": SimpleVocoder(cfg.mel_channels, cfg.vocoder_channels),
+    }
+    for name, mod in standalone.items():
+        mod.load_state_dict({k[len(name) + 1:]: v for k, v in sd.items() if k.startswith(name + ".")})
+        mod.to(gpu).eval()
+    for te in (m.text_encoder, standalone["text_encoder"]):
+        enc, mask = te(ids, lens)
+        assert maxabs(enc, g["encoder_output"]) <= ENC_TOL
+        assert torch.equal(mask.cpu(), torch.from_numpy(g["padding_mask"]))
+    enc = torch.from_numpy(g["encoder_output"]).to(gpu)
+    for dp in (m.duration_predictor, standalone["duration_predictor"]):
+        assert maxabs(dp(enc), g["duration_pred"]) <= ENC_TOL
+    reg = m.length_regulator(enc, torch.from_numpy(g["duration_pred"]).to(gpu))
+    assert torch.equal(reg.cpu(), torch.from_numpy(g["regulated_output"]))  # pure copy: exact
+    for dec in (m.decoder, standalone["decoder"]):
+        assert maxabs(dec(reg), g["mel"]) <= MEL_MAXABS_TOL
+    mel_bmt = torch.from_numpy(g["mel"]).to(gpu).transpose(1, 2).contiguous()
+    for voc in (m.vocoder, standalone["vocoder"]):
+        assert rms(voc(mel_bmt), g["audio"]) <= AUDIO_RMS_TOL
+
+
+def test_components_api(gpu):
+    """models.components used on their own (test_simple.py:49-63 pattern)."""
+    from models.components import (FeedForward, MultiHeadAttention, PositionalEncoding, TransformerEncoderLayer,
+                                   create_padding_mask)
+    torch.manual_seed(0)
+    H, heads, B, N = 64, 2, 2, 37
+    pe = PositionalEncoding(H).to(gpu)
+    x = torch.randn(B, N, H)
+    assert maxabs(pe(x.to(gpu)), x + pe.pe[:, :N].cpu()) <= 1e-6
+    mha = MultiHeadAttention(H, heads).eval()
+    lens = torch.tensor([N, 20])
+    mask = create_padding_mask(lens, N)
+    sd = {f"a.{k}": v for k, v in mha.state_dict().items()}
+    ref = orc.attention(sd, "a", x, heads, mask)
+    got = mha.to(gpu)(x.to(gpu), mask.to(gpu))
+    assert maxabs(got, ref) <= 1e-4
+    ffn = FeedForward(H, 2 * H).eval()
+    sd = {f"f.{k}": v for k, v in ffn.state_dict().items()}
+    assert maxabs(ffn.to(gpu)(x.to(gpu)), orc.feed_forward(sd, "f", x)) <= 1e-4
+    layer = TransformerEncoderLayer(H, heads, 2 * H).eval()
+    with torch.no_grad():
+        for p in layer.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    sd = {f"l.{k}": v.clone() for k, v in layer.state_dict().items()}
+    assert maxabs(layer.to(gpu)(x.to(gpu), mask.to(gpu)), orc.encoder_layer(sd, "l", x, heads, mask)) <= 1e-4
+
+
+def test_all_keys_masked_is_uniform(gpu):
+    """Length-0 utterances: every key -1e9 -> softmax is uniform (reference behaviour)."""
+    from models.components import MultiHeadAttention
+    torch.manual_seed(1)
+    mha = MultiHeadAttention(32, 2).eval()
+    x = torch.randn(2, 9, 32)
+    mask = torch.tensor([[False] * 9, [True] * 4 + [False] * 5])
+    sd = {f"a.{k}": v for k, v in mha.state_dict().items()}
+    assert maxabs(mha.to(gpu)(x.to(gpu), mask.to(gpu)), orc.attention(sd, "a", x, 2, mask)) <= 1e-5
+
+
+def test_tiny_model_api(gpu):
+    """test_simple.py:70-98 shape checks: hidden 32, heads 2 (hd 16), voc 64, max_target_length 30."""
+    from models.tts_model import M2TTSModel
+    torch.manual_seed(3)
+    m = M2TTSModel(vocab_size=100, hidden_dim=32, mel_channels=32, text_encoder_layers=1, decoder_layers=1,
+                   num_heads=2, vocoder_channels=64).eval()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    cfg = orc.OracleConfig(vocab_size=100, hidden_dim=32, mel_channels=32, text_encoder_layers=1,
+                           decoder_layers=1, num_heads=2, vocoder_channels=64)
+    ids = torch.randint(0, 100, (2, 10))
+    lens = torch.tensor([8, 6])
+    dur = torch.rand(2, 10) * 2 + 1
+    ref = orc.forward(sd, cfg, ids, lens, dur, 30)
+    out = m.to(gpu)(phoneme_ids=ids.to(gpu), phoneme_lengths=lens.to(gpu), target_durations=dur.to(gpu),
+                    max_target_length=30)
+    assert set(out) == set(ref)
+    for k in ("encoder_output", "duration_pred", "regulated_output", "mel_output", "audio_output"):
+        assert out[k].shape == ref[k].shape, k
+    assert maxabs(out["mel_output"], ref["mel_output"]) <= MEL_MAXABS_TOL
+    assert rms(out["audio_output"], ref["audio_output"]) <= AUDIO_RMS_TOL
+    info = m.get_model_size()
+    assert info["total_params"] == sum(p.numel() for p in m.parameters())
+
+
+def test_cli_sentence_stage1(gpu):
+    g = golden("cli_stage1")
+    m = build_model("s1", gpu)
+    ids, lens = _ids(g, gpu)
+    mel, audio = m.inference(ids, lens)
+    assert mel.shape == tuple(g["mel"].shape) == (1, 1280, 64)
+    assert maxabs(mel, g["mel"]) <= MEL_MAXABS_TOL
+    assert rms(audio, g["audio"]) <= AUDIO_RMS_TOL
+
+
+# ---------------------------------------------------------------------------
+# Benchmark shapes: full tensors vs the oracle where it is quick
+# on the host, fingerprints from the reference everywhere.
+def _check_fingerprint(fp, mel, audio):
+    B = audio.shape[0]
+    a = audio[:, 0].double().cpu()
+    assert mel.shape[1] == int(fp["T"][0])
+    assert maxabs(audio[:, 0, :256], fp["audio_head"]) <= 1e-3
+    assert maxabs(audio[:, 0, -256:], fp["audio_tail"]) <= 1e-3
+    assert rms(audio[:, 0, :256], fp["audio_head"]) <= AUDIO_RMS_TOL
+    n = a.shape[1]
+    # sum of squares: |d(sumsq)| <= 2*sqrt(sumsq)*||err|| ~ 2*sqrt(n*ms)*sqrt(n)*rms_tol
+    np.testing.assert_allclose(a.pow(2).sum(1).numpy(), fp["audio_sumsq"], rtol=2e-3, atol=n * 1e-6)
+    np.testing.assert_allclose(a.abs().amax(1).numpy(), fp["audio_maxabs"], atol=1e-3)
+    if "mel_head" in fp.files:
+        assert maxabs(mel[:, :4], fp["mel_head"]) <= MEL_MAXABS_TOL
+        assert maxabs(mel[:, -4:], fp["mel_tail"]) <= MEL_MAXABS_TOL
+    assert B == fp["audio_head"].shape[0]
+
+
+def test_vocoder_stage1_b32_full(gpu):
+    fp = golden("fp_s1_vocoder_B32_T500")
+    m = build_model("s1", gpu)
+    mel = torch.randn(32, 64, 500, generator=torch.Generator().manual_seed(int(fp["seed"])))
+    audio = m.vocoder(mel.to(gpu))
+    ref = orc.vocoder(golden_state("s1"), mel)
+    assert audio.shape == (32, 1, 32000)
+    assert rms(audio, ref) <= AUDIO_RMS_TOL
+    assert maxabs(audio, ref) <= 1e-3
+    assert maxabs(audio[:, 0, :256], fp["audio_head"]) <= 1e-3
+
+
+@pytest.mark.parametrize("stage,B,S", [("s1", 32, 100), ("s2", 64, 100)])
+def test_pipeline_bench_shapes(gpu, stage, B, S):
+    fp = golden(f"fp_{stage}_B{B}_S{S}")
+    m = build_model(stage, gpu)
+    ids = torch.from_numpy(fp["ids"])
+    lens = torch.from_numpy(fp["lengths"])
+    mel, audio = m.inference(ids.to(gpu), lens.to(gpu))
+    _check_fingerprint(fp, mel, audio)
+    ref_mel, ref_audio = orc.inference(golden_state(stage), stage_config(stage), ids, lens, as_written=False)
+    assert maxabs(mel, ref_mel) <= MEL_MAXABS_TOL
+    assert rms(audio, ref_audio) <= AUDIO_RMS_TOL
+
+
+def test_pipeline_longform_stage2(gpu):
+    """B=128, S=520 -> T=2600 (30.2 s of mel at hop 256): fingerprints only."""
+    fp = golden("fp_s2_B128_S520")
+    m = build_model("s2", gpu)
+    mel, audio = m.inference(torch.from_numpy(fp["ids"]).to(gpu), torch.from_numpy(fp["lengths"]).to(gpu))
+    assert audio.shape == (128, 1, 64 * 2600)
+    _check_fingerprint(fp, mel, audio)
+
+
+def test_repeatable_and_stream_ordered(gpu):
+    """Same inputs twice -> bitwise identical outputs (no atomics in the data path)."""
+    g = golden("s1_small")
+    m = build_model("s1", gpu)
+    ids, lens = _ids(g, gpu)
+    a = m.inference(ids, lens)
+    b = m.inference(ids, lens)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_weights_reload_invalidates_handle(gpu):
+    g = golden("s1_small")
+    m = build_model("s1", gpu)
+    ids, lens = _ids(g, gpu)
+    mel1, _ = m.inference(ids, lens)
+    with torch.no_grad():
+        m.decoder.mel_projection.bias.add_(1.0)
+    mel2, _ = m.inference(ids, lens)
+    assert maxabs(mel2 - 1.0, mel1) <= 1e-5
+
+
+def test_cpu_tensors_fail_loudly():
+    from models.tts_model import M2TTSModel
+    m = M2TTSModel().eval()
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        m.inference(torch.zeros(1, 4, dtype=torch.long), torch.tensor([4]))
