@@ -181,16 +181,17 @@ int32_t m2_add_positional(const float* x, const float* pe, int32_t B, int32_t S,
                           float* y, void* stream);
 
 /* ---- measurement ----------------------------------------------------------
- * Kernel timing with HIP events recorded on the launch stream around the
- * vocoder's dominant kernel (bench.py's roofline).  enable: allocate
- * `capacity` event pairs (not in a timed region); each m2_vocoder call then
- * records one pair while capacity lasts; read: synchronise the recorded
- * events and return their durations in ms (n_out = count) and reset.
- * m2_profile_kernel_name names the bracketed kernel. */
+ * Kernel timing with HIP events recorded on the launch stream around each of
+ * the fused vocoder's kernels (bench.py's roofline).  enable: allocate event
+ * pairs for `capacity` m2_vocoder calls (outside any timed region); each call
+ * then records one pair per kernel while capacity lasts.  read: synchronise
+ * and return durations in ms, call-major ([call][kernel]), n_out = count, and
+ * reset.  Kernels are named by m2_profile_kernel_name(i), i < count(). */
 int32_t m2_profile_enable(m2_model* model, int32_t capacity);
 int32_t m2_profile_read(m2_model* model, float* ms_out, int32_t capacity, int32_t* n_out);
 int32_t m2_profile_disable(m2_model* model);
-const char* m2_profile_kernel_name(void);
+int32_t m2_profile_kernel_count(void);
+const char* m2_profile_kernel_name(int32_t index);
 
 #ifdef __cplusplus
 }

@@ -1,11 +1,13 @@
 // C-ABI runtime: weight table, model handle, stage orchestration.
 // See include/m2tts_hip.h for the contract of every entry point.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "m2_common.h"
+#include "vocoder_fused.h"
 
 namespace m2 {
 
@@ -40,9 +42,7 @@ int32_t hip_status(hipError_t e, const char* where) {
 }
 
 static constexpr int kRates[4] = {4, 4, 2, 2};  // tts_model.py:244
-// The launch bench.py times with events: per-layer path, stage-0 resblock conv1.
-static constexpr int kProfStage = 0;
-static constexpr const char* kProfKernel = "conv_kernel<3,8,4,0,0> (vocoder resblock 0 conv1)";
+
 
 // ---------------------------------------------------------------------------
 // Weight table in M2TTSModel.state_dict() order (tts_model.py:303-343).
@@ -140,28 +140,14 @@ struct m2_model {
     const float *vin_w = nullptr, *vin_b = nullptr, *vout_w = nullptr, *vout_b = nullptr;
     const float *up_w[4] = {}, *up_b[4] = {};
     const float *rb_w1[4] = {}, *rb_b1[4] = {}, *rb_w2[4] = {}, *rb_b2[4] = {};
-    // measurement: event pairs recorded around the vocoder's dominant kernel
-    mutable std::vector<hipEvent_t> prof_begin, prof_end;
-    mutable int prof_next = 0;
+    // fused vocoder: packed weights
+    float* vbuf = nullptr;
+    m2::VocW vw{};
+    bool fused = false;
+    // measurement: per m2_vocoder call, an event pair around each fused kernel
+    mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
+    mutable int prof_calls = 0;
 };
-
-namespace {
-// Record the begin/end event of the next free pair (no-op when profiling is off).
-struct ProfScope {
-    const m2_model* m;
-    hipStream_t st;
-    int slot = -1;
-    ProfScope(const m2_model* mm, hipStream_t s) : m(mm), st(s) {
-        if (m->prof_next < (int)m->prof_begin.size()) {
-            slot = m->prof_next++;
-            (void)hipEventRecord(m->prof_begin[slot], st);
-        }
-    }
-    ~ProfScope() {
-        if (slot >= 0) (void)hipEventRecord(m->prof_end[slot], st);
-    }
-};
-}  // namespace
 
 using namespace m2;
 
@@ -373,6 +359,55 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     }
     m->vout_w = P("vocoder.output_conv.weight");
     m->vout_b = P("vocoder.output_conv.bias");
+
+    // Fused vocoder: pack conv / convT weights into MFMA A-fragment order.
+    m->fused = vocoder_fused_supported(cfg->mel_channels, cfg->vocoder_channels) && !std::getenv("M2_VOCODER_PERLAYER");
+    if (m->fused) {
+        auto fetch = [&](const std::string& n) {
+            const int i = idx(n);
+            std::vector<float> h((size_t)table[i].numel);
+            hipError_t er = hipMemcpyAsync(h.data(), weights[i], h.size() * sizeof(float), hipMemcpyDeviceToHost, st);
+            if (er == hipSuccess) er = hipStreamSynchronize(st);
+            if (er != hipSuccess) h.clear();
+            return h;
+        };
+        std::vector<std::vector<float>> parts;
+        std::vector<const float**> slots;
+        auto add = [&](std::vector<float> v, const float** slot) { parts.push_back(std::move(v)); slots.push_back(slot); };
+        const int M = cfg->mel_channels, C = cfg->vocoder_channels;
+        auto wi = fetch("vocoder.input_conv.weight");
+        if (wi.empty()) return bail(hipErrorUnknown, "fetch vocoder weights");
+        add(pack_conv3(wi.data(), C, M), &m->vw.wi);
+        add(fetch("vocoder.input_conv.bias"), &m->vw.bi);
+        int ch = C;
+        for (int k = 0; k < 4; ++k) {
+            const std::string u = "vocoder.upsamples." + std::to_string(k);
+            const std::string r = "vocoder.resblocks." + std::to_string(k);
+            auto wt = fetch(u + ".weight");
+            add(pack_convT(wt.data(), ch, ch / 2, kRates[k]), &m->vw.wt[k]);
+            add(fetch(u + ".bias"), &m->vw.bt[k]);
+            ch /= 2;
+            auto w1 = fetch(r + ".conv1.weight");
+            add(pack_conv3(w1.data(), ch, ch), &m->vw.w1[k]);
+            add(fetch(r + ".conv1.bias"), &m->vw.b1[k]);
+            auto w2 = fetch(r + ".conv2.weight");
+            add(pack_conv3(w2.data(), ch, ch), &m->vw.w2[k]);
+            add(fetch(r + ".conv2.bias"), &m->vw.b2[k]);
+        }
+        size_t tot = 0;
+        std::vector<size_t> offs;
+        for (auto& v : parts) { tot = align_up(tot, 64); offs.push_back(tot); tot += v.size(); }
+        std::vector<float> host(tot, 0.f);
+        for (size_t i = 0; i < parts.size(); ++i) std::copy(parts[i].begin(), parts[i].end(), host.begin() + offs[i]);
+        e = hipMalloc(&m->vbuf, std::max<size_t>(tot, 1) * sizeof(float));
+        if (e != hipSuccess) return bail(e, "hipMalloc(vocoder pack)");
+        e = hipMemcpyAsync(m->vbuf, host.data(), tot * sizeof(float), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) { (void)hipFree(m->vbuf); return bail(e, "upload vocoder pack"); }
+        for (size_t i = 0; i < parts.size(); ++i) *slots[i] = m->vbuf + offs[i];
+        m->vw.wo = m->vout_w;
+        m->vw.bo = m->vout_b;
+    }
     *out = m;
     return M2_OK;
 }
@@ -382,6 +417,7 @@ int32_t m2_profile_disable(m2_model* model);
 int32_t m2_model_destroy(m2_model* model) {
     if (!model) return M2_OK;
     m2_profile_disable(model);
+    if (model->vbuf) (void)hipFree(model->vbuf);
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -481,6 +517,18 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
     int32_t rc;
+    if (m->fused) {
+        const int call = m->prof_calls;
+        const bool rec = (size_t)(call + 1) * kVocKernels <= m->prof_begin.size();
+        if (rec) m->prof_calls++;
+        auto mark = [&](int kidx, bool begin) {
+            if (!rec) return;
+            const size_t slot = (size_t)call * kVocKernels + kidx;
+            (void)hipEventRecord(begin ? m->prof_begin[slot] : m->prof_end[slot], st);
+        };
+        return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vw,
+                                    buf[0], buf[1], out_audio, st, mark);
+    }
     int ch = m->cfg.vocoder_channels, L = T;
     float *cur = buf[0], *up = buf[1], *tmp = buf[2];
     if ((rc = launch_conv(mel, m->vin_w, m->vin_b, nullptr, nullptr, nullptr, 3, ACT_NONE, mel_layout == 1, B, m->cfg.mel_channels, ch, L, cur, st))) return rc;
@@ -488,10 +536,7 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
         if ((rc = launch_convT(cur, m->up_w[k], m->up_b[k], kRates[k], ACT_LEAKY, B, ch, ch / 2, L, up, st))) return rc;
         ch /= 2;
         L *= kRates[k];
-        if (k == kProfStage) {
-            ProfScope ps(m, st);
-            if ((rc = launch_conv(up, m->rb_w1[k], m->rb_b1[k], nullptr, nullptr, nullptr, 3, ACT_LEAKY, false, B, ch, ch, L, tmp, st))) return rc;
-        } else if ((rc = launch_conv(up, m->rb_w1[k], m->rb_b1[k], nullptr, nullptr, nullptr, 3, ACT_LEAKY, false, B, ch, ch, L, tmp, st))) return rc;
+        if ((rc = launch_conv(up, m->rb_w1[k], m->rb_b1[k], nullptr, nullptr, nullptr, 3, ACT_LEAKY, false, B, ch, ch, L, tmp, st))) return rc;
         if ((rc = launch_conv(tmp, m->rb_w2[k], m->rb_b2[k], nullptr, nullptr, up, 3, ACT_NONE, false, B, ch, ch, L, cur, st))) return rc;
     }
     return launch_conv(cur, m->vout_w, m->vout_b, nullptr, nullptr, nullptr, 3, ACT_TANH, false, B, ch, 1, L, out_audio, st);
@@ -561,31 +606,35 @@ int32_t m2_add_positional(const float* x, const float* pe, int32_t B, int32_t S,
     return launch_add_pe(x, pe, B, S, H, y, static_cast<hipStream_t>(stream));
 }
 
-const char* m2_profile_kernel_name(void) { return kProfKernel; }
+int32_t m2_profile_kernel_count(void) { return kVocKernels; }
+
+const char* m2_profile_kernel_name(int32_t index) {
+    return (index >= 0 && index < kVocKernels) ? kVocKernelNames[index] : "";
+}
 
 int32_t m2_profile_enable(m2_model* m, int32_t capacity) {
     M2_CHECK_ARG(m && capacity >= 0, "m2_profile_enable: bad argument");
     m2_profile_disable(m);
-    for (int i = 0; i < capacity; ++i) {
+    for (int i = 0; i < capacity * kVocKernels; ++i) {
         hipEvent_t a, b;
         M2_HIP(hipEventCreate(&a));
         M2_HIP(hipEventCreate(&b));
         m->prof_begin.push_back(a);
         m->prof_end.push_back(b);
     }
-    m->prof_next = 0;
+    m->prof_calls = 0;
     return M2_OK;
 }
 
 int32_t m2_profile_read(m2_model* m, float* ms_out, int32_t capacity, int32_t* n_out) {
     M2_CHECK_ARG(m && ms_out && n_out, "m2_profile_read: bad argument");
-    const int n = std::min<int>(capacity, m->prof_next);
+    const int n = std::min<int>(capacity, m->prof_calls * kVocKernels);
     for (int i = 0; i < n; ++i) {
         M2_HIP(hipEventSynchronize(m->prof_end[i]));
         M2_HIP(hipEventElapsedTime(&ms_out[i], m->prof_begin[i], m->prof_end[i]));
     }
     *n_out = n;
-    m->prof_next = 0;
+    m->prof_calls = 0;
     return M2_OK;
 }
 
@@ -595,7 +644,7 @@ int32_t m2_profile_disable(m2_model* m) {
     for (auto e : m->prof_end) (void)hipEventDestroy(e);
     m->prof_begin.clear();
     m->prof_end.clear();
-    m->prof_next = 0;
+    m->prof_calls = 0;
     return M2_OK;
 }
 

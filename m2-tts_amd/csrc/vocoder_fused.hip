@@ -1,0 +1,440 @@
+// Fused SimpleVocoder for gfx950 (tts_model.py:279-297).
+//
+// Three launches per vocoder pass instead of fourteen:
+//   head  : input_conv(M->C, k3) -> ConvT1(x4)+leaky -> ResBlock1        mel  -> U1 [B][C/2][4T]
+//   mid   : ConvT2(x4)+leaky -> ResBlock2                                 U1   -> U2 [B][C/4][16T]
+//   tail  : ConvT3(x2)+leaky -> ResBlock3 -> ConvT4(x2)+leaky -> ResBlock4
+//           -> output_conv(k3) -> tanh                                    U2   -> audio [B][1][64T]
+// Each workgroup owns one utterance and one window of positions and runs its
+// whole layer chain out of LDS; the window is widened by the exact receptive
+// field of the chain (k3 conv: +-1, ConvT(k=2r,s=r,p=r/2): one extra input
+// frame each side), so every kept output is the same arithmetic as the
+// unfused layer.  Positions outside [0, L) of every layer are stored as 0,
+// which is the zero padding the next conv sees in the reference.
+// The tail is where fusion pays most: its layers have 8-32 channels (1-12
+// FLOP/B unfused), fused the tail reads 32 ch of U2 and writes one sample row.
+//
+// Every conv / transposed conv is an implicit GEMM on the exact-f32 MFMA
+// v_mfma_f32_16x16x4_f32 (64 FLOP/clk/SIMD = the fp32 peak): rows = output
+// channels (A = packed weights, streamed from L2, one f32 per lane per MFMA),
+// columns = 16 positions (B = activations in LDS: lanes 0-15 read 16
+// consecutive positions of one channel row, lanes 16-63 the next 3 rows; rows
+// are padded to a stride = 16 mod 32 floats so the two 32-lane halves of a
+// ds_read_b32 hit disjoint banks).  K = (tap, channel).  ConvT is r GEMMs,
+// one per output phase, each with K = 2 taps x Cin (the 2-tap polyphase form).
+#include <functional>
+
+#include "m2_common.h"
+#include "vocoder_fused.h"
+
+namespace m2 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// An LDS activation window: row stride P (floats), absolute position of col 0.
+struct LB {
+    float* p;
+    int P;
+    int start;
+};
+
+constexpr int rup16(int n) { return (n + 15) / 16 * 16; }
+// Row stride >= cols with stride = 16 (mod 32): conflict-free B-operand reads.
+constexpr int pstride(int cols) { return ((cols + 15) / 32) * 32 + 16; }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// ---------------------------------------------------------------------------
+// Conv1d(k=3, pad=1) over an LDS window: abs positions [a0, a0+npos), all
+// COUT channels.  Epilogue: +bias, act, (+ residual read from `out` in place),
+// 0 outside [0, L).  Packed weights: Wp[mb][s][lane] = W[mb*16 + (lane&15)]
+// [ci][k] with k*CIN + ci = 4*s + (lane>>4)  (zero rows for co >= COUT).
+template <int CIN, int COUT, int NT, int ACT, bool RES>
+__device__ __forceinline__ void lconv3(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
+                                       LB out, int a0, int npos, int L, int wave, int nwaves) {
+    static_assert(CIN % 4 == 0, "CIN must be a multiple of 4");
+    constexpr int KC = CIN / 4, KS = 3 * KC, MB = (COUT + 15) / 16;
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int ntiles = (npos + 15) >> 4;
+    const int nch = (ntiles + NT - 1) / NT;
+    for (int item = wave; item < MB * nch; item += nwaves) {
+        const int mb = item % MB, tile0 = (item / MB) * NT;
+        const int nt = min(NT, ntiles - tile0);
+        f32x4 acc[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* wp = Wp + (size_t)mb * KS * 64 + lane;
+        const float* bp = in.p + lk * in.P + (a0 + tile0 * 16 + li - in.start - 1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll 8
+            for (int cb = 0; cb < KC; ++cb) {
+                const float a = wp[(k * KC + cb) * 64];
+                const float* br = bp + cb * 4 * in.P + k;
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    if (n < nt) acc[n] = mfma16(a, br[n * 16], acc[n]);
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (n < nt) {
+                const int j = (tile0 + n) * 16 + li;
+                const int t = a0 + j;
+                if (j < npos) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int co = mb * 16 + lk * 4 + r;
+                        if (co < COUT) {
+                            float v = act_t<ACT>(acc[n][r] + bias[co]);
+                            float* o = out.p + co * out.P + (t - out.start);
+                            if (RES) v += *o;
+                            *o = (t >= 0 && t < L) ? v : 0.f;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// leaky(ConvTranspose1d(k=2R, stride R, pad R/2)) over an LDS window: input
+// positions q in [q0, q0+nq) produce outputs t = q*R + ph, ph < R.  Phase ph
+// reads taps (q, q-1) if ph + R/2 < R else (q+1, q).  Packed weights:
+// Wp[ph][mb][s][lane] = W[ci][mb*16 + (lane&15)][k_tap] with
+// tap*CIN + ci = 4*s + (lane>>4).
+template <int CIN, int COUT, int R, int NT>
+__device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
+                                       LB out, int q0, int nq, int L, int wave, int nwaves) {
+    static_assert(CIN % 4 == 0, "CIN must be a multiple of 4");
+    constexpr int KC = CIN / 4, KS = 2 * KC, MB = (COUT + 15) / 16, PAD = R / 2;
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int ntiles = (nq + 15) >> 4;
+    const int nch = (ntiles + NT - 1) / NT;
+    for (int item = wave; item < R * MB * nch; item += nwaves) {
+        const int ph = item % R, rest = item / R;
+        const int mb = rest % MB, tile0 = (rest / MB) * NT;
+        const int nt = min(NT, ntiles - tile0);
+        const int d0 = (ph + PAD < R) ? 0 : 1;  // tap 0 offset; tap 1 is d0 - 1
+        f32x4 acc[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* wp = Wp + (size_t)(ph * MB + mb) * KS * 64 + lane;
+        const float* bp = in.p + lk * in.P + (q0 + tile0 * 16 + li - in.start + d0);
+#pragma unroll
+        for (int tap = 0; tap < 2; ++tap) {
+#pragma unroll 8
+            for (int cb = 0; cb < KC; ++cb) {
+                const float a = wp[(tap * KC + cb) * 64];
+                const float* br = bp + cb * 4 * in.P - tap;
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    if (n < nt) acc[n] = mfma16(a, br[n * 16], acc[n]);
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (n < nt) {
+                const int j = (tile0 + n) * 16 + li;
+                const int t = (q0 + j) * R + ph;
+                if (j < nq) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int co = mb * 16 + lk * 4 + r;
+                        if (co < COUT) {
+                            const float v = act_t<ACT_LEAKY>(acc[n][r] + bias[co]);
+                            out.p[co * out.P + (t - out.start)] = (t >= 0 && t < L) ? v : 0.f;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Global [rows][Lg] (or [Lg][rows] when TRANS) -> LDS window cols [0, ncols),
+// zero outside [0, Lg).
+template <bool TRANS>
+__device__ __forceinline__ void gload(const float* __restrict__ g, int rows, int Lg, LB dst, int ncols) {
+    const int n = rows * ncols;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int r, c;
+        if (TRANS) { c = i / rows; r = i - c * rows; }
+        else { r = i / ncols; c = i - r * ncols; }
+        const int t = dst.start + c;
+        float v = 0.f;
+        if (t >= 0 && t < Lg) v = TRANS ? g[(size_t)t * rows + r] : g[(size_t)r * Lg + t];
+        dst.p[r * dst.P + c] = v;
+    }
+}
+
+// LDS window -> global [rows][Lg], abs positions [a0, a0+n) clipped to Lg.
+__device__ __forceinline__ void gstore(float* __restrict__ g, int rows, int Lg, LB src, int a0, int n) {
+    const int m = rows * n;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const int r = i / n, c = i - r * n;
+        const int t = a0 + c;
+        if (t < Lg) g[(size_t)r * Lg + t] = src.p[r * src.P + (t - src.start)];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Window plans.  All column counts are exact receptive-field arithmetic; the
+// capacities also cover the garbage columns a 16-wide MFMA tile computes past
+// the last needed position (those columns are never stored).
+template <int M, int C, int TF>
+struct HeadPlan {
+    static constexpr int C1 = C / 2;
+    static constexpr int MEL_N = TF + 6;           // frames [f0-3, f0+TF+3)
+    static constexpr int A0_N = TF + 4;            // input conv out  [f0-2, f0+TF+2)
+    static constexpr int NQ = TF + 2;              // ConvT1 inputs   [f0-1, f0+TF+1)
+    static constexpr int H_N = 4 * TF + 2;         // RB1 conv1 out   [4f0-1, 4f0+4TF+1)
+    static constexpr int O_N = 4 * TF;             // RB1 out         [4f0, 4f0+4TF)
+    static constexpr int P_MEL = pstride(cmax(MEL_N, rup16(A0_N) + 2));
+    static constexpr int P_A0 = pstride(cmax(A0_N, rup16(NQ) + 2));
+    static constexpr int P_U = pstride(cmax(4 * NQ, rup16(H_N) + 4));
+    static constexpr int P_H = pstride(cmax(H_N, rup16(O_N) + 2));
+    static constexpr int R0 = cmax(M * P_MEL + C * P_A0, C1 * P_H);
+    static constexpr int R1 = C1 * P_U;
+    static constexpr int LDS_FLOATS = R0 + R1;
+};
+
+template <int CI, int W>
+struct MidPlan {  // U1 (CI ch, res 4) -> U2 (CI/2 ch, res 16); W res-4 positions
+    static constexpr int CO = CI / 2;
+    static constexpr int IN_N = W + 4;             // [p0-2, p0+W+2)
+    static constexpr int NQ = W + 2;               // ConvT2 inputs [p0-1, p0+W+1)
+    static constexpr int H_N = 4 * W + 2;          // [4p0-1, 4p0+4W+1)
+    static constexpr int O_N = 4 * W;              // [4p0, 4p0+4W)
+    static constexpr int P_IN = pstride(cmax(IN_N, rup16(NQ) + 2));
+    static constexpr int P_U = pstride(cmax(4 * NQ, rup16(H_N) + 4));
+    static constexpr int P_H = pstride(cmax(H_N, rup16(O_N) + 2));
+    static constexpr int R0 = cmax(CI * P_IN, CO * P_H);
+    static constexpr int R1 = CO * P_U;
+    static constexpr int LDS_FLOATS = R0 + R1;
+};
+
+template <int CI, int W>
+struct TailPlan {  // U2 (CI ch, res 16) -> audio (res 64); W res-16 positions
+    static constexpr int C3 = CI / 2, C4 = CI / 4;
+    static constexpr int IN_N = W + 8;             // [p0-4, p0+W+4)
+    static constexpr int NQ3 = W + 6;              // ConvT3 inputs [p0-3, p0+W+3) -> U3 [2p0-6, ..)
+    static constexpr int H3_N = 2 * W + 8;         // [2p0-4, 2p0+2W+4)
+    static constexpr int O3_N = 2 * W + 6;         // [2p0-3, 2p0+2W+3)
+    static constexpr int NQ4 = 2 * W + 4;          // ConvT4 inputs [2p0-2, 2p0+2W+2) -> U4 [4p0-4, ..)
+    static constexpr int H4_N = 4 * W + 4;         // [4p0-2, 4p0+4W+2)
+    static constexpr int O4_N = 4 * W + 2;         // [4p0-1, 4p0+4W+1)
+    static constexpr int A_N = 4 * W;              // audio [4p0, 4p0+4W)
+    static constexpr int P_IN = pstride(cmax(IN_N, rup16(NQ3) + 2));
+    static constexpr int P_U3 = pstride(cmax(2 * NQ3, cmax(rup16(H3_N) + 3, rup16(NQ4) + 5)));
+    static constexpr int P_H3 = pstride(cmax(H3_N, rup16(O3_N) + 2));
+    static constexpr int P_U4 = pstride(cmax(2 * NQ4, rup16(H4_N) + 3));
+    static constexpr int P_H4 = pstride(cmax(H4_N, rup16(O4_N) + 2));
+    // region A: U2in -> H3 -> U4 ; region B: U3 -> H4
+    static constexpr int RA = cmax(CI * P_IN, cmax(C3 * P_H3, C4 * P_U4));
+    static constexpr int RB = cmax(C3 * P_U3, C4 * P_H4);
+    static constexpr int LDS_FLOATS = RA + RB;
+};
+
+constexpr int kVocThreads = 512;  // 8 waves
+
+template <int M, int C, int TF, bool TRANS>
+__global__ __launch_bounds__(kVocThreads) void voc_head_kernel(const float* __restrict__ mel, int T, VocW w,
+                                                               float* __restrict__ U1) {
+    using Pl = HeadPlan<M, C, TF>;
+    constexpr int C1 = Pl::C1;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.y, f0 = blockIdx.x * TF;
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    LB melw{lds, Pl::P_MEL, f0 - 3};
+    LB a0w{lds + M * Pl::P_MEL, Pl::P_A0, f0 - 2};
+    LB hw{lds, Pl::P_H, 4 * f0 - 1};
+    LB uw{lds + Pl::R0, Pl::P_U, 4 * f0 - 4};
+    gload<TRANS>(mel + (size_t)b * M * T, M, T, melw, Pl::MEL_N);
+    __syncthreads();
+    lconv3<M, C, 2, ACT_NONE, false>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T, wave, nw);
+    __syncthreads();
+    lconvT<C, C1, 4, 2>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T, wave, nw);
+    __syncthreads();
+    lconv3<C1, C1, 2, ACT_LEAKY, false>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, Pl::H_N, 4 * T, wave, nw);
+    __syncthreads();
+    lconv3<C1, C1, 2, ACT_NONE, true>(w.w2[0], w.b2[0], hw, uw, 4 * f0, Pl::O_N, 4 * T, wave, nw);
+    __syncthreads();
+    gstore(U1 + (size_t)b * C1 * 4 * T, C1, 4 * T, uw, 4 * f0, Pl::O_N);
+}
+
+template <int CI, int W>
+__global__ __launch_bounds__(kVocThreads) void voc_mid_kernel(const float* __restrict__ U1, int L1, VocW w,
+                                                              float* __restrict__ U2) {
+    using Pl = MidPlan<CI, W>;
+    constexpr int CO = Pl::CO;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.y, p0 = blockIdx.x * W;
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int L2 = 4 * L1;
+    LB inw{lds, Pl::P_IN, p0 - 2};
+    LB hw{lds, Pl::P_H, 4 * p0 - 1};
+    LB uw{lds + Pl::R0, Pl::P_U, 4 * p0 - 4};
+    gload<false>(U1 + (size_t)b * CI * L1, CI, L1, inw, Pl::IN_N);
+    __syncthreads();
+    lconvT<CI, CO, 4, 4>(w.wt[1], w.bt[1], inw, uw, p0 - 1, Pl::NQ, L2, wave, nw);
+    __syncthreads();
+    lconv3<CO, CO, 4, ACT_LEAKY, false>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, Pl::H_N, L2, wave, nw);
+    __syncthreads();
+    lconv3<CO, CO, 4, ACT_NONE, true>(w.w2[1], w.b2[1], hw, uw, 4 * p0, Pl::O_N, L2, wave, nw);
+    __syncthreads();
+    gstore(U2 + (size_t)b * CO * L2, CO, L2, uw, 4 * p0, Pl::O_N);
+}
+
+template <int CI, int W>
+__global__ __launch_bounds__(kVocThreads) void voc_tail_kernel(const float* __restrict__ U2, int L2, VocW w,
+                                                               float* __restrict__ audio) {
+    using Pl = TailPlan<CI, W>;
+    constexpr int C3 = Pl::C3, C4 = Pl::C4;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.y, p0 = blockIdx.x * W;
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int L3 = 2 * L2, L4 = 4 * L2;
+    float* ra = lds;
+    float* rb = lds + Pl::RA;
+    LB inw{ra, Pl::P_IN, p0 - 4};
+    LB u3{rb, Pl::P_U3, 2 * p0 - 6};
+    LB h3{ra, Pl::P_H3, 2 * p0 - 4};
+    LB u4{ra, Pl::P_U4, 4 * p0 - 4};
+    LB h4{rb, Pl::P_H4, 4 * p0 - 2};
+    gload<false>(U2 + (size_t)b * CI * L2, CI, L2, inw, Pl::IN_N);
+    __syncthreads();
+    lconvT<CI, C3, 2, 4>(w.wt[2], w.bt[2], inw, u3, p0 - 3, Pl::NQ3, L3, wave, nw);
+    __syncthreads();
+    lconv3<C3, C3, 4, ACT_LEAKY, false>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, Pl::H3_N, L3, wave, nw);
+    __syncthreads();
+    lconv3<C3, C3, 4, ACT_NONE, true>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, Pl::O3_N, L3, wave, nw);
+    __syncthreads();
+    lconvT<C3, C4, 2, 4>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, wave, nw);
+    __syncthreads();
+    lconv3<C4, C4, 4, ACT_LEAKY, false>(w.w1[3], w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4, wave, nw);
+    __syncthreads();
+    lconv3<C4, C4, 4, ACT_NONE, true>(w.w2[3], w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4, wave, nw);
+    __syncthreads();
+    // output_conv (C4 -> 1, k3) + tanh: VALU, one position per thread, coalesced stores.
+    float* arow = audio + (size_t)b * L4;
+    const float bo = w.bo[0];
+    for (int j = threadIdx.x; j < Pl::A_N; j += blockDim.x) {
+        const int t = 4 * p0 + j;
+        if (t < L4) {
+            const float* x = u4.p + (t - 1 - u4.start);
+            float acc = 0.f;
+#pragma unroll
+            for (int ci = 0; ci < C4; ++ci) {
+                acc = fmaf(w.wo[ci * 3 + 0], x[ci * u4.P + 0], acc);
+                acc = fmaf(w.wo[ci * 3 + 1], x[ci * u4.P + 1], acc);
+                acc = fmaf(w.wo[ci * 3 + 2], x[ci * u4.P + 2], acc);
+            }
+            arow[t] = tanhf(acc + bo);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+namespace {
+template <typename K>
+int32_t set_lds(K kernel, size_t bytes) {
+    M2_CHECK_SHAPE(bytes <= 160 * 1024, "fused vocoder: LDS plan exceeds 160 KiB");
+    M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes));
+    return M2_OK;
+}
+
+template <int M, int C, int TF, int W2, int W3>
+int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
+                  hipStream_t st, const std::function<void(int, bool)>& mark) {
+    using HP = HeadPlan<M, C, TF>;
+    using MP = MidPlan<C / 2, W2>;
+    using TP = TailPlan<C / 4, W3>;
+    static bool attr = false;
+    if (!attr) {
+        int32_t rc;
+        if ((rc = set_lds(voc_head_kernel<M, C, TF, false>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_head_kernel<M, C, TF, true>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_mid_kernel<C / 2, W2>, MP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_tail_kernel<C / 4, W3>, TP::LDS_FLOATS * 4))) return rc;
+        attr = true;
+    }
+    mark(0, true);
+    if (trans)
+        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, true>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
+                           HP::LDS_FLOATS * 4, st, mel, T, w, U1);
+    else
+        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, false>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
+                           HP::LDS_FLOATS * 4, st, mel, T, w, U1);
+    mark(0, false);
+    M2_LAUNCHED("voc_head_kernel");
+    mark(1, true);
+    hipLaunchKernelGGL((voc_mid_kernel<C / 2, W2>), dim3(cdiv(4 * T, W2), B), dim3(kVocThreads), MP::LDS_FLOATS * 4,
+                       st, U1, 4 * T, w, U2);
+    mark(1, false);
+    M2_LAUNCHED("voc_mid_kernel");
+    mark(2, true);
+    hipLaunchKernelGGL((voc_tail_kernel<C / 4, W3>), dim3(cdiv(16 * T, W3), B), dim3(kVocThreads),
+                       TP::LDS_FLOATS * 4, st, U2, 16 * T, w, audio);
+    mark(2, false);
+    M2_LAUNCHED("voc_tail_kernel");
+    return M2_OK;
+}
+}  // namespace
+
+bool vocoder_fused_supported(int M, int C) {
+    return (M == 64 && C == 128) || (M == 80 && C == 256) || (M == 32 && C == 64);
+}
+
+int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, int T, const VocW& w, float* U1,
+                             float* U2, float* audio, hipStream_t st,
+                             const std::function<void(int, bool)>& mark) {
+    if (B == 0 || T == 0) return M2_OK;
+    if (M == 64 && C == 128) return voc_fused<64, 128, 28, 60, 240>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (M == 80 && C == 256) return voc_fused<80, 256, 12, 28, 120>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (M == 32 && C == 64) return voc_fused<32, 64, 28, 60, 240>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    return fail(M2_E_SHAPE, "fused vocoder: unsupported (mel_channels, vocoder_channels)");
+}
+
+const char* const kVocKernelNames[kVocKernels] = {
+    "voc_head_kernel (input_conv + ConvT1 + ResBlock1)",
+    "voc_mid_kernel (ConvT2 + ResBlock2)",
+    "voc_tail_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv)"};
+
+std::vector<float> pack_conv3(const float* W, int Cout, int Cin) {
+    const int MB = (Cout + 15) / 16, KS = 3 * Cin / 4;
+    std::vector<float> out((size_t)MB * KS * 64, 0.f);
+    for (int mb = 0; mb < MB; ++mb)
+        for (int s = 0; s < KS; ++s)
+            for (int lane = 0; lane < 64; ++lane) {
+                const int co = mb * 16 + (lane & 15), kk = 4 * s + (lane >> 4);
+                const int k = kk / Cin, ci = kk % Cin;
+                if (co < Cout) out[((size_t)mb * KS + s) * 64 + lane] = W[((size_t)co * Cin + ci) * 3 + k];
+            }
+    return out;
+}
+
+std::vector<float> pack_convT(const float* W, int Cin, int Cout, int R) {
+    const int MB = (Cout + 15) / 16, KS = 2 * Cin / 4, P = R / 2;
+    std::vector<float> out((size_t)R * MB * KS * 64, 0.f);
+    for (int ph = 0; ph < R; ++ph) {
+        const int k0 = (ph + P < R) ? ph + P : ph + P - R;  // tap 0: x[q] or x[q+1]
+        const int k1 = (ph + P < R) ? ph + P + R : ph + P;  // tap 1: x[q-1] or x[q]
+        for (int mb = 0; mb < MB; ++mb)
+            for (int s = 0; s < KS; ++s)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int co = mb * 16 + (lane & 15), kk = 4 * s + (lane >> 4);
+                    const int tap = kk / Cin, ci = kk % Cin;
+                    const int k = tap ? k1 : k0;
+                    if (co < Cout)
+                        out[(((size_t)ph * MB + mb) * KS + s) * 64 + lane] = W[((size_t)ci * Cout + co) * 2 * R + k];
+                }
+    }
+    return out;
+}
+
+}  // namespace m2

@@ -56,7 +56,8 @@ _SIGNATURES = {
     "m2_profile_enable": (c_i32, [c_vp, c_i32]),
     "m2_profile_read": (c_i32, [c_vp, ctypes.POINTER(c_f32), c_i32, ctypes.POINTER(c_i32)]),
     "m2_profile_disable": (c_i32, [c_vp]),
-    "m2_profile_kernel_name": (ctypes.c_char_p, []),
+    "m2_profile_kernel_count": (c_i32, []),
+    "m2_profile_kernel_name": (ctypes.c_char_p, [c_i32]),
 }
 
 # act codes (m2_common.h Act)
