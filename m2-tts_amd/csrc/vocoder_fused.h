@@ -25,8 +25,9 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
 constexpr int kVocKernels = 3;
 extern const char* const kVocKernelNames[kVocKernels];
 
-// Host-side packing into A-fragment order for v_mfma_f32_16x16x4_f32:
-// out[(mb*KS + s)*64 + lane] = A[row = mb*16 + (lane&15)][kk = 4*s + (lane>>4)].
+// Host-side packing into A-fragment order for v_mfma_f32_16x16x4_f32, k-steps
+// padded to KSP = roundup(KS, 4), layout [mb][s/4][lane][s%4] holding
+// A[row = mb*16 + (lane&15)][kk = 4*s + (lane>>4)].
 // conv3:  A[co][k*Cin + ci] = W[co][ci][k]            (W: [Cout][Cin][3])
 // convT:  per phase ph, A[co][tap*Cin + ci] = W[ci][co][k_tap(ph)]   (W: [Cin][Cout][2R])
 std::vector<float> pack_conv3(const float* W, int Cout, int Cin);

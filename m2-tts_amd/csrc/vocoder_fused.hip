@@ -22,6 +22,7 @@
 // are padded to a stride = 16 mod 32 floats so the two 32-lane halves of a
 // ds_read_b32 hit disjoint banks).  K = (tap, channel).  ConvT is r GEMMs,
 // one per output phase, each with K = 2 taps x Cin (the 2-tap polyphase form).
+#include <cstdlib>
 #include <functional>
 
 #include "m2_common.h"
@@ -46,13 +47,91 @@ constexpr int rup16(int n) { return (n + 15) / 16 * 16; }
 // Row stride >= cols with stride = 16 (mod 32): conflict-free B-operand reads.
 constexpr int pstride(int cols) { return ((cols + 15) / 32) * 32 + 16; }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
+// Compact row stride (multiple of 4, >= cols): up to 4-lane 2-way conflicts
+// between the two 16-lane halves of a read, in exchange for LDS capacity.
+constexpr int cstride(int cols) { return (cols + 3) / 4 * 4 + ((((cols + 3) / 4 * 4) % 32 == 0) ? 4 : 0); }
+constexpr int stride_for(int cols, bool compact) { return compact ? cstride(cols) : pstride(cols); }
 
 // ---------------------------------------------------------------------------
+// acc[n] += sum_s A(s) * B(s, n) over KS = NTAP*KC k-steps for NT 16-wide
+// column tiles.  A: packed weights, k-steps padded to KSP (multiple of 4),
+// laid out [s/4][lane][s%4] so one global_load_dwordx4 per lane fetches 4
+// k-steps (1 KiB per wave-instruction).  B(s, n) = bp[(s % KC)*4*P +
+// (s / KC)*OFFSTEP + n*16] from LDS (P, OFFSTEP compile-time: every B read
+// is a ds_read with an immediate offset off one per-item base address).  Register double buffer over k-blocks of
+// KB steps: block i+1's loads are in flight while block i's KB*NT MFMAs run
+// (KB = 8: 2 KiB of weights per wave in flight - the weight stream from L2 is
+// latency-bound, so bytes in flight set its rate).  Loads of tiles past `nt`
+// re-read the last live tile (no branch; nothing is stored from them).
+template <int KS>
+struct KPlan {
+    static constexpr int KSP = (KS + 3) / 4 * 4;
+    static constexpr int KB = (KSP % 8 == 0) ? 8 : 4;
+    static constexpr int NB = KSP / KB;
+};
+
+template <int KC, int NTAP, int NT, int P, int OFFSTEP>
+__device__ __forceinline__ void mma_run(const float* __restrict__ wp, const float* __restrict__ bp, int nt,
+                                        f32x4 (&acc)[NT]) {
+    constexpr int KS = NTAP * KC;
+    using KP = KPlan<KS>;
+    constexpr int KB = KP::KB, NB = KP::NB;
+    f32x4 a[2][KB / 4];
+    auto load = [&](int blk, f32x4 (&aa)[KB / 4]) {
+#pragma unroll
+        for (int q = 0; q < KB / 4; ++q) aa[q] = *reinterpret_cast<const f32x4*>(wp + (blk * (KB / 4) + q) * 256);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // One k-block: all B reads first (one LDS round trip per block), then the
+    // KB*NT MFMAs.  sched_barrier pins the order: hipcc otherwise sinks the
+    // next block's weight loads to the end of the block and interleaves
+    // ds_read -> lgkmcnt(0) -> 2 MFMAs, exposing an LDS round trip per pair.
+    auto compute = [&](int blk, const f32x4 (&aa)[KB / 4]) {
+        float bv[KB][NT];
+#pragma unroll
+        for (int i = 0; i < KB; ++i) {
+            const int s = blk * KB + i;
+            if (NB > 1 || s < KS) {
+                const float* br = bp + (s % KC) * 4 * P + (s / KC) * OFFSTEP;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) bv[i][n] = (n < nt) ? br[n * 16] : 0.f;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < KB; ++i) {
+            if (NB > 1 || blk * KB + i < KS) {
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    if (n < nt) acc[n] = mfma16(aa[i / 4][i % 4], bv[i][n], acc[n]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    static_assert(NB == 1 || KS % KB == 0, "multi-block K must be a multiple of the block");
+    load(0, a[0]);
+    int blk = 0;
+#pragma unroll 1
+    for (; blk + 2 < NB; blk += 2) {
+        load(blk + 1, a[1]);
+        compute(blk, a[0]);
+        load(blk + 2, a[0]);
+        compute(blk + 1, a[1]);
+    }
+    if (blk + 1 < NB) {
+        load(blk + 1, a[1]);
+        compute(blk, a[0]);
+        compute(blk + 1, a[1]);
+    } else {
+        compute(blk, a[0]);
+    }
+}
+
 // Conv1d(k=3, pad=1) over an LDS window: abs positions [a0, a0+npos), all
 // COUT channels.  Epilogue: +bias, act, (+ residual read from `out` in place),
 // 0 outside [0, L).  Packed weights: Wp[mb][s][lane] = W[mb*16 + (lane&15)]
 // [ci][k] with k*CIN + ci = 4*s + (lane>>4)  (zero rows for co >= COUT).
-template <int CIN, int COUT, int NT, int ACT, bool RES>
+template <int CIN, int COUT, int NT, int ACT, bool RES, int PIN>
 __device__ __forceinline__ void lconv3(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
                                        LB out, int a0, int npos, int L, int wave, int nwaves) {
     static_assert(CIN % 4 == 0, "CIN must be a multiple of 4");
@@ -66,19 +145,8 @@ __device__ __forceinline__ void lconv3(const float* __restrict__ Wp, const float
         f32x4 acc[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* wp = Wp + (size_t)mb * KS * 64 + lane;
-        const float* bp = in.p + lk * in.P + (a0 + tile0 * 16 + li - in.start - 1);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-#pragma unroll 8
-            for (int cb = 0; cb < KC; ++cb) {
-                const float a = wp[(k * KC + cb) * 64];
-                const float* br = bp + cb * 4 * in.P + k;
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    if (n < nt) acc[n] = mfma16(a, br[n * 16], acc[n]);
-            }
-        }
+        mma_run<KC, 3, NT, PIN, 1>(Wp + (size_t)mb * KPlan<KS>::KSP * 64 + lane * 4,
+                                   in.p + lk * PIN + (a0 + tile0 * 16 + li - in.start - 1), nt, acc);
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             if (n < nt) {
@@ -106,7 +174,7 @@ __device__ __forceinline__ void lconv3(const float* __restrict__ Wp, const float
 // reads taps (q, q-1) if ph + R/2 < R else (q+1, q).  Packed weights:
 // Wp[ph][mb][s][lane] = W[ci][mb*16 + (lane&15)][k_tap] with
 // tap*CIN + ci = 4*s + (lane>>4).
-template <int CIN, int COUT, int R, int NT>
+template <int CIN, int COUT, int R, int NT, int PIN>
 __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
                                        LB out, int q0, int nq, int L, int wave, int nwaves) {
     static_assert(CIN % 4 == 0, "CIN must be a multiple of 4");
@@ -122,19 +190,8 @@ __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float
         f32x4 acc[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* wp = Wp + (size_t)(ph * MB + mb) * KS * 64 + lane;
-        const float* bp = in.p + lk * in.P + (q0 + tile0 * 16 + li - in.start + d0);
-#pragma unroll
-        for (int tap = 0; tap < 2; ++tap) {
-#pragma unroll 8
-            for (int cb = 0; cb < KC; ++cb) {
-                const float a = wp[(tap * KC + cb) * 64];
-                const float* br = bp + cb * 4 * in.P - tap;
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    if (n < nt) acc[n] = mfma16(a, br[n * 16], acc[n]);
-            }
-        }
+        mma_run<KC, 2, NT, PIN, -1>(Wp + (size_t)(ph * MB + mb) * KPlan<KS>::KSP * 64 + lane * 4,
+                                    in.p + lk * PIN + (q0 + tile0 * 16 + li - in.start + d0), nt, acc);
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             if (n < nt) {
@@ -185,7 +242,7 @@ __device__ __forceinline__ void gstore(float* __restrict__ g, int rows, int Lg, 
 // Window plans.  All column counts are exact receptive-field arithmetic; the
 // capacities also cover the garbage columns a 16-wide MFMA tile computes past
 // the last needed position (those columns are never stored).
-template <int M, int C, int TF>
+template <int M, int C, int TF, bool CP = false>
 struct HeadPlan {
     static constexpr int C1 = C / 2;
     static constexpr int MEL_N = TF + 6;           // frames [f0-3, f0+TF+3)
@@ -193,10 +250,10 @@ struct HeadPlan {
     static constexpr int NQ = TF + 2;              // ConvT1 inputs   [f0-1, f0+TF+1)
     static constexpr int H_N = 4 * TF + 2;         // RB1 conv1 out   [4f0-1, 4f0+4TF+1)
     static constexpr int O_N = 4 * TF;             // RB1 out         [4f0, 4f0+4TF)
-    static constexpr int P_MEL = pstride(cmax(MEL_N, rup16(A0_N) + 2));
-    static constexpr int P_A0 = pstride(cmax(A0_N, rup16(NQ) + 2));
-    static constexpr int P_U = pstride(cmax(4 * NQ, rup16(H_N) + 4));
-    static constexpr int P_H = pstride(cmax(H_N, rup16(O_N) + 2));
+    static constexpr int P_MEL = stride_for(cmax(MEL_N, rup16(A0_N) + 2), CP);
+    static constexpr int P_A0 = stride_for(cmax(A0_N, rup16(NQ) + 2), CP);
+    static constexpr int P_U = stride_for(cmax(4 * NQ, rup16(H_N) + 4), CP);
+    static constexpr int P_H = stride_for(cmax(H_N, rup16(O_N) + 2), CP);
     static constexpr int R0 = cmax(M * P_MEL + C * P_A0, C1 * P_H);
     static constexpr int R1 = C1 * P_U;
     static constexpr int LDS_FLOATS = R0 + R1;
@@ -241,10 +298,29 @@ struct TailPlan {  // U2 (CI ch, res 16) -> audio (res 64); W res-16 positions
 
 constexpr int kVocThreads = 512;  // 8 waves
 
-template <int M, int C, int TF, bool TRANS>
-__global__ __launch_bounds__(kVocThreads) void voc_head_kernel(const float* __restrict__ mel, int T, VocW w,
+// Diagnostic build only (-DM2_STAMPS): per-wave s_memtime stamps at phase
+// boundaries, [kernel][workgroup][wave][16]; never part of the product build.
+#ifdef M2_STAMPS
+__device__ unsigned long long g_stamps[3][4096][8][16];
+#define STAMP(K, i)                                                                                      \
+    do {                                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        unsigned long long _t;                                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                      \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        const int _wg = blockIdx.y * gridDim.x + blockIdx.x;                                             \
+        if ((threadIdx.x & 63) == 0 && _wg < 4096) g_stamps[K][_wg][threadIdx.x >> 6][i] = _t;           \
+    } while (0)
+#else
+#define STAMP(K, i) \
+    do {            \
+    } while (0)
+#endif
+
+template <int M, int C, int TF, bool TRANS, bool CP>
+__global__ __launch_bounds__(kVocThreads, 4) void voc_head_kernel(const float* __restrict__ mel, int T, VocW w,
                                                                float* __restrict__ U1) {
-    using Pl = HeadPlan<M, C, TF>;
+    using Pl = HeadPlan<M, C, TF, CP>;
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.y, f0 = blockIdx.x * TF;
@@ -253,21 +329,33 @@ __global__ __launch_bounds__(kVocThreads) void voc_head_kernel(const float* __re
     LB a0w{lds + M * Pl::P_MEL, Pl::P_A0, f0 - 2};
     LB hw{lds, Pl::P_H, 4 * f0 - 1};
     LB uw{lds + Pl::R0, Pl::P_U, 4 * f0 - 4};
+    STAMP(0, 0);
     gload<TRANS>(mel + (size_t)b * M * T, M, T, melw, Pl::MEL_N);
+    STAMP(0, 1);
     __syncthreads();
-    lconv3<M, C, 2, ACT_NONE, false>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T, wave, nw);
+    STAMP(0, 2);
+    lconv3<M, C, 2, ACT_NONE, false, Pl::P_MEL>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T, wave, nw);
+    STAMP(0, 3);
     __syncthreads();
-    lconvT<C, C1, 4, 2>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T, wave, nw);
+    STAMP(0, 4);
+    lconvT<C, C1, 4, 2, Pl::P_A0>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T, wave, nw);
+    STAMP(0, 5);
     __syncthreads();
-    lconv3<C1, C1, 2, ACT_LEAKY, false>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, Pl::H_N, 4 * T, wave, nw);
+    STAMP(0, 6);
+    lconv3<C1, C1, 4, ACT_LEAKY, false, Pl::P_U>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, Pl::H_N, 4 * T, wave, nw);
+    STAMP(0, 7);
     __syncthreads();
-    lconv3<C1, C1, 2, ACT_NONE, true>(w.w2[0], w.b2[0], hw, uw, 4 * f0, Pl::O_N, 4 * T, wave, nw);
+    STAMP(0, 8);
+    lconv3<C1, C1, 4, ACT_NONE, true, Pl::P_H>(w.w2[0], w.b2[0], hw, uw, 4 * f0, Pl::O_N, 4 * T, wave, nw);
+    STAMP(0, 9);
     __syncthreads();
+    STAMP(0, 10);
     gstore(U1 + (size_t)b * C1 * 4 * T, C1, 4 * T, uw, 4 * f0, Pl::O_N);
+    STAMP(0, 11);
 }
 
 template <int CI, int W>
-__global__ __launch_bounds__(kVocThreads) void voc_mid_kernel(const float* __restrict__ U1, int L1, VocW w,
+__global__ __launch_bounds__(kVocThreads, 4) void voc_mid_kernel(const float* __restrict__ U1, int L1, VocW w,
                                                               float* __restrict__ U2) {
     using Pl = MidPlan<CI, W>;
     constexpr int CO = Pl::CO;
@@ -280,17 +368,17 @@ __global__ __launch_bounds__(kVocThreads) void voc_mid_kernel(const float* __res
     LB uw{lds + Pl::R0, Pl::P_U, 4 * p0 - 4};
     gload<false>(U1 + (size_t)b * CI * L1, CI, L1, inw, Pl::IN_N);
     __syncthreads();
-    lconvT<CI, CO, 4, 4>(w.wt[1], w.bt[1], inw, uw, p0 - 1, Pl::NQ, L2, wave, nw);
+    lconvT<CI, CO, 4, 4, Pl::P_IN>(w.wt[1], w.bt[1], inw, uw, p0 - 1, Pl::NQ, L2, wave, nw);
     __syncthreads();
-    lconv3<CO, CO, 4, ACT_LEAKY, false>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, Pl::H_N, L2, wave, nw);
+    lconv3<CO, CO, 4, ACT_LEAKY, false, Pl::P_U>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, Pl::H_N, L2, wave, nw);
     __syncthreads();
-    lconv3<CO, CO, 4, ACT_NONE, true>(w.w2[1], w.b2[1], hw, uw, 4 * p0, Pl::O_N, L2, wave, nw);
+    lconv3<CO, CO, 4, ACT_NONE, true, Pl::P_H>(w.w2[1], w.b2[1], hw, uw, 4 * p0, Pl::O_N, L2, wave, nw);
     __syncthreads();
     gstore(U2 + (size_t)b * CO * L2, CO, L2, uw, 4 * p0, Pl::O_N);
 }
 
 template <int CI, int W>
-__global__ __launch_bounds__(kVocThreads) void voc_tail_kernel(const float* __restrict__ U2, int L2, VocW w,
+__global__ __launch_bounds__(kVocThreads, 4) void voc_tail_kernel(const float* __restrict__ U2, int L2, VocW w,
                                                                float* __restrict__ audio) {
     using Pl = TailPlan<CI, W>;
     constexpr int C3 = Pl::C3, C4 = Pl::C4;
@@ -307,17 +395,17 @@ __global__ __launch_bounds__(kVocThreads) void voc_tail_kernel(const float* __re
     LB h4{rb, Pl::P_H4, 4 * p0 - 2};
     gload<false>(U2 + (size_t)b * CI * L2, CI, L2, inw, Pl::IN_N);
     __syncthreads();
-    lconvT<CI, C3, 2, 4>(w.wt[2], w.bt[2], inw, u3, p0 - 3, Pl::NQ3, L3, wave, nw);
+    lconvT<CI, C3, 2, 4, Pl::P_IN>(w.wt[2], w.bt[2], inw, u3, p0 - 3, Pl::NQ3, L3, wave, nw);
     __syncthreads();
-    lconv3<C3, C3, 4, ACT_LEAKY, false>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, Pl::H3_N, L3, wave, nw);
+    lconv3<C3, C3, 4, ACT_LEAKY, false, Pl::P_U3>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, Pl::H3_N, L3, wave, nw);
     __syncthreads();
-    lconv3<C3, C3, 4, ACT_NONE, true>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, Pl::O3_N, L3, wave, nw);
+    lconv3<C3, C3, 4, ACT_NONE, true, Pl::P_H3>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, Pl::O3_N, L3, wave, nw);
     __syncthreads();
-    lconvT<C3, C4, 2, 4>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, wave, nw);
+    lconvT<C3, C4, 2, 4, Pl::P_U3>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, wave, nw);
     __syncthreads();
-    lconv3<C4, C4, 4, ACT_LEAKY, false>(w.w1[3], w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4, wave, nw);
+    lconv3<C4, C4, 4, ACT_LEAKY, false, Pl::P_U4>(w.w1[3], w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4, wave, nw);
     __syncthreads();
-    lconv3<C4, C4, 4, ACT_NONE, true>(w.w2[3], w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4, wave, nw);
+    lconv3<C4, C4, 4, ACT_NONE, true, Pl::P_H4>(w.w2[3], w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4, wave, nw);
     __syncthreads();
     // output_conv (C4 -> 1, k3) + tanh: VALU, one position per thread, coalesced stores.
     float* arow = audio + (size_t)b * L4;
@@ -348,27 +436,27 @@ int32_t set_lds(K kernel, size_t bytes) {
     return M2_OK;
 }
 
-template <int M, int C, int TF, int W2, int W3>
+template <int M, int C, int TF, int W2, int W3, bool CP = false>
 int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                   hipStream_t st, const std::function<void(int, bool)>& mark) {
-    using HP = HeadPlan<M, C, TF>;
+    using HP = HeadPlan<M, C, TF, CP>;
     using MP = MidPlan<C / 2, W2>;
     using TP = TailPlan<C / 4, W3>;
     static bool attr = false;
     if (!attr) {
         int32_t rc;
-        if ((rc = set_lds(voc_head_kernel<M, C, TF, false>, HP::LDS_FLOATS * 4))) return rc;
-        if ((rc = set_lds(voc_head_kernel<M, C, TF, true>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_head_kernel<M, C, TF, false, CP>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_head_kernel<M, C, TF, true, CP>, HP::LDS_FLOATS * 4))) return rc;
         if ((rc = set_lds(voc_mid_kernel<C / 2, W2>, MP::LDS_FLOATS * 4))) return rc;
         if ((rc = set_lds(voc_tail_kernel<C / 4, W3>, TP::LDS_FLOATS * 4))) return rc;
         attr = true;
     }
     mark(0, true);
     if (trans)
-        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, true>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
+        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, true, CP>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
                            HP::LDS_FLOATS * 4, st, mel, T, w, U1);
     else
-        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, false>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
+        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, false, CP>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
                            HP::LDS_FLOATS * 4, st, mel, T, w, U1);
     mark(0, false);
     M2_LAUNCHED("voc_head_kernel");
@@ -394,33 +482,49 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
                              float* U2, float* audio, hipStream_t st,
                              const std::function<void(int, bool)>& mark) {
     if (B == 0 || T == 0) return M2_OK;
-    if (M == 64 && C == 128) return voc_fused<64, 128, 28, 60, 240>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    static const int plan = std::getenv("M2_VOC_PLAN") ? std::atoi(std::getenv("M2_VOC_PLAN")) : 0;
+    if (M == 64 && C == 128) {
+        if (plan == 1) return voc_fused<64, 128, 32, 64, 250, true>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+        return voc_fused<64, 128, 28, 60, 240>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    }
     if (M == 80 && C == 256) return voc_fused<80, 256, 12, 28, 120>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     if (M == 32 && C == 64) return voc_fused<32, 64, 28, 60, 240>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     return fail(M2_E_SHAPE, "fused vocoder: unsupported (mel_channels, vocoder_channels)");
 }
+
+#ifdef M2_STAMPS
+extern "C" int32_t m2_debug_stamps(void* host, size_t bytes) {
+    return (int32_t)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps));
+}
+#endif
 
 const char* const kVocKernelNames[kVocKernels] = {
     "voc_head_kernel (input_conv + ConvT1 + ResBlock1)",
     "voc_mid_kernel (ConvT2 + ResBlock2)",
     "voc_tail_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv)"};
 
+// Index of A-fragment element (m-block mb, k-step s, lane) in the packed
+// layout [mb][s/4][lane][s%4] with KSP (k-steps rounded up to 4) per m-block.
+static inline size_t apack_index(int mb, int s, int lane, int KSP) {
+    return (((size_t)mb * (KSP / 4) + s / 4) * 64 + lane) * 4 + (s % 4);
+}
+
 std::vector<float> pack_conv3(const float* W, int Cout, int Cin) {
-    const int MB = (Cout + 15) / 16, KS = 3 * Cin / 4;
-    std::vector<float> out((size_t)MB * KS * 64, 0.f);
+    const int MB = (Cout + 15) / 16, KS = 3 * Cin / 4, KSP = (KS + 3) / 4 * 4;
+    std::vector<float> out((size_t)MB * KSP * 64, 0.f);
     for (int mb = 0; mb < MB; ++mb)
         for (int s = 0; s < KS; ++s)
             for (int lane = 0; lane < 64; ++lane) {
                 const int co = mb * 16 + (lane & 15), kk = 4 * s + (lane >> 4);
                 const int k = kk / Cin, ci = kk % Cin;
-                if (co < Cout) out[((size_t)mb * KS + s) * 64 + lane] = W[((size_t)co * Cin + ci) * 3 + k];
+                if (co < Cout) out[apack_index(mb, s, lane, KSP)] = W[((size_t)co * Cin + ci) * 3 + k];
             }
     return out;
 }
 
 std::vector<float> pack_convT(const float* W, int Cin, int Cout, int R) {
-    const int MB = (Cout + 15) / 16, KS = 2 * Cin / 4, P = R / 2;
-    std::vector<float> out((size_t)R * MB * KS * 64, 0.f);
+    const int MB = (Cout + 15) / 16, KS = 2 * Cin / 4, P = R / 2, KSP = (KS + 3) / 4 * 4;
+    std::vector<float> out((size_t)R * MB * KSP * 64, 0.f);
     for (int ph = 0; ph < R; ++ph) {
         const int k0 = (ph + P < R) ? ph + P : ph + P - R;  // tap 0: x[q] or x[q+1]
         const int k1 = (ph + P < R) ? ph + P + R : ph + P;  // tap 1: x[q-1] or x[q]
@@ -430,8 +534,7 @@ std::vector<float> pack_convT(const float* W, int Cin, int Cout, int R) {
                     const int co = mb * 16 + (lane & 15), kk = 4 * s + (lane >> 4);
                     const int tap = kk / Cin, ci = kk % Cin;
                     const int k = tap ? k1 : k0;
-                    if (co < Cout)
-                        out[(((size_t)ph * MB + mb) * KS + s) * 64 + lane] = W[((size_t)ci * Cout + co) * 2 * R + k];
+                    if (co < Cout) out[apack_index(ph * MB + mb, s, lane, KSP)] = W[((size_t)ci * Cout + co) * 2 * R + k];
                 }
     }
     return out;

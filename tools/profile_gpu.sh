@@ -1,0 +1,23 @@
+#!/bin/bash
+# Profile one bench.py configuration on the GPU box with rocprofv3:
+# one kernel-trace/stats pass plus separate PMC passes (never combined with
+# sys/runtime traces).  Usage: tools/profile_gpu.sh <tag> [bench args...]
+# Output: gpurun_out/prof_<tag>/{trace,sq,lds,fetch,write}/...
+set -u
+tag=$1; shift
+export TMPDIR=/tmp
+out=gpurun_out/prof_$tag
+mkdir -p $out
+BENCH="python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-pipeline-extra $*"
+run() {  # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 240 rocprofv3 "$@" --output-format csv -d $out/$name -o run -- $BENCH > $out/$name.log 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"
+  return $rc
+}
+run trace --kernel-trace --stats &&
+run sq --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAVES GRBM_GUI_ACTIVE &&
+run lds --pmc SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_LDS_UNALIGNED_STALL &&
+run fetch --pmc FETCH_SIZE &&
+run write --pmc WRITE_SIZE
