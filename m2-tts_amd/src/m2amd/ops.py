@@ -142,27 +142,41 @@ def durations_for_regulator(durations: Tensor):
     return durations.clamp(-2**30, 2**30).to(torch.int32).contiguous(), 1
 
 
+def frame_counts(durations: Tensor, scale: float = 1.0):
+    """Counting half of the length regulator (m2_length_regulator_count):
+    returns (cum [B,S+1] int32 exclusive prefix sums, T [B] int32, Tmax [1] int32)."""
+    require_device(durations, what="length_regulator")
+    B, S = durations.shape
+    d, is_int = durations_for_regulator(durations)
+    dev = durations.device
+    cum = torch.empty(B, S + 1, device=dev, dtype=torch.int32)
+    tot = torch.empty(B, device=dev, dtype=torch.int32)
+    tmax = torch.empty(1, device=dev, dtype=torch.int32)
+    _lib.call("m2_length_regulator_count", _ptr(d), is_int, float(scale), B, S, _ptr(cum), _ptr(tot), _ptr(tmax),
+              stream_handle(dev))
+    return cum, tot, tmax
+
+
+def expand_frames(enc: Tensor, cum: Tensor, T_out: int) -> Tensor:
+    """Expanding half (m2_length_regulator_expand): [B,S,H] -> [B,T_out,H]."""
+    enc = f32c(enc)
+    B, S, H = enc.shape
+    out = torch.empty(B, T_out, H, device=enc.device, dtype=torch.float32)
+    _lib.call("m2_length_regulator_expand", _ptr(enc), _ptr(cum), B, S, H, T_out, _ptr(out), stream_handle(enc.device))
+    return out
+
+
 def regulate(enc: Tensor, durations: Tensor, max_length: Optional[int] = None, scale: float = 1.0) -> Tensor:
     """LengthRegulator.forward (tts_model.py:126-178) on the GPU: scan + gather.
 
     One device->host read of the batch maximum frame count, only when
     max_length is not given (it sizes the output)."""
     require_device(enc, durations, what="length_regulator")
-    enc = f32c(enc)
-    B, S, H = enc.shape
-    d, is_int = durations_for_regulator(durations)
-    dev = enc.device
-    cum = torch.empty(B, S + 1, device=dev, dtype=torch.int32)
-    tot = torch.empty(B, device=dev, dtype=torch.int32)
-    tmax = torch.empty(1, device=dev, dtype=torch.int32)
-    st = stream_handle(dev)
-    _lib.call("m2_length_regulator_count", _ptr(d), is_int, float(scale), B, S, _ptr(cum), _ptr(tot), _ptr(tmax), st)
+    cum, _, tmax = frame_counts(durations, scale)
     if max_length is None:
         # an utterance with no frames becomes one zero frame (tts_model.py:158-160)
         max_length = max(1, int(tmax.item()))
-    out = torch.empty(B, max_length, H, device=dev, dtype=torch.float32)
-    _lib.call("m2_length_regulator_expand", _ptr(enc), _ptr(cum), B, S, H, max_length, _ptr(out), st)
-    return out
+    return expand_frames(enc, cum, max_length)
 
 
 def batchnorm_eval_affine(weight: Tensor, bias: Tensor, mean: Tensor, var: Tensor, eps: float):

@@ -1,0 +1,113 @@
+"""Utterance-sharded inference across GPUs (one process per GPU, torch.distributed).
+
+The reference has no distributed code.  Sharding a
+global batch by utterance is exact with ONE coupling: the mel decoder is
+unmasked over frames and the length regulator pads every utterance to the
+batch maximum (tts_model.py:165-176, 211-228), so each utterance's mel depends
+on the GLOBAL frame count T.  The ranks therefore agree on T with one
+all-reduce(MAX) of a single int32 before the decoder; everything else is
+independent.  Collectives (RCCL over xGMI with the "nccl" backend; gloo in the
+CPU tests):
+  all_reduce(MAX)  1 x int32                       after the duration predictor
+  all_gather       mel [b, T, M] and audio [b, 1, 64T] shards (padded to ceil(B/N))
+Payloads are KB..MB, so the path is latency-bound; weights are replicated.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+Tensor = torch.Tensor
+
+
+def shard_bounds(batch: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous balanced split: rank r gets [lo, hi) (first B % N ranks get one more)."""
+    base, rem = divmod(batch, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+@dataclass
+class Stages:
+    """The per-shard stage functions.  ``hip_stages(model)`` binds the MI355X
+    kernels; tests bind the CPU oracle to check the sharding logic on gloo."""
+    encode: Callable[[Tensor, Optional[Tensor]], Tensor]          # ids, lengths -> enc [b,S,H]
+    durations: Callable[[Tensor], Tensor]                         # enc -> dur [b,S]
+    frame_totals: Callable[[Tensor, float], Tensor]               # dur, scale -> T_b [b] (int)
+    regulate: Callable[[Tensor, Tensor, int, float], Tensor]      # enc, dur, T, scale -> [b,T,H]
+    decode: Callable[[Tensor], Tensor]                            # [b,T,H] -> mel [b,T,M]
+    vocode: Callable[[Tensor], Tensor]                            # mel [b,T,M] -> audio [b,1,64T]
+
+
+def hip_stages(model) -> Stages:
+    from . import ops
+
+    def hm(t):
+        return model._hip(t.device)
+
+    def frame_totals(dur, scale):
+        _, tot, _ = ops.frame_counts(dur, scale)
+        return tot
+
+    def regulate(enc, dur, T, scale):
+        cum, _, _ = ops.frame_counts(dur, scale)
+        return ops.expand_frames(enc, cum, T)
+
+    return Stages(encode=lambda ids, lens: hm(ids).text_encoder(ids, lens)[0],
+                  durations=lambda enc: hm(enc).duration(enc),
+                  frame_totals=frame_totals, regulate=regulate,
+                  decode=lambda x: hm(x).decoder(x),
+                  vocode=lambda mel: hm(mel).vocoder(mel, layout_btm=True))
+
+
+def _gather_shards(local: Tensor, batch: int, world: int, group) -> Tensor:
+    """all_gather of per-rank utterance shards with unequal sizes -> [batch, ...]."""
+    per = -(-batch // world)
+    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    out = [parts[r][: shard_bounds(batch, world, r)[1] - shard_bounds(batch, world, r)[0]] for r in range(world)]
+    return torch.cat(out, dim=0)
+
+
+def sharded_inference(stages: Stages, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor],
+                      duration_scale: float = 1.0, group=None, gather: bool = True):
+    """M2TTSModel.inference (tts_model.py:402-438) over a global batch sharded by
+    utterance.  Every rank passes the same global ``phoneme_ids``/lengths
+    (or the same seed-generated tensors); rank r computes utterances
+    shard_bounds(B, N, r).  Returns (mel, audio) for the global batch when
+    ``gather``, else this rank's shard and its bounds."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    B = phoneme_ids.shape[0]
+    if gather and world > 1 and B < world:  # same decision on every rank, before any collective
+        raise ValueError("sharded_inference with gather needs at least one utterance per rank (B >= world)")
+    lo, hi = shard_bounds(B, world, rank)
+    ids = phoneme_ids[lo:hi]
+    lens = phoneme_lengths[lo:hi] if phoneme_lengths is not None else None
+    with torch.no_grad():
+        if hi > lo:
+            enc = stages.encode(ids, lens)
+            dur = stages.durations(enc)
+            t_local = int(stages.frame_totals(dur, duration_scale).max().item())
+        else:
+            enc = dur = None
+            t_local = 0
+        t = torch.tensor([t_local], dtype=torch.int32,
+                         device=phoneme_ids.device if phoneme_ids.is_cuda else "cpu")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        T = max(1, int(t.item()))  # all-empty batch -> one zero frame (tts_model.py:158-160)
+        if hi > lo:
+            reg = stages.regulate(enc, dur, T, duration_scale)
+            mel = stages.decode(reg)
+            audio = stages.vocode(mel)
+        else:
+            mel = audio = None
+    if not gather or world == 1:
+        return (mel, audio) if gather else (mel, audio, (lo, hi))
+    return _gather_shards(mel, B, world, group), _gather_shards(audio, B, world, group)

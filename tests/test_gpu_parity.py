@@ -303,8 +303,26 @@ def test_weights_reload_invalidates_handle(gpu):
     assert maxabs(mel2 - 1.0, mel1) <= 1e-5
 
 
-def test_cpu_tensors_fail_loudly():
-    from models.tts_model import M2TTSModel
-    m = M2TTSModel().eval()
-    with pytest.raises(RuntimeError, match="ROCm GPU"):
-        m.inference(torch.zeros(1, 4, dtype=torch.long), torch.tensor([4]))
+def test_cli_end_to_end_wav(gpu, tmp_path):
+    """scripts/synthesize.py main(): checkpoint (trainer dict format) -> WAV.
+    The PCM16 samples must equal the reference audio for the same sentence
+    quantised the same way, up to 1 LSB where fp32 noise straddles a rounding
+    boundary."""
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, str(ROOT / "m2-tts_amd" / "scripts"))
+    import synthesize
+    from utils.audio import float_to_pcm16, load_audio_pcm16
+    g = golden("cli_stage1")
+    ck = tmp_path / "stage1.pt"
+    cfg = {"model": {"text_encoder": {"vocab_size": 256, "hidden_dim": 64, "num_layers": 2, "num_heads": 2,
+                                      "dropout": 0.1}, "decoder": {"mel_channels": 64, "num_layers": 2},
+                     "vocoder": {"hidden_channels": 128}}}
+    torch.save({"model_state_dict": golden_state("s1"), "config": cfg, "step": 1}, ck)
+    out = tmp_path / "out.wav"
+    synthesize.main(["--text", str(g["text"]), "--checkpoint", str(ck), "--output", str(out)])
+    y, sr = load_audio_pcm16(out)
+    want = float_to_pcm16(g["audio"][0, 0]).astype(np.int32)
+    got = np.rint(y * 32768).astype(np.int32)
+    assert sr == 22050 and got.shape == want.shape == (81920,)
+    assert int(np.abs(got - want).max()) <= 1

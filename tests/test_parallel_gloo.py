@@ -1,0 +1,88 @@
+"""Utterance sharding (m2amd.parallel) on 2 CPU ranks over gloo, with the CPU
+oracle bound as the per-shard stages: the sharded result must equal the
+unsharded reference forward, including the batch-global frame padding that
+the unmasked decoder makes observable."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import m2tts_oracle as orc
+from conftest import golden, golden_state
+
+
+def oracle_stages(sd, cfg):
+    from m2amd.parallel import Stages
+
+    def frame_totals(dur, scale):
+        d = (dur * scale).trunc()
+        return torch.where(d > 0, d, torch.zeros_like(d)).sum(1).to(torch.int32)
+
+    return Stages(encode=lambda ids, lens: orc.text_encoder(sd, cfg, ids, lens)[0],
+                  durations=lambda enc: orc.duration_predictor(sd, enc),
+                  frame_totals=frame_totals,
+                  regulate=lambda enc, dur, T, scale: orc.length_regulator(enc, dur * scale if scale != 1.0 else dur, T),
+                  decode=lambda x: orc.mel_decoder(sd, cfg, x),
+                  vocode=lambda mel: orc.vocoder(sd, mel.transpose(1, 2)))
+
+
+def _worker(rank, world, port, outfile):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from m2amd.parallel import sharded_inference
+        torch.set_num_threads(2)
+        sd = golden_state("s1")
+        st = oracle_stages(sd, orc.STAGE1)
+        g = golden("s1_target_free")  # lengths [24, 17]
+        ids, lens = torch.from_numpy(g["ids"]), torch.from_numpy(g["lengths"])
+        # uneven global batch of 5 with different lengths -> different per-shard T
+        ids5 = torch.cat([ids, ids[:1], ids.flip(1)[:2]])
+        lens5 = torch.tensor([24, 17, 24, 9, 3])
+        out = {}
+        for tag, (i, l, scale) in {"b2": (ids, lens, 1.0), "b5": (ids5, lens5, 1.0), "b5s": (ids5, lens5, 1.3)}.items():
+            mel, audio = sharded_inference(st, i, l, duration_scale=scale)
+            out[tag] = (mel, audio)
+        if rank == 0:
+            import numpy as np
+            np.savez(outfile, **{f"{k}_{j}": v[j].numpy() for k, v in out.items() for j in range(2)})
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_inference_matches_unsharded_two_ranks(tmp_path):
+    import numpy as np
+    outfile = str(tmp_path / "res.npz")
+    mp.spawn(_worker, args=(2, _free_port(), outfile), nprocs=2, join=True)
+    z = np.load(outfile)
+    res = {k: (z[f"{k}_0"], z[f"{k}_1"]) for k in ("b2", "b5", "b5s")}
+    sd = golden_state("s1")
+    g = golden("s1_target_free")
+    ids, lens = torch.from_numpy(g["ids"]), torch.from_numpy(g["lengths"])
+    ids5 = torch.cat([ids, ids[:1], ids.flip(1)[:2]])
+    lens5 = torch.tensor([24, 17, 24, 9, 3])
+    for tag, (i, l, scale) in {"b2": (ids, lens, 1.0), "b5": (ids5, lens5, 1.0), "b5s": (ids5, lens5, 1.3)}.items():
+        mel, audio = orc.inference(sd, orc.STAGE1, i, l, duration_scale=scale, as_written=False)
+        assert res[tag][0].shape == tuple(mel.shape), tag
+        assert float(abs(res[tag][0] - mel.numpy()).max()) <= 1e-5, tag
+        assert float(abs(res[tag][1] - audio.numpy()).max()) <= 1e-5, tag
+
+
+def test_shard_bounds_cover_batch():
+    from m2amd.parallel import shard_bounds
+    for B in range(0, 20):
+        for N in range(1, 9):
+            spans = [shard_bounds(B, N, r) for r in range(N)]
+            assert spans[0][0] == 0 and spans[-1][1] == B
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
