@@ -22,6 +22,8 @@ namespace m2 {
 // output is read in its [B,S,H] layout (the reference's transpose(1,2) is a
 // view).  BatchNorm uses alpha = gamma/sqrt(var+eps), beta' = beta -
 // mean*alpha, the inference form PyTorch's CPU batch_norm evaluates.
+// Conv weights arrive packed [ci][k][co] (m2_model_create) so the lanes of a
+// wave - consecutive output channels - read consecutive weights.
 constexpr int DUR_TS = 32;
 
 __global__ __launch_bounds__(256) void duration_kernel(
@@ -47,11 +49,11 @@ __global__ __launch_bounds__(256) void duration_kernel(
         float v = 0.f;
         if (s >= 0 && s < S) {
             float acc = 0.f;
-            const float* wr = w1 + (size_t)co * H * 3;
             for (int ci = 0; ci < H; ++ci) {
-                acc = fmaf(wr[3 * ci + 0], X[(p + 0) * H + ci], acc);
-                acc = fmaf(wr[3 * ci + 1], X[(p + 1) * H + ci], acc);
-                acc = fmaf(wr[3 * ci + 2], X[(p + 2) * H + ci], acc);
+                const float* wr = w1 + (size_t)ci * 3 * H + co;
+                acc = fmaf(wr[0], X[(p + 0) * H + ci], acc);
+                acc = fmaf(wr[H], X[(p + 1) * H + ci], acc);
+                acc = fmaf(wr[2 * H], X[(p + 2) * H + ci], acc);
             }
             v = (acc + b1[co]) * a1[co] + c1[co];
             v = v > 0.f ? v : 0.f;
@@ -62,11 +64,11 @@ __global__ __launch_bounds__(256) void duration_kernel(
     for (int i = tid; i < DUR_TS * H; i += 256) {
         const int p = i / H, co = i - p * H;
         float acc = 0.f;
-        const float* wr = w2 + (size_t)co * H * 3;
         for (int ci = 0; ci < H; ++ci) {
-            acc = fmaf(wr[3 * ci + 0], Y1[(p + 0) * H + ci], acc);
-            acc = fmaf(wr[3 * ci + 1], Y1[(p + 1) * H + ci], acc);
-            acc = fmaf(wr[3 * ci + 2], Y1[(p + 2) * H + ci], acc);
+            const float* wr = w2 + (size_t)ci * 3 * H + co;
+            acc = fmaf(wr[0], Y1[(p + 0) * H + ci], acc);
+            acc = fmaf(wr[H], Y1[(p + 1) * H + ci], acc);
+            acc = fmaf(wr[2 * H], Y1[(p + 2) * H + ci], acc);
         }
         const float v = (acc + b2[co]) * a2[co] + c2[co];
         Y2[i] = v > 0.f ? v : 0.f;

@@ -273,6 +273,9 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     total = align_up(total, 64);
     const size_t bn_off = total;
     total += 4 * (size_t)H;
+    total = align_up(total, 64);
+    const size_t dw_off = total;  // duration conv weights re-laid out [ci][k][co], 2 layers
+    total += 2 * 3 * (size_t)H * H;
 
     auto* m = new m2_model();
     m->cfg = *cfg;
@@ -315,6 +318,20 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             host[(2 * j + 1) * H + c] = bnb[c] - bnm[c] * a;
         }
     }
+    std::vector<float> dpack(2 * 3 * (size_t)H * H);
+    for (int j = 0; j < 2; ++j) {
+        const std::string n = "duration_predictor.predictor.conv_layers." + std::to_string(j) + ".conv.weight";
+        std::vector<float> w((size_t)3 * H * H);
+        e = hipMemcpyAsync(w.data(), weights[idx(n)], w.size() * sizeof(float), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return bail(e, "hipMemcpyAsync(duration conv)");
+        for (int co = 0; co < H; ++co)
+            for (int ci = 0; ci < H; ++ci)
+                for (int k = 0; k < 3; ++k)
+                    dpack[(size_t)j * 3 * H * H + ((size_t)ci * 3 + k) * H + co] = w[((size_t)co * H + ci) * 3 + k];
+    }
+    e = hipMemcpyAsync(m->buf + dw_off, dpack.data(), dpack.size() * sizeof(float), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return bail(e, "hipMemcpyAsync(duration pack)");
     e = hipMemcpyAsync(m->buf + bn_off, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return bail(e, "hipMemcpyAsync(bn up)");
     e = hipStreamSynchronize(st);
@@ -334,7 +351,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     m->enc_nb = P("text_encoder.norm.bias");
     for (int j = 0; j < 2; ++j) {
         const std::string p = "duration_predictor.predictor.conv_layers." + std::to_string(j) + ".conv.";
-        m->dur[4 * j + 0] = P(p + "weight");
+        m->dur[4 * j + 0] = m->buf + dw_off + (size_t)j * 3 * H * H;
         m->dur[4 * j + 1] = P(p + "bias");
         m->dur[4 * j + 2] = m->buf + bn_off + (2 * j) * H;
         m->dur[4 * j + 3] = m->buf + bn_off + (2 * j + 1) * H;

@@ -63,10 +63,13 @@ constexpr int stride_for(int cols, bool compact) { return compact ? cstride(cols
 // (KB = 8: 2 KiB of weights per wave in flight - the weight stream from L2 is
 // latency-bound, so bytes in flight set its rate).  Loads of tiles past `nt`
 // re-read the last live tile (no branch; nothing is stored from them).
+#ifndef M2_KB8
+#define M2_KB8 0
+#endif
 template <int KS>
 struct KPlan {
     static constexpr int KSP = (KS + 3) / 4 * 4;
-    static constexpr int KB = (KSP % 8 == 0) ? 8 : 4;
+    static constexpr int KB = (KSP <= 8) ? KSP : ((KS % 8 == 0 && M2_KB8) ? 8 : 4);
     static constexpr int NB = KSP / KB;
 };
 
@@ -127,21 +130,46 @@ __device__ __forceinline__ void mma_run(const float* __restrict__ wp, const floa
     }
 }
 
+// Work distribution inside a layer.  Dynamic (-DM2_STATIC_SCHED=0): each wave takes the
+// next item from an LDS counter - waves sharing a SIMD progress at different
+// rates (issue arbitration favours the older wave), so a static item->wave
+// map leaves the SIMD idle behind the slowest wave at every layer barrier.
+// Static (default, 1-3 % faster measured on MI355X): item = wave, wave + nwaves, ...
+#ifndef M2_STATIC_SCHED
+#define M2_STATIC_SCHED 1
+#endif
+__device__ __forceinline__ int first_item(int* ctr) {
+    if (M2_STATIC_SCHED) return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int v = 0;
+    if ((threadIdx.x & 63) == 0) v = atomicAdd(ctr, 1);
+    return __builtin_amdgcn_readfirstlane(__shfl(v, 0));
+}
+__device__ __forceinline__ int next_item(int* ctr, int item) {
+    if (M2_STATIC_SCHED) return item + (blockDim.x >> 6);
+    return first_item(ctr);
+}
+
 // Conv1d(k=3, pad=1) over an LDS window: abs positions [a0, a0+npos), all
 // COUT channels.  Epilogue: +bias, act, (+ residual read from `out` in place),
 // 0 outside [0, L).  Packed weights: Wp[mb][s][lane] = W[mb*16 + (lane&15)]
 // [ci][k] with k*CIN + ci = 4*s + (lane>>4)  (zero rows for co >= COUT).
 template <int CIN, int COUT, int NT, int ACT, bool RES, int PIN>
 __device__ __forceinline__ void lconv3(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
-                                       LB out, int a0, int npos, int L, int wave, int nwaves) {
+                                       LB out, int a0, int npos, int L, int* ctr) {
     static_assert(CIN % 4 == 0, "CIN must be a multiple of 4");
     constexpr int KC = CIN / 4, KS = 3 * KC, MB = (COUT + 15) / 16;
     const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
     const int ntiles = (npos + 15) >> 4;
     const int nch = (ntiles + NT - 1) / NT;
-    for (int item = wave; item < MB * nch; item += nwaves) {
+    for (int item = first_item(ctr); item < MB * nch; item = next_item(ctr, item)) {
         const int mb = item % MB, tile0 = (item / MB) * NT;
         const int nt = min(NT, ntiles - tile0);
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = mb * 16 + lk * 4 + r;
+            bv[r] = co < COUT ? bias[co] : 0.f;  // issued before the MFMA loop: latency hidden
+        }
         f32x4 acc[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -157,7 +185,7 @@ __device__ __forceinline__ void lconv3(const float* __restrict__ Wp, const float
                     for (int r = 0; r < 4; ++r) {
                         const int co = mb * 16 + lk * 4 + r;
                         if (co < COUT) {
-                            float v = act_t<ACT>(acc[n][r] + bias[co]);
+                            float v = act_t<ACT>(acc[n][r] + bv[r]);
                             float* o = out.p + co * out.P + (t - out.start);
                             if (RES) v += *o;
                             *o = (t >= 0 && t < L) ? v : 0.f;
@@ -176,17 +204,23 @@ __device__ __forceinline__ void lconv3(const float* __restrict__ Wp, const float
 // tap*CIN + ci = 4*s + (lane>>4).
 template <int CIN, int COUT, int R, int NT, int PIN>
 __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
-                                       LB out, int q0, int nq, int L, int wave, int nwaves) {
+                                       LB out, int q0, int nq, int L, int* ctr) {
     static_assert(CIN % 4 == 0, "CIN must be a multiple of 4");
     constexpr int KC = CIN / 4, KS = 2 * KC, MB = (COUT + 15) / 16, PAD = R / 2;
     const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
     const int ntiles = (nq + 15) >> 4;
     const int nch = (ntiles + NT - 1) / NT;
-    for (int item = wave; item < R * MB * nch; item += nwaves) {
+    for (int item = first_item(ctr); item < R * MB * nch; item = next_item(ctr, item)) {
         const int ph = item % R, rest = item / R;
         const int mb = rest % MB, tile0 = (rest / MB) * NT;
         const int nt = min(NT, ntiles - tile0);
         const int d0 = (ph + PAD < R) ? 0 : 1;  // tap 0 offset; tap 1 is d0 - 1
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = mb * 16 + lk * 4 + r;
+            bv[r] = co < COUT ? bias[co] : 0.f;
+        }
         f32x4 acc[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -202,7 +236,7 @@ __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float
                     for (int r = 0; r < 4; ++r) {
                         const int co = mb * 16 + lk * 4 + r;
                         if (co < COUT) {
-                            const float v = act_t<ACT_LEAKY>(acc[n][r] + bias[co]);
+                            const float v = act_t<ACT_LEAKY>(acc[n][r] + bv[r]);
                             out.p[co * out.P + (t - out.start)] = (t >= 0 && t < L) ? v : 0.f;
                         }
                     }
@@ -217,6 +251,7 @@ __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float
 template <bool TRANS>
 __device__ __forceinline__ void gload(const float* __restrict__ g, int rows, int Lg, LB dst, int ncols) {
     const int n = rows * ncols;
+#pragma unroll 2
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         int r, c;
         if (TRANS) { c = i / rows; r = i - c * rows; }
@@ -231,6 +266,7 @@ __device__ __forceinline__ void gload(const float* __restrict__ g, int rows, int
 // LDS window -> global [rows][Lg], abs positions [a0, a0+n) clipped to Lg.
 __device__ __forceinline__ void gstore(float* __restrict__ g, int rows, int Lg, LB src, int a0, int n) {
     const int m = rows * n;
+#pragma unroll 2
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         const int r = i / n, c = i - r * n;
         const int t = a0 + c;
@@ -296,12 +332,40 @@ struct TailPlan {  // U2 (CI ch, res 16) -> audio (res 64); W res-16 positions
     static constexpr int LDS_FLOATS = RA + RB;
 };
 
-constexpr int kVocThreads = 512;  // 8 waves
+// ---------------------------------------------------------------------------
+// Tiling configurations.  WAVES waves per workgroup; NT_* = 16-position tiles
+// per work item of each layer, chosen so every layer splits into a multiple
+// of WAVES items; MINW = launch-bounds waves per SIMD (VGPR cap).
+struct CfgS1W8 {  // stage1: 8 waves, <= 74 KB LDS (2 workgroups / CU)
+    static constexpr int M = 64, C = 128, TF = 28, W2 = 60, W3 = 240, WAVES = 8, MINW = 5;
+    static constexpr bool CP = false;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+};
+struct CfgS1W16 {  // stage1: 16 waves, one workgroup per CU (152/132/131 KB LDS)
+    static constexpr int M = 64, C = 128, TF = 63, W2 = 125, W3 = 500, WAVES = 16, MINW = 4;
+    static constexpr bool CP = false;
+    static constexpr int NT_IN = 3, NT_T1 = 5, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 8, NT_R4 = 8;
+};
+struct CfgS1W16s {  // CfgS1W16 with ~2-3 smaller work items per wave for the dynamic schedule
+    static constexpr int M = 64, C = 128, TF = 63, W2 = 125, W3 = 500, WAVES = 16, MINW = 4;
+    static constexpr bool CP = false;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 2, NT_T2 = 2, NT_R2 = 2, NT_T3 = 2, NT_R3 = 2, NT_T4 = 4, NT_R4 = 4;
+};
+struct CfgS2W8 {
+    static constexpr int M = 80, C = 256, TF = 12, W2 = 28, W3 = 120, WAVES = 8, MINW = 5;
+    static constexpr bool CP = false;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+};
+struct CfgTinyW8 {  // M2TTSModel(hidden 32, mel 32, vocoder 64) as in the reference smoke tests
+    static constexpr int M = 32, C = 64, TF = 28, W2 = 60, W3 = 240, WAVES = 8, MINW = 5;
+    static constexpr bool CP = false;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+};
 
 // Diagnostic build only (-DM2_STAMPS): per-wave s_memtime stamps at phase
 // boundaries, [kernel][workgroup][wave][16]; never part of the product build.
 #ifdef M2_STAMPS
-__device__ unsigned long long g_stamps[3][4096][8][16];
+__device__ unsigned long long g_stamps[3][4096][16][16];
 #define STAMP(K, i)                                                                                      \
     do {                                                                                                 \
         __builtin_amdgcn_sched_barrier(0);                                                               \
@@ -317,14 +381,16 @@ __device__ unsigned long long g_stamps[3][4096][8][16];
     } while (0)
 #endif
 
-template <int M, int C, int TF, bool TRANS, bool CP>
-__global__ __launch_bounds__(kVocThreads, 4) void voc_head_kernel(const float* __restrict__ mel, int T, VocW w,
-                                                               float* __restrict__ U1) {
-    using Pl = HeadPlan<M, C, TF, CP>;
+template <class Cfg, bool TRANS>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(const float* __restrict__ mel, int T,
+                                                                             VocW w, float* __restrict__ U1) {
+    constexpr int M = Cfg::M, C = Cfg::C, TF = Cfg::TF;
+    using Pl = HeadPlan<M, C, TF, Cfg::CP>;
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.y, f0 = blockIdx.x * TF;
-    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ int ctr[8];  // per-layer work counters (32 B: keeps the dynamic LDS base 16-B aligned)
+    if (threadIdx.x < 8) ctr[threadIdx.x] = 0;
     LB melw{lds, Pl::P_MEL, f0 - 3};
     LB a0w{lds + M * Pl::P_MEL, Pl::P_A0, f0 - 2};
     LB hw{lds, Pl::P_H, 4 * f0 - 1};
@@ -334,19 +400,19 @@ __global__ __launch_bounds__(kVocThreads, 4) void voc_head_kernel(const float* _
     STAMP(0, 1);
     __syncthreads();
     STAMP(0, 2);
-    lconv3<M, C, 2, ACT_NONE, false, Pl::P_MEL>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T, wave, nw);
+    lconv3<M, C, Cfg::NT_IN, ACT_NONE, false, Pl::P_MEL>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T, ctr + 0);
     STAMP(0, 3);
     __syncthreads();
     STAMP(0, 4);
-    lconvT<C, C1, 4, 2, Pl::P_A0>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T, wave, nw);
+    lconvT<C, C1, 4, Cfg::NT_T1, Pl::P_A0>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T, ctr + 1);
     STAMP(0, 5);
     __syncthreads();
     STAMP(0, 6);
-    lconv3<C1, C1, 4, ACT_LEAKY, false, Pl::P_U>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, Pl::H_N, 4 * T, wave, nw);
+    lconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::P_U>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, Pl::H_N, 4 * T, ctr + 2);
     STAMP(0, 7);
     __syncthreads();
     STAMP(0, 8);
-    lconv3<C1, C1, 4, ACT_NONE, true, Pl::P_H>(w.w2[0], w.b2[0], hw, uw, 4 * f0, Pl::O_N, 4 * T, wave, nw);
+    lconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::P_H>(w.w2[0], w.b2[0], hw, uw, 4 * f0, Pl::O_N, 4 * T, ctr + 3);
     STAMP(0, 9);
     __syncthreads();
     STAMP(0, 10);
@@ -354,37 +420,51 @@ __global__ __launch_bounds__(kVocThreads, 4) void voc_head_kernel(const float* _
     STAMP(0, 11);
 }
 
-template <int CI, int W>
-__global__ __launch_bounds__(kVocThreads, 4) void voc_mid_kernel(const float* __restrict__ U1, int L1, VocW w,
-                                                              float* __restrict__ U2) {
+template <class Cfg>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(const float* __restrict__ U1, int L1,
+                                                                            VocW w, float* __restrict__ U2) {
+    constexpr int CI = Cfg::C / 2, W = Cfg::W2;
     using Pl = MidPlan<CI, W>;
     constexpr int CO = Pl::CO;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.y, p0 = blockIdx.x * W;
-    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ int ctr[8];  // per-layer work counters (32 B: keeps the dynamic LDS base 16-B aligned)
+    if (threadIdx.x < 8) ctr[threadIdx.x] = 0;
     const int L2 = 4 * L1;
     LB inw{lds, Pl::P_IN, p0 - 2};
     LB hw{lds, Pl::P_H, 4 * p0 - 1};
     LB uw{lds + Pl::R0, Pl::P_U, 4 * p0 - 4};
+    STAMP(1, 0);
     gload<false>(U1 + (size_t)b * CI * L1, CI, L1, inw, Pl::IN_N);
+    STAMP(1, 1);
     __syncthreads();
-    lconvT<CI, CO, 4, 4, Pl::P_IN>(w.wt[1], w.bt[1], inw, uw, p0 - 1, Pl::NQ, L2, wave, nw);
+    STAMP(1, 2);
+    lconvT<CI, CO, 4, Cfg::NT_T2, Pl::P_IN>(w.wt[1], w.bt[1], inw, uw, p0 - 1, Pl::NQ, L2, ctr + 0);
+    STAMP(1, 3);
     __syncthreads();
-    lconv3<CO, CO, 4, ACT_LEAKY, false, Pl::P_U>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, Pl::H_N, L2, wave, nw);
+    STAMP(1, 4);
+    lconv3<CO, CO, Cfg::NT_R2, ACT_LEAKY, false, Pl::P_U>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, Pl::H_N, L2, ctr + 1);
+    STAMP(1, 5);
     __syncthreads();
-    lconv3<CO, CO, 4, ACT_NONE, true, Pl::P_H>(w.w2[1], w.b2[1], hw, uw, 4 * p0, Pl::O_N, L2, wave, nw);
+    STAMP(1, 6);
+    lconv3<CO, CO, Cfg::NT_R2, ACT_NONE, true, Pl::P_H>(w.w2[1], w.b2[1], hw, uw, 4 * p0, Pl::O_N, L2, ctr + 2);
+    STAMP(1, 7);
     __syncthreads();
+    STAMP(1, 8);
     gstore(U2 + (size_t)b * CO * L2, CO, L2, uw, 4 * p0, Pl::O_N);
+    STAMP(1, 9);
 }
 
-template <int CI, int W>
-__global__ __launch_bounds__(kVocThreads, 4) void voc_tail_kernel(const float* __restrict__ U2, int L2, VocW w,
-                                                               float* __restrict__ audio) {
+template <class Cfg>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(const float* __restrict__ U2, int L2,
+                                                                             VocW w, float* __restrict__ audio) {
+    constexpr int CI = Cfg::C / 4, W = Cfg::W3;
     using Pl = TailPlan<CI, W>;
     constexpr int C3 = Pl::C3, C4 = Pl::C4;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.y, p0 = blockIdx.x * W;
-    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ int ctr[8];  // per-layer work counters (32 B: keeps the dynamic LDS base 16-B aligned)
+    if (threadIdx.x < 8) ctr[threadIdx.x] = 0;
     const int L3 = 2 * L2, L4 = 4 * L2;
     float* ra = lds;
     float* rb = lds + Pl::RA;
@@ -393,20 +473,34 @@ __global__ __launch_bounds__(kVocThreads, 4) void voc_tail_kernel(const float* _
     LB h3{ra, Pl::P_H3, 2 * p0 - 4};
     LB u4{ra, Pl::P_U4, 4 * p0 - 4};
     LB h4{rb, Pl::P_H4, 4 * p0 - 2};
+    STAMP(2, 0);
     gload<false>(U2 + (size_t)b * CI * L2, CI, L2, inw, Pl::IN_N);
     __syncthreads();
-    lconvT<CI, C3, 2, 4, Pl::P_IN>(w.wt[2], w.bt[2], inw, u3, p0 - 3, Pl::NQ3, L3, wave, nw);
+    STAMP(2, 1);
+    lconvT<CI, C3, 2, Cfg::NT_T3, Pl::P_IN>(w.wt[2], w.bt[2], inw, u3, p0 - 3, Pl::NQ3, L3, ctr + 0);
+    STAMP(2, 2);
     __syncthreads();
-    lconv3<C3, C3, 4, ACT_LEAKY, false, Pl::P_U3>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, Pl::H3_N, L3, wave, nw);
+    STAMP(2, 3);
+    lconv3<C3, C3, Cfg::NT_R3, ACT_LEAKY, false, Pl::P_U3>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, Pl::H3_N, L3, ctr + 1);
+    STAMP(2, 4);
     __syncthreads();
-    lconv3<C3, C3, 4, ACT_NONE, true, Pl::P_H3>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, Pl::O3_N, L3, wave, nw);
+    STAMP(2, 5);
+    lconv3<C3, C3, Cfg::NT_R3, ACT_NONE, true, Pl::P_H3>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, Pl::O3_N, L3, ctr + 2);
+    STAMP(2, 6);
     __syncthreads();
-    lconvT<C3, C4, 2, 4, Pl::P_U3>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, wave, nw);
+    STAMP(2, 7);
+    lconvT<C3, C4, 2, Cfg::NT_T4, Pl::P_U3>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, ctr + 3);
+    STAMP(2, 8);
     __syncthreads();
-    lconv3<C4, C4, 4, ACT_LEAKY, false, Pl::P_U4>(w.w1[3], w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4, wave, nw);
+    STAMP(2, 9);
+    lconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::P_U4>(w.w1[3], w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4, ctr + 4);
+    STAMP(2, 10);
     __syncthreads();
-    lconv3<C4, C4, 4, ACT_NONE, true, Pl::P_H4>(w.w2[3], w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4, wave, nw);
+    STAMP(2, 11);
+    lconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::P_H4>(w.w2[3], w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4, ctr + 5);
+    STAMP(2, 12);
     __syncthreads();
+    STAMP(2, 13);
     // output_conv (C4 -> 1, k3) + tanh: VALU, one position per thread, coalesced stores.
     float* arow = audio + (size_t)b * L4;
     const float bo = w.bo[0];
@@ -424,6 +518,7 @@ __global__ __launch_bounds__(kVocThreads, 4) void voc_tail_kernel(const float* _
             arow[t] = tanhf(acc + bo);
         }
     }
+    STAMP(2, 14);
 }
 
 // ---------------------------------------------------------------------------
@@ -436,38 +531,39 @@ int32_t set_lds(K kernel, size_t bytes) {
     return M2_OK;
 }
 
-template <int M, int C, int TF, int W2, int W3, bool CP = false>
+template <class Cfg>
 int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                   hipStream_t st, const std::function<void(int, bool)>& mark) {
-    using HP = HeadPlan<M, C, TF, CP>;
-    using MP = MidPlan<C / 2, W2>;
-    using TP = TailPlan<C / 4, W3>;
+    using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
+    using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
+    using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
+    constexpr int threads = Cfg::WAVES * 64;
     static bool attr = false;
     if (!attr) {
         int32_t rc;
-        if ((rc = set_lds(voc_head_kernel<M, C, TF, false, CP>, HP::LDS_FLOATS * 4))) return rc;
-        if ((rc = set_lds(voc_head_kernel<M, C, TF, true, CP>, HP::LDS_FLOATS * 4))) return rc;
-        if ((rc = set_lds(voc_mid_kernel<C / 2, W2>, MP::LDS_FLOATS * 4))) return rc;
-        if ((rc = set_lds(voc_tail_kernel<C / 4, W3>, TP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_head_kernel<Cfg, false>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_head_kernel<Cfg, true>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_mid_kernel<Cfg>, MP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_tail_kernel<Cfg>, TP::LDS_FLOATS * 4))) return rc;
         attr = true;
     }
     mark(0, true);
     if (trans)
-        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, true, CP>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
-                           HP::LDS_FLOATS * 4, st, mel, T, w, U1);
+        hipLaunchKernelGGL((voc_head_kernel<Cfg, true>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_FLOATS * 4,
+                           st, mel, T, w, U1);
     else
-        hipLaunchKernelGGL((voc_head_kernel<M, C, TF, false, CP>), dim3(cdiv(T, TF), B), dim3(kVocThreads),
-                           HP::LDS_FLOATS * 4, st, mel, T, w, U1);
+        hipLaunchKernelGGL((voc_head_kernel<Cfg, false>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_FLOATS * 4,
+                           st, mel, T, w, U1);
     mark(0, false);
     M2_LAUNCHED("voc_head_kernel");
     mark(1, true);
-    hipLaunchKernelGGL((voc_mid_kernel<C / 2, W2>), dim3(cdiv(4 * T, W2), B), dim3(kVocThreads), MP::LDS_FLOATS * 4,
-                       st, U1, 4 * T, w, U2);
+    hipLaunchKernelGGL((voc_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(threads), MP::LDS_FLOATS * 4, st, U1,
+                       4 * T, w, U2);
     mark(1, false);
     M2_LAUNCHED("voc_mid_kernel");
     mark(2, true);
-    hipLaunchKernelGGL((voc_tail_kernel<C / 4, W3>), dim3(cdiv(16 * T, W3), B), dim3(kVocThreads),
-                       TP::LDS_FLOATS * 4, st, U2, 16 * T, w, audio);
+    hipLaunchKernelGGL((voc_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(threads), TP::LDS_FLOATS * 4, st,
+                       U2, 16 * T, w, audio);
     mark(2, false);
     M2_LAUNCHED("voc_tail_kernel");
     return M2_OK;
@@ -482,13 +578,19 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
                              float* U2, float* audio, hipStream_t st,
                              const std::function<void(int, bool)>& mark) {
     if (B == 0 || T == 0) return M2_OK;
-    static const int plan = std::getenv("M2_VOC_PLAN") ? std::atoi(std::getenv("M2_VOC_PLAN")) : 0;
+    static const int plan = std::getenv("M2_VOC_PLAN") ? std::atoi(std::getenv("M2_VOC_PLAN")) : -1;
     if (M == 64 && C == 128) {
-        if (plan == 1) return voc_fused<64, 128, 32, 64, 250, true>(mel, trans, B, T, w, U1, U2, audio, st, mark);
-        return voc_fused<64, 128, 28, 60, 240>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+        // Workgroup rounds: one 16-wave WG per CU; 8-wave WGs pair up.  Pick the
+        // tiling whose workgroup count wastes the least of its last round.
+        const int n16 = B * cdiv(T, CfgS1W16::TF), n8 = B * cdiv(T, CfgS1W8::TF);
+        const double waste16 = (double)cdiv(n16, 256) * 256 / n16, waste8 = (double)cdiv(n8, 512) * 512 / n8;
+        const bool w16 = plan == 2 || (plan < 0 && waste16 <= waste8);
+        if (plan == 3) return voc_fused<CfgS1W16s>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+        if (w16) return voc_fused<CfgS1W16>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+        return voc_fused<CfgS1W8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     }
-    if (M == 80 && C == 256) return voc_fused<80, 256, 12, 28, 120>(mel, trans, B, T, w, U1, U2, audio, st, mark);
-    if (M == 32 && C == 64) return voc_fused<32, 64, 28, 60, 240>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (M == 80 && C == 256) return voc_fused<CfgS2W8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (M == 32 && C == 64) return voc_fused<CfgTinyW8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     return fail(M2_E_SHAPE, "fused vocoder: unsupported (mel_channels, vocoder_channels)");
 }
 

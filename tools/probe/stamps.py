@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Read per-wave phase stamps from the M2_STAMPS diagnostic build.
+"""Per-wave phase stamps from the M2_STAMPS diagnostic build (never the product).
 M2TTS_HIP_LIB=m2-tts_amd/csrc/build_stamps/libm2tts_hip_stamps.so python tools/probe/stamps.py B"""
 import ctypes
 import sys
@@ -14,6 +14,12 @@ sys.path.insert(0, str(ROOT / "m2-tts_amd" / "src"))
 import bench  # noqa: E402
 from m2amd import _lib  # noqa: E402
 
+PHASES = {
+    0: ["gload", "bar", "inconv", "bar", "convT1", "bar", "rb1c1", "bar", "rb1c2", "bar", "gstore"],
+    1: ["gload", "bar", "convT2", "bar", "rb2c1", "bar", "rb2c2", "bar", "gstore"],
+    2: ["gload+bar", "convT3", "bar", "rb3c1", "bar", "rb3c2", "bar", "convT4", "bar", "rb4c1", "bar", "rb4c2", "bar",
+        "outconv"],
+}
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 dev = torch.device("cuda", 0)
 lib = _lib.load()
@@ -22,17 +28,20 @@ mel = torch.randn(B, 64, 500, device=dev)
 for _ in range(3):
     model.vocoder(mel)
 torch.cuda.synchronize()
-n = 3 * 4096 * 8 * 16
-buf = np.zeros(n, dtype=np.uint64)
+buf = np.zeros(3 * 4096 * 16 * 16, dtype=np.uint64)
 lib.m2_debug_stamps.restype = ctypes.c_int32
-rc = lib.m2_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
-st = buf.reshape(3, 4096, 8, 16)[0]
-nwg = B * 18
-st = st[:nwg].astype(np.int64)
-names = ["gload", "bar", "inconv", "bar", "convT1", "bar", "rb1c1", "bar", "rb1c2", "bar", "gstore"]
-d = np.diff(st[:, :, :12], axis=2)  # [wg][wave][11]
-print(f"B={B} WGs={nwg}  cycles (median over WGs of the max over waves | mean over waves)")
-tot = (st[:, :, 11] - st[:, :, 0]).max(axis=1)
-for i, nm in enumerate(names):
-    print(f"  {nm:8s} max-wave {np.median(d[:, :, i].max(axis=1)):8.0f}   mean-wave {np.median(d[:, :, i].mean(axis=1)):8.0f}")
-print(f"  total(wave0 start -> last gstore) median {np.median(tot):.0f} cycles; kernel span {st[:, :, 11].max() - st[:, :, 0].min()} cycles")
+lib.m2_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
+all_st = buf.reshape(3, 4096, 16, 16).astype(np.int64)
+for k, names in PHASES.items():
+    st = all_st[k]
+    used = st[:, 0, 0] != 0
+    st = st[used]
+    nph = len(names)
+    nw = int((st[0, :, 0] != 0).sum())
+    st = st[:, :nw, : nph + 1]
+    d = np.diff(st, axis=2)
+    tot = (st[:, :, nph] - st[:, :, 0]).max(axis=1)
+    print(f"kernel {k}: WGs={st.shape[0]} waves={nw}; cycles: median over WGs of (max over waves | mean over waves)")
+    for i, nm in enumerate(names):
+        print(f"   {nm:10s} {np.median(d[:, :, i].max(axis=1)):8.0f} | {np.median(d[:, :, i].mean(axis=1)):8.0f}")
+    print(f"   total      {np.median(tot):8.0f}")
