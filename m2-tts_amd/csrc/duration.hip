@@ -10,24 +10,79 @@
 // The reference's regulator is a Python double loop with one host sync per
 // phoneme; here it is one scan kernel and one gather kernel, and the only
 // host round trip left is the caller's read of T_max to size the output.
+#include <algorithm>
+
 #include "m2_common.h"
 
 namespace m2 {
 
 // ---------------------------------------------------------------------------
-// One workgroup per (utterance, 32-phoneme tile).  The encoder rows of the
+// One workgroup per (utterance, 16-phoneme tile).  The encoder rows of the
 // tile plus a 2-phoneme halo each side are staged in LDS; conv1 is evaluated
 // on the tile +-1 (positions outside [0,S) are the zero padding conv2 sees),
 // conv2 on the tile, then the k=1 projection and softplus.  The encoder
 // output is read in its [B,S,H] layout (the reference's transpose(1,2) is a
 // view).  BatchNorm uses alpha = gamma/sqrt(var+eps), beta' = beta -
 // mean*alpha, the inference form PyTorch's CPU batch_norm evaluates.
-// Conv weights arrive packed [ci][k][co] (m2_model_create) so the lanes of a
-// wave - consecutive output channels - read consecutive weights.
-constexpr int DUR_TS = 32;
+// Conv weights arrive packed [ci][k][co] (m2_model_create) and are staged in
+// LDS one layer at a time (3*H*H floats: 48 KiB at H=64, 108 KiB at H=96):
+// the inner loop is then LDS-only - lanes (consecutive co) read consecutive
+// weights, the activation rows are float4 broadcasts.  The whole predictor is
+// ~0.2 GFLOP at B=32, S=100; what matters is not waiting on L2 per FMA.
+constexpr int DUR_TS = 16;
+
+// out[p][co] (+)= sum_{ci in chunk, k} W[ci][k][co] * in[p + k][ci] for p in
+// [0, np), with the weight rows of channels [ci0, ci0 + cc) staged in Ws.
+__device__ __forceinline__ void dur_conv_chunk(const float* in, const float* Ws, int H, int np, int ci0,
+                                               int cc, bool first, float* out) {
+    for (int i = threadIdx.x; i < np * H; i += 256) {
+        const int p = i / H, co = i - p * H;
+        const float* x0 = in + p * H + ci0;
+        const float* w0 = Ws + co;
+        float acc = first ? 0.f : out[i];
+        for (int ci = 0; ci < cc; ci += 4) {
+            const float4 u0 = *reinterpret_cast<const float4*>(x0 + ci);
+            const float4 u1 = *reinterpret_cast<const float4*>(x0 + H + ci);
+            const float4 u2 = *reinterpret_cast<const float4*>(x0 + 2 * H + ci);
+            acc = fmaf(w0[0], u0.x, acc); acc = fmaf(w0[H], u1.x, acc); acc = fmaf(w0[2 * H], u2.x, acc);
+            w0 += 3 * H;
+            acc = fmaf(w0[0], u0.y, acc); acc = fmaf(w0[H], u1.y, acc); acc = fmaf(w0[2 * H], u2.y, acc);
+            w0 += 3 * H;
+            acc = fmaf(w0[0], u0.z, acc); acc = fmaf(w0[H], u1.z, acc); acc = fmaf(w0[2 * H], u2.z, acc);
+            w0 += 3 * H;
+            acc = fmaf(w0[0], u0.w, acc); acc = fmaf(w0[H], u1.w, acc); acc = fmaf(w0[2 * H], u2.w, acc);
+            w0 += 3 * H;
+        }
+        out[i] = acc;
+    }
+}
+
+// One conv layer: weights streamed through LDS in chunks of `cc` input
+// channels (all of them at once for H <= 108), then bias, BN, ReLU, and zero
+// for rows whose position pos0 + p is outside [0, S).
+__device__ __forceinline__ void dur_conv(const float* in, float* Ws, const float* __restrict__ w, int H, int cc,
+                                         int np, int pos0, int S, const float* __restrict__ b,
+                                         const float* __restrict__ a, const float* __restrict__ c,
+                                         float* out) {
+    for (int ci0 = 0; ci0 < H; ci0 += cc) {
+        const int n = 3 * min(cc, H - ci0) * H;
+        const float* src = w + (size_t)ci0 * 3 * H;
+        __syncthreads();  // previous chunk's readers are done with Ws
+        for (int i = threadIdx.x * 4; i < n; i += 256 * 4)
+            *reinterpret_cast<float4*>(Ws + i) = *reinterpret_cast<const float4*>(src + i);
+        __syncthreads();
+        dur_conv_chunk(in, Ws, H, np, ci0, min(cc, H - ci0), ci0 == 0, out);
+    }
+    for (int i = threadIdx.x; i < np * H; i += 256) {
+        const int p = i / H, co = i - p * H, s = pos0 + p;
+        float v = (out[i] + b[co]) * a[co] + c[co];
+        v = v > 0.f ? v : 0.f;
+        out[i] = (s >= 0 && s < S) ? v : 0.f;
+    }
+}
 
 __global__ __launch_bounds__(256) void duration_kernel(
-    const float* __restrict__ enc, int S, int H, const float* __restrict__ w1,
+    const float* __restrict__ enc, int S, int H, int cc, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ a2,
     const float* __restrict__ c2, const float* __restrict__ pw, const float* __restrict__ pb,
@@ -36,6 +91,7 @@ __global__ __launch_bounds__(256) void duration_kernel(
     float* X = lds;                          // [TS+4][H]  s0-2 .. s0+TS+1
     float* Y1 = X + (DUR_TS + 4) * H;        // [TS+2][H]  s0-1 .. s0+TS
     float* Y2 = Y1 + (DUR_TS + 2) * H;       // [TS][H]    s0   .. s0+TS-1
+    float* Ws = Y2 + DUR_TS * H;             // [3*cc][H]  weight chunk
     const int b = blockIdx.y, s0 = blockIdx.x * DUR_TS, tid = threadIdx.x;
     const float* e = enc + (size_t)b * S * H;
 
@@ -43,36 +99,8 @@ __global__ __launch_bounds__(256) void duration_kernel(
         const int p = i / H, c = i - p * H, s = s0 - 2 + p;
         X[i] = (s >= 0 && s < S) ? e[(size_t)s * H + c] : 0.f;
     }
-    __syncthreads();
-    for (int i = tid; i < (DUR_TS + 2) * H; i += 256) {
-        const int p = i / H, co = i - p * H, s = s0 - 1 + p;
-        float v = 0.f;
-        if (s >= 0 && s < S) {
-            float acc = 0.f;
-            for (int ci = 0; ci < H; ++ci) {
-                const float* wr = w1 + (size_t)ci * 3 * H + co;
-                acc = fmaf(wr[0], X[(p + 0) * H + ci], acc);
-                acc = fmaf(wr[H], X[(p + 1) * H + ci], acc);
-                acc = fmaf(wr[2 * H], X[(p + 2) * H + ci], acc);
-            }
-            v = (acc + b1[co]) * a1[co] + c1[co];
-            v = v > 0.f ? v : 0.f;
-        }
-        Y1[i] = v;
-    }
-    __syncthreads();
-    for (int i = tid; i < DUR_TS * H; i += 256) {
-        const int p = i / H, co = i - p * H;
-        float acc = 0.f;
-        for (int ci = 0; ci < H; ++ci) {
-            const float* wr = w2 + (size_t)ci * 3 * H + co;
-            acc = fmaf(wr[0], Y1[(p + 0) * H + ci], acc);
-            acc = fmaf(wr[H], Y1[(p + 1) * H + ci], acc);
-            acc = fmaf(wr[2 * H], Y1[(p + 2) * H + ci], acc);
-        }
-        const float v = (acc + b2[co]) * a2[co] + c2[co];
-        Y2[i] = v > 0.f ? v : 0.f;
-    }
+    dur_conv(X, Ws, w1, H, cc, DUR_TS + 2, s0 - 1, S, b1, a1, c1, Y1);
+    dur_conv(Y1, Ws, w2, H, cc, DUR_TS, s0, S, b2, a2, c2, Y2);
     __syncthreads();
     // k=1 projection H -> 1: one wave per phoneme, shuffle reduction.
     const int lane = tid & 63, wave = tid >> 6;
@@ -163,15 +191,19 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict_
 int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur,
                         hipStream_t st) {
     if (B == 0 || S == 0) return M2_OK;
-    const size_t lds = sizeof(float) * (3 * DUR_TS + 6) * H;
-    M2_CHECK_SHAPE(lds <= 160 * 1024, "duration: hidden_dim too large");
+    // LDS: activations (3*TS+6)*H + a weight chunk of cc input channels 3*cc*H.
+    const size_t act = (size_t)(3 * DUR_TS + 6) * H;
+    const size_t room = 160 * 1024 / sizeof(float);
+    M2_CHECK_SHAPE(H % 4 == 0 && act + 12 * (size_t)H <= room, "duration: hidden_dim must be a multiple of 4 and <= 630");
+    const int cc = (int)std::min<size_t>((size_t)H, (room - act) / (3 * (size_t)H) / 4 * 4);
+    const size_t lds = sizeof(float) * (act + 3 * (size_t)cc * H);
     static bool attr_set = false;
     if (!attr_set) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(duration_kernel),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL(duration_kernel, dim3(cdiv(S, DUR_TS), B), dim3(256), lds, st, enc, S, H,
+    hipLaunchKernelGGL(duration_kernel, dim3(cdiv(S, DUR_TS), B), dim3(256), lds, st, enc, S, H, cc,
                        p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9], dur);
     M2_LAUNCHED("duration_kernel");
     return M2_OK;

@@ -141,92 +141,140 @@ __global__ __launch_bounds__(256) void linear_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Attention core, one query per lane, keys streamed through LDS in chunks of
-// 64 with an online (running max / running sum) softmax.  Scores are
-// (q.k) * scale with the scale applied after the dot product and masked keys
-// set to exactly -1e9, as the reference does, so a fully masked row is a
-// uniform average - the same as the reference's softmax over -1e9s.
+// Attention core on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32), flash-style.
+//
+// Workgroup = 4 waves = 64 queries of one (utterance, head); keys stream
+// through LDS in chunks of 64.  Each wave owns 16 queries and works on the
+// TRANSPOSED problem so that no register shuffles sit between the two GEMMs:
+//   S^T[key][q] = K . Q^T    A = K rows from LDS, B = Q (registers, whole loop)
+//   O^T[d][q]  += V^T . P^T  A = V^T rows from LDS, B = P^T straight from the
+//                            S^T accumulators
+// A 16x16 accumulator lane holds column q = lane&15 and rows 4*(lane>>4)+r, so
+// after S^T a lane owns keys {4g + r} of ONE query (g = lane>>4): exactly the
+// B operand of the PV product when k-step r takes keys {4g + r : g} (a fixed
+// permutation of the 16 keys, applied to V^T's reads as well).  QK^T uses the
+// k-order d = 16t + 4g + c so both operands are float4 reads.  Softmax
+// statistics are per query, i.e. per lane: the running max is reduced over
+// the 4 lane groups (2 xor-shuffles) once per 64-key chunk; the running sum
+// stays a per-lane partial until the end.
+// Scores are (q.k) * scale with masked keys set to exactly -1e9 as the
+// reference does (a fully masked row becomes a uniform average, as there);
+// keys past N get weight 0.  components.py:72-86
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int ATT_KC = 64;  // keys per LDS chunk
+
 template <int HD>
-__global__ __launch_bounds__(64) void attention_kernel(const float* __restrict__ qkv,
-                                                       const uint8_t* __restrict__ key_mask,
-                                                       int N, int H, float scale,
-                                                       float* __restrict__ out) {
-    constexpr int KC = 64;
-    __shared__ __attribute__((aligned(16))) float Ks[KC * HD];
-    __shared__ __attribute__((aligned(16))) float Vs[KC * HD];
-    __shared__ float Mk[KC];
+__global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv,
+                                                        const uint8_t* __restrict__ key_mask,
+                                                        int N, int H, float scale,
+                                                        float* __restrict__ out) {
+    static_assert(HD % 16 == 0, "head_dim must be a multiple of 16");
+    constexpr int KSTR = HD + 4;       // Ks row stride (floats)
+    constexpr int VSTR = ATT_KC + 4;   // Vt row stride
+    constexpr int NT = HD / 16;        // 16-wide d tiles
+    __shared__ __attribute__((aligned(16))) float Ks[ATT_KC * KSTR];
+    __shared__ __attribute__((aligned(16))) float Vt[HD * VSTR];
+    __shared__ float Mk[ATT_KC];
     const int b = blockIdx.z, hh = blockIdx.y;
-    const int tid = threadIdx.x;
-    const int qi = blockIdx.x * 64 + tid;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, g = lane >> 4;
     const size_t row3 = (size_t)3 * H;
-    const float* base = qkv + (size_t)b * N * row3;
-    const bool valid = qi < N;
+    const float* base = qkv + (size_t)b * N * row3 + hh * HD;
+    const int qi = blockIdx.x * 64 + wave * 16 + li;
 
-    float q[HD], o[HD];
+    float4 q[NT];
 #pragma unroll
-    for (int d = 0; d < HD; ++d) { q[d] = valid ? base[qi * row3 + hh * HD + d] : 0.f; o[d] = 0.f; }
-    float m = -INFINITY, l = 0.f;
+    for (int t = 0; t < NT; ++t)
+        q[t] = qi < N ? *reinterpret_cast<const float4*>(base + qi * row3 + 16 * t + 4 * g)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
 
-    for (int j0 = 0; j0 < N; j0 += KC) {
+    for (int j0 = 0; j0 < N; j0 += ATT_KC) {
         __syncthreads();
-        for (int i = tid; i < KC * HD; i += 64) {
-            const int key = i / HD, d = i - key * HD;
+        for (int i = tid; i < ATT_KC * (HD / 4); i += 256) {
+            const int key = i / (HD / 4), d4 = i - key * (HD / 4);
             const int j = j0 + key;
-            Ks[i] = j < N ? base[j * row3 + H + hh * HD + d] : 0.f;
-            Vs[i] = j < N ? base[j * row3 + 2 * H + hh * HD + d] : 0.f;
+            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+            if (j < N) {
+                kv = *reinterpret_cast<const float4*>(base + j * row3 + H + 4 * d4);
+                vv = *reinterpret_cast<const float4*>(base + j * row3 + 2 * H + 4 * d4);
+            }
+            *reinterpret_cast<float4*>(Ks + key * KSTR + 4 * d4) = kv;
+            Vt[(4 * d4 + 0) * VSTR + key] = vv.x;
+            Vt[(4 * d4 + 1) * VSTR + key] = vv.y;
+            Vt[(4 * d4 + 2) * VSTR + key] = vv.z;
+            Vt[(4 * d4 + 3) * VSTR + key] = vv.w;
         }
-        {
+        if (tid < ATT_KC) {
             const int j = j0 + tid;
             // 0: live key, 1: masked (score -1e9), 2: past the end (weight 0)
             Mk[tid] = j >= N ? 2.f : ((key_mask && key_mask[(size_t)b * N + j] == 0) ? 1.f : 0.f);
         }
         __syncthreads();
-        float sc[KC];
+
+        float s[4][4];  // [16-key block][r]: key 16*kb + 4*g + r of query li
         float cmax = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < KC; ++j) {
-            float dot = 0.f;
-            const float4* kr = reinterpret_cast<const float4*>(Ks + j * HD);
+        for (int kb = 0; kb < 4; ++kb) {
+            f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int d4 = 0; d4 < HD / 4; ++d4) {
-                const float4 kv = kr[d4];
-                dot = fmaf(q[4 * d4 + 0], kv.x, dot);
-                dot = fmaf(q[4 * d4 + 1], kv.y, dot);
-                dot = fmaf(q[4 * d4 + 2], kv.z, dot);
-                dot = fmaf(q[4 * d4 + 3], kv.w, dot);
+            for (int t = 0; t < NT; ++t) {
+                const float4 a = *reinterpret_cast<const float4*>(Ks + (16 * kb + li) * KSTR + 16 * t + 4 * g);
+                st = mfma16(a.x, q[t].x, st);
+                st = mfma16(a.y, q[t].y, st);
+                st = mfma16(a.z, q[t].z, st);
+                st = mfma16(a.w, q[t].w, st);
             }
-            float s = dot * scale;
-            const float mk = Mk[j];
-            s = mk == 0.f ? s : (mk == 1.f ? kMaskFill : -INFINITY);
-            sc[j] = s;
-            cmax = fmaxf(cmax, s);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float mk = Mk[16 * kb + 4 * g + r];
+                const float v = st[r] * scale;
+                s[kb][r] = mk == 0.f ? v : (mk == 1.f ? kMaskFill : -INFINITY);
+                cmax = fmaxf(cmax, s[kb][r]);
+            }
         }
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
         const float mn = fmaxf(m, cmax);
-        const float corr = expf(m - mn);  // m=-inf on the first chunk -> 0
-        l *= corr;
+        const float corr = expf(m - mn);  // m = -inf on the first chunk -> 0
+        lsum *= corr;
 #pragma unroll
-        for (int d = 0; d < HD; ++d) o[d] *= corr;
+        for (int t = 0; t < NT; ++t) acc[t] *= corr;
 #pragma unroll
-        for (int j = 0; j < KC; ++j) {
-            const float p = expf(sc[j] - mn);
-            l += p;
-            const float4* vr = reinterpret_cast<const float4*>(Vs + j * HD);
+        for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
-            for (int d4 = 0; d4 < HD / 4; ++d4) {
-                const float4 vv = vr[d4];
-                o[4 * d4 + 0] = fmaf(p, vv.x, o[4 * d4 + 0]);
-                o[4 * d4 + 1] = fmaf(p, vv.y, o[4 * d4 + 1]);
-                o[4 * d4 + 2] = fmaf(p, vv.z, o[4 * d4 + 2]);
-                o[4 * d4 + 3] = fmaf(p, vv.w, o[4 * d4 + 3]);
+            for (int r = 0; r < 4; ++r) {
+                s[kb][r] = expf(s[kb][r] - mn);
+                lsum += s[kb][r];
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float4 v = *reinterpret_cast<const float4*>(Vt + (16 * t + li) * VSTR + 16 * kb + 4 * g);
+                acc[t] = mfma16(v.x, s[kb][0], acc[t]);
+                acc[t] = mfma16(v.y, s[kb][1], acc[t]);
+                acc[t] = mfma16(v.z, s[kb][2], acc[t]);
+                acc[t] = mfma16(v.w, s[kb][3], acc[t]);
             }
         }
         m = mn;
     }
-    if (!valid) return;
-    const float inv = 1.0f / l;
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    if (qi >= N) return;
+    const float inv = 1.0f / lsum;
     float* orow = out + ((size_t)b * N + qi) * H + hh * HD;
 #pragma unroll
-    for (int d = 0; d < HD; ++d) orow[d] = o[d] * inv;
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) orow[16 * t + 4 * g + r] = acc[t][r] * inv;
 }
 
 // ---------------------------------------------------------------------------
@@ -303,12 +351,14 @@ int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, in
     const int hd = H / heads;
     if (B == 0 || N == 0) return M2_OK;
     const float scale = (float)(1.0 / std::sqrt((double)hd));  // components.py:510, fp32 at the mul
+    // float4 reads of q/k/v rows: H and the head offsets must be 16-B aligned
+    M2_CHECK_SHAPE(H % 4 == 0, "attention: hidden_dim must be a multiple of 4");
     dim3 grid(cdiv(N, 64), heads, B);
     switch (hd) {
-        case 16: hipLaunchKernelGGL(attention_kernel<16>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
-        case 32: hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
-        case 48: hipLaunchKernelGGL(attention_kernel<48>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
-        case 64: hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(64), 0, st, qkv, mask, N, H, scale, out); break;
+        case 16: hipLaunchKernelGGL(attention_kernel<16>, grid, dim3(256), 0, st, qkv, mask, N, H, scale, out); break;
+        case 32: hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(256), 0, st, qkv, mask, N, H, scale, out); break;
+        case 48: hipLaunchKernelGGL(attention_kernel<48>, grid, dim3(256), 0, st, qkv, mask, N, H, scale, out); break;
+        case 64: hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(256), 0, st, qkv, mask, N, H, scale, out); break;
         default: return fail(M2_E_SHAPE, "attention: head_dim must be 16, 32, 48 or 64");
     }
     M2_LAUNCHED("attention_kernel");
