@@ -192,6 +192,12 @@ int32_t m2_profile_read(m2_model* model, float* ms_out, int32_t capacity, int32_
 int32_t m2_profile_disable(m2_model* model);
 int32_t m2_profile_kernel_count(void);
 const char* m2_profile_kernel_name(int32_t index);
+/* The same kernel as launched by this model (symbol prefix = rocprofv3 name). */
+const char* m2_profile_kernel_name_for(const m2_model* model, int32_t index);
+/* Vocoder arithmetic of this model: 0 per-layer fp32 kernels, 1 fused exact-f32
+ * MFMA (v_mfma_f32_16x16x4_f32), 2 fused split-f16 MFMA (fp32 operands as
+ * f16 hi/lo pairs, 3 products per fp32 product, fp32 accumulation). */
+int32_t m2_vocoder_path(const m2_model* model);
 
 #ifdef __cplusplus
 }

@@ -144,6 +144,10 @@ struct m2_model {
     float* vbuf = nullptr;
     m2::VocW vw{};
     bool fused = false;
+    // split-f16 vocoder (vocoder_x3.hip): packed hi/lo weights; preferred when supported
+    void* xbuf = nullptr;
+    m2::VocX vx{};
+    bool x3 = false;
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
     mutable int prof_calls = 0;
@@ -424,6 +428,54 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
         for (size_t i = 0; i < parts.size(); ++i) *slots[i] = m->vbuf + offs[i];
         m->vw.wo = m->vout_w;
         m->vw.bo = m->vout_b;
+
+        // Split-f16 packs (default path when the shapes are supported and every
+        // weight is inside the f16 range; M2_VOC_F32=1 keeps the exact-f32 MFMA).
+        if (vocoder_x3_supported(M, C) && !std::getenv("M2_VOC_F32")) {
+            bool ok = true;
+            std::vector<std::vector<uint16_t>> xp;
+            std::vector<const vx_u32x4**> xs;
+            xp.push_back(pack_x3_conv3(wi.data(), C, M, vocoder_x3_mel_pad(M), &ok));
+            xs.push_back(&m->vx.wi);
+            int c2 = C;
+            for (int k = 0; k < 4; ++k) {
+                const std::string u = "vocoder.upsamples." + std::to_string(k);
+                const std::string r = "vocoder.resblocks." + std::to_string(k);
+                auto wt = fetch(u + ".weight");
+                xp.push_back(pack_x3_convT(wt.data(), c2, c2 / 2, kRates[k], &ok));
+                xs.push_back(&m->vx.wt[k]);
+                c2 /= 2;
+                auto w1 = fetch(r + ".conv1.weight");
+                xp.push_back(pack_x3_conv3(w1.data(), c2, c2, c2, &ok));
+                xs.push_back(&m->vx.w1[k]);
+                auto w2 = fetch(r + ".conv2.weight");
+                xp.push_back(pack_x3_conv3(w2.data(), c2, c2, c2, &ok));
+                xs.push_back(&m->vx.w2[k]);
+            }
+            if (ok) {
+                size_t xt = 0;
+                std::vector<size_t> xo;
+                for (auto& v : xp) { xt = align_up(xt, 128); xo.push_back(xt); xt += v.size(); }
+                std::vector<uint16_t> hx(xt, 0);
+                for (size_t i = 0; i < xp.size(); ++i) std::copy(xp[i].begin(), xp[i].end(), hx.begin() + xo[i]);
+                e = hipMalloc(&m->xbuf, std::max<size_t>(xt, 1) * sizeof(uint16_t));
+                if (e != hipSuccess) { (void)hipFree(m->vbuf); return bail(e, "hipMalloc(x3 pack)"); }
+                e = hipMemcpyAsync(m->xbuf, hx.data(), xt * sizeof(uint16_t), hipMemcpyHostToDevice, st);
+                if (e == hipSuccess) e = hipStreamSynchronize(st);
+                if (e != hipSuccess) { (void)hipFree(m->vbuf); (void)hipFree(m->xbuf); return bail(e, "upload x3 pack"); }
+                for (size_t i = 0; i < xp.size(); ++i)
+                    *xs[i] = reinterpret_cast<const vx_u32x4*>(static_cast<uint16_t*>(m->xbuf) + xo[i]);
+                m->vx.bi = m->vw.bi;
+                for (int k = 0; k < 4; ++k) {
+                    m->vx.bt[k] = m->vw.bt[k];
+                    m->vx.b1[k] = m->vw.b1[k];
+                    m->vx.b2[k] = m->vw.b2[k];
+                }
+                m->vx.wo = m->vw.wo;
+                m->vx.bo = m->vw.bo;
+                m->x3 = true;
+            }
+        }
     }
     *out = m;
     return M2_OK;
@@ -435,6 +487,7 @@ int32_t m2_model_destroy(m2_model* model) {
     if (!model) return M2_OK;
     m2_profile_disable(model);
     if (model->vbuf) (void)hipFree(model->vbuf);
+    if (model->xbuf) (void)hipFree(model->xbuf);
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -543,6 +596,9 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
             const size_t slot = (size_t)call * kVocKernels + kidx;
             (void)hipEventRecord(begin ? m->prof_begin[slot] : m->prof_end[slot], st);
         };
+        if (m->x3)
+            return launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vx,
+                                     buf[0], buf[1], out_audio, st, mark);
         return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vw,
                                     buf[0], buf[1], out_audio, st, mark);
     }
@@ -627,6 +683,16 @@ int32_t m2_profile_kernel_count(void) { return kVocKernels; }
 
 const char* m2_profile_kernel_name(int32_t index) {
     return (index >= 0 && index < kVocKernels) ? kVocKernelNames[index] : "";
+}
+
+const char* m2_profile_kernel_name_for(const m2_model* m, int32_t index) {
+    if (!m || index < 0 || index >= kVocKernels) return "";
+    return m->x3 ? kVocX3KernelNames[index] : kVocKernelNames[index];
+}
+
+int32_t m2_vocoder_path(const m2_model* m) {
+    if (!m) return -1;
+    return m->x3 ? 2 : (m->fused ? 1 : 0);
 }
 
 int32_t m2_profile_enable(m2_model* m, int32_t capacity) {

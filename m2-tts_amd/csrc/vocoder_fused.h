@@ -1,5 +1,6 @@
 // Fused vocoder: packed-weight table and launcher (vocoder_fused.hip).
 #pragma once
+#include <cstdint>
 #include <functional>
 #include <vector>
 
@@ -24,6 +25,7 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
 
 constexpr int kVocKernels = 3;
 extern const char* const kVocKernelNames[kVocKernels];
+extern const char* const kVocX3KernelNames[kVocKernels];
 
 // Host-side packing into A-fragment order for v_mfma_f32_16x16x4_f32, k-steps
 // padded to KSP = roundup(KS, 4), layout [mb][s/4][lane][s%4] holding
@@ -32,5 +34,31 @@ extern const char* const kVocKernelNames[kVocKernels];
 // convT:  per phase ph, A[co][tap*Cin + ci] = W[ci][co][k_tap(ph)]   (W: [Cin][Cout][2R])
 std::vector<float> pack_conv3(const float* W, int Cout, int Cin);
 std::vector<float> pack_convT(const float* W, int Cin, int Cout, int R);
+
+// ---------------------------------------------------------------------------
+// Split-f16 vocoder (vocoder_x3.hip): conv / convT weights packed as f16
+// hi/lo pairs in v_mfma_f32_16x16x32_f16 A-fragment order; biases and the
+// output conv stay fp32.
+typedef unsigned int vx_u32x4 __attribute__((ext_vector_type(4)));
+struct VocX {
+    const vx_u32x4* wi;
+    const float* bi;
+    const vx_u32x4* wt[4];
+    const float* bt[4];
+    const vx_u32x4* w1[4];
+    const float* b1[4];
+    const vx_u32x4* w2[4];
+    const float* b2[4];
+    const float *wo, *bo;
+};
+
+bool vocoder_x3_supported(int M, int C);
+int vocoder_x3_mel_pad(int M);  // input-conv channel count after padding to the k-block layout
+// U1/U2: workspace for the intermediates (same bytes as fp32 [B][C/2][4T] / [B][C/4][16T]).
+int32_t launch_vocoder_x3(const float* mel, bool trans, int M, int C, int B, int T, const VocX& w, void* U1, void* U2,
+                          float* audio, hipStream_t st, const std::function<void(int, bool)>& mark);
+// range_ok is cleared when a weight is outside the f16 range (|w| >= 65504).
+std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPad, bool* range_ok);
+std::vector<uint16_t> pack_x3_convT(const float* W, int Cin, int Cout, int R, bool* range_ok);
 
 }  // namespace m2

@@ -1,0 +1,557 @@
+// Fused SimpleVocoder on the f16 MFMA with a three-product split (gfx950).
+//
+// Same three launches and the same exact-halo windows as vocoder_fused.hip
+// (head: input_conv -> ConvT1 -> ResBlock1, mid: ConvT2 -> ResBlock2, tail:
+// ConvT3 -> ResBlock3 -> ConvT4 -> ResBlock4 -> output_conv -> tanh), but the
+// GEMMs run on v_mfma_f32_16x16x32_f16 (16 cycles for 16K FLOP, 16x the
+// FLOP rate of the f32 MFMA) with every fp32 operand x carried as two halves
+//     x_hi = f16(x),  x_lo = f16((x - x_hi) * 2^11)
+// and every product as
+//     a.b ~= a_hi.b_hi + (a_hi.b_lo + a_lo.b_hi) * 2^-11
+// accumulated in fp32 (two accumulators per tile, combined in the epilogue).
+// The dropped a_lo.b_lo term is 2^-22 relative, and each half-product is
+// exact in the fp32 accumulator, so the result carries fp32-level error:
+// simulated over the whole stage1/stage2 vocoder (tools/probe/split_sim.py)
+// the waveform RMS error vs fp64 is 1.6e-7 against 1.5e-7 for plain fp32
+// convolution (plain f16 operands: 3.1e-4, outside the 1e-4 bound).  Three
+// MFMAs per product leave 16/3 = 5.3x the exact-f32 MFMA rate.  Range: |x| and
+// |w| must stay below 65504 (f16 max); weights are checked at model creation.
+//
+// Data layout.  Activations live position-major: one row per position holding
+// hi[C] then lo[C] (f16), rows padded to a stride RS with RS/16 = 2 (mod 4) so
+// the 16-lane groups of a ds_read_b128 hit 16 distinct 16-B bank quads.  An
+// MFMA B fragment (lane = position j, 8 consecutive channels of one tap) is
+// one ds_read_b128 for the hi half and one for the lo half.  The global
+// intermediates U1 [B][4T] and U2 [B][16T] use the same row format (4*C
+// bytes per position, the bytes of an fp32 tensor), so the next kernel copies
+// rows without converting.  Weights are packed per (phase, m-block, k-block of
+// 32) as [hi|lo][lane][8 halves]: two global_load_dwordx4 per lane.
+// K order: k-block kb, lane group g = lane>>4 covers octet o = 4kb+g of the
+// (tap, channel/8) sequence; any k order shared by A and B gives the same sum.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+
+#include "m2_common.h"
+#include "vocoder_fused.h"
+
+namespace m2 {
+namespace x3 {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef vx_u32x4 u32x4;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr float kLoS = 2048.f, kLoI = 1.f / 2048.f;
+
+__device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+// Row stride in bytes for C channels: >= 4C, multiple of 16, (RS/16) % 4 == 2
+// (C = 8: 32 B, 2-way conflicts between rows 8 apart are accepted).
+constexpr int rs_for(int C) {
+    int u = (4 * C + 15) / 16;
+    if (C <= 8) return u * 16;
+    while (u % 4 != 2) ++u;
+    return u * 16;
+}
+constexpr int rup16(int n) { return (n + 15) / 16 * 16; }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// An LDS activation window: rows of RS bytes, absolute position of row 0.
+struct XW {
+    unsigned char* p;
+    int start;
+};
+
+__device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const _Float16 h = (_Float16)v[r];
+        hi[r] = h;
+        lo[r] = (_Float16)((v[r] - (float)h) * kLoS);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// acc[n] += A_hi.B_hi, cor[n] += A_hi.B_lo + A_lo.B_hi over all k-blocks, for
+// NT 16-position tiles.  wp: this lane's A slot of k-block 0 (u32x4 units,
+// k-block stride 128 = hi + lo).  bp: LDS row of this lane's position for
+// tap 0 and k-block 0, before the lane-group offset.  Tap k reads row
+// bp + k*STEP (STEP = +1 for conv3 [t-1, t, t+1], -1 for the ConvT taps).
+template <int CIN, int NTAP, int STEP, int RSI, int NT>
+__device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp, int nt,
+                                       f32x4 (&acc)[NT], f32x4 (&cor)[NT]) {
+    constexpr int NOCT = CIN / 8, NK = NTAP * NOCT, NKB = (NK + 3) / 4;
+    static_assert(CIN % 8 == 0 && (NOCT <= 2 || NOCT % 4 == 0), "channel count must be 8, 16 or a multiple of 32");
+    constexpr int Q = NOCT >= 4 ? 4 : NOCT;  // lane groups per tap row
+    const int g = (threadIdx.x & 63) >> 4;
+    const unsigned char* bl = bp + (g / Q) * STEP * RSI + (g % Q) * 16;
+    // Padding octets of the last k-block (zero weights) re-read octet 0's
+    // bytes: always inside the window and finite.
+    const unsigned char* bl_last = (4 * (NKB - 1) + g < NK) ? bl : bp;
+    u32x4 a[2][2];
+    a[0][0] = wp[0];
+    a[0][1] = wp[64];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        if (kb + 1 < NKB) {
+            a[(kb + 1) & 1][0] = wp[(kb + 1) * 128];
+            a[(kb + 1) & 1][1] = wp[(kb + 1) * 128 + 64];
+        }
+        constexpr int TPK = NOCT >= 4 ? 0 : 4 / Q;  // taps per k-block when a tap row has < 4 octets
+        const int tap = NOCT >= 4 ? kb / (NOCT / 4) : kb * TPK;
+        const int col = NOCT >= 4 ? (kb % (NOCT / 4)) * 64 : 0;
+        const unsigned char* b0 = (kb == NKB - 1 ? bl_last : bl) + tap * STEP * RSI + col;
+        u32x4 bh[NT], blo[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (n < nt) {
+                bh[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI);
+                blo[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (n < nt) {
+                acc[n] = mfma_h(a[kb & 1][0], bh[n], acc[n]);
+                cor[n] = mfma_h(a[kb & 1][0], blo[n], cor[n]);
+                cor[n] = mfma_h(a[kb & 1][1], bh[n], cor[n]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int CIN, int NTAP>
+constexpr int nkb() { return (NTAP * (CIN / 8) + 3) / 4; }
+
+// Epilogue for one tile: v = act(acc + cor*2^-11 + bias) [+ residual], 0
+// outside [0, L), split and stored as hi/lo at row `t`.
+template <int COUT, int RSO, int ACT, bool RES>
+__device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, const float (&bv)[4], XW out, int t,
+                                           int co0, int L) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[r] + cor[r] * kLoI + bv[r]);
+    unsigned char* row = out.p + (t - out.start) * RSO + co0 * 2;
+    if (RES) {
+        const h4 hi = *reinterpret_cast<const h4*>(row), lo = *reinterpret_cast<const h4*>(row + 2 * COUT);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)hi[r] + (float)lo[r] * kLoI;
+    }
+    if (t < 0 || t >= L) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = 0.f;
+    }
+    h4 hi, lo;
+    split4(v, hi, lo);
+    *reinterpret_cast<h4*>(row) = hi;
+    *reinterpret_cast<h4*>(row + 2 * COUT) = lo;
+}
+
+// Conv1d(k=3, pad=1): abs positions [a0, a0+npos) of `out` from `in`.
+template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO>
+__device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
+                                       int a0, int npos, int L) {
+    constexpr int MB = (COUT + 15) / 16, NKB = nkb<CIN, 3>();
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    const int ntiles = (npos + 15) >> 4, nch = (ntiles + NT - 1) / NT;
+    const int nw = blockDim.x >> 6;
+#pragma unroll 1
+    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < MB * nch; item += nw) {
+        const int mb = item % MB, tile0 = (item / MB) * NT;
+        const int nt = min(NT, ntiles - tile0);
+        const int co0 = mb * 16 + 4 * g;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = co0 + r < COUT ? bias[co0 + r] : 0.f;
+        f32x4 acc[NT], cor[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = cor[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma_x3<CIN, 3, 1, RSI, NT>(Wp + (size_t)mb * NKB * 128 + lane,
+                                   in.p + (a0 + tile0 * 16 + li - 1 - in.start) * RSI, nt, acc, cor);
+        if (co0 < COUT) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int j = (tile0 + n) * 16 + li;
+                if (n < nt && j < npos) store_tile<COUT, RSO, ACT, RES>(acc[n], cor[n], bv, out, a0 + j, co0, L);
+            }
+        }
+    }
+}
+
+// leaky(ConvTranspose1d(k=2R, stride R, pad R/2)): inputs q in [q0, q0+nq)
+// give outputs t = q*R + ph.  Phase ph reads taps (q, q-1) if ph + R/2 < R,
+// else (q+1, q): B base row q + d0, tap k at row q + d0 - k.
+template <int CIN, int COUT, int R, int NT, int RSI, int RSO>
+__device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
+                                       int q0, int nq, int L) {
+    constexpr int MB = (COUT + 15) / 16, NKB = nkb<CIN, 2>(), PAD = R / 2;
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    const int ntiles = (nq + 15) >> 4, nch = (ntiles + NT - 1) / NT;
+    const int nw = blockDim.x >> 6;
+#pragma unroll 1
+    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < R * MB * nch; item += nw) {
+        const int ph = item % R, rest = item / R;
+        const int mb = rest % MB, tile0 = (rest / MB) * NT;
+        const int nt = min(NT, ntiles - tile0);
+        const int d0 = (ph + PAD < R) ? 0 : 1;
+        const int co0 = mb * 16 + 4 * g;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = co0 + r < COUT ? bias[co0 + r] : 0.f;
+        f32x4 acc[NT], cor[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = cor[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma_x3<CIN, 2, -1, RSI, NT>(Wp + (size_t)(ph * MB + mb) * NKB * 128 + lane,
+                                    in.p + (q0 + tile0 * 16 + li + d0 - in.start) * RSI, nt, acc, cor);
+        if (co0 < COUT) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int j = (tile0 + n) * 16 + li;
+                if (n < nt && j < nq)
+                    store_tile<COUT, RSO, ACT_LEAKY, false>(acc[n], cor[n], bv, out, (q0 + j) * R + ph, co0, L);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Global <-> LDS.
+// mel -> window rows [0, n) (abs start + r), MP channels (zero past M).
+template <bool TRANS, int M, int MP, int RS>
+__device__ __forceinline__ void gload_mel(const float* __restrict__ g, int T, XW dst, int n) {
+    if (TRANS) {  // [T][M]: a row of M contiguous floats per frame
+        constexpr int C4 = MP / 4;
+        for (int i = threadIdx.x; i < n * C4; i += blockDim.x) {
+            const int r = i / C4, c = (i - r * C4) * 4, t = dst.start + r;
+            float v[4] = {0.f, 0.f, 0.f, 0.f};
+            if (t >= 0 && t < T && c < M) {
+                const float4 x = *reinterpret_cast<const float4*>(g + (size_t)t * M + c);
+                v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+            }
+            h4 hi, lo;
+            split4(v, hi, lo);
+            unsigned char* row = dst.p + r * RS + c * 2;
+            *reinterpret_cast<h4*>(row) = hi;
+            *reinterpret_cast<h4*>(row + 2 * MP) = lo;
+        }
+    } else {  // [M][T]: consecutive threads read consecutive frames of one channel
+        for (int i = threadIdx.x; i < n * MP; i += blockDim.x) {
+            const int c = i / n, r = i - c * n, t = dst.start + r;
+            const float x = (t >= 0 && t < T && c < M) ? g[(size_t)c * T + t] : 0.f;
+            const _Float16 h = (_Float16)x;
+            _Float16* row = reinterpret_cast<_Float16*>(dst.p + r * RS);
+            row[c] = h;
+            row[MP + c] = (_Float16)((x - (float)h) * kLoS);
+        }
+    }
+}
+
+// rows of 4C bytes (hi|lo) at global positions [start, start+n), zero outside [0, Lg)
+template <int C, int RS>
+__device__ __forceinline__ void gload_rows(const unsigned char* __restrict__ g, int Lg, XW dst, int n) {
+    constexpr int Q = C / 4;  // 16-B chunks per row
+    for (int i = threadIdx.x; i < n * Q; i += blockDim.x) {
+        const int r = i / Q, q = i - r * Q, t = dst.start + r;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (t >= 0 && t < Lg) v = *reinterpret_cast<const u32x4*>(g + (size_t)t * 4 * C + q * 16);
+        *reinterpret_cast<u32x4*>(dst.p + r * RS + q * 16) = v;
+    }
+}
+
+template <int C, int RS>
+__device__ __forceinline__ void gstore_rows(unsigned char* __restrict__ g, int Lg, XW src, int a0, int n) {
+    constexpr int Q = C / 4;
+    for (int i = threadIdx.x; i < n * Q; i += blockDim.x) {
+        const int r = i / Q, q = i - r * Q, t = a0 + r;
+        if (t < Lg)
+            *reinterpret_cast<u32x4*>(g + (size_t)t * 4 * C + q * 16) =
+                *reinterpret_cast<const u32x4*>(src.p + (t - src.start) * RS + q * 16);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Window plans (rows; the same receptive-field arithmetic as the f32 plans).
+template <int MP, int C, int TF>
+struct HeadPlan {
+    static constexpr int C1 = C / 2;
+    static constexpr int RS_M = rs_for(MP), RS_C = rs_for(C), RS_1 = rs_for(C1);
+    static constexpr int MEL_N = TF + 6, A0_N = TF + 4, NQ = TF + 2, H_N = 4 * TF + 2, O_N = 4 * TF;
+    static constexpr int CAP_MEL = cmax(MEL_N, rup16(A0_N) + 2);
+    static constexpr int CAP_A0 = cmax(A0_N, rup16(NQ) + 2);
+    static constexpr int CAP_U = cmax(4 * NQ, rup16(H_N) + 4);
+    static constexpr int CAP_H = cmax(H_N, rup16(O_N) + 2);
+    static constexpr int R0 = cmax(CAP_MEL * RS_M + CAP_A0 * RS_C, CAP_H * RS_1);
+    static constexpr int LDS_BYTES = R0 + CAP_U * RS_1;
+};
+
+template <int CI, int W>
+struct MidPlan {
+    static constexpr int CO = CI / 2;
+    static constexpr int RS_I = rs_for(CI), RS_O = rs_for(CO);
+    static constexpr int IN_N = W + 4, NQ = W + 2, H_N = 4 * W + 2, O_N = 4 * W;
+    static constexpr int CAP_IN = cmax(IN_N, rup16(NQ) + 2);
+    static constexpr int CAP_U = cmax(4 * NQ, rup16(H_N) + 4);
+    static constexpr int CAP_H = cmax(H_N, rup16(O_N) + 2);
+    static constexpr int R0 = cmax(CAP_IN * RS_I, CAP_H * RS_O);
+    static constexpr int LDS_BYTES = R0 + CAP_U * RS_O;
+};
+
+template <int CI, int W>
+struct TailPlan {
+    static constexpr int C3 = CI / 2, C4 = CI / 4;
+    static constexpr int RS_I = rs_for(CI), RS_3 = rs_for(C3), RS_4 = rs_for(C4);
+    static constexpr int IN_N = W + 8, NQ3 = W + 6, H3_N = 2 * W + 8, O3_N = 2 * W + 6;
+    static constexpr int NQ4 = 2 * W + 4, H4_N = 4 * W + 4, O4_N = 4 * W + 2, A_N = 4 * W;
+    static constexpr int CAP_IN = cmax(IN_N, rup16(NQ3) + 2);
+    static constexpr int CAP_U3 = cmax(2 * NQ3, cmax(rup16(H3_N) + 3, rup16(NQ4) + 5));
+    static constexpr int CAP_H3 = cmax(H3_N, rup16(O3_N) + 2);
+    static constexpr int CAP_U4 = cmax(2 * NQ4, rup16(H4_N) + 3);
+    static constexpr int CAP_H4 = cmax(H4_N, rup16(O4_N) + 2);
+    static constexpr int RA = cmax(CAP_IN * RS_I, cmax(CAP_H3 * RS_3, CAP_U4 * RS_4));
+    static constexpr int RB = cmax(CAP_U3 * RS_3, CAP_H4 * RS_4);
+    static constexpr int LDS_BYTES = RA + RB;
+};
+
+// Tilings: WAVES per workgroup, NT_* tiles per work item, MINW launch bound.
+struct CfgS1 {
+    static constexpr int M = 64, MP = 64, C = 128, TF = 28, W2 = 60, W3 = 192, WAVES = 8, MINW = 2;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+};
+struct CfgS2 {
+    static constexpr int M = 80, MP = 96, C = 256, TF = 12, W2 = 28, W3 = 120, WAVES = 8, MINW = 2;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+};
+
+template <class Cfg, bool TRANS>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_head_kernel(const float* __restrict__ mel, int T,
+                                                                            VocX w, unsigned char* __restrict__ U1) {
+    constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
+    using Pl = HeadPlan<MP, C, TF>;
+    constexpr int C1 = Pl::C1;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int b = blockIdx.y, f0 = blockIdx.x * TF;
+    XW melw{lds, f0 - 3};
+    XW a0w{lds + Pl::CAP_MEL * Pl::RS_M, f0 - 2};
+    XW hw{lds, 4 * f0 - 1};
+    XW uw{lds + Pl::R0, 4 * f0 - 4};
+    gload_mel<TRANS, M, MP, Pl::RS_M>(mel + (size_t)b * M * T, T, melw, Pl::MEL_N);
+    __syncthreads();
+    xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T);
+    __syncthreads();
+    xconvT<C, C1, 4, Cfg::NT_T1, Pl::RS_C, Pl::RS_1>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T);
+    __syncthreads();
+    xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, Pl::H_N,
+                                                                     4 * T);
+    __syncthreads();
+    xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1>(w.w2[0], w.b2[0], hw, uw, 4 * f0, Pl::O_N, 4 * T);
+    __syncthreads();
+    gstore_rows<C1, Pl::RS_1>(U1 + (size_t)b * 4 * T * 4 * C1, 4 * T, uw, 4 * f0, Pl::O_N);
+}
+
+template <class Cfg>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_mid_kernel(const unsigned char* __restrict__ U1,
+                                                                           int L1, VocX w,
+                                                                           unsigned char* __restrict__ U2) {
+    constexpr int CI = Cfg::C / 2, W = Cfg::W2;
+    using Pl = MidPlan<CI, W>;
+    constexpr int CO = Pl::CO;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int b = blockIdx.y, p0 = blockIdx.x * W;
+    const int L2 = 4 * L1;
+    XW inw{lds, p0 - 2};
+    XW hw{lds, 4 * p0 - 1};
+    XW uw{lds + Pl::R0, 4 * p0 - 4};
+    gload_rows<CI, Pl::RS_I>(U1 + (size_t)b * L1 * 4 * CI, L1, inw, Pl::IN_N);
+    __syncthreads();
+    xconvT<CI, CO, 4, Cfg::NT_T2, Pl::RS_I, Pl::RS_O>(w.wt[1], w.bt[1], inw, uw, p0 - 1, Pl::NQ, L2);
+    __syncthreads();
+    xconv3<CO, CO, Cfg::NT_R2, ACT_LEAKY, false, Pl::RS_O, Pl::RS_O>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, Pl::H_N,
+                                                                     L2);
+    __syncthreads();
+    xconv3<CO, CO, Cfg::NT_R2, ACT_NONE, true, Pl::RS_O, Pl::RS_O>(w.w2[1], w.b2[1], hw, uw, 4 * p0, Pl::O_N, L2);
+    __syncthreads();
+    gstore_rows<CO, Pl::RS_O>(U2 + (size_t)b * L2 * 4 * CO, L2, uw, 4 * p0, Pl::O_N);
+}
+
+template <class Cfg>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_tail_kernel(const unsigned char* __restrict__ U2,
+                                                                            int L2, VocX w,
+                                                                            float* __restrict__ audio) {
+    constexpr int CI = Cfg::C / 4, W = Cfg::W3;
+    using Pl = TailPlan<CI, W>;
+    constexpr int C3 = Pl::C3, C4 = Pl::C4;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int b = blockIdx.y, p0 = blockIdx.x * W;
+    const int L3 = 2 * L2, L4 = 4 * L2;
+    unsigned char* ra = lds;
+    unsigned char* rb = lds + Pl::RA;
+    XW inw{ra, p0 - 4};
+    XW u3{rb, 2 * p0 - 6};
+    XW h3{ra, 2 * p0 - 4};
+    XW u4{ra, 4 * p0 - 4};
+    XW h4w{rb, 4 * p0 - 2};
+    gload_rows<CI, Pl::RS_I>(U2 + (size_t)b * L2 * 4 * CI, L2, inw, Pl::IN_N);
+    __syncthreads();
+    xconvT<CI, C3, 2, Cfg::NT_T3, Pl::RS_I, Pl::RS_3>(w.wt[2], w.bt[2], inw, u3, p0 - 3, Pl::NQ3, L3);
+    __syncthreads();
+    xconv3<C3, C3, Cfg::NT_R3, ACT_LEAKY, false, Pl::RS_3, Pl::RS_3>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, Pl::H3_N,
+                                                                     L3);
+    __syncthreads();
+    xconv3<C3, C3, Cfg::NT_R3, ACT_NONE, true, Pl::RS_3, Pl::RS_3>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, Pl::O3_N, L3);
+    __syncthreads();
+    xconvT<C3, C4, 2, Cfg::NT_T4, Pl::RS_3, Pl::RS_4>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4);
+    __syncthreads();
+    xconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::RS_4, Pl::RS_4>(w.w1[3], w.b1[3], u4, h4w, 4 * p0 - 2, Pl::H4_N,
+                                                                     L4);
+    __syncthreads();
+    xconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::RS_4, Pl::RS_4>(w.w2[3], w.b2[3], h4w, u4, 4 * p0 - 1, Pl::O4_N, L4);
+    __syncthreads();
+    // output_conv (C4 -> 1, k3) + tanh on the VALU, one sample per thread.
+    float* arow = audio + (size_t)b * L4;
+    const float bo = w.bo[0];
+    for (int j = threadIdx.x; j < Pl::A_N; j += blockDim.x) {
+        const int t = 4 * p0 + j;
+        if (t < L4) {
+            const unsigned char* x = u4.p + (t - 1 - u4.start) * Pl::RS_4;
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const _Float16* hr = reinterpret_cast<const _Float16*>(x + k * Pl::RS_4);
+#pragma unroll
+                for (int ci = 0; ci < C4; ++ci)
+                    acc = fmaf(w.wo[ci * 3 + k], (float)hr[ci] + (float)hr[C4 + ci] * kLoI, acc);
+            }
+            arow[t] = tanhf(acc + bo);
+        }
+    }
+}
+
+template <typename K>
+int32_t set_lds(K kernel, size_t bytes) {
+    M2_CHECK_SHAPE(bytes <= 160 * 1024, "x3 vocoder: LDS plan exceeds 160 KiB");
+    M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes));
+    return M2_OK;
+}
+
+template <class Cfg>
+int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1, void* U2, float* audio,
+            hipStream_t st, const std::function<void(int, bool)>& mark) {
+    using HP = HeadPlan<Cfg::MP, Cfg::C, Cfg::TF>;
+    using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
+    using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
+    constexpr int threads = Cfg::WAVES * 64;
+    static bool attr = false;
+    if (!attr) {
+        int32_t rc;
+        if ((rc = set_lds(x3_head_kernel<Cfg, false>, HP::LDS_BYTES))) return rc;
+        if ((rc = set_lds(x3_head_kernel<Cfg, true>, HP::LDS_BYTES))) return rc;
+        if ((rc = set_lds(x3_mid_kernel<Cfg>, MP::LDS_BYTES))) return rc;
+        if ((rc = set_lds(x3_tail_kernel<Cfg>, TP::LDS_BYTES))) return rc;
+        attr = true;
+    }
+    auto* u1 = static_cast<unsigned char*>(U1);
+    auto* u2 = static_cast<unsigned char*>(U2);
+    mark(0, true);
+    if (trans)
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, true>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_BYTES, st,
+                           mel, T, w, u1);
+    else
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, false>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_BYTES, st,
+                           mel, T, w, u1);
+    mark(0, false);
+    M2_LAUNCHED("x3_head_kernel");
+    mark(1, true);
+    hipLaunchKernelGGL((x3_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(threads), MP::LDS_BYTES, st, u1,
+                       4 * T, w, u2);
+    mark(1, false);
+    M2_LAUNCHED("x3_mid_kernel");
+    mark(2, true);
+    hipLaunchKernelGGL((x3_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(threads), TP::LDS_BYTES, st, u2,
+                       16 * T, w, audio);
+    mark(2, false);
+    M2_LAUNCHED("x3_tail_kernel");
+    return M2_OK;
+}
+
+}  // namespace x3
+
+const char* const kVocX3KernelNames[kVocKernels] = {
+    "x3_head_kernel (input_conv + ConvT1 + ResBlock1)",
+    "x3_mid_kernel (ConvT2 + ResBlock2)",
+    "x3_tail_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv)"};
+
+bool vocoder_x3_supported(int M, int C) { return (M == 64 && C == 128) || (M == 80 && C == 256); }
+
+int vocoder_x3_mel_pad(int M) { return M == 80 ? 96 : M; }
+
+int32_t launch_vocoder_x3(const float* mel, bool trans, int M, int C, int B, int T, const VocX& w, void* U1, void* U2,
+                          float* audio, hipStream_t st, const std::function<void(int, bool)>& mark) {
+    if (B == 0 || T == 0) return M2_OK;
+    if (M == 64 && C == 128) return x3::run<x3::CfgS1>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (M == 80 && C == 256) return x3::run<x3::CfgS2>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    return fail(M2_E_SHAPE, "x3 vocoder: unsupported (mel_channels, vocoder_channels)");
+}
+
+// ---------------------------------------------------------------------------
+// Host packing: [group = phase*MB + mb][kb][hi|lo][lane][8 halves] with
+// A[co = mb*16 + (lane&15)][octet o = 4kb + (lane>>4), element e] =
+// W(ph, co, ci = (o % NOCT)*8 + e, tap = o / NOCT); zero for co >= Cout or o >= NK.
+namespace {
+void put(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) {
+    if (!(std::fabs(v) < 65504.f)) *range_ok = false;
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)((v - (float)h) * 2048.f);
+    uint16_t hb, lb;
+    std::memcpy(&hb, &h, 2);
+    std::memcpy(&lb, &l, 2);
+    out[idx] = hb;
+    out[idx + 64 * 8] = lb;
+}
+
+template <typename Wf>
+std::vector<uint16_t> pack_x3(int NPH, int Cout, int Cin, int NTAP, Wf W, bool* range_ok) {
+    const int MB = (Cout + 15) / 16, NOCT = Cin / 8, NK = NTAP * NOCT, NKB = (NK + 3) / 4;
+    std::vector<uint16_t> out((size_t)NPH * MB * NKB * 2 * 64 * 8, 0);
+    for (int ph = 0; ph < NPH; ++ph)
+        for (int mb = 0; mb < MB; ++mb)
+            for (int kb = 0; kb < NKB; ++kb)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int co = mb * 16 + (lane & 15), o = 4 * kb + (lane >> 4);
+                    if (co >= Cout || o >= NK) continue;
+                    const int tap = o / NOCT;
+                    for (int e = 0; e < 8; ++e) {
+                        const int ci = (o % NOCT) * 8 + e;
+                        const size_t idx = ((((size_t)(ph * MB + mb) * NKB + kb) * 2) * 64 + lane) * 8 + e;
+                        put(out, idx, W(ph, co, ci, tap), range_ok);
+                    }
+                }
+    return out;
+}
+}  // namespace
+
+std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPad, bool* range_ok) {
+    return pack_x3(1, Cout, CinPad, 3,
+                   [&](int, int co, int ci, int tap) { return ci < Cin ? W[((size_t)co * Cin + ci) * 3 + tap] : 0.f; },
+                   range_ok);
+}
+
+std::vector<uint16_t> pack_x3_convT(const float* W, int Cin, int Cout, int R, bool* range_ok) {
+    const int P = R / 2;
+    return pack_x3(R, Cout, Cin, 2,
+                   [&](int ph, int co, int ci, int tap) {
+                       const int k0 = (ph + P < R) ? ph + P : ph + P - R;  // tap 0: x[q] or x[q+1]
+                       const int k1 = (ph + P < R) ? ph + P + R : ph + P;  // tap 1: x[q-1] or x[q]
+                       return W[((size_t)ci * Cout + co) * 2 * R + (tap ? k1 : k0)];
+                   },
+                   range_ok);
+}
+
+}  // namespace m2

@@ -58,6 +58,8 @@ _SIGNATURES = {
     "m2_profile_disable": (c_i32, [c_vp]),
     "m2_profile_kernel_count": (c_i32, []),
     "m2_profile_kernel_name": (ctypes.c_char_p, [c_i32]),
+    "m2_profile_kernel_name_for": (ctypes.c_char_p, [c_vp, c_i32]),
+    "m2_vocoder_path": (c_i32, [c_vp]),
 }
 
 # act codes (m2_common.h Act)

@@ -28,7 +28,7 @@ def main():
     model = bench.fixture_model(dev)
     hm = model._hip(dev)
     nk = lib.m2_profile_kernel_count()
-    print("B, " + ", ".join(lib.m2_profile_kernel_name(i).decode().split()[0] for i in range(nk)) + ", total_ms")
+    print("B, " + ", ".join(lib.m2_profile_kernel_name_for(hm.handle, i).decode().split()[0] for i in range(nk)) + ", total_ms")
     for B in [int(x) for x in a.batches.split(",")]:
         mel = torch.randn(B, 64, a.frames, device=dev)
         for _ in range(3):
