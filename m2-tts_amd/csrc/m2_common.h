@@ -52,7 +52,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 
 template <int ACT>
 __device__ __forceinline__ float act_t(float v) {
-    if constexpr (ACT == ACT_LEAKY) return v > 0.f ? v : v * kLeaky;
+    if constexpr (ACT == ACT_LEAKY) return fmaxf(v, v * kLeaky);  // == (v > 0 ? v : 0.1v) for 0 < slope < 1
     else if constexpr (ACT == ACT_TANH) return tanhf(v);
     else if constexpr (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
     else return v;

@@ -435,7 +435,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             bool ok = true;
             std::vector<std::vector<uint16_t>> xp;
             std::vector<const vx_u32x4**> xs;
-            xp.push_back(pack_x3_conv3(wi.data(), C, M, vocoder_x3_mel_pad(M), &ok));
+            xp.push_back(pack_x3_conv3(wi.data(), C, M, vocoder_x3_mel_pad(M), &ok, false));
             xs.push_back(&m->vx.wi);
             int c2 = C;
             for (int k = 0; k < 4; ++k) {
@@ -446,10 +446,10 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 xs.push_back(&m->vx.wt[k]);
                 c2 /= 2;
                 auto w1 = fetch(r + ".conv1.weight");
-                xp.push_back(pack_x3_conv3(w1.data(), c2, c2, c2, &ok));
+                xp.push_back(pack_x3_conv3(w1.data(), c2, c2, c2, &ok, false));
                 xs.push_back(&m->vx.w1[k]);
                 auto w2 = fetch(r + ".conv2.weight");
-                xp.push_back(pack_x3_conv3(w2.data(), c2, c2, c2, &ok));
+                xp.push_back(pack_x3_conv3(w2.data(), c2, c2, c2, &ok, true));
                 xs.push_back(&m->vx.w2[k]);
             }
             if (ok) {

@@ -58,7 +58,10 @@ int vocoder_x3_mel_pad(int M);  // input-conv channel count after padding to the
 int32_t launch_vocoder_x3(const float* mel, bool trans, int M, int C, int B, int T, const VocX& w, void* U1, void* U2,
                           float* audio, hipStream_t st, const std::function<void(int, bool)>& mark);
 // range_ok is cleared when a weight is outside the f16 range (|w| >= 65504).
-std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPad, bool* range_ok);
+// res: ResBlock conv2 - for 8/16 channels the residual x is folded into the
+// GEMM as an identity block on the padding octets (vocoder_x3.hip, mma_x3).
+constexpr bool res_fold_channels(int C) { return C == 8 || C == 16; }
+std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPad, bool* range_ok, bool res);
 std::vector<uint16_t> pack_x3_convT(const float* W, int Cin, int Cout, int R, bool* range_ok);
 
 }  // namespace m2

@@ -78,21 +78,35 @@ __device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
 
 // ---------------------------------------------------------------------------
 // acc[n] += A_hi.B_hi, cor[n] += A_hi.B_lo + A_lo.B_hi over all k-blocks, for
-// NT 16-position tiles.  wp: this lane's A slot of k-block 0 (u32x4 units,
-// k-block stride 128 = hi + lo).  bp: LDS row of this lane's position for
-// tap 0 and k-block 0, before the lane-group offset.  Tap k reads row
-// bp + k*STEP (STEP = +1 for conv3 [t-1, t, t+1], -1 for the ConvT taps).
-template <int CIN, int NTAP, int STEP, int RSI, int NT>
-__device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp, int nt,
-                                       f32x4 (&acc)[NT], f32x4 (&cor)[NT]) {
+// NT 16-position tiles (NT compile-time: no per-tile guards, which would
+// make the MFMA chain conditional code and blow up register allocation).
+// wp: this lane's A slot of k-block 0 (u32x4 units, k-block stride 128 =
+// hi + lo).  bp: LDS row of this lane's position for tap 0 and k-block 0,
+// before the lane-group offset.  Tap k reads row bp + k*STEP (STEP = +1 for
+// conv3 [t-1, t, t+1], -1 for the ConvT taps).
+// XR (residual fold, 8- and 16-channel ResBlock conv2): the padding octets
+// of the last k-block read the block input x at the output row (xr) and the
+// packed weights hold the identity there, so the GEMM itself adds x.
+template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR>
+__device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
+                                       const unsigned char* xr, f32x4 (&acc)[NT], f32x4 (&cor)[NT]) {
     constexpr int NOCT = CIN / 8, NK = NTAP * NOCT, NKB = (NK + 3) / 4;
     static_assert(CIN % 8 == 0 && (NOCT <= 2 || NOCT % 4 == 0), "channel count must be 8, 16 or a multiple of 32");
-    constexpr int Q = NOCT >= 4 ? 4 : NOCT;  // lane groups per tap row
+    static_assert(!XR || 4 * NKB - NK == NOCT, "residual fold needs exactly one row of padding octets");
+    constexpr int Q = NOCT >= 4 ? 4 : NOCT;     // lane groups per tap row
+    constexpr int TPK = NOCT >= 4 ? 0 : 4 / Q;  // taps per k-block when a tap row has < 4 octets
+    auto koff = [](int kb) {
+        const int tap = NOCT >= 4 ? kb / (NOCT / 4) : kb * TPK;
+        const int col = NOCT >= 4 ? (kb % (NOCT / 4)) * 64 : 0;
+        return tap * STEP * RSI + col;
+    };
     const int g = (threadIdx.x & 63) >> 4;
     const unsigned char* bl = bp + (g / Q) * STEP * RSI + (g % Q) * 16;
-    // Padding octets of the last k-block (zero weights) re-read octet 0's
-    // bytes: always inside the window and finite.
-    const unsigned char* bl_last = (4 * (NKB - 1) + g < NK) ? bl : bp;
+    // Last k-block: padding octets (zero weights) re-read octet 0's bytes -
+    // inside the window and finite - or, with XR, x's octet (o - NK).
+    const int o_last = 4 * (NKB - 1) + g;
+    const unsigned char* b_last = o_last < NK ? bl + koff(NKB - 1)
+                                              : (XR ? xr + (o_last - NK) * 16 : bp + koff(NKB - 1));
     u32x4 a[2][2];
     a[0][0] = wp[0];
     a[0][1] = wp[64];
@@ -102,26 +116,19 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
             a[(kb + 1) & 1][0] = wp[(kb + 1) * 128];
             a[(kb + 1) & 1][1] = wp[(kb + 1) * 128 + 64];
         }
-        constexpr int TPK = NOCT >= 4 ? 0 : 4 / Q;  // taps per k-block when a tap row has < 4 octets
-        const int tap = NOCT >= 4 ? kb / (NOCT / 4) : kb * TPK;
-        const int col = NOCT >= 4 ? (kb % (NOCT / 4)) * 64 : 0;
-        const unsigned char* b0 = (kb == NKB - 1 ? bl_last : bl) + tap * STEP * RSI + col;
+        const unsigned char* b0 = kb == NKB - 1 ? b_last : bl + koff(kb);
         u32x4 bh[NT], blo[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            if (n < nt) {
-                bh[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI);
-                blo[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
-            }
+            bh[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI);
+            blo[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            if (n < nt) {
-                acc[n] = mfma_h(a[kb & 1][0], bh[n], acc[n]);
-                cor[n] = mfma_h(a[kb & 1][0], blo[n], cor[n]);
-                cor[n] = mfma_h(a[kb & 1][1], bh[n], cor[n]);
-            }
+            acc[n] = mfma_h(a[kb & 1][0], bh[n], acc[n]);
+            cor[n] = mfma_h(a[kb & 1][0], blo[n], cor[n]);
+            cor[n] = mfma_h(a[kb & 1][1], bh[n], cor[n]);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -130,21 +137,22 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
 template <int CIN, int NTAP>
 constexpr int nkb() { return (NTAP * (CIN / 8) + 3) / 4; }
 
-// Epilogue for one tile: v = act(acc + cor*2^-11 + bias) [+ residual], 0
-// outside [0, L), split and stored as hi/lo at row `t`.
+// Epilogue for one tile (acc already holds the bias): v = act(acc +
+// cor*2^-11) [+ residual read back from `out`], 0 outside [0, L) (only
+// evaluated for tiles that reach past an edge), split and stored as hi/lo.
 template <int COUT, int RSO, int ACT, bool RES>
-__device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, const float (&bv)[4], XW out, int t,
-                                           int co0, int L) {
+__device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, XW out, int t, int co0, int L,
+                                           bool edge) {
     float v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[r] + cor[r] * kLoI + bv[r]);
+    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(fmaf(cor[r], kLoI, acc[r]));
     unsigned char* row = out.p + (t - out.start) * RSO + co0 * 2;
     if (RES) {
         const h4 hi = *reinterpret_cast<const h4*>(row), lo = *reinterpret_cast<const h4*>(row + 2 * COUT);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (float)hi[r] + (float)lo[r] * kLoI;
+        for (int r = 0; r < 4; ++r) v[r] += fmaf((float)lo[r], kLoI, (float)hi[r]);
     }
-    if (t < 0 || t >= L) {
+    if (edge && (t < 0 || t >= L)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = 0.f;
     }
@@ -154,123 +162,191 @@ __device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, c
     *reinterpret_cast<h4*>(row + 2 * COUT) = lo;
 }
 
-// Conv1d(k=3, pad=1): abs positions [a0, a0+npos) of `out` from `in`.
-template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO>
-__device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
-                                       int a0, int npos, int L) {
-    constexpr int MB = (COUT + 15) / 16, NKB = nkb<CIN, 3>();
-    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-    const int ntiles = (npos + 15) >> 4, nch = (ntiles + NT - 1) / NT;
-    const int nw = blockDim.x >> 6;
-#pragma unroll 1
-    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < MB * nch; item += nw) {
-        const int mb = item % MB, tile0 = (item / MB) * NT;
-        const int nt = min(NT, ntiles - tile0);
-        const int co0 = mb * 16 + 4 * g;
-        float bv[4];
+// Does 3-tap packing fold the ResBlock residual into the GEMM (see mma_x3)?
+// Must agree with the host packer (res_fold_channels in vocoder_fused.h).
+template <int C>
+constexpr bool kFold = res_fold_channels(C);
+
+// One work item: NTT tiles of one (phase, m-block) row starting at tile0.
+// Output position of column j (relative to the layer's first input q0 / a0):
+// t = (p0 + j) * RR + ph (RR = 1, ph = 0 for conv3).
+template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int ACT, bool RES, bool XR, int RR,
+          int JMAX>
+__device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
+                                         const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
+                                         int ph, int tile0, int L) {
+    f32x4 acc[NTT], cor[NTT];
+    {
+        f32x4 bv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[r] = co0 + r < COUT ? bias[co0 + r] : 0.f;
-        f32x4 acc[NT], cor[NT];
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = cor[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        mma_x3<CIN, 3, 1, RSI, NT>(Wp + (size_t)mb * NKB * 128 + lane,
-                                   in.p + (a0 + tile0 * 16 + li - 1 - in.start) * RSI, nt, acc, cor);
-        if (co0 < COUT) {
+        for (int n = 0; n < NTT; ++n) {
+            acc[n] = bv;
+            cor[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR>(wp, bp, xr, acc, cor);
+    const bool edge = (p0 + tile0 * 16) * RR < 0 || (p0 + (tile0 + NTT) * 16) * RR > L;
+    if (co0 < COUT) {
+        const int li = threadIdx.x & 15;
 #pragma unroll
-            for (int n = 0; n < NT; ++n) {
-                const int j = (tile0 + n) * 16 + li;
-                if (n < nt && j < npos) store_tile<COUT, RSO, ACT, RES>(acc[n], cor[n], bv, out, a0 + j, co0, L);
-            }
+        for (int n = 0; n < NTT; ++n) {
+            const int j = (tile0 + n) * 16 + li;
+            if (((tile0 + n + 1) * 16 <= JMAX) || j < JMAX)
+                store_tile<COUT, RSO, ACT, RES>(acc[n], cor[n], out, (p0 + j) * RR + ph, co0, L, edge);
         }
     }
 }
 
-// leaky(ConvTranspose1d(k=2R, stride R, pad R/2)): inputs q in [q0, q0+nq)
+// Work items of a layer: (row, chunk) with each row's NTILES split into
+// NCH = ceil(NTILES / NT) chunks whose sizes differ by at most one tile
+// (25 tiles, NT 4: seven chunks of 3-4 rather than six of 4 and one of 1),
+// dealt round-robin over the waves.  Chunk sizes are compile-time (QLO or
+// QLO + 1): two instantiations of the item body, no per-tile guards.
+template <int NTILES, int NT>
+struct Chunks {
+    static constexpr int NCH = (NTILES + NT - 1) / NT, QLO = NTILES / NCH, QHI = QLO + (NTILES % NCH ? 1 : 0);
+    __device__ static int lo(int k) { return k * NTILES / NCH; }
+};
+
+// Conv1d(k=3, pad=1): abs positions [a0, a0+NPOS) of `out` from `in`.
+// RES: out += conv(in) (ResBlock conv2, x = out), folded into the GEMM for
+// 8/16 channels, read back in the epilogue otherwise.
+template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS>
+__device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
+                                       int a0, int L) {
+    constexpr int MB = (COUT + 15) / 16, NKB = nkb<CIN, 3>();
+    constexpr bool FOLD = RES && kFold<CIN>;
+    static_assert(!FOLD || (CIN == COUT && RSI == RSO), "folded residual: x has the conv's input layout");
+    using CH = Chunks<(NPOS + 15) / 16, NT>;
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+#pragma unroll 1
+    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < MB * CH::NCH; item += blockDim.x >> 6) {
+        const int mb = item % MB, k = item / MB;
+        const int tile0 = CH::lo(k), nt = CH::lo(k + 1) - tile0;
+        const int co0 = mb * 16 + 4 * g;
+        const int p = a0 + tile0 * 16 + li;  // this lane's output position in tile 0
+        const u32x4* wp = Wp + (size_t)mb * NKB * 128 + lane;
+        const unsigned char* bp = in.p + (p - 1 - in.start) * RSI;
+        const unsigned char* xr = out.p + (p - out.start) * RSO;
+        if (nt == CH::QHI)
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS>(wp, bias, bp, xr, out, co0,
+                                                                                        a0, 0, tile0, L);
+        else
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS>(wp, bias, bp, xr, out, co0,
+                                                                                        a0, 0, tile0, L);
+    }
+}
+
+// leaky(ConvTranspose1d(k=2R, stride R, pad R/2)): inputs q in [q0, q0+NQ)
 // give outputs t = q*R + ph.  Phase ph reads taps (q, q-1) if ph + R/2 < R,
 // else (q+1, q): B base row q + d0, tap k at row q + d0 - k.
-template <int CIN, int COUT, int R, int NT, int RSI, int RSO>
+template <int CIN, int COUT, int R, int NT, int RSI, int RSO, int NQ>
 __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
-                                       int q0, int nq, int L) {
+                                       int q0, int L) {
     constexpr int MB = (COUT + 15) / 16, NKB = nkb<CIN, 2>(), PAD = R / 2;
+    using CH = Chunks<(NQ + 15) / 16, NT>;
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-    const int ntiles = (nq + 15) >> 4, nch = (ntiles + NT - 1) / NT;
-    const int nw = blockDim.x >> 6;
 #pragma unroll 1
-    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < R * MB * nch; item += nw) {
-        const int ph = item % R, rest = item / R;
-        const int mb = rest % MB, tile0 = (rest / MB) * NT;
-        const int nt = min(NT, ntiles - tile0);
+    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < R * MB * CH::NCH;
+         item += blockDim.x >> 6) {
+        const int row = item % (R * MB), k = item / (R * MB);  // row = ph*MB + mb
+        const int ph = row / MB, mb = row - ph * MB;
+        const int tile0 = CH::lo(k), nt = CH::lo(k + 1) - tile0;
         const int d0 = (ph + PAD < R) ? 0 : 1;
         const int co0 = mb * 16 + 4 * g;
-        float bv[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = co0 + r < COUT ? bias[co0 + r] : 0.f;
-        f32x4 acc[NT], cor[NT];
-#pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = cor[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        mma_x3<CIN, 2, -1, RSI, NT>(Wp + (size_t)(ph * MB + mb) * NKB * 128 + lane,
-                                    in.p + (q0 + tile0 * 16 + li + d0 - in.start) * RSI, nt, acc, cor);
-        if (co0 < COUT) {
-#pragma unroll
-            for (int n = 0; n < NT; ++n) {
-                const int j = (tile0 + n) * 16 + li;
-                if (n < nt && j < nq)
-                    store_tile<COUT, RSO, ACT_LEAKY, false>(acc[n], cor[n], bv, out, (q0 + j) * R + ph, co0, L);
-            }
-        }
+        const u32x4* wp = Wp + (size_t)row * NKB * 128 + lane;
+        const unsigned char* bp = in.p + (q0 + tile0 * 16 + li + d0 - in.start) * RSI;
+        if (nt == CH::QHI)
+            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ>(wp, bias, bp, nullptr, out,
+                                                                                        co0, q0, ph, tile0, L);
+        else
+            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ>(wp, bias, bp, nullptr, out,
+                                                                                        co0, q0, ph, tile0, L);
     }
 }
 
 // ---------------------------------------------------------------------------
-// Global <-> LDS.
-// mel -> window rows [0, n) (abs start + r), MP channels (zero past M).
-template <bool TRANS, int M, int MP, int RS>
-__device__ __forceinline__ void gload_mel(const float* __restrict__ g, int T, XW dst, int n) {
+// Global <-> LDS.  Trip counts are compile-time (NTHR threads, N rows) so
+// every thread issues all its global loads before the first LDS store.
+// mel -> window rows [0, N) (abs start + r), MP channels (zero past M).
+template <bool TRANS, int M, int MP, int RS, int N, int NTHR>
+__device__ __forceinline__ void gload_mel(const float* __restrict__ g, int T, XW dst) {
     if (TRANS) {  // [T][M]: a row of M contiguous floats per frame
-        constexpr int C4 = MP / 4;
-        for (int i = threadIdx.x; i < n * C4; i += blockDim.x) {
+        constexpr int C4 = MP / 4, TOT = N * C4, IT = (TOT + NTHR - 1) / NTHR;
+        float4 x[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = threadIdx.x + k * NTHR;
             const int r = i / C4, c = (i - r * C4) * 4, t = dst.start + r;
-            float v[4] = {0.f, 0.f, 0.f, 0.f};
-            if (t >= 0 && t < T && c < M) {
-                const float4 x = *reinterpret_cast<const float4*>(g + (size_t)t * M + c);
-                v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+            x[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i < TOT && t >= 0 && t < T && c < M) x[k] = *reinterpret_cast<const float4*>(g + (size_t)t * M + c);
+        }
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = threadIdx.x + k * NTHR;
+            if (i < TOT) {
+                const int r = i / C4, c = (i - r * C4) * 4;
+                const float v[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+                h4 hi, lo;
+                split4(v, hi, lo);
+                unsigned char* row = dst.p + r * RS + c * 2;
+                *reinterpret_cast<h4*>(row) = hi;
+                *reinterpret_cast<h4*>(row + 2 * MP) = lo;
             }
-            h4 hi, lo;
-            split4(v, hi, lo);
-            unsigned char* row = dst.p + r * RS + c * 2;
-            *reinterpret_cast<h4*>(row) = hi;
-            *reinterpret_cast<h4*>(row + 2 * MP) = lo;
         }
     } else {  // [M][T]: consecutive threads read consecutive frames of one channel
-        for (int i = threadIdx.x; i < n * MP; i += blockDim.x) {
-            const int c = i / n, r = i - c * n, t = dst.start + r;
-            const float x = (t >= 0 && t < T && c < M) ? g[(size_t)c * T + t] : 0.f;
-            const _Float16 h = (_Float16)x;
-            _Float16* row = reinterpret_cast<_Float16*>(dst.p + r * RS);
-            row[c] = h;
-            row[MP + c] = (_Float16)((x - (float)h) * kLoS);
+        constexpr int TOT = N * MP, IT = (TOT + NTHR - 1) / NTHR;
+        float x[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = threadIdx.x + k * NTHR;
+            const int c = i / N, r = i - c * N, t = dst.start + r;
+            x[k] = (i < TOT && t >= 0 && t < T && c < M) ? g[(size_t)c * T + t] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = threadIdx.x + k * NTHR;
+            if (i < TOT) {
+                const int c = i / N, r = i - c * N;
+                const _Float16 h = (_Float16)x[k];
+                _Float16* row = reinterpret_cast<_Float16*>(dst.p + r * RS);
+                row[c] = h;
+                row[MP + c] = (_Float16)((x[k] - (float)h) * kLoS);
+            }
         }
     }
 }
 
-// rows of 4C bytes (hi|lo) at global positions [start, start+n), zero outside [0, Lg)
-template <int C, int RS>
-__device__ __forceinline__ void gload_rows(const unsigned char* __restrict__ g, int Lg, XW dst, int n) {
-    constexpr int Q = C / 4;  // 16-B chunks per row
-    for (int i = threadIdx.x; i < n * Q; i += blockDim.x) {
+// rows of 4C bytes (hi|lo) at global positions [start, start+N), zero outside [0, Lg)
+template <int C, int RS, int N, int NTHR>
+__device__ __forceinline__ void gload_rows(const unsigned char* __restrict__ g, int Lg, XW dst) {
+    constexpr int Q = C / 4, TOT = N * Q, IT = (TOT + NTHR - 1) / NTHR;  // 16-B chunks
+    u32x4 v[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int i = threadIdx.x + k * NTHR;
         const int r = i / Q, q = i - r * Q, t = dst.start + r;
-        u32x4 v = u32x4{0u, 0u, 0u, 0u};
-        if (t >= 0 && t < Lg) v = *reinterpret_cast<const u32x4*>(g + (size_t)t * 4 * C + q * 16);
-        *reinterpret_cast<u32x4*>(dst.p + r * RS + q * 16) = v;
+        v[k] = u32x4{0u, 0u, 0u, 0u};
+        if (i < TOT && t >= 0 && t < Lg) v[k] = *reinterpret_cast<const u32x4*>(g + (size_t)t * 4 * C + q * 16);
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int i = threadIdx.x + k * NTHR;
+        const int r = i / Q, q = i - r * Q;
+        if (i < TOT) *reinterpret_cast<u32x4*>(dst.p + r * RS + q * 16) = v[k];
     }
 }
 
-template <int C, int RS>
-__device__ __forceinline__ void gstore_rows(unsigned char* __restrict__ g, int Lg, XW src, int a0, int n) {
-    constexpr int Q = C / 4;
-    for (int i = threadIdx.x; i < n * Q; i += blockDim.x) {
+template <int C, int RS, int N, int NTHR>
+__device__ __forceinline__ void gstore_rows(unsigned char* __restrict__ g, int Lg, XW src, int a0) {
+    constexpr int Q = C / 4, TOT = N * Q, IT = (TOT + NTHR - 1) / NTHR;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int i = threadIdx.x + k * NTHR;
         const int r = i / Q, q = i - r * Q, t = a0 + r;
-        if (t < Lg)
+        if (i < TOT && t < Lg)
             *reinterpret_cast<u32x4*>(g + (size_t)t * 4 * C + q * 16) =
                 *reinterpret_cast<const u32x4*>(src.p + (t - src.start) * RS + q * 16);
     }
@@ -329,6 +405,25 @@ struct CfgS2 {
     static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
 };
 
+// Diagnostic build only (-DM2_STAMPS): per-wave s_memtime stamps at phase
+// boundaries, [kernel][workgroup][wave][16] (tools/probe/stamps.py --x3).
+#ifdef M2_STAMPS
+__device__ unsigned long long g_x3_stamps[3][4096][16][16];
+#define XSTAMP(K, i)                                                                                     \
+    do {                                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        unsigned long long _t;                                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                      \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        const int _wg = blockIdx.y * gridDim.x + blockIdx.x;                                             \
+        if ((threadIdx.x & 63) == 0 && _wg < 4096) g_x3_stamps[K][_wg][threadIdx.x >> 6][i] = _t;        \
+    } while (0)
+#else
+#define XSTAMP(K, i) \
+    do {             \
+    } while (0)
+#endif
+
 template <class Cfg, bool TRANS>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_head_kernel(const float* __restrict__ mel, int T,
                                                                             VocX w, unsigned char* __restrict__ U1) {
@@ -341,18 +436,29 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_head_kernel(con
     XW a0w{lds + Pl::CAP_MEL * Pl::RS_M, f0 - 2};
     XW hw{lds, 4 * f0 - 1};
     XW uw{lds + Pl::R0, 4 * f0 - 4};
-    gload_mel<TRANS, M, MP, Pl::RS_M>(mel + (size_t)b * M * T, T, melw, Pl::MEL_N);
+    XSTAMP(0, 0);
+    gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::WAVES * 64>(mel + (size_t)b * M * T, T, melw);
+    XSTAMP(0, 1);
     __syncthreads();
-    xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T);
+    XSTAMP(0, 2);
+    xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N>(w.wi, w.bi, melw, a0w, f0 - 2, T);
+    XSTAMP(0, 3);
     __syncthreads();
-    xconvT<C, C1, 4, Cfg::NT_T1, Pl::RS_C, Pl::RS_1>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T);
+    XSTAMP(0, 4);
+    xconvT<C, C1, 4, Cfg::NT_T1, Pl::RS_C, Pl::RS_1, Pl::NQ>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, 4 * T);
+    XSTAMP(0, 5);
     __syncthreads();
-    xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, Pl::H_N,
-                                                                     4 * T);
+    XSTAMP(0, 6);
+    xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, 4 * T);
+    XSTAMP(0, 7);
     __syncthreads();
-    xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1>(w.w2[0], w.b2[0], hw, uw, 4 * f0, Pl::O_N, 4 * T);
+    XSTAMP(0, 8);
+    xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N>(w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T);
+    XSTAMP(0, 9);
     __syncthreads();
-    gstore_rows<C1, Pl::RS_1>(U1 + (size_t)b * 4 * T * 4 * C1, 4 * T, uw, 4 * f0, Pl::O_N);
+    XSTAMP(0, 10);
+    gstore_rows<C1, Pl::RS_1, Pl::O_N, Cfg::WAVES * 64>(U1 + (size_t)b * 4 * T * 4 * C1, 4 * T, uw, 4 * f0);
+    XSTAMP(0, 11);
 }
 
 template <class Cfg>
@@ -368,16 +474,25 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_mid_kernel(cons
     XW inw{lds, p0 - 2};
     XW hw{lds, 4 * p0 - 1};
     XW uw{lds + Pl::R0, 4 * p0 - 4};
-    gload_rows<CI, Pl::RS_I>(U1 + (size_t)b * L1 * 4 * CI, L1, inw, Pl::IN_N);
+    XSTAMP(1, 0);
+    gload_rows<CI, Pl::RS_I, Pl::IN_N, Cfg::WAVES * 64>(U1 + (size_t)b * L1 * 4 * CI, L1, inw);
+    XSTAMP(1, 1);
     __syncthreads();
-    xconvT<CI, CO, 4, Cfg::NT_T2, Pl::RS_I, Pl::RS_O>(w.wt[1], w.bt[1], inw, uw, p0 - 1, Pl::NQ, L2);
+    XSTAMP(1, 2);
+    xconvT<CI, CO, 4, Cfg::NT_T2, Pl::RS_I, Pl::RS_O, Pl::NQ>(w.wt[1], w.bt[1], inw, uw, p0 - 1, L2);
+    XSTAMP(1, 3);
     __syncthreads();
-    xconv3<CO, CO, Cfg::NT_R2, ACT_LEAKY, false, Pl::RS_O, Pl::RS_O>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, Pl::H_N,
-                                                                     L2);
+    XSTAMP(1, 4);
+    xconv3<CO, CO, Cfg::NT_R2, ACT_LEAKY, false, Pl::RS_O, Pl::RS_O, Pl::H_N>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, L2);
+    XSTAMP(1, 5);
     __syncthreads();
-    xconv3<CO, CO, Cfg::NT_R2, ACT_NONE, true, Pl::RS_O, Pl::RS_O>(w.w2[1], w.b2[1], hw, uw, 4 * p0, Pl::O_N, L2);
+    XSTAMP(1, 6);
+    xconv3<CO, CO, Cfg::NT_R2, ACT_NONE, true, Pl::RS_O, Pl::RS_O, Pl::O_N>(w.w2[1], w.b2[1], hw, uw, 4 * p0, L2);
+    XSTAMP(1, 7);
     __syncthreads();
-    gstore_rows<CO, Pl::RS_O>(U2 + (size_t)b * L2 * 4 * CO, L2, uw, 4 * p0, Pl::O_N);
+    XSTAMP(1, 8);
+    gstore_rows<CO, Pl::RS_O, Pl::O_N, Cfg::WAVES * 64>(U2 + (size_t)b * L2 * 4 * CO, L2, uw, 4 * p0);
+    XSTAMP(1, 9);
 }
 
 template <class Cfg>
@@ -397,22 +512,35 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_tail_kernel(con
     XW h3{ra, 2 * p0 - 4};
     XW u4{ra, 4 * p0 - 4};
     XW h4w{rb, 4 * p0 - 2};
-    gload_rows<CI, Pl::RS_I>(U2 + (size_t)b * L2 * 4 * CI, L2, inw, Pl::IN_N);
+    XSTAMP(2, 0);
+    gload_rows<CI, Pl::RS_I, Pl::IN_N, Cfg::WAVES * 64>(U2 + (size_t)b * L2 * 4 * CI, L2, inw);
+    XSTAMP(2, 1);
     __syncthreads();
-    xconvT<CI, C3, 2, Cfg::NT_T3, Pl::RS_I, Pl::RS_3>(w.wt[2], w.bt[2], inw, u3, p0 - 3, Pl::NQ3, L3);
+    XSTAMP(2, 2);
+    xconvT<CI, C3, 2, Cfg::NT_T3, Pl::RS_I, Pl::RS_3, Pl::NQ3>(w.wt[2], w.bt[2], inw, u3, p0 - 3, L3);
+    XSTAMP(2, 3);
     __syncthreads();
-    xconv3<C3, C3, Cfg::NT_R3, ACT_LEAKY, false, Pl::RS_3, Pl::RS_3>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, Pl::H3_N,
-                                                                     L3);
+    XSTAMP(2, 4);
+    xconv3<C3, C3, Cfg::NT_R3, ACT_LEAKY, false, Pl::RS_3, Pl::RS_3, Pl::H3_N>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, L3);
+    XSTAMP(2, 5);
     __syncthreads();
-    xconv3<C3, C3, Cfg::NT_R3, ACT_NONE, true, Pl::RS_3, Pl::RS_3>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, Pl::O3_N, L3);
+    XSTAMP(2, 6);
+    xconv3<C3, C3, Cfg::NT_R3, ACT_NONE, true, Pl::RS_3, Pl::RS_3, Pl::O3_N>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, L3);
+    XSTAMP(2, 7);
     __syncthreads();
-    xconvT<C3, C4, 2, Cfg::NT_T4, Pl::RS_3, Pl::RS_4>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4);
+    XSTAMP(2, 8);
+    xconvT<C3, C4, 2, Cfg::NT_T4, Pl::RS_3, Pl::RS_4, Pl::NQ4>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, L4);
+    XSTAMP(2, 9);
     __syncthreads();
-    xconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::RS_4, Pl::RS_4>(w.w1[3], w.b1[3], u4, h4w, 4 * p0 - 2, Pl::H4_N,
-                                                                     L4);
+    XSTAMP(2, 10);
+    xconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::RS_4, Pl::RS_4, Pl::H4_N>(w.w1[3], w.b1[3], u4, h4w, 4 * p0 - 2, L4);
+    XSTAMP(2, 11);
     __syncthreads();
-    xconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::RS_4, Pl::RS_4>(w.w2[3], w.b2[3], h4w, u4, 4 * p0 - 1, Pl::O4_N, L4);
+    XSTAMP(2, 12);
+    xconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::RS_4, Pl::RS_4, Pl::O4_N>(w.w2[3], w.b2[3], h4w, u4, 4 * p0 - 1, L4);
+    XSTAMP(2, 13);
     __syncthreads();
+    XSTAMP(2, 14);
     // output_conv (C4 -> 1, k3) + tanh on the VALU, one sample per thread.
     float* arow = audio + (size_t)b * L4;
     const float bo = w.bo[0];
@@ -431,6 +559,7 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_tail_kernel(con
             arow[t] = tanhf(acc + bo);
         }
     }
+    XSTAMP(2, 15);
 }
 
 template <typename K>
@@ -488,6 +617,13 @@ const char* const kVocX3KernelNames[kVocKernels] = {
     "x3_mid_kernel (ConvT2 + ResBlock2)",
     "x3_tail_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv)"};
 
+#ifdef M2_STAMPS
+extern "C" int32_t m2_debug_stamps_x3(void* host, size_t bytes) {
+    return (int32_t)hipMemcpyFromSymbol(host, HIP_SYMBOL(x3::g_x3_stamps),
+                                        bytes < sizeof(x3::g_x3_stamps) ? bytes : sizeof(x3::g_x3_stamps));
+}
+#endif
+
 bool vocoder_x3_supported(int M, int C) { return (M == 64 && C == 128) || (M == 80 && C == 256); }
 
 int vocoder_x3_mel_pad(int M) { return M == 80 ? 96 : M; }
@@ -537,10 +673,22 @@ std::vector<uint16_t> pack_x3(int NPH, int Cout, int Cin, int NTAP, Wf W, bool* 
 }
 }  // namespace
 
-std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPad, bool* range_ok) {
-    return pack_x3(1, Cout, CinPad, 3,
-                   [&](int, int co, int ci, int tap) { return ci < Cin ? W[((size_t)co * Cin + ci) * 3 + tap] : 0.f; },
-                   range_ok);
+std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPad, bool* range_ok, bool res) {
+    std::vector<uint16_t> out = pack_x3(
+        1, Cout, CinPad, 3,
+        [&](int, int co, int ci, int tap) { return ci < Cin ? W[((size_t)co * Cin + ci) * 3 + tap] : 0.f; }, range_ok);
+    if (res && res_fold_channels(Cin)) {
+        // Identity on the padding octets of the last k-block (x octet o - NK):
+        // hi = 1.0 (0x3c00), lo = 0.
+        const int NOCT = Cin / 8, NK = 3 * NOCT, NKB = (NK + 3) / 4, kb = NKB - 1;
+        for (int lane = 0; lane < 64; ++lane) {
+            const int co = lane & 15, o = 4 * kb + (lane >> 4);
+            if (o < NK || co >= Cout) continue;
+            for (int e = 0; e < 8; ++e)
+                if ((o - NK) * 8 + e == co) out[(((size_t)kb * 2) * 64 + lane) * 8 + e] = 0x3c00;
+        }
+    }
+    return out;
 }
 
 std::vector<uint16_t> pack_x3_convT(const float* W, int Cin, int Cout, int R, bool* range_ok) {

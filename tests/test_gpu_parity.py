@@ -326,3 +326,25 @@ def test_cli_end_to_end_wav(gpu, tmp_path):
     got = np.rint(y * 32768).astype(np.int32)
     assert sr == 22050 and got.shape == want.shape == (81920,)
     assert int(np.abs(got - want).max()) <= 1
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_vocoder_arithmetic_paths(gpu, stage, monkeypatch):
+    """Default = split-f16 MFMA (path 2); M2_VOC_F32=1 = exact-f32 MFMA (path 1).
+    Both within the waveform bound of the CPU oracle, and close to each other."""
+    from m2amd import _lib
+    lib = _lib.load()
+    mel = torch.randn(3, stage_config(stage).mel_channels, 137, generator=torch.Generator().manual_seed(7))
+    ref = orc.vocoder(golden_state(stage), mel)
+    out = {}
+    for path, env in ((2, None), (1, "1")):
+        if env is None:
+            monkeypatch.delenv("M2_VOC_F32", raising=False)
+        else:
+            monkeypatch.setenv("M2_VOC_F32", env)
+        m = build_model(stage, gpu)
+        assert lib.m2_vocoder_path(m._hip(gpu).handle) == path
+        out[path] = m.vocoder(mel.to(gpu)).cpu()
+        assert rms(out[path], ref) <= AUDIO_RMS_TOL
+        assert maxabs(out[path], ref) <= 1e-4
+    assert maxabs(out[1], out[2]) <= 1e-4

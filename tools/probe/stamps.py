@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-wave phase stamps from the M2_STAMPS diagnostic build (never the product).
-M2TTS_HIP_LIB=m2-tts_amd/csrc/build_stamps/libm2tts_hip_stamps.so python tools/probe/stamps.py B"""
+M2TTS_HIP_LIB=m2-tts_amd/csrc/build_stamps/libm2tts_hip_stamps.so python tools/probe/stamps.py B [--x3]
+(--x3: the split-f16 kernels, whose phases are [layer, barrier] pairs)"""
 import ctypes
 import sys
 from pathlib import Path
@@ -20,7 +21,17 @@ PHASES = {
     2: ["gload+bar", "convT3", "bar", "rb3c1", "bar", "rb3c2", "bar", "convT4", "bar", "rb4c1", "bar", "rb4c2", "bar",
         "outconv"],
 }
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+X3 = {
+    0: ["gload", "bar", "inconv", "bar", "convT1", "bar", "rb1c1", "bar", "rb1c2", "bar", "gstore"],
+    1: ["gload", "bar", "convT2", "bar", "rb2c1", "bar", "rb2c2", "bar", "gstore"],
+    2: ["gload", "bar", "convT3", "bar", "rb3c1", "bar", "rb3c2", "bar", "convT4", "bar", "rb4c1", "bar", "rb4c2",
+        "bar", "outconv"],
+}
+x3 = "--x3" in sys.argv
+argv = [a for a in sys.argv[1:] if a != "--x3"]
+if x3:
+    PHASES = X3
+B = int(argv[0]) if argv else 4
 dev = torch.device("cuda", 0)
 lib = _lib.load()
 model = bench.fixture_model(dev)
@@ -29,8 +40,9 @@ for _ in range(3):
     model.vocoder(mel)
 torch.cuda.synchronize()
 buf = np.zeros(3 * 4096 * 16 * 16, dtype=np.uint64)
-lib.m2_debug_stamps.restype = ctypes.c_int32
-lib.m2_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
+fn = lib.m2_debug_stamps_x3 if x3 else lib.m2_debug_stamps
+fn.restype = ctypes.c_int32
+fn(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
 all_st = buf.reshape(3, 4096, 16, 16).astype(np.int64)
 for k, names in PHASES.items():
     st = all_st[k]
