@@ -107,15 +107,18 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
     const int o_last = 4 * (NKB - 1) + g;
     const unsigned char* b_last = o_last < NK ? bl + koff(NKB - 1)
                                               : (XR ? xr + (o_last - NK) * 16 : bp + koff(NKB - 1));
-    u32x4 a[2][2];
-    a[0][0] = wp[0];
-    a[0][1] = wp[64];
+    // Weight fragments stream PD k-blocks ahead (PD = all of them up to 4):
+    // one L2 round trip per item rather than one per k-block (a k-block is
+    // only 3*NT MFMAs, shorter than an L2 hit), at most 32 VGPRs in flight.
+    constexpr int PD = NKB < 4 ? NKB : 4;
+    u32x4 a[PD][2];
+#pragma unroll
+    for (int kb = 0; kb < PD; ++kb) {
+        a[kb][0] = wp[kb * 128];
+        a[kb][1] = wp[kb * 128 + 64];
+    }
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-        if (kb + 1 < NKB) {
-            a[(kb + 1) & 1][0] = wp[(kb + 1) * 128];
-            a[(kb + 1) & 1][1] = wp[(kb + 1) * 128 + 64];
-        }
         const unsigned char* b0 = kb == NKB - 1 ? b_last : bl + koff(kb);
         u32x4 bh[NT], blo[NT];
 #pragma unroll
@@ -124,11 +127,16 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
             blo[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
         }
         __builtin_amdgcn_sched_barrier(0);
+        const u32x4 ah = a[kb % PD][0], al = a[kb % PD][1];
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            acc[n] = mfma_h(a[kb & 1][0], bh[n], acc[n]);
-            cor[n] = mfma_h(a[kb & 1][0], blo[n], cor[n]);
-            cor[n] = mfma_h(a[kb & 1][1], bh[n], cor[n]);
+            acc[n] = mfma_h(ah, bh[n], acc[n]);
+            cor[n] = mfma_h(ah, blo[n], cor[n]);
+            cor[n] = mfma_h(al, bh[n], cor[n]);
+        }
+        if (kb + PD < NKB) {
+            a[kb % PD][0] = wp[(kb + PD) * 128];
+            a[kb % PD][1] = wp[(kb + PD) * 128 + 64];
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -354,54 +362,62 @@ __device__ __forceinline__ void gstore_rows(unsigned char* __restrict__ g, int L
 
 // ---------------------------------------------------------------------------
 // Window plans (rows; the same receptive-field arithmetic as the f32 plans).
+// Two LDS regions per kernel, A then B, with buffers aliased by lifetime.
+// Region-A buffers are sized to the rows actually written; the garbage
+// columns of a partial 16-wide tile may read past them into region B, which
+// only feeds columns that are never stored (an MFMA output column depends
+// on its own B column only).  Region-B buffers keep the full read extent.
 template <int MP, int C, int TF>
-struct HeadPlan {
+struct HeadPlan {  // A: a0 | h   B: mel | u
     static constexpr int C1 = C / 2;
     static constexpr int RS_M = rs_for(MP), RS_C = rs_for(C), RS_1 = rs_for(C1);
     static constexpr int MEL_N = TF + 6, A0_N = TF + 4, NQ = TF + 2, H_N = 4 * TF + 2, O_N = 4 * TF;
     static constexpr int CAP_MEL = cmax(MEL_N, rup16(A0_N) + 2);
-    static constexpr int CAP_A0 = cmax(A0_N, rup16(NQ) + 2);
     static constexpr int CAP_U = cmax(4 * NQ, rup16(H_N) + 4);
-    static constexpr int CAP_H = cmax(H_N, rup16(O_N) + 2);
-    static constexpr int R0 = cmax(CAP_MEL * RS_M + CAP_A0 * RS_C, CAP_H * RS_1);
-    static constexpr int LDS_BYTES = R0 + CAP_U * RS_1;
+    static constexpr int RA = cmax(A0_N * RS_C, H_N * RS_1);
+    static constexpr int LDS_BYTES = RA + cmax(CAP_MEL * RS_M, CAP_U * RS_1);
 };
 
 template <int CI, int W>
-struct MidPlan {
+struct MidPlan {  // A: in | h   B: u
     static constexpr int CO = CI / 2;
     static constexpr int RS_I = rs_for(CI), RS_O = rs_for(CO);
     static constexpr int IN_N = W + 4, NQ = W + 2, H_N = 4 * W + 2, O_N = 4 * W;
-    static constexpr int CAP_IN = cmax(IN_N, rup16(NQ) + 2);
     static constexpr int CAP_U = cmax(4 * NQ, rup16(H_N) + 4);
-    static constexpr int CAP_H = cmax(H_N, rup16(O_N) + 2);
-    static constexpr int R0 = cmax(CAP_IN * RS_I, CAP_H * RS_O);
-    static constexpr int LDS_BYTES = R0 + CAP_U * RS_O;
+    static constexpr int RA = cmax(IN_N * RS_I, H_N * RS_O);
+    static constexpr int LDS_BYTES = RA + CAP_U * RS_O;
 };
 
 template <int CI, int W>
-struct TailPlan {
+struct TailPlan {  // A: in | h3 | u4   B: u3 | h4
     static constexpr int C3 = CI / 2, C4 = CI / 4;
     static constexpr int RS_I = rs_for(CI), RS_3 = rs_for(C3), RS_4 = rs_for(C4);
     static constexpr int IN_N = W + 8, NQ3 = W + 6, H3_N = 2 * W + 8, O3_N = 2 * W + 6;
     static constexpr int NQ4 = 2 * W + 4, H4_N = 4 * W + 4, O4_N = 4 * W + 2, A_N = 4 * W;
-    static constexpr int CAP_IN = cmax(IN_N, rup16(NQ3) + 2);
     static constexpr int CAP_U3 = cmax(2 * NQ3, cmax(rup16(H3_N) + 3, rup16(NQ4) + 5));
-    static constexpr int CAP_H3 = cmax(H3_N, rup16(O3_N) + 2);
-    static constexpr int CAP_U4 = cmax(2 * NQ4, rup16(H4_N) + 3);
     static constexpr int CAP_H4 = cmax(H4_N, rup16(O4_N) + 2);
-    static constexpr int RA = cmax(CAP_IN * RS_I, cmax(CAP_H3 * RS_3, CAP_U4 * RS_4));
-    static constexpr int RB = cmax(CAP_U3 * RS_3, CAP_H4 * RS_4);
-    static constexpr int LDS_BYTES = RA + RB;
+    static constexpr int RA = cmax(IN_N * RS_I, cmax(H3_N * RS_3, 2 * NQ4 * RS_4));
+    static constexpr int LDS_BYTES = RA + cmax(CAP_U3 * RS_3, CAP_H4 * RS_4);
 };
 
-// Tilings: WAVES per workgroup, NT_* tiles per work item, MINW launch bound.
+// Tilings.  Per kernel: waves per workgroup (*W), window (TF frames / W2 /
+// W3 positions), launch-bound waves per SIMD (*MIN: 4 -> <= 128 VGPRs), and
+// NT_* = tile-chunk size per layer, chosen so each layer's items come to a
+// multiple of the wave count.  Stage1 at B=32, T=500 (bench): head 8 x 32 =
+// 256 workgroups (one per CU), mid 16 x 32 = 512 (two rounds), tail 48 x 32 =
+// 1536 at two per CU (three full rounds).
 struct CfgS1 {
-    static constexpr int M = 64, MP = 64, C = 128, TF = 28, W2 = 60, W3 = 192, WAVES = 8, MINW = 2;
-    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+    static constexpr int M = 64, MP = 64, C = 128;
+    static constexpr int TF = 63, HW = 16, HMIN = 4;
+    static constexpr int W2 = 125, MW = 16, MMIN = 4;
+    static constexpr int W3 = 168, TW = 8, TMIN = 4;
+    static constexpr int NT_IN = 3, NT_T1 = 5, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 3, NT_R3 = 3, NT_T4 = 3, NT_R4 = 6;
 };
 struct CfgS2 {
-    static constexpr int M = 80, MP = 96, C = 256, TF = 12, W2 = 28, W3 = 120, WAVES = 8, MINW = 2;
+    static constexpr int M = 80, MP = 96, C = 256;
+    static constexpr int TF = 12, HW = 8, HMIN = 2;
+    static constexpr int W2 = 28, MW = 8, MMIN = 2;
+    static constexpr int W3 = 120, TW = 8, TMIN = 2;
     static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
 };
 
@@ -425,19 +441,19 @@ __device__ unsigned long long g_x3_stamps[3][4096][16][16];
 #endif
 
 template <class Cfg, bool TRANS>
-__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_head_kernel(const float* __restrict__ mel, int T,
+__global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const float* __restrict__ mel, int T,
                                                                             VocX w, unsigned char* __restrict__ U1) {
     constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
     using Pl = HeadPlan<MP, C, TF>;
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, f0 = blockIdx.x * TF;
-    XW melw{lds, f0 - 3};
-    XW a0w{lds + Pl::CAP_MEL * Pl::RS_M, f0 - 2};
+    XW a0w{lds, f0 - 2};
     XW hw{lds, 4 * f0 - 1};
-    XW uw{lds + Pl::R0, 4 * f0 - 4};
+    XW melw{lds + Pl::RA, f0 - 3};
+    XW uw{lds + Pl::RA, 4 * f0 - 4};
     XSTAMP(0, 0);
-    gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::WAVES * 64>(mel + (size_t)b * M * T, T, melw);
+    gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melw);
     XSTAMP(0, 1);
     __syncthreads();
     XSTAMP(0, 2);
@@ -457,12 +473,12 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_head_kernel(con
     XSTAMP(0, 9);
     __syncthreads();
     XSTAMP(0, 10);
-    gstore_rows<C1, Pl::RS_1, Pl::O_N, Cfg::WAVES * 64>(U1 + (size_t)b * 4 * T * 4 * C1, 4 * T, uw, 4 * f0);
+    gstore_rows<C1, Pl::RS_1, Pl::O_N, Cfg::HW * 64>(U1 + (size_t)b * 4 * T * 4 * C1, 4 * T, uw, 4 * f0);
     XSTAMP(0, 11);
 }
 
 template <class Cfg>
-__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_mid_kernel(const unsigned char* __restrict__ U1,
+__global__ __launch_bounds__(Cfg::MW * 64, Cfg::MMIN) void x3_mid_kernel(const unsigned char* __restrict__ U1,
                                                                            int L1, VocX w,
                                                                            unsigned char* __restrict__ U2) {
     constexpr int CI = Cfg::C / 2, W = Cfg::W2;
@@ -473,9 +489,9 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_mid_kernel(cons
     const int L2 = 4 * L1;
     XW inw{lds, p0 - 2};
     XW hw{lds, 4 * p0 - 1};
-    XW uw{lds + Pl::R0, 4 * p0 - 4};
+    XW uw{lds + Pl::RA, 4 * p0 - 4};
     XSTAMP(1, 0);
-    gload_rows<CI, Pl::RS_I, Pl::IN_N, Cfg::WAVES * 64>(U1 + (size_t)b * L1 * 4 * CI, L1, inw);
+    gload_rows<CI, Pl::RS_I, Pl::IN_N, Cfg::MW * 64>(U1 + (size_t)b * L1 * 4 * CI, L1, inw);
     XSTAMP(1, 1);
     __syncthreads();
     XSTAMP(1, 2);
@@ -491,12 +507,12 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_mid_kernel(cons
     XSTAMP(1, 7);
     __syncthreads();
     XSTAMP(1, 8);
-    gstore_rows<CO, Pl::RS_O, Pl::O_N, Cfg::WAVES * 64>(U2 + (size_t)b * L2 * 4 * CO, L2, uw, 4 * p0);
+    gstore_rows<CO, Pl::RS_O, Pl::O_N, Cfg::MW * 64>(U2 + (size_t)b * L2 * 4 * CO, L2, uw, 4 * p0);
     XSTAMP(1, 9);
 }
 
 template <class Cfg>
-__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_tail_kernel(const unsigned char* __restrict__ U2,
+__global__ __launch_bounds__(Cfg::TW * 64, Cfg::TMIN) void x3_tail_kernel(const unsigned char* __restrict__ U2,
                                                                             int L2, VocX w,
                                                                             float* __restrict__ audio) {
     constexpr int CI = Cfg::C / 4, W = Cfg::W3;
@@ -513,7 +529,7 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void x3_tail_kernel(con
     XW u4{ra, 4 * p0 - 4};
     XW h4w{rb, 4 * p0 - 2};
     XSTAMP(2, 0);
-    gload_rows<CI, Pl::RS_I, Pl::IN_N, Cfg::WAVES * 64>(U2 + (size_t)b * L2 * 4 * CI, L2, inw);
+    gload_rows<CI, Pl::RS_I, Pl::IN_N, Cfg::TW * 64>(U2 + (size_t)b * L2 * 4 * CI, L2, inw);
     XSTAMP(2, 1);
     __syncthreads();
     XSTAMP(2, 2);
@@ -576,7 +592,6 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     using HP = HeadPlan<Cfg::MP, Cfg::C, Cfg::TF>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
-    constexpr int threads = Cfg::WAVES * 64;
     static bool attr = false;
     if (!attr) {
         int32_t rc;
@@ -590,20 +605,20 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     auto* u2 = static_cast<unsigned char*>(U2);
     mark(0, true);
     if (trans)
-        hipLaunchKernelGGL((x3_head_kernel<Cfg, true>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_BYTES, st,
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, true>), dim3(cdiv(T, Cfg::TF), B), dim3(Cfg::HW * 64), HP::LDS_BYTES, st,
                            mel, T, w, u1);
     else
-        hipLaunchKernelGGL((x3_head_kernel<Cfg, false>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_BYTES, st,
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, false>), dim3(cdiv(T, Cfg::TF), B), dim3(Cfg::HW * 64), HP::LDS_BYTES, st,
                            mel, T, w, u1);
     mark(0, false);
     M2_LAUNCHED("x3_head_kernel");
     mark(1, true);
-    hipLaunchKernelGGL((x3_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(threads), MP::LDS_BYTES, st, u1,
+    hipLaunchKernelGGL((x3_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(Cfg::MW * 64), MP::LDS_BYTES, st, u1,
                        4 * T, w, u2);
     mark(1, false);
     M2_LAUNCHED("x3_mid_kernel");
     mark(2, true);
-    hipLaunchKernelGGL((x3_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(threads), TP::LDS_BYTES, st, u2,
+    hipLaunchKernelGGL((x3_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(Cfg::TW * 64), TP::LDS_BYTES, st, u2,
                        16 * T, w, audio);
     mark(2, false);
     M2_LAUNCHED("x3_tail_kernel");
