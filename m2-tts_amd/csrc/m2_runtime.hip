@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "m2_common.h"
+#include "transformer_fused.h"
 #include "vocoder_fused.h"
 
 namespace m2 {
@@ -127,6 +128,8 @@ static bool config_ok(const m2_config* c) {
 // ---------------------------------------------------------------------------
 struct m2_layer_w {
     const float *qkv_w, *out_w, *out_b, *ff1_w, *ff1_b, *ff2_w, *ff2_b, *n1_w, *n1_b, *n2_w, *n2_b;
+    // B-fragment packs for the fused layer kernels (transformer_fused.hip)
+    const float *qkv_p = nullptr, *out_p = nullptr, *ff1_p = nullptr, *ff2_p = nullptr;
 };
 
 struct m2_model {
@@ -137,6 +140,8 @@ struct m2_model {
     const float *emb = nullptr, *pe = nullptr, *enc_nw = nullptr, *enc_nb = nullptr;
     const float* dur[10] = {};  // w1,b1,alpha1,beta1, w2,b2,alpha2,beta2, proj_w, proj_b
     const float *dec_nw = nullptr, *dec_nb = nullptr, *mel_w = nullptr, *mel_b = nullptr;
+    const float* mel_p = nullptr;  // packed mel projection (fused path)
+    bool tfused = false;           // transformer layers on ln_gemm + attention + post_attn
     const float *vin_w = nullptr, *vin_b = nullptr, *vout_w = nullptr, *vout_b = nullptr;
     const float *up_w[4] = {}, *up_b[4] = {};
     const float *rb_w1[4] = {}, *rb_b1[4] = {}, *rb_w2[4] = {}, *rb_b2[4] = {};
@@ -216,6 +221,12 @@ int32_t run_layer(const m2_model* m, const m2_layer_w& L, const float* x_in, flo
                   const uint8_t* mask, int B, int N, hipStream_t st) {
     const int H = m->cfg.hidden_dim, R = B * N;
     int32_t rc;
+    if (m->tfused) {
+        if ((rc = launch_ln_gemm(x_in, L.n1_w, L.n1_b, L.qkv_p, nullptr, ACT_NONE, R, H, 3 * H, wb.qkv, st))) return rc;
+        if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st))) return rc;
+        return launch_post_attn(wb.att, x_in, L.out_p, L.out_b, L.n2_w, L.n2_b, L.ff1_p, L.ff1_b, L.ff2_p, L.ff2_b, R, H,
+                                x, st);
+    }
     if ((rc = launch_linear(x_in, L.n1_w, L.n1_b, L.qkv_w, nullptr, nullptr, ACT_NONE, R, H, 3 * H, wb.qkv, st))) return rc;
     if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st))) return rc;
     if ((rc = launch_linear(wb.att, nullptr, nullptr, L.out_w, L.out_b, x_in, ACT_NONE, R, H, H, x, st))) return rc;
@@ -280,6 +291,10 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     total = align_up(total, 64);
     const size_t dw_off = total;  // duration conv weights re-laid out [ci][k][co], 2 layers
     total += 2 * 3 * (size_t)H * H;
+    total = align_up(total, 64);
+    const size_t tf_off = total;  // fused-layer B-fragment packs: 8H^2 per layer + mel projection
+    const int n_layers = cfg->text_encoder_layers + cfg->decoder_layers;
+    total += (size_t)n_layers * 8 * H * H + (size_t)cfg->mel_channels * H;
 
     auto* m = new m2_model();
     m->cfg = *cfg;
@@ -351,6 +366,37 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     };
     for (int i = 0; i < cfg->text_encoder_layers; ++i) m->enc.push_back(layer("text_encoder.layers." + std::to_string(i)));
     for (int i = 0; i < cfg->decoder_layers; ++i) m->dec.push_back(layer("decoder.layers." + std::to_string(i)));
+    // Fused transformer layers: pack qkv / out / ffn / mel-projection weights
+    // in B-fragment order (M2_TF_UNFUSED=1 keeps the five-linear layer).
+    m->tfused = tf_fused_supported(H, 3 * H) && tf_fused_supported(H, cfg->mel_channels) &&
+                !std::getenv("M2_TF_UNFUSED");
+    if (m->tfused) {
+        size_t o = tf_off;
+        auto pack_up = [&](const std::string& n, int N, int K, const float** slot) -> hipError_t {
+            std::vector<float> w((size_t)N * K);
+            hipError_t er = hipMemcpyAsync(w.data(), weights[idx(n)], w.size() * sizeof(float), hipMemcpyDeviceToHost, st);
+            if (er == hipSuccess) er = hipStreamSynchronize(st);
+            if (er != hipSuccess) return er;
+            const std::vector<float> pk = pack_bfrag(w.data(), N, K);
+            er = hipMemcpyAsync(m->buf + o, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice, st);
+            if (er == hipSuccess) er = hipStreamSynchronize(st);
+            *slot = m->buf + o;
+            o += pk.size();
+            return er;
+        };
+        for (int i = 0; i < n_layers && e == hipSuccess; ++i) {
+            const bool is_enc = i < cfg->text_encoder_layers;
+            m2_layer_w& L = is_enc ? m->enc[i] : m->dec[i - cfg->text_encoder_layers];
+            const std::string p = (is_enc ? "text_encoder.layers." + std::to_string(i)
+                                          : "decoder.layers." + std::to_string(i - cfg->text_encoder_layers));
+            if (e == hipSuccess) e = pack_up(p + ".self_attn.qkv.weight", 3 * H, H, &L.qkv_p);
+            if (e == hipSuccess) e = pack_up(p + ".self_attn.out_proj.weight", H, H, &L.out_p);
+            if (e == hipSuccess) e = pack_up(p + ".ffn.linear1.weight", 2 * H, H, &L.ff1_p);
+            if (e == hipSuccess) e = pack_up(p + ".ffn.linear2.weight", H, 2 * H, &L.ff2_p);
+        }
+        if (e == hipSuccess) e = pack_up("decoder.mel_projection.weight", cfg->mel_channels, H, &m->mel_p);
+        if (e != hipSuccess) return bail(e, "pack transformer weights");
+    }
     m->enc_nw = P("text_encoder.norm.weight");
     m->enc_nb = P("text_encoder.norm.bias");
     for (int j = 0; j < 2; ++j) {
@@ -572,6 +618,9 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
         if ((rc = run_layer(m, L, cur, wb.x, wb, nullptr, B, T, st))) return rc;
         cur = wb.x;
     }
+    if (m->tfused)
+        return launch_ln_gemm(cur, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b, ACT_NONE, B * T, H, m->cfg.mel_channels,
+                              out_mel, st);
     return launch_linear(cur, m->dec_nw, m->dec_nb, m->mel_w, m->mel_b, nullptr, ACT_NONE, B * T, H,
                          m->cfg.mel_channels, out_mel, st);
 }

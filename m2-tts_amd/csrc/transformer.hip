@@ -168,6 +168,11 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 
 constexpr int ATT_KC = 64;  // keys per LDS chunk
 
+// Softmax in base 2: scores are carried as (q.k)*scale*log2(e) and
+// exponentiated with v_exp_f32 (exp2); a masked key's -1e9 becomes
+// -1e9*log2(e) (still exp -> 0, and equal across a fully masked row).
+constexpr float kLog2e = 1.4426950408889634f;
+
 template <int HD>
 __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv,
                                                         const uint8_t* __restrict__ key_mask,
@@ -177,16 +182,52 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     constexpr int KSTR = HD + 4;       // Ks row stride (floats)
     constexpr int VSTR = ATT_KC + 4;   // Vt row stride
     constexpr int NT = HD / 16;        // 16-wide d tiles
-    __shared__ __attribute__((aligned(16))) float Ks[ATT_KC * KSTR];
-    __shared__ __attribute__((aligned(16))) float Vt[HD * VSTR];
-    __shared__ float Mk[ATT_KC];
+    constexpr int IT = ATT_KC * (HD / 4) / 256;  // float4 of K (and of V) per thread per chunk
+    // Two chunk buffers: chunk c+1 is fetched into registers while chunk c is
+    // consumed, then stored into the other buffer - one barrier per chunk.
+    __shared__ __attribute__((aligned(16))) float Ks[2][ATT_KC * KSTR];
+    __shared__ __attribute__((aligned(16))) float Vt[2][HD * VSTR];
+    __shared__ float Mk[2][ATT_KC];
     const int b = blockIdx.z, hh = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, g = lane >> 4;
     const size_t row3 = (size_t)3 * H;
     const float* base = qkv + (size_t)b * N * row3 + hh * HD;
     const int qi = blockIdx.x * 64 + wave * 16 + li;
+    const float sl2 = scale * kLog2e;
 
+    float4 kr[IT], vr[IT];
+    float mkr = 0.f;
+    auto fetch = [&](int j0) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256, key = i / (HD / 4), d4 = i - key * (HD / 4), j = j0 + key;
+            kr[it] = vr[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j < N) {
+                kr[it] = *reinterpret_cast<const float4*>(base + j * row3 + H + 4 * d4);
+                vr[it] = *reinterpret_cast<const float4*>(base + j * row3 + 2 * H + 4 * d4);
+            }
+        }
+        if (tid < ATT_KC) {
+            const int j = j0 + tid;
+            // 0: live key, 1: masked (score -1e9), 2: past the end (weight 0)
+            mkr = j >= N ? 2.f : ((key_mask && key_mask[(size_t)b * N + j] == 0) ? 1.f : 0.f);
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256, key = i / (HD / 4), d4 = i - key * (HD / 4);
+            *reinterpret_cast<float4*>(&Ks[buf][key * KSTR + 4 * d4]) = kr[it];
+            Vt[buf][(4 * d4 + 0) * VSTR + key] = vr[it].x;
+            Vt[buf][(4 * d4 + 1) * VSTR + key] = vr[it].y;
+            Vt[buf][(4 * d4 + 2) * VSTR + key] = vr[it].z;
+            Vt[buf][(4 * d4 + 3) * VSTR + key] = vr[it].w;
+        }
+        if (tid < ATT_KC) Mk[buf][tid] = mkr;
+    };
+
+    fetch(0);
     float4 q[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -196,38 +237,25 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
+    stash(0);
+    __syncthreads();
 
-    for (int j0 = 0; j0 < N; j0 += ATT_KC) {
-        __syncthreads();
-        for (int i = tid; i < ATT_KC * (HD / 4); i += 256) {
-            const int key = i / (HD / 4), d4 = i - key * (HD / 4);
-            const int j = j0 + key;
-            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
-            if (j < N) {
-                kv = *reinterpret_cast<const float4*>(base + j * row3 + H + 4 * d4);
-                vv = *reinterpret_cast<const float4*>(base + j * row3 + 2 * H + 4 * d4);
-            }
-            *reinterpret_cast<float4*>(Ks + key * KSTR + 4 * d4) = kv;
-            Vt[(4 * d4 + 0) * VSTR + key] = vv.x;
-            Vt[(4 * d4 + 1) * VSTR + key] = vv.y;
-            Vt[(4 * d4 + 2) * VSTR + key] = vv.z;
-            Vt[(4 * d4 + 3) * VSTR + key] = vv.w;
-        }
-        if (tid < ATT_KC) {
-            const int j = j0 + tid;
-            // 0: live key, 1: masked (score -1e9), 2: past the end (weight 0)
-            Mk[tid] = j >= N ? 2.f : ((key_mask && key_mask[(size_t)b * N + j] == 0) ? 1.f : 0.f);
-        }
-        __syncthreads();
-
-        float s[4][4];  // [16-key block][r]: key 16*kb + 4*g + r of query li
+    const int nch = (N + ATT_KC - 1) / ATT_KC;
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nch) fetch((c + 1) * ATT_KC);
+        const float* K = Ks[buf];
+        const float* V = Vt[buf];
+        const float* MK = Mk[buf];
+        float s[4][4];  // [16-key block][r]: key 16*kb + 4*g + r of query li (base-2 scores)
         float cmax = -INFINITY;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
             f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const float4 a = *reinterpret_cast<const float4*>(Ks + (16 * kb + li) * KSTR + 16 * t + 4 * g);
+                const float4 a = *reinterpret_cast<const float4*>(K + (16 * kb + li) * KSTR + 16 * t + 4 * g);
                 st = mfma16(a.x, q[t].x, st);
                 st = mfma16(a.y, q[t].y, st);
                 st = mfma16(a.z, q[t].z, st);
@@ -235,16 +263,16 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float mk = Mk[16 * kb + 4 * g + r];
-                const float v = st[r] * scale;
-                s[kb][r] = mk == 0.f ? v : (mk == 1.f ? kMaskFill : -INFINITY);
+                const float mk = MK[16 * kb + 4 * g + r];
+                const float v = st[r] * sl2;
+                s[kb][r] = mk == 0.f ? v : (mk == 1.f ? kMaskFill * kLog2e : -INFINITY);
                 cmax = fmaxf(cmax, s[kb][r]);
             }
         }
         cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
         cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
         const float mn = fmaxf(m, cmax);
-        const float corr = expf(m - mn);  // m = -inf on the first chunk -> 0
+        const float corr = exp2f(m - mn);  // m = -inf on the first chunk -> 0
         lsum *= corr;
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] *= corr;
@@ -252,12 +280,12 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
         for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                s[kb][r] = expf(s[kb][r] - mn);
+                s[kb][r] = exp2f(s[kb][r] - mn);
                 lsum += s[kb][r];
             }
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const float4 v = *reinterpret_cast<const float4*>(Vt + (16 * t + li) * VSTR + 16 * kb + 4 * g);
+                const float4 v = *reinterpret_cast<const float4*>(V + (16 * t + li) * VSTR + 16 * kb + 4 * g);
                 acc[t] = mfma16(v.x, s[kb][0], acc[t]);
                 acc[t] = mfma16(v.y, s[kb][1], acc[t]);
                 acc[t] = mfma16(v.z, s[kb][2], acc[t]);
@@ -265,6 +293,10 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
             }
         }
         m = mn;
+        if (c + 1 < nch) {
+            stash(buf ^ 1);  // the other buffer was last read in chunk c-1, before the previous barrier
+            __syncthreads();
+        }
     }
     lsum += __shfl_xor(lsum, 16);
     lsum += __shfl_xor(lsum, 32);

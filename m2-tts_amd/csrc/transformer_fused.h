@@ -1,0 +1,21 @@
+// Fused transformer-layer kernels (transformer_fused.hip).
+#pragma once
+#include <vector>
+
+#include "m2_common.h"
+
+namespace m2 {
+
+// Hidden sizes with fused-layer instantiations (N_out: output width of ln_gemm).
+bool tf_fused_supported(int H, int N_out);
+// W [N][K] row-major (nn.Linear.weight) -> B-fragment order for v_mfma_f32_16x16x4_f32.
+std::vector<float> pack_bfrag(const float* W, int N, int K);
+// y[R][N] = LN(x)[R][K] . W^T (+ bias); Wp from pack_bfrag.
+int32_t launch_ln_gemm(const float* x, const float* g, const float* b, const float* Wp, const float* bias, int act,
+                       int R, int K, int N, float* y, hipStream_t st);
+// y = o + FFN(LN2(o)), o = x + att . Wo^T + bo (packed Wo, W1, W2); y may alias x.
+int32_t launch_post_attn(const float* att, const float* x, const float* Wo, const float* bo, const float* g2,
+                         const float* b2n, const float* W1, const float* b1, const float* W2, const float* b2, int R,
+                         int H, float* y, hipStream_t st);
+
+}  // namespace m2

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--filter", default="")
     ap.add_argument("--json")
+    ap.add_argument("--traffic", help="write {kernel short name: HBM bytes per dispatch} (bench.py roofline.traffic)")
     a = ap.parse_args()
     res = {k: v for k, v in load(a.dir).items() if a.filter in k}
     for k, v in sorted(res.items()):
@@ -54,6 +55,13 @@ def main():
             print(f"   -> HBM bytes/dispatch (2xFETCH + WRITE): {rd + wr:.4g}  (read {rd:.4g}, write {wr:.4g})")
     if a.json:
         json.dump(res, open(a.json, "w"), indent=1)
+    if a.traffic:
+        tr = {}
+        for k, v in res.items():
+            if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+                short = k.split("(")[0].split("<")[0].split("::")[-1].strip()
+                tr[short] = round(2 * v["FETCH_SIZE"] * 1024 + v["WRITE_SIZE"] * 1024)
+        json.dump(tr, open(a.traffic, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
