@@ -190,6 +190,10 @@ int32_t m2_add_positional(const float* x, const float* pe, int32_t B, int32_t S,
 int32_t m2_profile_enable(m2_model* model, int32_t capacity);
 int32_t m2_profile_read(m2_model* model, float* ms_out, int32_t capacity, int32_t* n_out);
 int32_t m2_profile_disable(m2_model* model);
+/* Record event pairs only around the kernels whose bit is set (default all);
+ * m2_profile_read reports -1 for the others.  Every recorded event costs a
+ * few microseconds of pipeline drain between kernels. */
+int32_t m2_profile_select(m2_model* model, uint32_t kernel_mask);
 int32_t m2_profile_kernel_count(void);
 const char* m2_profile_kernel_name(int32_t index);
 /* The same kernel as launched by this model (symbol prefix = rocprofv3 name). */

@@ -156,6 +156,7 @@ struct m2_model {
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
     mutable int prof_calls = 0;
+    uint32_t prof_mask = ~0u;  // which kernels get an event pair (m2_profile_select)
 };
 
 using namespace m2;
@@ -641,7 +642,7 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
         const bool rec = (size_t)(call + 1) * kVocKernels <= m->prof_begin.size();
         if (rec) m->prof_calls++;
         auto mark = [&](int kidx, bool begin) {
-            if (!rec) return;
+            if (!rec || !((m->prof_mask >> kidx) & 1u)) return;
             const size_t slot = (size_t)call * kVocKernels + kidx;
             (void)hipEventRecord(begin ? m->prof_begin[slot] : m->prof_end[slot], st);
         };
@@ -749,8 +750,10 @@ int32_t m2_profile_enable(m2_model* m, int32_t capacity) {
     m2_profile_disable(m);
     for (int i = 0; i < capacity * kVocKernels; ++i) {
         hipEvent_t a, b;
-        M2_HIP(hipEventCreate(&a));
-        M2_HIP(hipEventCreate(&b));
+        // No system-scope fence: a default event writes back and invalidates
+        // L2 at every record, which costs the next kernel its warm weights.
+        M2_HIP(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+        M2_HIP(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
         m->prof_begin.push_back(a);
         m->prof_end.push_back(b);
     }
@@ -762,11 +765,19 @@ int32_t m2_profile_read(m2_model* m, float* ms_out, int32_t capacity, int32_t* n
     M2_CHECK_ARG(m && ms_out && n_out, "m2_profile_read: bad argument");
     const int n = std::min<int>(capacity, m->prof_calls * kVocKernels);
     for (int i = 0; i < n; ++i) {
+        ms_out[i] = -1.f;  // kernel not selected
+        if (!((m->prof_mask >> (i % kVocKernels)) & 1u)) continue;
         M2_HIP(hipEventSynchronize(m->prof_end[i]));
         M2_HIP(hipEventElapsedTime(&ms_out[i], m->prof_begin[i], m->prof_end[i]));
     }
     *n_out = n;
     m->prof_calls = 0;
+    return M2_OK;
+}
+
+int32_t m2_profile_select(m2_model* m, uint32_t kernel_mask) {
+    M2_CHECK_ARG(m, "m2_profile_select: null model");
+    m->prof_mask = kernel_mask;
     return M2_OK;
 }
 

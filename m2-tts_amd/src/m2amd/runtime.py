@@ -38,9 +38,30 @@ def weight_names(cfg: _lib.M2Config):
     return names
 
 
+# Structural changes (a parameter, buffer or submodule registered or replaced
+# anywhere) bump this generation; in-place updates (load_state_dict's copy_,
+# optimizer steps, param.data = ...) show up in the tensors' version counters
+# and storage pointers.  Walking state_dict() on every call cost ~150 us of
+# host time per forward - more than the vocoder's GPU time at B=32.
+_GEN = [0]
+
+
+def _bump(*_args):
+    _GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump)
+torch.nn.modules.module.register_module_buffer_registration_hook(_bump)
+torch.nn.modules.module.register_module_module_registration_hook(_bump)
+
+
 def state_key(module: torch.nn.Module) -> Tuple:
     """Identity of the weights as stored right now (storage + version counters)."""
-    return tuple((t.data_ptr(), t._version) for t in module.state_dict(keep_vars=True).values())
+    cache = module.__dict__.get("_m2_state_tensors")
+    if cache is None or cache[0] != _GEN[0] or cache[1] != id(module):
+        cache = (_GEN[0], id(module), list(module.state_dict(keep_vars=True).values()))
+        module.__dict__["_m2_state_tensors"] = cache
+    return (cache[0],) + tuple([(t.data_ptr(), t._version) for t in cache[2]])
 
 
 class HipModel:
