@@ -17,97 +17,93 @@
 namespace m2 {
 
 // ---------------------------------------------------------------------------
-// One workgroup per (utterance, 16-phoneme tile).  The encoder rows of the
-// tile plus a 2-phoneme halo each side are staged in LDS; conv1 is evaluated
-// on the tile +-1 (positions outside [0,S) are the zero padding conv2 sees),
-// conv2 on the tile, then the k=1 projection and softplus.  The encoder
-// output is read in its [B,S,H] layout (the reference's transpose(1,2) is a
-// view).  BatchNorm uses alpha = gamma/sqrt(var+eps), beta' = beta -
-// mean*alpha, the inference form PyTorch's CPU batch_norm evaluates.
-// Conv weights arrive packed [ci][k][co] (m2_model_create) and are staged in
-// LDS one layer at a time (3*H*H floats: 48 KiB at H=64, 108 KiB at H=96):
-// the inner loop is then LDS-only - lanes (consecutive co) read consecutive
-// weights, the activation rows are float4 broadcasts.  The whole predictor is
-// ~0.2 GFLOP at B=32, S=100; what matters is not waiting on L2 per FMA.
-constexpr int DUR_TS = 16;
+// One workgroup (4 waves) per (utterance, 30-phoneme tile).  Both k=3 convs
+// are GEMMs on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32): rows = 32
+// positions (two 16-row blocks), columns = 16 output channels per wave
+// (n-blocks nb = wave, wave+4, ...), K = (tap, channel) = 3H.  A = activation
+// rows in LDS (stride H+2: a ds_read_b32 half-wave of 16 rows x 2 k-lanes hits
+// 32 banks), B = conv weights packed in B-fragment order (m2_model_create;
+// L2-resident).  conv1 covers positions [s0-1, s0+31) so conv2 can produce
+// [s0, s0+30) (30 of its 32 rows; outside [0,S) conv1 stores the zero padding
+// conv2 sees).  Epilogue: +bias, BatchNorm (alpha = gamma/sqrt(var+eps),
+// beta' = beta - mean*alpha, the inference form PyTorch's CPU batch_norm
+// evaluates), ReLU.  Then the k=1 projection (one wave per phoneme) and
+// softplus.  The encoder output is read in its [B,S,H] layout (the
+// reference's transpose(1,2) is a view).
+constexpr int DUR_TS = 30;
 
-// out[p][co] (+)= sum_{ci in chunk, k} W[ci][k][co] * in[p + k][ci] for p in
-// [0, np), with the weight rows of channels [ci0, ci0 + cc) staged in Ws.
-__device__ __forceinline__ void dur_conv_chunk(const float* in, const float* Ws, int H, int np, int ci0,
-                                               int cc, bool first, float* out) {
-    for (int i = threadIdx.x; i < np * H; i += 256) {
-        const int p = i / H, co = i - p * H;
-        const float* x0 = in + p * H + ci0;
-        const float* w0 = Ws + co;
-        float acc = first ? 0.f : out[i];
-        for (int ci = 0; ci < cc; ci += 4) {
-            const float4 u0 = *reinterpret_cast<const float4*>(x0 + ci);
-            const float4 u1 = *reinterpret_cast<const float4*>(x0 + H + ci);
-            const float4 u2 = *reinterpret_cast<const float4*>(x0 + 2 * H + ci);
-            acc = fmaf(w0[0], u0.x, acc); acc = fmaf(w0[H], u1.x, acc); acc = fmaf(w0[2 * H], u2.x, acc);
-            w0 += 3 * H;
-            acc = fmaf(w0[0], u0.y, acc); acc = fmaf(w0[H], u1.y, acc); acc = fmaf(w0[2 * H], u2.y, acc);
-            w0 += 3 * H;
-            acc = fmaf(w0[0], u0.z, acc); acc = fmaf(w0[H], u1.z, acc); acc = fmaf(w0[2 * H], u2.z, acc);
-            w0 += 3 * H;
-            acc = fmaf(w0[0], u0.w, acc); acc = fmaf(w0[H], u1.w, acc); acc = fmaf(w0[2 * H], u2.w, acc);
-            w0 += 3 * H;
+typedef float dur_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int H>
+__device__ __forceinline__ void dur_conv_mfma(const float* in, const float4* __restrict__ Wp,
+                                              const float* __restrict__ b, const float* __restrict__ a,
+                                              const float* __restrict__ c, float* out, int pos0, int S) {
+    constexpr int XS = H + 2;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    for (int nb = wave; nb < H / 16; nb += 4) {
+        const float4* wp = Wp + (size_t)nb * (3 * H / 16) * 64 + lane;
+        dur_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+        for (int tap = 0; tap < 3; ++tap) {
+            const float* x0 = in + (i + tap) * XS + g;
+            const float* x1 = x0 + 16 * XS;
+#pragma unroll
+            for (int s4 = 0; s4 < H / 16; ++s4) {
+                const float4 w = wp[(tap * (H / 16) + s4) * 64];
+                const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = (4 * s4 + q) * 4;
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[k], wv[q], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[k], wv[q], acc1, 0, 0, 0);
+                }
+            }
         }
-        out[i] = acc;
+        const int co = nb * 16 + i;
+        const float bb = b[co], aa = a[co], cc = c[co];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = rb * 16 + 4 * g + r, s = pos0 + row;
+                float v = ((rb ? acc1[r] : acc0[r]) + bb) * aa + cc;
+                v = v > 0.f ? v : 0.f;
+                out[row * XS + co] = (s >= 0 && s < S) ? v : 0.f;
+            }
     }
 }
 
-// One conv layer: weights streamed through LDS in chunks of `cc` input
-// channels (all of them at once for H <= 108), then bias, BN, ReLU, and zero
-// for rows whose position pos0 + p is outside [0, S).
-__device__ __forceinline__ void dur_conv(const float* in, float* Ws, const float* __restrict__ w, int H, int cc,
-                                         int np, int pos0, int S, const float* __restrict__ b,
-                                         const float* __restrict__ a, const float* __restrict__ c,
-                                         float* out) {
-    for (int ci0 = 0; ci0 < H; ci0 += cc) {
-        const int n = 3 * min(cc, H - ci0) * H;
-        const float* src = w + (size_t)ci0 * 3 * H;
-        __syncthreads();  // previous chunk's readers are done with Ws
-        for (int i = threadIdx.x * 4; i < n; i += 256 * 4)
-            *reinterpret_cast<float4*>(Ws + i) = *reinterpret_cast<const float4*>(src + i);
-        __syncthreads();
-        dur_conv_chunk(in, Ws, H, np, ci0, min(cc, H - ci0), ci0 == 0, out);
-    }
-    for (int i = threadIdx.x; i < np * H; i += 256) {
-        const int p = i / H, co = i - p * H, s = pos0 + p;
-        float v = (out[i] + b[co]) * a[co] + c[co];
-        v = v > 0.f ? v : 0.f;
-        out[i] = (s >= 0 && s < S) ? v : 0.f;
-    }
-}
-
+template <int H>
 __global__ __launch_bounds__(256) void duration_kernel(
-    const float* __restrict__ enc, int S, int H, int cc, const float* __restrict__ w1,
-    const float* __restrict__ b1, const float* __restrict__ a1, const float* __restrict__ c1,
-    const float* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ a2,
-    const float* __restrict__ c2, const float* __restrict__ pw, const float* __restrict__ pb,
-    float* __restrict__ dur) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* X = lds;                          // [TS+4][H]  s0-2 .. s0+TS+1
-    float* Y1 = X + (DUR_TS + 4) * H;        // [TS+2][H]  s0-1 .. s0+TS
-    float* Y2 = Y1 + (DUR_TS + 2) * H;       // [TS][H]    s0   .. s0+TS-1
-    float* Ws = Y2 + DUR_TS * H;             // [3*cc][H]  weight chunk
+    const float* __restrict__ enc, int S, const float4* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ a1, const float* __restrict__ c1, const float4* __restrict__ w2,
+    const float* __restrict__ b2, const float* __restrict__ a2, const float* __restrict__ c2,
+    const float* __restrict__ pw, const float* __restrict__ pb, float* __restrict__ dur) {
+    constexpr int XS = H + 2;
+    __shared__ float X[34 * XS];   // positions s0-2 .. s0+31
+    __shared__ float Y1[34 * XS];  // s0-1 .. s0+30 (+2 spare rows read by conv2's unused rows)
+    __shared__ float Y2[32 * XS];  // s0 .. s0+29 (+2 unused)
     const int b = blockIdx.y, s0 = blockIdx.x * DUR_TS, tid = threadIdx.x;
     const float* e = enc + (size_t)b * S * H;
-
-    for (int i = tid; i < (DUR_TS + 4) * H; i += 256) {
-        const int p = i / H, c = i - p * H, s = s0 - 2 + p;
-        X[i] = (s >= 0 && s < S) ? e[(size_t)s * H + c] : 0.f;
+    for (int idx = tid; idx < 34 * (H / 4); idx += 256) {
+        const int p = idx / (H / 4), c4 = (idx - p * (H / 4)) * 4, s = s0 - 2 + p;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s >= 0 && s < S) v = *reinterpret_cast<const float4*>(e + (size_t)s * H + c4);
+        float* d = X + p * XS + c4;
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
-    dur_conv(X, Ws, w1, H, cc, DUR_TS + 2, s0 - 1, S, b1, a1, c1, Y1);
-    dur_conv(Y1, Ws, w2, H, cc, DUR_TS, s0, S, b2, a2, c2, Y2);
+    for (int idx = tid; idx < 2 * XS; idx += 256) Y1[32 * XS + idx] = 0.f;
+    __syncthreads();
+    dur_conv_mfma<H>(X, w1, b1, a1, c1, Y1, s0 - 1, S);
+    __syncthreads();
+    dur_conv_mfma<H>(Y1, w2, b2, a2, c2, Y2, s0, S);
     __syncthreads();
     // k=1 projection H -> 1: one wave per phoneme, shuffle reduction.
     const int lane = tid & 63, wave = tid >> 6;
     for (int p = wave; p < DUR_TS; p += 4) {
         const int s = s0 + p;
         float acc = 0.f;
-        for (int ci = lane; ci < H; ci += 64) acc = fmaf(pw[ci], Y2[p * H + ci], acc);
+        for (int ci = lane; ci < H; ci += 64) acc = fmaf(pw[ci], Y2[p * XS + ci], acc);
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0 && s < S) {
             const float x = acc + pb[0];
@@ -188,23 +184,24 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur,
-                        hipStream_t st) {
+// p: w1 (packed), b1, alpha1, beta1, w2 (packed), b2, alpha2, beta2, proj_w, proj_b
+int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st) {
     if (B == 0 || S == 0) return M2_OK;
-    // LDS: activations (3*TS+6)*H + a weight chunk of cc input channels 3*cc*H.
-    const size_t act = (size_t)(3 * DUR_TS + 6) * H;
-    const size_t room = 160 * 1024 / sizeof(float);
-    M2_CHECK_SHAPE(H % 4 == 0 && act + 12 * (size_t)H <= room, "duration: hidden_dim must be a multiple of 4 and <= 630");
-    const int cc = (int)std::min<size_t>((size_t)H, (room - act) / (3 * (size_t)H) / 4 * 4);
-    const size_t lds = sizeof(float) * (act + 3 * (size_t)cc * H);
-    static bool attr_set = false;
-    if (!attr_set) {
-        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(duration_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
+    const dim3 grid(cdiv(S, DUR_TS), B), blk(256);
+    auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
+#define M2_DUR(HH)                                                                                              \
+    case HH:                                                                                                    \
+        hipLaunchKernelGGL(duration_kernel<HH>, grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], p[3], f4(p[4]), \
+                           p[5], p[6], p[7], p[8], p[9], dur);                                                  \
+        break;
+    switch (H) {
+        M2_DUR(32)
+        M2_DUR(64)
+        M2_DUR(96)
+        M2_DUR(128)
+        default: return fail(M2_E_SHAPE, "duration: hidden_dim must be 32, 64, 96 or 128");
     }
-    hipLaunchKernelGGL(duration_kernel, dim3(cdiv(S, DUR_TS), B), dim3(256), lds, st, enc, S, H, cc,
-                       p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9], dur);
+#undef M2_DUR
     M2_LAUNCHED("duration_kernel");
     return M2_OK;
 }

@@ -290,7 +290,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     const size_t bn_off = total;
     total += 4 * (size_t)H;
     total = align_up(total, 64);
-    const size_t dw_off = total;  // duration conv weights re-laid out [ci][k][co], 2 layers
+    const size_t dw_off = total;  // duration conv weights, B-fragment order, 2 layers
     total += 2 * 3 * (size_t)H * H;
     total = align_up(total, 64);
     const size_t tf_off = total;  // fused-layer B-fragment packs: 8H^2 per layer + mel projection
@@ -338,17 +338,19 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             host[(2 * j + 1) * H + c] = bnb[c] - bnm[c] * a;
         }
     }
+    // Duration convs: W[co][ci][tap] -> GEMM B matrix [co][tap*H + ci] -> B-fragment order.
     std::vector<float> dpack(2 * 3 * (size_t)H * H);
     for (int j = 0; j < 2; ++j) {
         const std::string n = "duration_predictor.predictor.conv_layers." + std::to_string(j) + ".conv.weight";
-        std::vector<float> w((size_t)3 * H * H);
+        std::vector<float> w((size_t)3 * H * H), wt((size_t)3 * H * H);
         e = hipMemcpyAsync(w.data(), weights[idx(n)], w.size() * sizeof(float), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return bail(e, "hipMemcpyAsync(duration conv)");
         for (int co = 0; co < H; ++co)
             for (int ci = 0; ci < H; ++ci)
-                for (int k = 0; k < 3; ++k)
-                    dpack[(size_t)j * 3 * H * H + ((size_t)ci * 3 + k) * H + co] = w[((size_t)co * H + ci) * 3 + k];
+                for (int k = 0; k < 3; ++k) wt[(size_t)co * 3 * H + k * H + ci] = w[((size_t)co * H + ci) * 3 + k];
+        const std::vector<float> pk = pack_bfrag(wt.data(), H, 3 * H);
+        std::copy(pk.begin(), pk.end(), dpack.begin() + (size_t)j * 3 * H * H);
     }
     e = hipMemcpyAsync(m->buf + dw_off, dpack.data(), dpack.size() * sizeof(float), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return bail(e, "hipMemcpyAsync(duration pack)");

@@ -348,3 +348,17 @@ def test_vocoder_arithmetic_paths(gpu, stage, monkeypatch):
         assert rms(out[path], ref) <= AUDIO_RMS_TOL
         assert maxabs(out[path], ref) <= 1e-4
     assert maxabs(out[1], out[2]) <= 1e-4
+
+
+@pytest.mark.parametrize("stage", STAGES)
+@pytest.mark.parametrize("env", ["M2_TF_UNFUSED", "M2_VOCODER_PERLAYER"])
+def test_alternate_kernel_paths(gpu, stage, env, monkeypatch):
+    """The unfused transformer layer (five linears) and the per-layer vocoder
+    kernels stay parity-green: inference vs the reference's fixture."""
+    monkeypatch.setenv(env, "1")
+    g = golden(f"{stage}_small")
+    m = build_model(stage, gpu)
+    ids, lens = _ids(g, gpu)
+    mel, audio = m.inference(ids, lens)
+    assert maxabs(mel, g["mel"]) <= MEL_MAXABS_TOL
+    assert rms(audio, g["audio"]) <= AUDIO_RMS_TOL
