@@ -153,6 +153,8 @@ struct m2_model {
     void* xbuf = nullptr;
     m2::VocX vx{};
     bool x3 = false;
+    void* tbuf = nullptr;  // pipelined stage1 tail pack (vx.tp / vx.tpb)
+    bool tailp = false;
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
     mutable int prof_calls = 0;
@@ -523,6 +525,45 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 m->vx.wo = m->vw.wo;
                 m->vx.bo = m->vw.bo;
                 m->x3 = true;
+                // stage1: the last two upsampling stages as one pipelined
+                // kernel (M2_VOC_TAIL_X3=1 keeps the x3 tail kernel).
+                if (M == 64 && C == 128 && !std::getenv("M2_VOC_TAIL_X3")) {
+                    const char* names[14] = {
+                        "vocoder.upsamples.2.weight",         "vocoder.upsamples.2.bias",
+                        "vocoder.resblocks.2.conv1.weight", "vocoder.resblocks.2.conv1.bias",
+                        "vocoder.resblocks.2.conv2.weight", "vocoder.resblocks.2.conv2.bias",
+                        "vocoder.upsamples.3.weight",         "vocoder.upsamples.3.bias",
+                        "vocoder.resblocks.3.conv1.weight", "vocoder.resblocks.3.conv1.bias",
+                        "vocoder.resblocks.3.conv2.weight", "vocoder.resblocks.3.conv2.bias",
+                        "vocoder.output_conv.weight",         "vocoder.output_conv.bias"};
+                    std::vector<float> hw[14];
+                    bool got = true;
+                    for (int i = 0; i < 14; ++i) got = got && !(hw[i] = fetch(names[i])).empty();
+                    const TailpSrc src{hw[0].data(), hw[1].data(), hw[2].data(),  hw[3].data(),  hw[4].data(),
+                                       hw[5].data(), hw[6].data(), hw[7].data(),  hw[8].data(),  hw[9].data(),
+                                       hw[10].data(), hw[11].data(), hw[12].data(), hw[13].data()};
+                    std::vector<uint16_t> pw;
+                    std::vector<float> pb;
+                    bool rok = true;
+                    if (got && pack_tailp(src, &pw, &pb, &rok) && rok) {
+                        const size_t wb = pw.size() * sizeof(uint16_t);
+                        e = hipMalloc(&m->tbuf, wb + pb.size() * sizeof(float));
+                        if (e == hipSuccess) e = hipMemcpyAsync(m->tbuf, pw.data(), wb, hipMemcpyHostToDevice, st);
+                        if (e == hipSuccess)
+                            e = hipMemcpyAsync(static_cast<char*>(m->tbuf) + wb, pb.data(), pb.size() * sizeof(float),
+                                               hipMemcpyHostToDevice, st);
+                        if (e == hipSuccess) e = hipStreamSynchronize(st);
+                        if (e != hipSuccess) {
+                            (void)hipFree(m->vbuf);
+                            (void)hipFree(m->xbuf);
+                            if (m->tbuf) (void)hipFree(m->tbuf);
+                            return bail(e, "upload tailp pack");
+                        }
+                        m->vx.tp = static_cast<const vx_u32x4*>(m->tbuf);
+                        m->vx.tpb = reinterpret_cast<const float*>(static_cast<char*>(m->tbuf) + wb);
+                        m->tailp = true;
+                    }
+                }
             }
         }
     }
@@ -537,6 +578,7 @@ int32_t m2_model_destroy(m2_model* model) {
     m2_profile_disable(model);
     if (model->vbuf) (void)hipFree(model->vbuf);
     if (model->xbuf) (void)hipFree(model->xbuf);
+    if (model->tbuf) (void)hipFree(model->tbuf);
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -739,6 +781,7 @@ const char* m2_profile_kernel_name(int32_t index) {
 
 const char* m2_profile_kernel_name_for(const m2_model* m, int32_t index) {
     if (!m || index < 0 || index >= kVocKernels) return "";
+    if (m->tailp && index == 2) return kVocTailpKernelName;
     return m->x3 ? kVocX3KernelNames[index] : kVocKernelNames[index];
 }
 

@@ -50,7 +50,54 @@ struct VocX {
     const vx_u32x4* w2[4];
     const float* b2[4];
     const float *wo, *bo;
+    // pipelined stage1 tail (vocoder_tailp.hip); null = the x3 tail kernel
+    const vx_u32x4* tp;
+    const float* tpb;
 };
+
+// Pipelined stage1 tail (vocoder_tailp.hip): ConvT3, ResBlock3, ConvT4,
+// ResBlock4 and output_conv in polyphase form over the columns q of U2.
+// Layer l (0..6) has nmb(l) m-blocks of 16 rows and nkb(l) k-blocks of 32;
+// kslot(l, mb, kb, g) is what lane group g reads in k-block kb: ring (0 = the
+// layer's input, 1 = the residual ring), column offset dq, input octet; pad
+// slots carry zero weights.  The same table packs the weights (host) and
+// addresses the B fragments (device).
+namespace tp {
+struct Slot {
+    int res, dq, oct, pad;
+};
+constexpr int kLayers = 7, kUnits = 22;
+constexpr int nmb(int l) { return l == 6 ? 1 : 2; }
+constexpr int nkb(int l) { return (l == 4 || l == 5) ? 1 : 2; }
+constexpr int unit0(int l) { return l <= 4 ? 4 * l : (l == 5 ? 18 : 20); }
+constexpr Slot kslot(int l, int mb, int kb, int g) {
+    if (l == 4 || l == 5)  // k3 on 4 phases of 8 channels: rows (p, p+1) read phases p-1 .. p+2
+        return mb == 0 ? (g == 0 ? Slot{0, -1, 3, 0} : Slot{0, 0, g - 1, 0})
+                       : (g == 3 ? Slot{0, 1, 0, 0} : Slot{0, 0, g + 1, 0});
+    if (l == 0)  // ConvT3: phase 0 reads columns q and q-1, phase 1 reads q+1 and q
+        return Slot{0, mb == 0 ? (kb == 0 ? 0 : -1) : (kb == 0 ? 1 : 0), g, 0};
+    if (kb == 0) return Slot{0, 0, g, 0};  // the whole column q
+    if (g < 2) {
+        if (l == 6)  // output conv: phase 0 also reads (q-1, phase 3), phase 3 (q+1, phase 0)
+            return g == 0 ? Slot{0, -1, 3, 0} : Slot{0, 1, 0, 0};
+        // 2 phases of 16 channels: phase 0 also reads (q-1, phase 1), phase 1 (q+1, phase 0)
+        return mb == 0 ? Slot{0, -1, 2 + g, 0} : Slot{0, 1, g, 0};
+    }
+    if (l == 2) return Slot{1, 0, 2 * mb + (g - 2), 0};  // ResBlock3 residual x (identity weights)
+    return Slot{0, 0, g, 1};  // pad: a distinct octet per lane group keeps the read conflict-free
+}
+}  // namespace tp
+
+// Raw fp32 reference weights of the five tail modules (host pointers).
+struct TailpSrc {
+    const float *wt3, *bt3, *w31, *b31, *w32, *b32, *wt4, *bt4, *w41, *b41, *w42, *b42, *wo, *bo;
+};
+// false when a layer's non-zero weights do not fit the slot table (cannot
+// happen for the stage1 shapes; the x3 tail is kept then).
+bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
+int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
+                             hipStream_t st);
+extern const char* const kVocTailpKernelName;
 
 bool vocoder_x3_supported(int M, int C);
 int vocoder_x3_mel_pad(int M);  // input-conv channel count after padding to the k-block layout

@@ -1,0 +1,427 @@
+// Pipelined SimpleVocoder tail for stage1 (tts_model.py:279-297, the last two
+// upsampling stages): ConvT3 (32 -> 16, x2) + leaky, ResBlock3, ConvT4
+// (16 -> 8, x2) + leaky, ResBlock4, output_conv (8 -> 1) + tanh, with the
+// split-f16 arithmetic of vocoder_x3.hip (every fp32 operand as f16 hi/lo,
+// three v_mfma_f32_16x16x32_f16 per product, fp32 accumulate).
+//
+// Polyphase form.  Everything is indexed by the column q of the tail's input
+// U2 (32 channels at 16T).  ConvT3's output u3 (16 channels at t3 = 2q + p3)
+// is stored as a 32-row column (p3, channel); ConvT4's output u4 (8 channels
+// at t4 = 4q + p4) as a 32-row column (p4, channel); the audio as a 4-row
+// column.  In this form every layer is a k3-over-q convolution with 32 output
+// rows = two 16-row m-blocks, whose K is a list of (dq, input octet) slots
+// (tp::kslot): a k=3 conv on a P-phase signal reads tap t+d at column
+// q + floor((p+d)/P), phase (p+d) mod P.  The 8-channel layers fill all 16
+// rows of an m-block (two phases), where the natural layout fills 8.
+//
+// Systolic pipeline.  One workgroup owns a strip of 16*NCH columns of one
+// utterance and runs 14 waves with fixed roles: a loader wave streams U2 into
+// an LDS ring, and each of the 7 layers is done by one wave per m-block, all with
+// their weights (2 KB per (m-block, k-block) fragment pair) and biases held in
+// VGPRs for the whole strip.  In step s the wave of layer l computes chunk
+// k = s - l - 1 (16 columns) from the ring its producer wrote in steps s-1 and
+// s-2; one s_barrier per step.  Rings hold 4 chunks (64 columns), so a
+// producer writing chunk k+1 never meets its consumer reading chunks k and
+// k-1 (or a residual reader two chunks behind).  Layer l's chunk k covers
+// columns [qa + 6 - l + 16k, +16): each layer lags its input by one column,
+// the receptive field of its k3 taps, so chunk k of layer l+1 needs exactly
+// chunks k and k-1 of layer l.  Chunk -1 is the warm-up: its leftmost columns
+// read never-written ring rows and are garbage, but an MFMA output column
+// depends on its own B column only, and layer l is valid from column
+// qa - 8 + l of chunk -1 on while later layers need it from qa - 6 + l.
+// Columns outside [0, L2) store 0 (the next conv's zero padding).
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "m2_common.h"
+#include "vocoder_fused.h"
+
+namespace m2 {
+namespace tp {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef vx_u32x4 u32x4;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr float kLoS = 2048.f, kLoI = 1.f / 2048.f;
+constexpr int RS = 160;           // ring row stride: 128 B (hi[32] lo[32]) + pad, RS/16 = 2 mod 4
+constexpr int RROWS = 64;         // 4 chunks of 16 columns
+constexpr int RING = RROWS * RS;  // bytes per ring
+constexpr int NRING = 7;          // R0 = U2 input, R(l+1) = output of layer l (l = 0..5)
+constexpr int LDS_BYTES = NRING * RING;
+constexpr int NWAVES = 14;        // 13 layer waves (one m-block each) + 1 loader
+
+__device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+// LDS hand-off between roles: the step's ds_writes complete, then the
+// workgroup barrier.  No vmcnt wait (the loader's prefetches stay in flight),
+// and the "memory" clobber keeps the compiler from moving LDS accesses across.
+__device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Diagnostic build only (-DM2_STAMPS): per-wave s_memtime at the start of
+// every step (after the barrier) and before its barrier, [workgroup][wave]
+// [step + 1][2]; [62] kernel entry, [63] exit (tools/probe/stamps_tailp.py).
+#ifdef M2_STAMPS
+__device__ unsigned long long g_tp_stamps[1024][NWAVES][64][2];
+#define TPSTAMP(i, j)                                                                                  \
+    do {                                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        unsigned long long _t;                                                                         \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        const int _wg = blockIdx.y * gridDim.x + blockIdx.x;                                           \
+        if ((threadIdx.x & 63) == 0 && _wg < 1024) g_tp_stamps[_wg][threadIdx.x >> 6][(i)][(j)] = _t; \
+    } while (0)
+#else
+#define TPSTAMP(i, j) \
+    do {              \
+    } while (0)
+#endif
+
+// tanh(x) = 1 - 2 / (1 + e^{2x}) on v_exp_f32 / v_rcp_f32: absolute error
+// ~1e-7 (saturates to +-1 through inf / 0), against ~40 instructions for tanhf.
+__device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * x)); }
+
+__device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const _Float16 h = (_Float16)v[r];
+        hi[r] = h;
+        lo[r] = (_Float16)((v[r] - (float)h) * kLoS);
+    }
+}
+
+template <int L, int MB0, int NMB, int NCH>
+__device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
+                                           const u32x4* __restrict__ W, const float* __restrict__ bias,
+                                           float* __restrict__ arow) {
+    constexpr int NKB = nkb(L);
+    constexpr int ACT = (L == 2 || L == 5) ? ACT_NONE : ACT_LEAKY;  // layer 6: tanh below
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    u32x4 a[NMB][NKB][2];
+    float bv[NMB][4];
+    int roff[NMB][NKB], boff[NMB][NKB];
+#pragma unroll
+    for (int m = 0; m < NMB; ++m) {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            const int u = unit0(L) + (MB0 + m) * NKB + kb;
+            a[m][kb][0] = W[u * 128 + lane];
+            a[m][kb][1] = W[u * 128 + 64 + lane];
+            const Slot sl = kslot(L, MB0 + m, kb, g);
+            // input ring R(L) holds layer L-1's columns, one column ahead of
+            // layer L's; the residual ring R1 (layer 2 only) two columns ahead.
+            roff[m][kb] = sl.dq - (sl.res ? 2 : 1);
+            boff[m][kb] = (sl.res ? 1 : L) * RING + sl.oct * 16;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 32 + (MB0 + m) * 16 + 4 * g + r];
+    }
+    const int sL = qa + 6 - L;
+#pragma unroll 1
+    for (int s = -1; s < NCH + 7; ++s) {
+        TPSTAMP(s + 1, 0);
+        const int k = s - (L + 1);
+        if (k >= -1 && k < NCH) {
+            u32x4 bh[NMB][NKB], bl[NMB][NKB];
+#pragma unroll
+            for (int m = 0; m < NMB; ++m)
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb) {
+                    const int row = (16 * k + li + roff[m][kb]) & (RROWS - 1);
+                    const unsigned char* p = lds + boff[m][kb] + row * RS;
+                    bh[m][kb] = *reinterpret_cast<const u32x4*>(p);
+                    bl[m][kb] = *reinterpret_cast<const u32x4*>(p + 64);
+                }
+            f32x4 acc[NMB], cor[NMB];
+#pragma unroll
+            for (int m = 0; m < NMB; ++m) {
+                acc[m] = f32x4{bv[m][0], bv[m][1], bv[m][2], bv[m][3]};
+                cor[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+                    acc[m] = mfma_h(a[m][kb][0], bh[m][kb], acc[m]);
+                    cor[m] = mfma_h(a[m][kb][0], bl[m][kb], cor[m]);
+                    cor[m] = mfma_h(a[m][kb][1], bh[m][kb], cor[m]);
+                }
+            const int x = sL + 16 * k + li;  // this lane's column
+            if constexpr (L == 6) {
+                // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
+                if (g == 0 && k >= 0 && x >= 0 && x < L2) {
+                    float4 o;
+                    o.x = tanh_fast(fmaf(cor[0][0], kLoI, acc[0][0]));
+                    o.y = tanh_fast(fmaf(cor[0][1], kLoI, acc[0][1]));
+                    o.z = tanh_fast(fmaf(cor[0][2], kLoI, acc[0][2]));
+                    o.w = tanh_fast(fmaf(cor[0][3], kLoI, acc[0][3]));
+                    *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
+                }
+            } else {
+                const bool zero = edge && (x < 0 || x >= L2);
+                const int orow = (16 * k + li) & (RROWS - 1);
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(fmaf(cor[m][r], kLoI, acc[m][r]));
+                    const int cbyte = 2 * (16 * (MB0 + m) + 4 * g);
+                    if constexpr (L == 5) {  // ResBlock4 residual: u4 (R4) two columns ahead
+                        const unsigned char* xp = lds + 4 * RING + ((16 * k + li - 2) & (RROWS - 1)) * RS + cbyte;
+                        const h4 xh = *reinterpret_cast<const h4*>(xp), xl = *reinterpret_cast<const h4*>(xp + 64);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] += fmaf((float)xl[r], kLoI, (float)xh[r]);
+                    }
+                    if (zero) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = 0.f;
+                    }
+                    h4 hi, lo;
+                    split4(v, hi, lo);
+                    // Lane groups 0/1 (and 2/3) hold channels 0-3 / 4-7 (8-11 /
+                    // 12-15) of the m-block; one permlane16 swap per dword gives
+                    // group 0 the hi octet of channels 0-7 and group 1 its lo
+                    // octet (groups 2/3: channels 8-15), so each lane stores one
+                    // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
+                    // 8-B halves (ds_write_b64, 4-way).
+                    u32x2 hv = __builtin_bit_cast(u32x2, hi), lv = __builtin_bit_cast(u32x2, lo);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const auto sw = __builtin_amdgcn_permlane16_swap(hv[j], lv[j], false, false);
+                        hv[j] = sw[0];
+                        lv[j] = sw[1];
+                    }
+                    unsigned char* op = lds + (L + 1) * RING + orow * RS + 32 * (MB0 + m) + 64 * (g & 1) + 16 * (g >> 1);
+                    *reinterpret_cast<u32x4*>(op) = u32x4{hv[0], hv[1], lv[0], lv[1]};
+                }
+            }
+        }
+        TPSTAMP(s + 1, 1);
+        step_barrier();
+    }
+}
+
+// U2 rows (128 B: hi[32] lo[32], the mid kernel's output format) into ring R0,
+// two chunks ahead: chunk c = columns [qa + 7 + 16c, +16), zero outside [0, L2).
+template <int NCH>
+__device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, const unsigned char* __restrict__ u2) {
+    const int lane = threadIdx.x & 63, r = lane >> 3, pc = lane & 7;
+    // Every step issues its two loads unconditionally (column clamped into the
+    // utterance, zeroed when written) so the compiler can count them: the
+    // write of chunk s then waits with vmcnt(4) for its own loads only, not
+    // for the two younger chunks still in flight.
+    auto fetch = [&](int c, u32x4 (&v)[2]) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int col = min(max(qa + 7 + 16 * c + r + 8 * h, 0), L2 - 1);
+            v[h] = *reinterpret_cast<const u32x4*>(u2 + (size_t)col * 128 + pc * 16);
+        }
+    };
+    // Three register buffers used in rotation by a loop unrolled by three, so
+    // no register that a load in flight writes is ever copied (a copy would
+    // wait for that load).
+    u32x4 buf[3][2];
+    auto step = [&](int s, u32x4 (&cur)[2], u32x4 (&ahead)[2]) {
+        fetch(s + 2, ahead);
+        if (s < NCH) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int col = qa + 7 + 16 * s + r + 8 * h;
+                const bool in = col >= 0 && col < L2;
+                const u32x4 z{0u, 0u, 0u, 0u};
+                const int row = (16 * s + r + 8 * h) & (RROWS - 1);
+                *reinterpret_cast<u32x4*>(lds + row * RS + pc * 16) = in ? cur[h] : z;
+            }
+        }
+        step_barrier();
+    };
+    fetch(-1, buf[0]);
+    fetch(0, buf[1]);
+    int s = -1;
+#pragma unroll 1
+    for (; s + 2 <= NCH + 6; s += 3) {  // covers every step with work (s <= NCH - 1)
+        step(s, buf[0], buf[2]);
+        step(s + 1, buf[1], buf[0]);
+        step(s + 2, buf[2], buf[1]);
+    }
+#pragma unroll 1
+    for (; s <= NCH + 6; ++s) step_barrier();
+}
+
+template <int NCH>
+__global__ __launch_bounds__(NWAVES * 64, 7) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
+                                                                const u32x4* __restrict__ W,
+                                                                const float* __restrict__ bias,
+                                                                float* __restrict__ audio) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
+    float* arow = audio + (size_t)b * 4 * L2;
+    TPSTAMP(62, 0);
+    switch (w) {
+        case 0: layer_role<0, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 1: layer_role<0, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 2: layer_role<1, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 3: layer_role<1, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 4: layer_role<2, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 5: layer_role<2, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 6: layer_role<3, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 7: layer_role<3, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 8: layer_role<4, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 9: layer_role<4, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 10: layer_role<5, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 11: layer_role<5, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 12: layer_role<6, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        default: loader_role<NCH>(lds, qa, L2, U2 + (size_t)b * L2 * 128); break;
+    }
+    TPSTAMP(63, 0);
+}
+
+template <int NCH>
+int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp_kernel<NCH>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        attr = true;
+    }
+    hipLaunchKernelGGL((tailp_kernel<NCH>), dim3(cdiv(L2, 16 * NCH), B), dim3(NWAVES * 64), LDS_BYTES, st,
+                       static_cast<const unsigned char*>(U2), L2, W, bias, audio);
+    M2_LAUNCHED("tailp_kernel");
+    return M2_OK;
+}
+
+}  // namespace tp
+
+#ifdef M2_STAMPS
+extern "C" int32_t m2_debug_stamps_tailp(void* host, size_t bytes) {
+    return (int32_t)hipMemcpyFromSymbol(host, HIP_SYMBOL(tp::g_tp_stamps),
+                                        bytes < sizeof(tp::g_tp_stamps) ? bytes : sizeof(tp::g_tp_stamps));
+}
+#endif
+
+const char* const kVocTailpKernelName =
+    "tailp_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, pipelined)";
+
+int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
+                             hipStream_t st) {
+    if (B == 0 || L2 == 0) return M2_OK;
+    static const int nch = [] {
+        const char* e = std::getenv("M2_TAILP_NCH");
+        const int v = e ? std::atoi(e) : 32;
+        return (v == 16 || v == 64) ? v : 32;
+    }();
+    if (nch == 16) return tp::launch<16>(U2, L2, B, W, bias, audio, st);
+    if (nch == 64) return tp::launch<64>(U2, L2, B, W, bias, audio, st);
+    return tp::launch<32>(U2, L2, B, W, bias, audio, st);
+}
+
+// ---------------------------------------------------------------------------
+// Host packing.  Each layer is first written as a dense polyphase matrix
+// Wd[row][dq + 1][input row] (32 x 3 x 32), then cut into (m-block, k-block)
+// fragment pairs along tp::kslot: A[row = mb*16 + (lane&15)][slot g = lane>>4,
+// element e] = Wd[row][dq + 1][8*oct + e]; pad slots are zero, residual slots
+// (layer 2) the identity.  Every non-zero of Wd must sit on a slot.
+namespace {
+
+int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+struct Dense {
+    std::vector<float> w = std::vector<float>(32 * 3 * 32, 0.f);
+    float& at(int row, int dq, int in) { return w[(row * 3 + dq + 1) * 32 + in]; }
+};
+
+// ConvTranspose1d(k=4, stride 2, pad 1), W [Cin][Cout][4], on a Pin-phase input
+// (Cin channels per phase) -> 2*Pin phases of Cout channels (tts_model.py:255-263):
+// out[2i] = x[i] W1 + x[i-1] W3, out[2i+1] = x[i+1] W0 + x[i] W2.
+void dense_convT2(Dense& d, const float* W, int Pin, int Cin, int Cout) {
+    const int taps[2][2][2] = {{{0, 1}, {-1, 3}}, {{1, 0}, {0, 2}}};  // [s][j] = (input offset, kernel tap)
+    for (int pin = 0; pin < Pin; ++pin)
+        for (int s = 0; s < 2; ++s)
+            for (int j = 0; j < 2; ++j) {
+                const int pp = pin + taps[s][j][0], dq = floordiv(pp, Pin), p2 = pp - dq * Pin, kk = taps[s][j][1];
+                for (int co = 0; co < Cout; ++co)
+                    for (int ci = 0; ci < Cin; ++ci)
+                        d.at((2 * pin + s) * Cout + co, dq, p2 * Cin + ci) += W[((size_t)ci * Cout + co) * 4 + kk];
+            }
+}
+
+// Conv1d(k=3, pad 1), W [Cout][Cin][3], on a P-phase signal.
+void dense_conv3(Dense& d, const float* W, int P, int Cin, int Cout) {
+    for (int p = 0; p < P; ++p)
+        for (int k = 0; k < 3; ++k) {
+            const int pp = p + k - 1, dq = floordiv(pp, P), p2 = pp - dq * P;
+            for (int co = 0; co < Cout; ++co)
+                for (int ci = 0; ci < Cin; ++ci) d.at(p * Cout + co, dq, p2 * Cin + ci) += W[((size_t)co * Cin + ci) * 3 + k];
+        }
+}
+
+void put_split(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) {
+    if (!(std::fabs(v) < 65504.f)) *range_ok = false;
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)((v - (float)h) * 2048.f);
+    uint16_t hb, lb;
+    std::memcpy(&hb, &h, 2);
+    std::memcpy(&lb, &l, 2);
+    out[idx] = hb;
+    out[idx + 64 * 8] = lb;
+}
+
+}  // namespace
+
+bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
+    Dense d[tp::kLayers];
+    dense_convT2(d[0], s.wt3, 1, 32, 16);
+    dense_conv3(d[1], s.w31, 2, 16, 16);
+    dense_conv3(d[2], s.w32, 2, 16, 16);
+    dense_convT2(d[3], s.wt4, 2, 16, 8);
+    dense_conv3(d[4], s.w41, 4, 8, 8);
+    dense_conv3(d[5], s.w42, 4, 8, 8);
+    dense_conv3(d[6], s.wo, 4, 8, 1);
+    const int nrows[tp::kLayers] = {32, 32, 32, 32, 32, 32, 4};
+    for (int l = 0; l < tp::kLayers; ++l)
+        for (int row = 0; row < 32; ++row)
+            for (int dq = -1; dq <= 1; ++dq)
+                for (int in = 0; in < 32; ++in) {
+                    if (d[l].at(row, dq, in) == 0.f) continue;
+                    bool missing = row < nrows[l];
+                    for (int kb = 0; missing && kb < tp::nkb(l); ++kb)
+                        for (int g = 0; g < 4; ++g) {
+                            const tp::Slot sl = tp::kslot(l, row / 16, kb, g);
+                            if (!sl.pad && !sl.res && sl.dq == dq && sl.oct == in / 8) missing = false;
+                        }
+                    if (missing) return false;  // a non-zero weight that no slot reads
+                }
+    wout->assign((size_t)tp::kUnits * 2 * 64 * 8, 0);
+    for (int l = 0; l < tp::kLayers; ++l)
+        for (int mb = 0; mb < tp::nmb(l); ++mb)
+            for (int kb = 0; kb < tp::nkb(l); ++kb) {
+                const int u = tp::unit0(l) + mb * tp::nkb(l) + kb;
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int row = mb * 16 + (lane & 15);
+                    const tp::Slot sl = tp::kslot(l, mb, kb, lane >> 4);
+                    for (int e = 0; e < 8; ++e) {
+                        float v = 0.f;
+                        if (row < nrows[l] && !sl.pad)
+                            v = sl.res ? (row == 8 * sl.oct + e ? 1.f : 0.f) : d[l].at(row, sl.dq, 8 * sl.oct + e);
+                        put_split(*wout, (((size_t)u * 2) * 64 + lane) * 8 + e, v, range_ok);
+                    }
+                }
+            }
+    bout->assign(tp::kLayers * 32, 0.f);
+    const float* bsrc[tp::kLayers] = {s.bt3, s.b31, s.b32, s.bt4, s.b41, s.b42, s.bo};
+    const int cper[tp::kLayers] = {16, 16, 16, 8, 8, 8, 1};
+    for (int l = 0; l < tp::kLayers; ++l)
+        for (int row = 0; row < nrows[l]; ++row) (*bout)[l * 32 + row] = bsrc[l][row % cper[l]];
+    return true;
+}
+
+}  // namespace m2

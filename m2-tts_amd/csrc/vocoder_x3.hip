@@ -618,6 +618,11 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     mark(1, false);
     M2_LAUNCHED("x3_mid_kernel");
     mark(2, true);
+    if (w.tp) {  // stage1: the pipelined tail (vocoder_tailp.hip)
+        const int32_t rc = launch_vocoder_tailp(u2, 16 * T, B, w.tp, w.tpb, audio, st);
+        mark(2, false);
+        return rc;
+    }
     hipLaunchKernelGGL((x3_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(Cfg::TW * 64), TP::LDS_BYTES, st, u2,
                        16 * T, w, audio);
     mark(2, false);
