@@ -16,12 +16,12 @@
 //
 // Systolic pipeline.  One workgroup owns a strip of 16*NCH columns of one
 // utterance and runs 14 waves with fixed roles: a loader wave streams U2 into
-// an LDS ring, and each of the 7 layers is done by one wave per m-block, all with
-// their weights (2 KB per (m-block, k-block) fragment pair) and biases held in
-// VGPRs for the whole strip.  In step s the wave of layer l computes chunk
-// k = s - l - 1 (16 columns) from the ring its producer wrote in steps s-1 and
-// s-2; one s_barrier per step.  Rings hold 4 chunks (64 columns), so a
-// producer writing chunk k+1 never meets its consumer reading chunks k and
+// an LDS ring, and each of the 7 layers is done by one wave per m-block, all
+// with their weights (2 KB per (m-block, k-block) fragment pair) and biases
+// held in VGPRs for the whole strip.  In step s the wave of layer l computes
+// chunk k = s - l - 1 (16 columns) from the ring its producer wrote in steps
+// s-1 and s-2; one s_barrier per step.  Rings hold 4 chunks (64 columns), so
+// a producer writing chunk k+1 never meets its consumer reading chunks k and
 // k-1 (or a residual reader two chunks behind).  Layer l's chunk k covers
 // columns [qa + 6 - l + 16k, +16): each layer lags its input by one column,
 // the receptive field of its k3 taps, so chunk k of layer l+1 needs exactly
@@ -47,7 +47,7 @@ typedef vx_u32x4 u32x4;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr float kLoS = 2048.f, kLoI = 1.f / 2048.f;
+constexpr float kLoI = 1.f / 2048.f;
 constexpr int RS = 160;           // ring row stride: 128 B (hi[32] lo[32]) + pad, RS/16 = 2 mod 4
 constexpr int RROWS = 64;         // 4 chunks of 16 columns
 constexpr int RING = RROWS * RS;  // bytes per ring
@@ -62,6 +62,8 @@ __device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
 // LDS hand-off between roles: the step's ds_writes complete, then the
 // workgroup barrier.  No vmcnt wait (the loader's prefetches stay in flight),
 // and the "memory" clobber keeps the compiler from moving LDS accesses across.
+// (An LDS-flag protocol that lets the roles run decoupled measured slower:
+// 48 vs 35.5 us, its polls sit on every hand-off of the chain.)
 __device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Diagnostic build only (-DM2_STAMPS): per-wave s_memtime at the start of
@@ -88,13 +90,16 @@ __device__ unsigned long long g_tp_stamps[1024][NWAVES][64][2];
 // ~1e-7 (saturates to +-1 through inf / 0), against ~40 instructions for tanhf.
 __device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * x)); }
 
-__device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const _Float16 h = (_Float16)v[r];
-        hi[r] = h;
-        lo[r] = (_Float16)((v[r] - (float)h) * kLoS);
-    }
+// Unscaled split of the pipeline's own rings: hi = f16(v), lo = f16(v - hi)
+// (the x3 kernels scale lo by 2^11; here lo may be an f16 subnormal, an
+// absolute error of at most 2^-25 per value: waveform RMS 3e-7 against 1.6e-7
+// scaled, tools/probe/split_sim.py).  One v_cvt_pk_f16_f32 per pair for hi and
+// one v_fma_mix{lo,hi}_f16 per value for lo (v - hi rounded once), against
+// five instructions per value for the scaled form.
+__device__ __forceinline__ void split2u(float v0, float v1, unsigned& hi, unsigned& lo) {
+    hi = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v0, v1));
+    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(v0));
+    asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(v1));
 }
 
 template <int L, int MB0, int NMB, int NCH>
@@ -103,6 +108,9 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                                            float* __restrict__ arow) {
     constexpr int NKB = nkb(L);
     constexpr int ACT = (L == 2 || L == 5) ? ACT_NONE : ACT_LEAKY;  // layer 6: tanh below
+    // lo scale: layer 0 reads U2 in the x3 kernels' format (lo * 2^11, weights
+    // packed to match); the rings between the layers hold unscaled lo.
+    constexpr float CS = L == 0 ? kLoI : 1.f;
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
     u32x4 a[NMB][NKB][2];
     float bv[NMB][4];
@@ -158,10 +166,10 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                 // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
                 if (g == 0 && k >= 0 && x >= 0 && x < L2) {
                     float4 o;
-                    o.x = tanh_fast(fmaf(cor[0][0], kLoI, acc[0][0]));
-                    o.y = tanh_fast(fmaf(cor[0][1], kLoI, acc[0][1]));
-                    o.z = tanh_fast(fmaf(cor[0][2], kLoI, acc[0][2]));
-                    o.w = tanh_fast(fmaf(cor[0][3], kLoI, acc[0][3]));
+                    o.x = tanh_fast(acc[0][0] + cor[0][0]);
+                    o.y = tanh_fast(acc[0][1] + cor[0][1]);
+                    o.z = tanh_fast(acc[0][2] + cor[0][2]);
+                    o.w = tanh_fast(acc[0][3] + cor[0][3]);
                     *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
                 }
             } else {
@@ -171,27 +179,28 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                 for (int m = 0; m < NMB; ++m) {
                     float v[4];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(fmaf(cor[m][r], kLoI, acc[m][r]));
+                    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(fmaf(cor[m][r], CS, acc[m][r]));
                     const int cbyte = 2 * (16 * (MB0 + m) + 4 * g);
                     if constexpr (L == 5) {  // ResBlock4 residual: u4 (R4) two columns ahead
                         const unsigned char* xp = lds + 4 * RING + ((16 * k + li - 2) & (RROWS - 1)) * RS + cbyte;
                         const h4 xh = *reinterpret_cast<const h4*>(xp), xl = *reinterpret_cast<const h4*>(xp + 64);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] += fmaf((float)xl[r], kLoI, (float)xh[r]);
+                        for (int r = 0; r < 4; ++r) v[r] += (float)xh[r] + (float)xl[r];
                     }
                     if (zero) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) v[r] = 0.f;
                     }
-                    h4 hi, lo;
-                    split4(v, hi, lo);
+                    unsigned h0, h1, l0, l1;
+                    split2u(v[0], v[1], h0, l0);
+                    split2u(v[2], v[3], h1, l1);
+                    u32x2 hv{h0, h1}, lv{l0, l1};
                     // Lane groups 0/1 (and 2/3) hold channels 0-3 / 4-7 (8-11 /
                     // 12-15) of the m-block; one permlane16 swap per dword gives
                     // group 0 the hi octet of channels 0-7 and group 1 its lo
                     // octet (groups 2/3: channels 8-15), so each lane stores one
                     // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
                     // 8-B halves (ds_write_b64, 4-way).
-                    u32x2 hv = __builtin_bit_cast(u32x2, hi), lv = __builtin_bit_cast(u32x2, lo);
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
                         const auto sw = __builtin_amdgcn_permlane16_swap(hv[j], lv[j], false, false);
@@ -364,10 +373,10 @@ void dense_conv3(Dense& d, const float* W, int P, int Cin, int Cout) {
         }
 }
 
-void put_split(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) {
+void put_split(std::vector<uint16_t>& out, size_t idx, float v, float lo_scale, bool* range_ok) {
     if (!(std::fabs(v) < 65504.f)) *range_ok = false;
     const _Float16 h = (_Float16)v;
-    const _Float16 l = (_Float16)((v - (float)h) * 2048.f);
+    const _Float16 l = (_Float16)((v - (float)h) * lo_scale);
     uint16_t hb, lb;
     std::memcpy(&hb, &h, 2);
     std::memcpy(&lb, &l, 2);
@@ -412,7 +421,7 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
                         float v = 0.f;
                         if (row < nrows[l] && !sl.pad)
                             v = sl.res ? (row == 8 * sl.oct + e ? 1.f : 0.f) : d[l].at(row, sl.dq, 8 * sl.oct + e);
-                        put_split(*wout, (((size_t)u * 2) * 64 + lane) * 8 + e, v, range_ok);
+                        put_split(*wout, (((size_t)u * 2) * 64 + lane) * 8 + e, v, l == 0 ? 2048.f : 1.f, range_ok);
                     }
                 }
             }
