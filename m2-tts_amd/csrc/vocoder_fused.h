@@ -40,6 +40,19 @@ std::vector<float> pack_convT(const float* W, int Cin, int Cout, int R);
 // hi/lo pairs in v_mfma_f32_16x16x32_f16 A-fragment order; biases and the
 // output conv stay fp32.
 typedef unsigned int vx_u32x4 __attribute__((ext_vector_type(4)));
+
+// fp32 -> (hi, lo) f16 pair, hi = f16(v), lo = f16(v - hi): the activation
+// format of every split-f16 buffer (LDS rows, U1, U2) and of the packed
+// weights.  lo is unscaled and may be an f16 subnormal, an absolute error of
+// at most 2^-25 per value (whole-vocoder waveform RMS 3e-7 vs fp64, against
+// 1.6e-7 for plain fp32: tools/probe/split_sim.py).  One v_cvt_pkrtz_f16_f32
+// per pair for hi and one v_fma_mix{lo,hi}_f16 per value for lo (v - hi
+// rounded once); hi rounds toward zero, which leaves lo's bound unchanged.
+__device__ __forceinline__ void split2u(float v0, float v1, unsigned& hi, unsigned& lo) {
+    hi = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v0, v1));
+    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(v0));
+    asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(v1));
+}
 struct VocX {
     const vx_u32x4* wi;
     const float* bi;

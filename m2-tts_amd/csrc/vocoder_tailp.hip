@@ -47,7 +47,6 @@ typedef vx_u32x4 u32x4;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr float kLoI = 1.f / 2048.f;
 constexpr int RS = 160;           // ring row stride: 128 B (hi[32] lo[32]) + pad, RS/16 = 2 mod 4
 constexpr int RROWS = 64;         // 4 chunks of 16 columns
 constexpr int RING = RROWS * RS;  // bytes per ring
@@ -90,27 +89,12 @@ __device__ unsigned long long g_tp_stamps[1024][NWAVES][64][2];
 // ~1e-7 (saturates to +-1 through inf / 0), against ~40 instructions for tanhf.
 __device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * x)); }
 
-// Unscaled split of the pipeline's own rings: hi = f16(v), lo = f16(v - hi)
-// (the x3 kernels scale lo by 2^11; here lo may be an f16 subnormal, an
-// absolute error of at most 2^-25 per value: waveform RMS 3e-7 against 1.6e-7
-// scaled, tools/probe/split_sim.py).  One v_cvt_pk_f16_f32 per pair for hi and
-// one v_fma_mix{lo,hi}_f16 per value for lo (v - hi rounded once), against
-// five instructions per value for the scaled form.
-__device__ __forceinline__ void split2u(float v0, float v1, unsigned& hi, unsigned& lo) {
-    hi = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v0, v1));
-    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(v0));
-    asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(v1));
-}
-
 template <int L, int MB0, int NMB, int NCH>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
                                            float* __restrict__ arow) {
     constexpr int NKB = nkb(L);
     constexpr int ACT = (L == 2 || L == 5) ? ACT_NONE : ACT_LEAKY;  // layer 6: tanh below
-    // lo scale: layer 0 reads U2 in the x3 kernels' format (lo * 2^11, weights
-    // packed to match); the rings between the layers hold unscaled lo.
-    constexpr float CS = L == 0 ? kLoI : 1.f;
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
     u32x4 a[NMB][NKB][2];
     float bv[NMB][4];
@@ -179,7 +163,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                 for (int m = 0; m < NMB; ++m) {
                     float v[4];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(fmaf(cor[m][r], CS, acc[m][r]));
+                    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[m][r] + cor[m][r]);
                     const int cbyte = 2 * (16 * (MB0 + m) + 4 * g);
                     if constexpr (L == 5) {  // ResBlock4 residual: u4 (R4) two columns ahead
                         const unsigned char* xp = lds + 4 * RING + ((16 * k + li - 2) & (RROWS - 1)) * RS + cbyte;
@@ -373,10 +357,10 @@ void dense_conv3(Dense& d, const float* W, int P, int Cin, int Cout) {
         }
 }
 
-void put_split(std::vector<uint16_t>& out, size_t idx, float v, float lo_scale, bool* range_ok) {
+void put_split(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) {
     if (!(std::fabs(v) < 65504.f)) *range_ok = false;
     const _Float16 h = (_Float16)v;
-    const _Float16 l = (_Float16)((v - (float)h) * lo_scale);
+    const _Float16 l = (_Float16)(v - (float)h);
     uint16_t hb, lb;
     std::memcpy(&hb, &h, 2);
     std::memcpy(&lb, &l, 2);
@@ -421,7 +405,7 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
                         float v = 0.f;
                         if (row < nrows[l] && !sl.pad)
                             v = sl.res ? (row == 8 * sl.oct + e ? 1.f : 0.f) : d[l].at(row, sl.dq, 8 * sl.oct + e);
-                        put_split(*wout, (((size_t)u * 2) * 64 + lane) * 8 + e, v, l == 0 ? 2048.f : 1.f, range_ok);
+                        put_split(*wout, (((size_t)u * 2) * 64 + lane) * 8 + e, v, range_ok);
                     }
                 }
             }

@@ -5,14 +5,14 @@
 // ConvT3 -> ResBlock3 -> ConvT4 -> ResBlock4 -> output_conv -> tanh), but the
 // GEMMs run on v_mfma_f32_16x16x32_f16 (16 cycles for 16K FLOP, 16x the
 // FLOP rate of the f32 MFMA) with every fp32 operand x carried as two halves
-//     x_hi = f16(x),  x_lo = f16((x - x_hi) * 2^11)
+//     x_hi = f16(x),  x_lo = f16(x - x_hi)        (split2u, vocoder_fused.h)
 // and every product as
-//     a.b ~= a_hi.b_hi + (a_hi.b_lo + a_lo.b_hi) * 2^-11
-// accumulated in fp32 (two accumulators per tile, combined in the epilogue).
+//     a.b ~= a_hi.b_hi + (a_hi.b_lo + a_lo.b_hi)
+// accumulated in fp32 (two accumulators per tile, summed in the epilogue).
 // The dropped a_lo.b_lo term is 2^-22 relative, and each half-product is
 // exact in the fp32 accumulator, so the result carries fp32-level error:
 // simulated over the whole stage1/stage2 vocoder (tools/probe/split_sim.py)
-// the waveform RMS error vs fp64 is 1.6e-7 against 1.5e-7 for plain fp32
+// the waveform RMS error vs fp64 is 3e-7 against 1.5e-7 for plain fp32
 // convolution (plain f16 operands: 3.1e-4, outside the 1e-4 bound).  Three
 // MFMAs per product leave 16/3 = 5.3x the exact-f32 MFMA rate.  Range: |x| and
 // |w| must stay below 65504 (f16 max); weights are checked at model creation.
@@ -44,7 +44,6 @@ typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef vx_u32x4 u32x4;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr float kLoS = 2048.f, kLoI = 1.f / 2048.f;
 
 __device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
@@ -68,12 +67,12 @@ struct XW {
 };
 
 __device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const _Float16 h = (_Float16)v[r];
-        hi[r] = h;
-        lo[r] = (_Float16)((v[r] - (float)h) * kLoS);
-    }
+    unsigned h0, h1, l0, l1;
+    split2u(v[0], v[1], h0, l0);
+    split2u(v[2], v[3], h1, l1);
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    hi = __builtin_bit_cast(h4, u32x2{h0, h1});
+    lo = __builtin_bit_cast(h4, u32x2{l0, l1});
 }
 
 // ---------------------------------------------------------------------------
@@ -145,20 +144,20 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
 template <int CIN, int NTAP>
 constexpr int nkb() { return (NTAP * (CIN / 8) + 3) / 4; }
 
-// Epilogue for one tile (acc already holds the bias): v = act(acc +
-// cor*2^-11) [+ residual read back from `out`], 0 outside [0, L) (only
+// Epilogue for one tile (acc already holds the bias): v = act(acc + cor)
+// [+ residual read back from `out`], 0 outside [0, L) (only
 // evaluated for tiles that reach past an edge), split and stored as hi/lo.
 template <int COUT, int RSO, int ACT, bool RES>
 __device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, XW out, int t, int co0, int L,
                                            bool edge) {
     float v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(fmaf(cor[r], kLoI, acc[r]));
+    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[r] + cor[r]);
     unsigned char* row = out.p + (t - out.start) * RSO + co0 * 2;
     if (RES) {
         const h4 hi = *reinterpret_cast<const h4*>(row), lo = *reinterpret_cast<const h4*>(row + 2 * COUT);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += fmaf((float)lo[r], kLoI, (float)hi[r]);
+        for (int r = 0; r < 4; ++r) v[r] += (float)hi[r] + (float)lo[r];
     }
     if (edge && (t < 0 || t >= L)) {
 #pragma unroll
@@ -321,7 +320,7 @@ __device__ __forceinline__ void gload_mel(const float* __restrict__ g, int T, XW
                 const _Float16 h = (_Float16)x[k];
                 _Float16* row = reinterpret_cast<_Float16*>(dst.p + r * RS);
                 row[c] = h;
-                row[MP + c] = (_Float16)((x[k] - (float)h) * kLoS);
+                row[MP + c] = (_Float16)(x[k] - (float)h);
             }
         }
     }
@@ -570,7 +569,7 @@ __global__ __launch_bounds__(Cfg::TW * 64, Cfg::TMIN) void x3_tail_kernel(const 
                 const _Float16* hr = reinterpret_cast<const _Float16*>(x + k * Pl::RS_4);
 #pragma unroll
                 for (int ci = 0; ci < C4; ++ci)
-                    acc = fmaf(w.wo[ci * 3 + k], (float)hr[ci] + (float)hr[C4 + ci] * kLoI, acc);
+                    acc = fmaf(w.wo[ci * 3 + k], (float)hr[ci] + (float)hr[C4 + ci], acc);
             }
             arow[t] = tanhf(acc + bo);
         }
@@ -664,7 +663,7 @@ namespace {
 void put(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) {
     if (!(std::fabs(v) < 65504.f)) *range_ok = false;
     const _Float16 h = (_Float16)v;
-    const _Float16 l = (_Float16)((v - (float)h) * 2048.f);
+    const _Float16 l = (_Float16)(v - (float)h);
     uint16_t hb, lb;
     std::memcpy(&hb, &h, 2);
     std::memcpy(&lb, &l, 2);

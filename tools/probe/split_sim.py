@@ -38,6 +38,9 @@ for stage, cfg in (('s1', O.STAGE1), ('s2', O.STAGE2)):
                 if mode == 'f16x3':
                     xh, xl = split16(x); wh, wl = split16(wt)
                     y = fn(xh, wh, None, *a, **k) + (fn(xh, wl, None, *a, **k) + fn(xl, wh, None, *a, **k)) / 2.0**11
+                elif mode == 'f16x3u':  # the kernels' format: lo = f16(x - hi), unscaled (may be subnormal)
+                    xh, xl = split16(x, 1.0); wh, wl = split16(wt, 1.0)
+                    y = fn(xh, wh, None, *a, **k) + (fn(xh, wl, None, *a, **k) + fn(xl, wh, None, *a, **k))
                 elif mode == 'bf16x3':
                     xh, xl = splitbf(x); wh, wl = splitbf(wt)
                     y = fn(xh, wh, None, *a, **k) + fn(xh, wl, None, *a, **k) + fn(xl, wh, None, *a, **k)
@@ -53,6 +56,6 @@ for stage, cfg in (('s1', O.STAGE1), ('s2', O.STAGE2)):
     ref = run('f64')
     rms = lambda a: float(torch.sqrt(torch.mean(a.double() ** 2)))
     print(stage, 'audio rms', rms(ref))
-    for mode in ('f32', 'f16x3', 'bf16x3', 'f16'):
+    for mode in ('f32', 'f16x3', 'f16x3u', 'bf16x3', 'f16'):
         y = run(mode)
         print(f'  {mode:7s} rms err {rms(y - ref):.3e}  max {float((y - ref).abs().max()):.3e}')
