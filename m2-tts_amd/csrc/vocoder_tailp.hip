@@ -87,7 +87,7 @@ __device__ unsigned long long g_tp_stamps[1024][NWAVES][64][2];
 
 // tanh(x) = 1 - 2 / (1 + e^{2x}) on v_exp_f32 / v_rcp_f32: absolute error
 // ~1e-7 (saturates to +-1 through inf / 0), against ~40 instructions for tanhf.
-__device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * x)); }
+__device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
 
 template <int L, int MB0, int NMB, int NCH>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
@@ -222,7 +222,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     // wait for that load).
     u32x4 buf[3][2];
     auto step = [&](int s, u32x4 (&cur)[2], u32x4 (&ahead)[2]) {
-        fetch(s + 2, ahead);
+        fetch(min(s + 2, NCH - 1), ahead);  // past the strip: re-read the last chunk (an L2 hit)
         if (s < NCH) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -259,6 +259,12 @@ __global__ __launch_bounds__(NWAVES * 64, 7) void tailp_kernel(const unsigned ch
     const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
     float* arow = audio + (size_t)b * 4 * L2;
     TPSTAMP(62, 0);
+    // Later layers get higher issue priority: they are the younger waves of
+    // the workgroup and lose VALU arbitration on age (MI355X_MICROARCH.md, two
+    // waves per SIMD), while the step waits for the slowest role (-1.5 %).
+    if (w >= 9) __builtin_amdgcn_s_setprio(3);
+    else if (w >= 6) __builtin_amdgcn_s_setprio(2);
+    else if (w >= 3) __builtin_amdgcn_s_setprio(1);
     switch (w) {
         case 0: layer_role<0, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
         case 1: layer_role<0, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
