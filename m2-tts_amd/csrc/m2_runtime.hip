@@ -155,6 +155,8 @@ struct m2_model {
     bool x3 = false;
     void* tbuf = nullptr;  // pipelined stage1 tail pack (vx.tp / vx.tpb)
     bool tailp = false;
+    void* mbuf = nullptr;  // pipelined stage1 mid pack (vx.mp / vx.mpb)
+    bool midp = false;
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
     mutable int prof_calls = 0;
@@ -564,6 +566,39 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                         m->tailp = true;
                     }
                 }
+                // stage1: the second upsampling stage as one pipelined kernel
+                // (M2_VOC_MID_X3=1 keeps the x3 mid kernel).
+                if (M == 64 && C == 128 && !std::getenv("M2_VOC_MID_X3")) {
+                    const char* names[6] = {"vocoder.upsamples.1.weight",         "vocoder.upsamples.1.bias",
+                                            "vocoder.resblocks.1.conv1.weight", "vocoder.resblocks.1.conv1.bias",
+                                            "vocoder.resblocks.1.conv2.weight", "vocoder.resblocks.1.conv2.bias"};
+                    std::vector<float> hw[6];
+                    bool got = true;
+                    for (int i = 0; i < 6; ++i) got = got && !(hw[i] = fetch(names[i])).empty();
+                    const MidpSrc src{hw[0].data(), hw[1].data(), hw[2].data(), hw[3].data(), hw[4].data(), hw[5].data()};
+                    std::vector<uint16_t> pw;
+                    std::vector<float> pb;
+                    bool rok = true;
+                    if (got && pack_midp(src, &pw, &pb, &rok) && rok) {
+                        const size_t wb = pw.size() * sizeof(uint16_t);
+                        e = hipMalloc(&m->mbuf, wb + pb.size() * sizeof(float));
+                        if (e == hipSuccess) e = hipMemcpyAsync(m->mbuf, pw.data(), wb, hipMemcpyHostToDevice, st);
+                        if (e == hipSuccess)
+                            e = hipMemcpyAsync(static_cast<char*>(m->mbuf) + wb, pb.data(), pb.size() * sizeof(float),
+                                               hipMemcpyHostToDevice, st);
+                        if (e == hipSuccess) e = hipStreamSynchronize(st);
+                        if (e != hipSuccess) {
+                            (void)hipFree(m->vbuf);
+                            (void)hipFree(m->xbuf);
+                            if (m->tbuf) (void)hipFree(m->tbuf);
+                            if (m->mbuf) (void)hipFree(m->mbuf);
+                            return bail(e, "upload midp pack");
+                        }
+                        m->vx.mp = static_cast<const vx_u32x4*>(m->mbuf);
+                        m->vx.mpb = reinterpret_cast<const float*>(static_cast<char*>(m->mbuf) + wb);
+                        m->midp = true;
+                    }
+                }
             }
         }
     }
@@ -579,6 +614,7 @@ int32_t m2_model_destroy(m2_model* model) {
     if (model->vbuf) (void)hipFree(model->vbuf);
     if (model->xbuf) (void)hipFree(model->xbuf);
     if (model->tbuf) (void)hipFree(model->tbuf);
+    if (model->mbuf) (void)hipFree(model->mbuf);
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -782,6 +818,7 @@ const char* m2_profile_kernel_name(int32_t index) {
 const char* m2_profile_kernel_name_for(const m2_model* m, int32_t index) {
     if (!m || index < 0 || index >= kVocKernels) return "";
     if (m->tailp && index == 2) return kVocTailpKernelName;
+    if (m->midp && index == 1) return kVocMidpKernelName;
     return m->x3 ? kVocX3KernelNames[index] : kVocKernelNames[index];
 }
 

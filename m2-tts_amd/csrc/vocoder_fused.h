@@ -66,6 +66,9 @@ struct VocX {
     // pipelined stage1 tail (vocoder_tailp.hip); null = the x3 tail kernel
     const vx_u32x4* tp;
     const float* tpb;
+    // pipelined stage1 mid stage (vocoder_midp.hip); null = the x3 mid kernel
+    const vx_u32x4* mp;
+    const float* mpb;
 };
 
 // Pipelined stage1 tail (vocoder_tailp.hip): ConvT3, ResBlock3, ConvT4,
@@ -100,6 +103,31 @@ constexpr Slot kslot(int l, int mb, int kb, int g) {
     return Slot{0, 0, g, 1};  // pad: a distinct octet per lane group keeps the read conflict-free
 }
 }  // namespace tp
+
+// Pipelined stage1 mid stage (vocoder_midp.hip): ConvT2 (layer 0), ResBlock2
+// conv1 / conv2 (layers 1, 2) in polyphase form over the columns q of U1, 8
+// m-blocks (phase s = mb / 2) per layer; mslot(l, s, kb, g) as tp::kslot.
+namespace mp {
+struct MSlot {
+    int dq, oct;
+};
+constexpr int kUnits = 80;
+constexpr int mkb(int l) { return l == 0 ? 4 : 3; }
+constexpr int munit0(int l) { return l == 0 ? 0 : (l == 1 ? 32 : 56); }
+constexpr MSlot mslot(int l, int s, int kb, int g) {
+    if (l == 0)  // ConvT2: phases 0, 1 read columns q, q-1; phases 2, 3 read q+1, q (64 ch: 2 k-blocks each)
+        return MSlot{kb < 2 ? (s < 2 ? 0 : 1) : (s < 2 ? -1 : 0), 4 * (kb & 1) + g};
+    const int pp = s + kb - 1, dq = pp < 0 ? -1 : pp / 4;  // tap t2 + kb - 1: phase pp mod 4 of column q + dq
+    return MSlot{dq, 4 * (pp - 4 * dq) + g};
+}
+}  // namespace mp
+struct MidpSrc {
+    const float *wt, *bt, *w1, *b1, *w2, *b2;
+};
+bool pack_midp(const MidpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
+int32_t launch_vocoder_midp(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2,
+                            hipStream_t st);
+extern const char* const kVocMidpKernelName;
 
 // Raw fp32 reference weights of the five tail modules (host pointers).
 struct TailpSrc {

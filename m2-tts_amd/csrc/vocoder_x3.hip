@@ -612,10 +612,15 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     mark(0, false);
     M2_LAUNCHED("x3_head_kernel");
     mark(1, true);
-    hipLaunchKernelGGL((x3_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(Cfg::MW * 64), MP::LDS_BYTES, st, u1,
-                       4 * T, w, u2);
+    if (w.mp) {  // stage1: the pipelined mid stage (vocoder_midp.hip)
+        const int32_t rc = launch_vocoder_midp(u1, 4 * T, B, w.mp, w.mpb, u2, st);
+        if (rc) return rc;
+    } else {
+        hipLaunchKernelGGL((x3_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(Cfg::MW * 64), MP::LDS_BYTES, st,
+                           u1, 4 * T, w, u2);
+        M2_LAUNCHED("x3_mid_kernel");
+    }
     mark(1, false);
-    M2_LAUNCHED("x3_mid_kernel");
     mark(2, true);
     if (w.tp) {  // stage1: the pipelined tail (vocoder_tailp.hip)
         const int32_t rc = launch_vocoder_tailp(u2, 16 * T, B, w.tp, w.tpb, audio, st);

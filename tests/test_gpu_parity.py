@@ -351,10 +351,10 @@ def test_vocoder_arithmetic_paths(gpu, stage, monkeypatch):
 
 
 @pytest.mark.parametrize("stage", STAGES)
-@pytest.mark.parametrize("env", ["M2_TF_UNFUSED", "M2_VOCODER_PERLAYER", "M2_VOC_TAIL_X3"])
+@pytest.mark.parametrize("env", ["M2_TF_UNFUSED", "M2_VOCODER_PERLAYER", "M2_VOC_TAIL_X3", "M2_VOC_MID_X3"])
 def test_alternate_kernel_paths(gpu, stage, env, monkeypatch):
     """The unfused transformer layer (five linears), the per-layer vocoder
-    kernels and the x3 tail kernel (instead of the pipelined stage1 tail) stay
+    kernels and the x3 tail / mid kernels (instead of the pipelined stage1 ones) stay
     parity-green: inference vs the reference's fixture."""
     monkeypatch.setenv(env, "1")
     g = golden(f"{stage}_small")
