@@ -89,6 +89,20 @@ __device__ unsigned long long g_tp_stamps[1024][NWAVES][64][2];
 // ~1e-7 (saturates to +-1 through inf / 0), against ~40 instructions for tanhf.
 __device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
 
+// Staggered epilogues (TP_DEFER bit l: layer l stores chunk k one step after
+// computing it, keeping acc / cor across the barrier, so its epilogue overlaps
+// the other roles' reads and MFMAs).  Layer l computes chunk k in step
+// k + off_l(l); its consumer one step after the store.  Layers 1 and 4 must not
+// defer: the residual readers two layers down would then meet the ring slot
+// their producer is rewriting.
+#ifndef TP_DEFER
+#define TP_DEFER 0
+#endif
+constexpr bool defer_l(int l) { return (TP_DEFER >> l) & 1; }
+constexpr int off_l(int l) { return l == 0 ? 1 : off_l(l - 1) + 1 + (defer_l(l - 1) ? 1 : 0); }
+constexpr int last_step(int nch) { return nch - 1 + off_l(6) + (defer_l(6) ? 1 : 0); }
+static_assert(!defer_l(1) && !defer_l(4), "layers 1 and 4 feed residual readers: no deferral");
+
 template <int L, int MB0, int NMB, int NCH>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
@@ -116,85 +130,109 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
         for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 32 + (MB0 + m) * 16 + 4 * g + r];
     }
     const int sL = qa + 6 - L;
-#pragma unroll 1
-    for (int s = -1; s < NCH + 7; ++s) {
-        TPSTAMP(s + 1, 0);
-        const int k = s - (L + 1);
-        if (k >= -1 && k < NCH) {
-            u32x4 bh[NMB][NKB], bl[NMB][NKB];
+    constexpr bool DEF = defer_l(L);
+    f32x4 acc[NMB], cor[NMB];
+    h4 rxh[NMB], rxl[NMB];  // layer 5: the residual x, read with the B fragments
+    // Reads (+ residual) and MFMAs of chunk k into acc / cor.
+    auto compute = [&](int k) {
+        u32x4 bh[NMB][NKB], bl[NMB][NKB];
 #pragma unroll
-            for (int m = 0; m < NMB; ++m)
+        for (int m = 0; m < NMB; ++m)
 #pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) {
-                    const int row = (16 * k + li + roff[m][kb]) & (RROWS - 1);
-                    const unsigned char* p = lds + boff[m][kb] + row * RS;
-                    bh[m][kb] = *reinterpret_cast<const u32x4*>(p);
-                    bl[m][kb] = *reinterpret_cast<const u32x4*>(p + 64);
-                }
-            f32x4 acc[NMB], cor[NMB];
+            for (int kb = 0; kb < NKB; ++kb) {
+                const int row = (16 * k + li + roff[m][kb]) & (RROWS - 1);
+                const unsigned char* p = lds + boff[m][kb] + row * RS;
+                bh[m][kb] = *reinterpret_cast<const u32x4*>(p);
+                bl[m][kb] = *reinterpret_cast<const u32x4*>(p + 64);
+            }
+        if constexpr (L == 5) {  // ResBlock4 residual: u4 (R4) two columns ahead
 #pragma unroll
             for (int m = 0; m < NMB; ++m) {
-                acc[m] = f32x4{bv[m][0], bv[m][1], bv[m][2], bv[m][3]};
-                cor[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const unsigned char* xp =
+                    lds + 4 * RING + ((16 * k + li - 2) & (RROWS - 1)) * RS + 2 * (16 * (MB0 + m) + 4 * g);
+                rxh[m] = *reinterpret_cast<const h4*>(xp);
+                rxl[m] = *reinterpret_cast<const h4*>(xp + 64);
             }
+        }
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
+        for (int m = 0; m < NMB; ++m) {
+            acc[m] = f32x4{bv[m][0], bv[m][1], bv[m][2], bv[m][3]};
+            cor[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
-                for (int m = 0; m < NMB; ++m) {
-                    acc[m] = mfma_h(a[m][kb][0], bh[m][kb], acc[m]);
-                    cor[m] = mfma_h(a[m][kb][0], bl[m][kb], cor[m]);
-                    cor[m] = mfma_h(a[m][kb][1], bh[m][kb], cor[m]);
-                }
-            const int x = sL + 16 * k + li;  // this lane's column
-            if constexpr (L == 6) {
-                // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
-                if (g == 0 && k >= 0 && x >= 0 && x < L2) {
-                    float4 o;
-                    o.x = tanh_fast(acc[0][0] + cor[0][0]);
-                    o.y = tanh_fast(acc[0][1] + cor[0][1]);
-                    o.z = tanh_fast(acc[0][2] + cor[0][2]);
-                    o.w = tanh_fast(acc[0][3] + cor[0][3]);
-                    *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
-                }
-            } else {
-                const bool zero = edge && (x < 0 || x >= L2);
-                const int orow = (16 * k + li) & (RROWS - 1);
+        for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-                for (int m = 0; m < NMB; ++m) {
-                    float v[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[m][r] + cor[m][r]);
-                    const int cbyte = 2 * (16 * (MB0 + m) + 4 * g);
-                    if constexpr (L == 5) {  // ResBlock4 residual: u4 (R4) two columns ahead
-                        const unsigned char* xp = lds + 4 * RING + ((16 * k + li - 2) & (RROWS - 1)) * RS + cbyte;
-                        const h4 xh = *reinterpret_cast<const h4*>(xp), xl = *reinterpret_cast<const h4*>(xp + 64);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] += (float)xh[r] + (float)xl[r];
-                    }
-                    if (zero) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = 0.f;
-                    }
-                    unsigned h0, h1, l0, l1;
-                    split2u(v[0], v[1], h0, l0);
-                    split2u(v[2], v[3], h1, l1);
-                    u32x2 hv{h0, h1}, lv{l0, l1};
-                    // Lane groups 0/1 (and 2/3) hold channels 0-3 / 4-7 (8-11 /
-                    // 12-15) of the m-block; one permlane16 swap per dword gives
-                    // group 0 the hi octet of channels 0-7 and group 1 its lo
-                    // octet (groups 2/3: channels 8-15), so each lane stores one
-                    // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
-                    // 8-B halves (ds_write_b64, 4-way).
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const auto sw = __builtin_amdgcn_permlane16_swap(hv[j], lv[j], false, false);
-                        hv[j] = sw[0];
-                        lv[j] = sw[1];
-                    }
-                    unsigned char* op = lds + (L + 1) * RING + orow * RS + 32 * (MB0 + m) + 64 * (g & 1) + 16 * (g >> 1);
-                    *reinterpret_cast<u32x4*>(op) = u32x4{hv[0], hv[1], lv[0], lv[1]};
-                }
+            for (int m = 0; m < NMB; ++m) {
+                acc[m] = mfma_h(a[m][kb][0], bh[m][kb], acc[m]);
+                cor[m] = mfma_h(a[m][kb][0], bl[m][kb], cor[m]);
+                cor[m] = mfma_h(a[m][kb][1], bh[m][kb], cor[m]);
             }
+    };
+    // Activation, split and store of chunk k from acc / cor.
+    auto epilogue = [&](int k) {
+        const int x = sL + 16 * k + li;  // this lane's column
+        if constexpr (L == 6) {
+            // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
+            if (g == 0 && k >= 0 && x >= 0 && x < L2) {
+                float4 o;
+                o.x = tanh_fast(acc[0][0] + cor[0][0]);
+                o.y = tanh_fast(acc[0][1] + cor[0][1]);
+                o.z = tanh_fast(acc[0][2] + cor[0][2]);
+                o.w = tanh_fast(acc[0][3] + cor[0][3]);
+                *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
+            }
+        } else {
+            const bool zero = edge && (x < 0 || x >= L2);
+            const int orow = (16 * k + li) & (RROWS - 1);
+#pragma unroll
+            for (int m = 0; m < NMB; ++m) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[m][r] + cor[m][r]);
+                if constexpr (L == 5) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)rxh[m][r] + (float)rxl[m][r];
+                }
+                if (zero) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = 0.f;
+                }
+                unsigned h0, h1, l0, l1;
+                split2u(v[0], v[1], h0, l0);
+                split2u(v[2], v[3], h1, l1);
+                u32x2 hv{h0, h1}, lv{l0, l1};
+                // Lane groups 0/1 (and 2/3) hold channels 0-3 / 4-7 (8-11 /
+                // 12-15) of the m-block; one permlane16 swap per dword gives
+                // group 0 the hi octet of channels 0-7 and group 1 its lo
+                // octet (groups 2/3: channels 8-15), so each lane stores one
+                // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
+                // 8-B halves (ds_write_b64, 4-way).
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const auto sw = __builtin_amdgcn_permlane16_swap(hv[j], lv[j], false, false);
+                    hv[j] = sw[0];
+                    lv[j] = sw[1];
+                }
+                unsigned char* op = lds + (L + 1) * RING + orow * RS + 32 * (MB0 + m) + 64 * (g & 1) + 16 * (g >> 1);
+                *reinterpret_cast<u32x4*>(op) = u32x4{hv[0], hv[1], lv[0], lv[1]};
+            }
+        }
+    };
+    int kp = -2;  // deferred roles: the chunk whose epilogue is pending
+#pragma unroll 1
+    for (int s = -1; s <= last_step(NCH); ++s) {
+        TPSTAMP(s + 1, 0);
+        const int k = s - off_l(L);
+        if constexpr (DEF) {
+            if (kp >= -1) epilogue(kp);
+            kp = -2;
+            if (k >= -1 && k < NCH) {
+                compute(k);
+                kp = k;
+            }
+        } else if (k >= -1 && k < NCH) {
+            compute(k);
+            epilogue(k);
         }
         TPSTAMP(s + 1, 1);
         step_barrier();
@@ -239,13 +277,13 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     fetch(0, buf[1]);
     int s = -1;
 #pragma unroll 1
-    for (; s + 2 <= NCH + 6; s += 3) {  // covers every step with work (s <= NCH - 1)
+    for (; s + 2 <= last_step(NCH); s += 3) {  // covers every step with work (s <= NCH - 1)
         step(s, buf[0], buf[2]);
         step(s + 1, buf[1], buf[0]);
         step(s + 2, buf[2], buf[1]);
     }
 #pragma unroll 1
-    for (; s <= NCH + 6; ++s) step_barrier();
+    for (; s <= last_step(NCH); ++s) step_barrier();
 }
 
 template <int NCH>

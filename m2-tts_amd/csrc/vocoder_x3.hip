@@ -405,12 +405,20 @@ struct TailPlan {  // A: in | h3 | u4   B: u3 | h4
 // multiple of the wave count.  Stage1 at B=32, T=500 (bench): head 8 x 32 =
 // 256 workgroups (one per CU), mid 16 x 32 = 512 (two rounds), tail 48 x 32 =
 // 1536 at two per CU (three full rounds).
+#ifndef X3_HEAD_TF  // head tiling experiments (tools/probe): frames per window, waves, tile chunks
+#define X3_HEAD_TF 63
+#define X3_HEAD_HW 16
+#define X3_NT_IN 3
+#define X3_NT_T1 5
+#define X3_NT_R1 4
+#endif
 struct CfgS1 {
     static constexpr int M = 64, MP = 64, C = 128;
-    static constexpr int TF = 63, HW = 16, HMIN = 4;
+    static constexpr int TF = X3_HEAD_TF, HW = X3_HEAD_HW, HMIN = 4;
     static constexpr int W2 = 125, MW = 16, MMIN = 4;
     static constexpr int W3 = 168, TW = 8, TMIN = 4;
-    static constexpr int NT_IN = 3, NT_T1 = 5, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 3, NT_R3 = 3, NT_T4 = 3, NT_R4 = 6;
+    static constexpr int NT_IN = X3_NT_IN, NT_T1 = X3_NT_T1, NT_R1 = X3_NT_R1, NT_T2 = 4, NT_R2 = 4, NT_T3 = 3,
+                         NT_R3 = 3, NT_T4 = 3, NT_R4 = 6;
 };
 struct CfgS2 {
     static constexpr int M = 80, MP = 96, C = 256;
