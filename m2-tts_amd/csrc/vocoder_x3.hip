@@ -147,14 +147,20 @@ constexpr int nkb() { return (NTAP * (CIN / 8) + 3) / 4; }
 // Epilogue for one tile (acc already holds the bias): v = act(acc + cor)
 // [+ residual read back from `out`], 0 outside [0, L) (only
 // evaluated for tiles that reach past an edge), split and stored as hi/lo.
+// Executed by every lane (the permlane16 swap reads the partner lane group);
+// `store` says whether this lane's 16 B are written.  After the swap lane group
+// 0 (2) holds the hi halves of channels 0-7 (8-15) of the m-block and group 1
+// (3) the lo halves: one ds_write_b128 per lane instead of two ds_write_b64
+// (2-way instead of 4-way bank conflicts on RS/16 = 2 mod 4 rows).
 template <int COUT, int RSO, int ACT, bool RES>
 __device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, XW out, int t, int co0, int L,
-                                           bool edge) {
+                                           bool edge, bool store) {
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[r] + cor[r]);
-    unsigned char* row = out.p + (t - out.start) * RSO + co0 * 2;
+    unsigned char* rowp = out.p + (t - out.start) * RSO;
     if (RES) {
+        const unsigned char* row = rowp + co0 * 2;
         const h4 hi = *reinterpret_cast<const h4*>(row), lo = *reinterpret_cast<const h4*>(row + 2 * COUT);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += (float)hi[r] + (float)lo[r];
@@ -163,10 +169,15 @@ __device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, X
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = 0.f;
     }
-    h4 hi, lo;
-    split4(v, hi, lo);
-    *reinterpret_cast<h4*>(row) = hi;
-    *reinterpret_cast<h4*>(row + 2 * COUT) = lo;
+    unsigned h0, h1, l0, l1;
+    split2u(v[0], v[1], h0, l0);
+    split2u(v[2], v[3], h1, l1);
+    const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
+    const int g = (threadIdx.x & 63) >> 4;
+    if (store)
+        *reinterpret_cast<u32x4*>(rowp + 2 * (co0 - 4 * g + 8 * (g >> 1)) + (g & 1) * 2 * COUT) =
+            u32x4{s0[0], s1[0], s0[1], s1[1]};
 }
 
 // Does 3-tap packing fold the ResBlock residual into the GEMM (see mma_x3)?
@@ -195,14 +206,13 @@ __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const flo
     }
     mma_x3<CIN, NTAP, STEP, RSI, NTT, XR>(wp, bp, xr, acc, cor);
     const bool edge = (p0 + tile0 * 16) * RR < 0 || (p0 + (tile0 + NTT) * 16) * RR > L;
-    if (co0 < COUT) {
-        const int li = threadIdx.x & 15;
+    const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
+    const bool rows_ok = co0 - 4 * g + 8 * (g >> 1) < COUT;  // after the swap: this lane's 8 channels
 #pragma unroll
-        for (int n = 0; n < NTT; ++n) {
-            const int j = (tile0 + n) * 16 + li;
-            if (((tile0 + n + 1) * 16 <= JMAX) || j < JMAX)
-                store_tile<COUT, RSO, ACT, RES>(acc[n], cor[n], out, (p0 + j) * RR + ph, co0, L, edge);
-        }
+    for (int n = 0; n < NTT; ++n) {
+        const int j = (tile0 + n) * 16 + li;
+        const bool col_ok = ((tile0 + n + 1) * 16 <= JMAX) || j < JMAX;
+        store_tile<COUT, RSO, ACT, RES>(acc[n], cor[n], out, (p0 + j) * RR + ph, co0, L, edge, rows_ok && col_ok);
     }
 }
 
@@ -303,24 +313,30 @@ __device__ __forceinline__ void gload_mel(const float* __restrict__ g, int T, XW
                 *reinterpret_cast<h4*>(row + 2 * MP) = lo;
             }
         }
-    } else {  // [M][T]: consecutive threads read consecutive frames of one channel
-        constexpr int TOT = N * MP, IT = (TOT + NTHR - 1) / NTHR;
-        float x[IT];
+    } else {  // [M][T]: an item = 8 channels of one frame; consecutive threads take consecutive frames
+        constexpr int OCT = MP / 8, TOT = N * OCT, IT = (TOT + NTHR - 1) / NTHR;
+        float x[IT][8];
 #pragma unroll
         for (int k = 0; k < IT; ++k) {
             const int i = threadIdx.x + k * NTHR;
-            const int c = i / N, r = i - c * N, t = dst.start + r;
-            x[k] = (i < TOT && t >= 0 && t < T && c < M) ? g[(size_t)c * T + t] : 0.f;
+            const int o = i / N, r = i - o * N, t = dst.start + r;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = 8 * o + e;
+                x[k][e] = (i < TOT && t >= 0 && t < T && c < M) ? g[(size_t)c * T + t] : 0.f;
+            }
         }
 #pragma unroll
         for (int k = 0; k < IT; ++k) {
             const int i = threadIdx.x + k * NTHR;
             if (i < TOT) {
-                const int c = i / N, r = i - c * N;
-                const _Float16 h = (_Float16)x[k];
-                _Float16* row = reinterpret_cast<_Float16*>(dst.p + r * RS);
-                row[c] = h;
-                row[MP + c] = (_Float16)(x[k] - (float)h);
+                const int o = i / N, r = i - o * N;
+                unsigned hh[4], ll[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) split2u(x[k][2 * e], x[k][2 * e + 1], hh[e], ll[e]);
+                unsigned char* row = dst.p + r * RS + 16 * o;
+                *reinterpret_cast<u32x4*>(row) = u32x4{hh[0], hh[1], hh[2], hh[3]};
+                *reinterpret_cast<u32x4*>(row + 2 * MP) = u32x4{ll[0], ll[1], ll[2], ll[3]};
             }
         }
     }
