@@ -73,35 +73,40 @@ struct VocX {
 
 // Pipelined stage1 tail (vocoder_tailp.hip): ConvT3, ResBlock3, ConvT4,
 // ResBlock4 and output_conv in polyphase form over the columns q of U2.
-// Layer l (0..6) has nmb(l) m-blocks of 16 rows and nkb(l) k-blocks of 32;
-// kslot(l, mb, kb, g) is what lane group g reads in k-block kb: ring (0 = the
-// layer's input, 1 = the residual ring), column offset dq, input octet; pad
-// slots carry zero weights.  The same table packs the weights (host) and
-// addresses the B fragments (device).
+// Layer l (0..6) has nmb(l) m-blocks of 16 rows and nkb(l) k-blocks of 32.
+// A k-block's B fragment is one of the layer's nfrag(l) fragments,
+// frag(l, mb, kb); fslot(l, f, g) is what lane group g reads for fragment f:
+// column offset dq and input octet of the layer's input ring.  Fragments are
+// shared between the m-blocks of a layer wherever their taps allow, so one
+// wave doing both m-blocks reads each fragment once; a slot an m-block does
+// not use carries zero weights (its dense polyphase matrix is zero there).
+// The same tables pack the weights (host) and address the fragments (device).
 namespace tp {
 struct Slot {
-    int res, dq, oct, pad;
+    int dq, oct;
 };
 constexpr int kLayers = 7, kUnits = 22;
 constexpr int nmb(int l) { return l == 6 ? 1 : 2; }
 constexpr int nkb(int l) { return (l == 4 || l == 5) ? 1 : 2; }
+constexpr int nfrag(int l) { return l == 0 ? 3 : 2; }
 constexpr int unit0(int l) { return l <= 4 ? 4 * l : (l == 5 ? 18 : 20); }
-constexpr Slot kslot(int l, int mb, int kb, int g) {
-    if (l == 4 || l == 5)  // k3 on 4 phases of 8 channels: rows (p, p+1) read phases p-1 .. p+2
-        return mb == 0 ? (g == 0 ? Slot{0, -1, 3, 0} : Slot{0, 0, g - 1, 0})
-                       : (g == 3 ? Slot{0, 1, 0, 0} : Slot{0, 0, g + 1, 0});
-    if (l == 0)  // ConvT3: phase 0 reads columns q and q-1, phase 1 reads q+1 and q
-        return Slot{0, mb == 0 ? (kb == 0 ? 0 : -1) : (kb == 0 ? 1 : 0), g, 0};
-    if (kb == 0) return Slot{0, 0, g, 0};  // the whole column q
-    if (g < 2) {
-        if (l == 6)  // output conv: phase 0 also reads (q-1, phase 3), phase 3 (q+1, phase 0)
-            return g == 0 ? Slot{0, -1, 3, 0} : Slot{0, 1, 0, 0};
-        // 2 phases of 16 channels: phase 0 also reads (q-1, phase 1), phase 1 (q+1, phase 0)
-        return mb == 0 ? Slot{0, -1, 2 + g, 0} : Slot{0, 1, g, 0};
-    }
-    if (l == 2) return Slot{1, 0, 2 * mb + (g - 2), 0};  // ResBlock3 residual x (identity weights)
-    return Slot{0, 0, g, 1};  // pad: a distinct octet per lane group keeps the read conflict-free
+// ConvT3: phase 0 reads columns q, q-1 (fragments 0, 1), phase 1 q+1, q (2, 0);
+// ResBlock4 convs: m-block (phases p, p+1) reads phases p-1 .. p+2, one
+// fragment per m-block; the others: whole column q, then the neighbours.
+constexpr int frag(int l, int mb, int kb) {
+    return l == 0 ? (mb == 0 ? kb : (kb == 0 ? 2 : 0)) : ((l == 4 || l == 5) ? mb : kb);
 }
+constexpr Slot fslot(int l, int f, int g) {
+    if (l == 0) return Slot{f == 0 ? 0 : (f == 1 ? -1 : 1), g};
+    if (l == 4 || l == 5)
+        return f == 0 ? (g == 0 ? Slot{-1, 3} : Slot{0, g - 1}) : (g == 3 ? Slot{1, 0} : Slot{0, g + 1});
+    if (f == 0) return Slot{0, g};  // the whole column q
+    if (l == 6)  // output conv: phase 0 also reads (q-1, phase 3), phase 3 (q+1, phase 0); g 2, 3: (q, g) again
+        return g == 0 ? Slot{-1, 3} : (g == 1 ? Slot{1, 0} : Slot{0, g});
+    // 2 phases of 16 channels: phase 0 also reads (q-1, phase 1), phase 1 (q+1, phase 0)
+    return g < 2 ? Slot{-1, 2 + g} : Slot{1, g - 2};
+}
+constexpr Slot kslot(int l, int mb, int kb, int g) { return fslot(l, frag(l, mb, kb), g); }
 }  // namespace tp
 
 // Pipelined stage1 mid stage (vocoder_midp.hip): ConvT2 (layer 0), ResBlock2

@@ -15,8 +15,9 @@
 // rows of an m-block (two phases), where the natural layout fills 8.
 //
 // Systolic pipeline.  One workgroup owns a strip of 16*NCH columns of one
-// utterance and runs 14 waves with fixed roles: a loader wave streams U2 into
-// an LDS ring, and each of the 7 layers is done by one wave per m-block, all
+// utterance and runs 8 waves with fixed roles: a loader wave streams U2 into
+// an LDS ring, and each of the 7 layers is done by one wave for all its
+// m-blocks (which share B fragments, tp::frag, so each is read from LDS once),
 // with their weights (2 KB per (m-block, k-block) fragment pair) and biases
 // held in VGPRs for the whole strip.  In step s the wave of layer l computes
 // chunk k = s - l - 1 (16 columns) from the ring its producer wrote in steps
@@ -33,6 +34,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "m2_common.h"
@@ -52,7 +54,7 @@ constexpr int RROWS = 64;         // 4 chunks of 16 columns
 constexpr int RING = RROWS * RS;  // bytes per ring
 constexpr int NRING = 7;          // R0 = U2 input, R(l+1) = output of layer l (l = 0..5)
 constexpr int LDS_BYTES = NRING * RING;
-constexpr int NWAVES = 14;        // 13 layer waves (one m-block each) + 1 loader
+constexpr int NWAVES = 8;         // 7 layer waves (all m-blocks of a layer) + 1 loader
 
 __device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
@@ -89,159 +91,195 @@ __device__ unsigned long long g_tp_stamps[1024][NWAVES][64][2];
 // ~1e-7 (saturates to +-1 through inf / 0), against ~40 instructions for tanhf.
 __device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
 
-// Staggered epilogues (TP_DEFER bit l: layer l stores chunk k one step after
-// computing it, keeping acc / cor across the barrier, so its epilogue overlaps
-// the other roles' reads and MFMAs).  Layer l computes chunk k in step
-// k + off_l(l); its consumer one step after the store.  Layers 1 and 4 must not
-// defer: the residual readers two layers down would then meet the ring slot
-// their producer is rewriting.
-#ifndef TP_DEFER
-#define TP_DEFER 0
-#endif
-constexpr bool defer_l(int l) { return (TP_DEFER >> l) & 1; }
-constexpr int off_l(int l) { return l == 0 ? 1 : off_l(l - 1) + 1 + (defer_l(l - 1) ? 1 : 0); }
-constexpr int last_step(int nch) { return nch - 1 + off_l(6) + (defer_l(6) ? 1 : 0); }
-static_assert(!defer_l(1) && !defer_l(4), "layers 1 and 4 feed residual readers: no deferral");
+// Layer l computes chunk k in step k + l + 1; the last step is layer 6's
+// chunk NCH - 1.  (Staggered epilogues, where some layers store chunk k one
+// step after computing it, measured slower and were dropped.)
+constexpr int off_l(int l) { return l + 1; }
+constexpr int last_step(int nch) { return nch - 1 + off_l(6); }
 
-template <int L, int MB0, int NMB, int NCH>
+// max(x, y) as a bare v_max_f32: fmaxf (and fmed3 with inf, which the
+// compiler turns back into it) adds a NaN-quieting v_max(x, x) per MFMA result.
+__device__ __forceinline__ float vmax(float x, float y) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
+template <int V>
+using ic = std::integral_constant<int, V>;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// One wave per layer (all NMB m-blocks).  Everything lane-dependent that does
+// not change along the strip is precomputed: the weights, biases and the LDS
+// addresses of the fragment reads, residual reads and epilogue stores for the
+// four ring phases j = k mod 4 (the step loop is unrolled by four, so j is a
+// compile-time index).  Per step and m-block the epilogue is then leaky (a
+// packed multiply and two max), the split (3 VALU per pair), two permlane16
+// swaps and one ds_write_b128; the zeroing of columns outside [0, L2) is a
+// scalar branch taken only by chunks that straddle an utterance end.
+template <int L, int NMB, int NCH>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
                                            float* __restrict__ arow) {
-    constexpr int NKB = nkb(L);
-    constexpr int ACT = (L == 2 || L == 5) ? ACT_NONE : ACT_LEAKY;  // layer 6: tanh below
+    constexpr int NKB = nkb(L), NF = nfrag(L);
+    // ResBlock conv2: + x (the ConvT output, ring R(L-1), two columns ahead),
+    // added by two more MFMAs per m-block with an identity A (x hi, x lo) on
+    // one more shared fragment: 4 MFMA issues instead of 24 VALU per step.
+    constexpr bool RES = L == 2 || L == 5;
+    constexpr int ACT = RES ? ACT_NONE : ACT_LEAKY;  // layer 6: tanh below
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    // Fragment f is read iff one of this wave's (m-block, k-block) uses it.
+    auto used = [](int f) {
+        bool u = false;
+        for (int m = 0; m < NMB; ++m)
+            for (int kb = 0; kb < NKB; ++kb) u = u || frag(L, m, kb) == f;
+        return u;
+    };
     u32x4 a[NMB][NKB][2];
     float bv[NMB][4];
-    int roff[NMB][NKB], boff[NMB][NKB];
 #pragma unroll
     for (int m = 0; m < NMB; ++m) {
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) {
-            const int u = unit0(L) + (MB0 + m) * NKB + kb;
+            const int u = unit0(L) + m * NKB + kb;
             a[m][kb][0] = W[u * 128 + lane];
             a[m][kb][1] = W[u * 128 + 64 + lane];
-            const Slot sl = kslot(L, MB0 + m, kb, g);
-            // input ring R(L) holds layer L-1's columns, one column ahead of
-            // layer L's; the residual ring R1 (layer 2 only) two columns ahead.
-            roff[m][kb] = sl.dq - (sl.res ? 2 : 1);
-            boff[m][kb] = (sl.res ? 1 : L) * RING + sl.oct * 16;
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 32 + (MB0 + m) * 16 + 4 * g + r];
+        for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 32 + m * 16 + 4 * g + r];
     }
-    const int sL = qa + 6 - L;
-    constexpr bool DEF = defer_l(L);
-    f32x4 acc[NMB], cor[NMB];
-    h4 rxh[NMB], rxl[NMB];  // layer 5: the residual x, read with the B fragments
-    // Reads (+ residual) and MFMAs of chunk k into acc / cor.
-    auto compute = [&](int k) {
-        u32x4 bh[NMB][NKB], bl[NMB][NKB];
+    // input ring R(L) holds layer L-1's columns one column ahead of layer L's,
+    // the residual ring R(L-1) two columns ahead; rows wrap mod 64.
+    unsigned radr[NF][4], xadr[4], oadr[4];
 #pragma unroll
-        for (int m = 0; m < NMB; ++m)
+    for (int j = 0; j < 4; ++j) {
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) {
-                const int row = (16 * k + li + roff[m][kb]) & (RROWS - 1);
-                const unsigned char* p = lds + boff[m][kb] + row * RS;
-                bh[m][kb] = *reinterpret_cast<const u32x4*>(p);
-                bl[m][kb] = *reinterpret_cast<const u32x4*>(p + 64);
-            }
-        if constexpr (L == 5) {  // ResBlock4 residual: u4 (R4) two columns ahead
-#pragma unroll
-            for (int m = 0; m < NMB; ++m) {
-                const unsigned char* xp =
-                    lds + 4 * RING + ((16 * k + li - 2) & (RROWS - 1)) * RS + 2 * (16 * (MB0 + m) + 4 * g);
-                rxh[m] = *reinterpret_cast<const h4*>(xp);
-                rxl[m] = *reinterpret_cast<const h4*>(xp + 64);
-            }
+        for (int f = 0; f < NF; ++f) {
+            const Slot sl = fslot(L, f, g);
+            radr[f][j] = L * RING + sl.oct * 16 + ((16 * j + li + sl.dq - 1) & (RROWS - 1)) * RS;
         }
+        xadr[j] = (L - 1) * RING + ((16 * j + li - 2) & (RROWS - 1)) * RS + 16 * g;
+        oadr[j] = (L + 1) * RING + ((16 * j + li) & (RROWS - 1)) * RS + 64 * (g & 1) + 16 * (g >> 1);
+    }
+    // identity A of m-block m: row li takes input row 16m + li = 8g + e
+    u32x4 aid[NMB];
 #pragma unroll
-        for (int m = 0; m < NMB; ++m) {
-            acc[m] = f32x4{bv[m][0], bv[m][1], bv[m][2], bv[m][3]};
-            cor[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < NMB; ++m) {
+        h8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (_Float16)(16 * m + li == 8 * g + e ? 1.f : 0.f);
+        aid[m] = __builtin_bit_cast(u32x4, v);
+    }
+    const int sL = qa + 6 - L;  // first column of chunk 0
+    auto work = [&](int k, auto jc) {
+        constexpr int j = decltype(jc)::value;
+        u32x4 bh[NF], bl[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+            if (used(f)) {
+                bh[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][j]);
+                bl[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][j] + 64);
+            }
+        u32x4 xh, xl;
+        if constexpr (RES) {
+            xh = *reinterpret_cast<const u32x4*>(lds + xadr[j]);
+            xl = *reinterpret_cast<const u32x4*>(lds + xadr[j] + 64);
         }
+        // hi*hi, hi*lo and lo*hi into one fp32 accumulator per m-block
+        f32x4 acc[NMB];
+#pragma unroll
+        for (int m = 0; m < NMB; ++m) acc[m] = f32x4{bv[m][0], bv[m][1], bv[m][2], bv[m][3]};
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-            for (int m = 0; m < NMB; ++m) {
-                acc[m] = mfma_h(a[m][kb][0], bh[m][kb], acc[m]);
-                cor[m] = mfma_h(a[m][kb][0], bl[m][kb], cor[m]);
-                cor[m] = mfma_h(a[m][kb][1], bh[m][kb], cor[m]);
-            }
-    };
-    // Activation, split and store of chunk k from acc / cor.
-    auto epilogue = [&](int k) {
-        const int x = sL + 16 * k + li;  // this lane's column
+            for (int pr = 0; pr < 3; ++pr)
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+                    const int f = frag(L, m, kb);
+                    acc[m] = mfma_h(a[m][kb][pr == 2], pr == 1 ? bl[f] : bh[f], acc[m]);
+                }
+        if constexpr (RES) {
+#pragma unroll
+            for (int m = 0; m < NMB; ++m) acc[m] = mfma_h(aid[m], xh, acc[m]);
+#pragma unroll
+            for (int m = 0; m < NMB; ++m) acc[m] = mfma_h(aid[m], xl, acc[m]);
+        }
+        const int x0 = sL + 16 * k;  // this chunk's first column
         if constexpr (L == 6) {
             // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
+            const int x = x0 + li;
             if (g == 0 && k >= 0 && x >= 0 && x < L2) {
                 float4 o;
-                o.x = tanh_fast(acc[0][0] + cor[0][0]);
-                o.y = tanh_fast(acc[0][1] + cor[0][1]);
-                o.z = tanh_fast(acc[0][2] + cor[0][2]);
-                o.w = tanh_fast(acc[0][3] + cor[0][3]);
+                o.x = tanh_fast(acc[0][0]);
+                o.y = tanh_fast(acc[0][1]);
+                o.z = tanh_fast(acc[0][2]);
+                o.w = tanh_fast(acc[0][3]);
                 *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
             }
         } else {
-            const bool zero = edge && (x < 0 || x >= L2);
-            const int orow = (16 * k + li) & (RROWS - 1);
+            const bool straddle = edge && (x0 < 0 || x0 + 16 > L2);  // wave-uniform
 #pragma unroll
             for (int m = 0; m < NMB; ++m) {
                 float v[4];
+                if constexpr (ACT == ACT_LEAKY) {
+                    const f2 s0 = f2{acc[m][0], acc[m][1]} * kLeaky, s1 = f2{acc[m][2], acc[m][3]} * kLeaky;
+                    v[0] = vmax(acc[m][0], s0.x);
+                    v[1] = vmax(acc[m][1], s0.y);
+                    v[2] = vmax(acc[m][2], s1.x);
+                    v[3] = vmax(acc[m][3], s1.y);
+                } else {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[m][r] + cor[m][r]);
-                if constexpr (L == 5) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)rxh[m][r] + (float)rxl[m][r];
+                    for (int r = 0; r < 4; ++r) v[r] = acc[m][r];
                 }
-                if (zero) {
+                if (straddle) {
+                    const int x = x0 + li;
+                    if (x < 0 || x >= L2) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = 0.f;
+                        for (int r = 0; r < 4; ++r) v[r] = 0.f;
+                    }
                 }
                 unsigned h0, h1, l0, l1;
                 split2u(v[0], v[1], h0, l0);
                 split2u(v[2], v[3], h1, l1);
-                u32x2 hv{h0, h1}, lv{l0, l1};
                 // Lane groups 0/1 (and 2/3) hold channels 0-3 / 4-7 (8-11 /
                 // 12-15) of the m-block; one permlane16 swap per dword gives
                 // group 0 the hi octet of channels 0-7 and group 1 its lo
                 // octet (groups 2/3: channels 8-15), so each lane stores one
                 // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
                 // 8-B halves (ds_write_b64, 4-way).
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const auto sw = __builtin_amdgcn_permlane16_swap(hv[j], lv[j], false, false);
-                    hv[j] = sw[0];
-                    lv[j] = sw[1];
-                }
-                unsigned char* op = lds + (L + 1) * RING + orow * RS + 32 * (MB0 + m) + 64 * (g & 1) + 16 * (g >> 1);
-                *reinterpret_cast<u32x4*>(op) = u32x4{hv[0], hv[1], lv[0], lv[1]};
+                const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
+                const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
+                *reinterpret_cast<u32x4*>(lds + oadr[j] + 32 * m) = u32x4{s0[0], s1[0], s0[1], s1[1]};
             }
         }
     };
-    int kp = -2;  // deferred roles: the chunk whose epilogue is pending
-#pragma unroll 1
-    for (int s = -1; s <= last_step(NCH); ++s) {
-        TPSTAMP(s + 1, 0);
-        const int k = s - off_l(L);
-        if constexpr (DEF) {
-            if (kp >= -1) epilogue(kp);
-            kp = -2;
-            if (k >= -1 && k < NCH) {
-                compute(k);
-                kp = k;
-            }
-        } else if (k >= -1 && k < NCH) {
-            compute(k);
-            epilogue(k);
+    constexpr int LAST = last_step(NCH);
+    auto step = [&](int s, auto jc) {
+        if (s <= LAST) {
+            TPSTAMP(s + 1, 0);
+            const int k = s - off_l(L);
+            if (k >= -1 && k < NCH) work(k, jc);
+            TPSTAMP(s + 1, 1);
+            step_barrier();
         }
-        TPSTAMP(s + 1, 1);
-        step_barrier();
+    };
+    // step s handles chunk k = s - L - 1, ring phase k & 3: (J0 + i) & 3 in copy i
+    constexpr int J0 = (-1 - off_l(L)) & 3;
+#pragma unroll 1
+    for (int s = -1; s <= LAST; s += 4) {
+        step(s, ic<J0>{});
+        step(s + 1, ic<(J0 + 1) & 3>{});
+        step(s + 2, ic<(J0 + 2) & 3>{});
+        step(s + 3, ic<(J0 + 3) & 3>{});
     }
 }
 
 // U2 rows (128 B: hi[32] lo[32], the mid kernel's output format) into ring R0,
 // two chunks ahead: chunk c = columns [qa + 7 + 16c, +16), zero outside [0, L2).
-template <int NCH>
+// EDGE: the strip's columns (with the prologue / epilogue chunks) may leave
+// [0, L2); interior strips skip the clamps and the zero selects.
+template <int NCH, bool EDGE>
 __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, const unsigned char* __restrict__ u2) {
     const int lane = threadIdx.x & 63, r = lane >> 3, pc = lane & 7;
     // Every step issues its two loads unconditionally (column clamped into the
@@ -251,7 +289,8 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     auto fetch = [&](int c, u32x4 (&v)[2]) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int col = min(max(qa + 7 + 16 * c + r + 8 * h, 0), L2 - 1);
+            int col = qa + 7 + 16 * c + r + 8 * h;
+            if (EDGE) col = min(max(col, 0), L2 - 1);
             v[h] = *reinterpret_cast<const u32x4*>(u2 + (size_t)col * 128 + pc * 16);
         }
     };
@@ -265,7 +304,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int col = qa + 7 + 16 * s + r + 8 * h;
-                const bool in = col >= 0 && col < L2;
+                const bool in = !EDGE || (col >= 0 && col < L2);
                 const u32x4 z{0u, 0u, 0u, 0u};
                 const int row = (16 * s + r + 8 * h) & (RROWS - 1);
                 *reinterpret_cast<u32x4*>(lds + row * RS + pc * 16) = in ? cur[h] : z;
@@ -287,7 +326,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
 }
 
 template <int NCH>
-__global__ __launch_bounds__(NWAVES * 64, 7) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
+__global__ __launch_bounds__(NWAVES * 64, 4) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
                                                                 const u32x4* __restrict__ W,
                                                                 const float* __restrict__ bias,
                                                                 float* __restrict__ audio) {
@@ -300,24 +339,21 @@ __global__ __launch_bounds__(NWAVES * 64, 7) void tailp_kernel(const unsigned ch
     // Later layers get higher issue priority: they are the younger waves of
     // the workgroup and lose VALU arbitration on age (MI355X_MICROARCH.md, two
     // waves per SIMD), while the step waits for the slowest role (-1.5 %).
-    if (w >= 9) __builtin_amdgcn_s_setprio(3);
-    else if (w >= 6) __builtin_amdgcn_s_setprio(2);
-    else if (w >= 3) __builtin_amdgcn_s_setprio(1);
+    if (w >= 5) __builtin_amdgcn_s_setprio(3);
+    else if (w >= 3) __builtin_amdgcn_s_setprio(2);
+    else if (w >= 1) __builtin_amdgcn_s_setprio(1);
     switch (w) {
-        case 0: layer_role<0, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 1: layer_role<0, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 2: layer_role<1, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 3: layer_role<1, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 4: layer_role<2, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 5: layer_role<2, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 6: layer_role<3, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 7: layer_role<3, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 8: layer_role<4, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 9: layer_role<4, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 10: layer_role<5, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 11: layer_role<5, 1, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 12: layer_role<6, 0, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        default: loader_role<NCH>(lds, qa, L2, U2 + (size_t)b * L2 * 128); break;
+        case 0: layer_role<0, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 1: layer_role<1, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 2: layer_role<2, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 3: layer_role<3, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 4: layer_role<4, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 5: layer_role<5, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 6: layer_role<6, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        default:
+            if (edge) loader_role<NCH, true>(lds, qa, L2, U2 + (size_t)b * L2 * 128);
+            else loader_role<NCH, false>(lds, qa, L2, U2 + (size_t)b * L2 * 128);
+            break;
     }
     TPSTAMP(63, 0);
 }
@@ -365,8 +401,8 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
 // Host packing.  Each layer is first written as a dense polyphase matrix
 // Wd[row][dq + 1][input row] (32 x 3 x 32), then cut into (m-block, k-block)
 // fragment pairs along tp::kslot: A[row = mb*16 + (lane&15)][slot g = lane>>4,
-// element e] = Wd[row][dq + 1][8*oct + e]; pad slots are zero, residual slots
-// (layer 2) the identity.  Every non-zero of Wd must sit on a slot.
+// element e] = Wd[row][dq + 1][8*oct + e], zero on a repeated slot.  Every
+// non-zero of Wd must sit on a slot.
 namespace {
 
 int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -433,7 +469,7 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
                     for (int kb = 0; missing && kb < tp::nkb(l); ++kb)
                         for (int g = 0; g < 4; ++g) {
                             const tp::Slot sl = tp::kslot(l, row / 16, kb, g);
-                            if (!sl.pad && !sl.res && sl.dq == dq && sl.oct == in / 8) missing = false;
+                            if (sl.dq == dq && sl.oct == in / 8) missing = false;
                         }
                     if (missing) return false;  // a non-zero weight that no slot reads
                 }
@@ -443,12 +479,17 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
             for (int kb = 0; kb < tp::nkb(l); ++kb) {
                 const int u = tp::unit0(l) + mb * tp::nkb(l) + kb;
                 for (int lane = 0; lane < 64; ++lane) {
-                    const int row = mb * 16 + (lane & 15);
-                    const tp::Slot sl = tp::kslot(l, mb, kb, lane >> 4);
+                    const int row = mb * 16 + (lane & 15), g = lane >> 4;
+                    const tp::Slot sl = tp::kslot(l, mb, kb, g);
+                    // a (dq, octet) the m-block already reads in an earlier slot gets zeros
+                    bool dup = false;
+                    for (int j = 0; j < kb * 4 + g; ++j) {
+                        const tp::Slot o = tp::kslot(l, mb, j / 4, j % 4);
+                        dup = dup || (o.dq == sl.dq && o.oct == sl.oct);
+                    }
                     for (int e = 0; e < 8; ++e) {
                         float v = 0.f;
-                        if (row < nrows[l] && !sl.pad)
-                            v = sl.res ? (row == 8 * sl.oct + e ? 1.f : 0.f) : d[l].at(row, sl.dq, 8 * sl.oct + e);
+                        if (row < nrows[l] && !dup) v = d[l].at(row, sl.dq, 8 * sl.oct + e);
                         put_split(*wout, (((size_t)u * 2) * 64 + lane) * 8 + e, v, range_ok);
                     }
                 }
