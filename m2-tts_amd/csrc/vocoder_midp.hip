@@ -27,6 +27,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "m2_common.h"
@@ -54,7 +55,27 @@ __device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
 
 __device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// max(x, y) as a bare v_max_f32 (fmaxf adds a NaN-quieting v_max(x, x) per
+// MFMA result).
+__device__ __forceinline__ float vmax(float x, float y) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
+template <int V>
+using ic = std::integral_constant<int, V>;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 // Layer L (0 ConvT2, 1 conv1, 2 conv2) of phase S: both m-blocks 2S, 2S+1.
+// As in vocoder_tailp.hip: one fp32 accumulator per m-block for the three
+// split products, LDS addresses precomputed for the four ring phases
+// j = k mod 4 (step loop unrolled by four), leaky as a packed multiply and
+// bare max, zeroing as a wave-uniform branch on chunks that straddle an
+// utterance end, and conv2's residual (ConvT2's output, ring R1, two columns
+// ahead: channels 32S .. 32S+31 = one fragment shared by both m-blocks) as
+// two identity-A MFMAs per m-block instead of 24 VALU.
 template <int L, int S, int NCH>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, bool edge,
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
@@ -66,7 +87,6 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
     u32x4 a[2][NKB][2];
     float bv[2][4];
-    int rowc[NKB], boff[NKB];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -78,96 +98,124 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[h][r] = bias[L * 128 + 32 * S + 16 * h + 4 * g + r];
     }
+    unsigned radr[NKB][4], xadr[4], oadr[4];
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-        const MSlot sl = mslot(L, S, kb, g);
-        rowc[kb] = sl.dq - 1;  // the input ring runs one column ahead of this layer
-        boff[kb] = IN_OFF + sl.oct * 16;
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            const MSlot sl = mslot(L, S, kb, g);  // the input ring runs one column ahead of this layer
+            radr[kb][j] = IN_OFF + sl.oct * 16 + ((16 * j + li + sl.dq - 1) & (RROWS - 1)) * RSI;
+        }
+        xadr[j] = R1_OFF + ((16 * j + li - 2) & (RROWS - 1)) * RS1 + 64 * S + 16 * g;
+        oadr[j] = (L == 0 ? R1_OFF : R2_OFF) + ((16 * j + li) & (RROWS - 1)) * RS1 + 64 * S + 256 * (g & 1) +
+                  16 * (g >> 1);
+    }
+    u32x4 aid[2];  // identity A of m-block h: row li takes fragment row 16h + li = 8g + e
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        h8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (_Float16)(16 * h + li == 8 * g + e ? 1.f : 0.f);
+        aid[h] = __builtin_bit_cast(u32x4, v);
     }
     const int sL = qa + 2 - L;
-#pragma unroll 1
-    for (int s = -1; s < NCH + 3; ++s) {
-        const int k = s - (L + 1);
-        if (k >= -1 && k < NCH) {
-            f32x4 acc[2], cor[2];
+    auto work = [&](int k, auto jc) {
+        constexpr int j = decltype(jc)::value;
+        u32x4 bh[NKB], bl[NKB];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                acc[h] = f32x4{bv[h][0], bv[h][1], bv[h][2], bv[h][3]};
-                cor[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kb = 0; kb < NKB; ++kb) {
+            bh[kb] = *reinterpret_cast<const u32x4*>(lds + radr[kb][j]);
+            bl[kb] = *reinterpret_cast<const u32x4*>(lds + radr[kb][j] + LO_IN);
+        }
+        u32x4 xh, xl;
+        if constexpr (L == 2) {
+            xh = *reinterpret_cast<const u32x4*>(lds + xadr[j]);
+            xl = *reinterpret_cast<const u32x4*>(lds + xadr[j] + 256);
+        }
+        f32x4 acc[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc[h] = f32x4{bv[h][0], bv[h][1], bv[h][2], bv[h][3]};
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int pr = 0; pr < 3; ++pr)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) acc[h] = mfma_h(a[h][kb][pr == 2], pr == 1 ? bl[kb] : bh[kb], acc[h]);
+        if constexpr (L == 2) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) acc[h] = mfma_h(aid[h], xh, acc[h]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) acc[h] = mfma_h(aid[h], xl, acc[h]);
+        }
+        const int x0 = sL + 16 * k;  // this chunk's first column
+        const bool straddle = edge && (x0 < 0 || x0 + 16 > L1);  // wave-uniform
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float v[4];
+            if constexpr (L < 2) {
+                const f2 s0 = f2{acc[h][0], acc[h][1]} * kLeaky, s1 = f2{acc[h][2], acc[h][3]} * kLeaky;
+                v[0] = vmax(acc[h][0], s0.x);
+                v[1] = vmax(acc[h][1], s0.y);
+                v[2] = vmax(acc[h][2], s1.x);
+                v[3] = vmax(acc[h][3], s1.y);
+                if (straddle) {
+                    const int x = x0 + li;
+                    if (x < 0 || x >= L1) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = 0.f;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[h][r];
             }
-            u32x4 bh[NKB], bl[NKB];
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) {
-                const unsigned char* p = lds + boff[kb] + ((16 * k + li + rowc[kb]) & (RROWS - 1)) * RSI;
-                bh[kb] = *reinterpret_cast<const u32x4*>(p);
-                bl[kb] = *reinterpret_cast<const u32x4*>(p + LO_IN);
-            }
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    acc[h] = mfma_h(a[h][kb][0], bh[kb], acc[h]);
-                    cor[h] = mfma_h(a[h][kb][0], bl[kb], cor[h]);
-                    cor[h] = mfma_h(a[h][kb][1], bh[kb], cor[h]);
-                }
-            const int x = sL + 16 * k + li;  // this lane's column
-            const bool zero = edge && (x < 0 || x >= L1);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[h][r] + cor[h][r];
-                if constexpr (L < 2) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT_LEAKY>(v[r]);
-                } else {  // residual: ConvT2's output (R1) two columns ahead
-                    const unsigned char* xp = lds + R1_OFF + ((16 * k + li - 2) & (RROWS - 1)) * RS1 +
-                                              2 * (32 * S + 16 * h + 4 * g);
-                    const h4 xh = *reinterpret_cast<const h4*>(xp), xl = *reinterpret_cast<const h4*>(xp + 256);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)xh[r] + (float)xl[r];
-                }
-                if (L < 2 && zero) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = 0.f;
-                }
-                unsigned h0, h1, l0, l1;
-                split2u(v[0], v[1], h0, l0);
-                split2u(v[2], v[3], h1, l1);
-                u32x2 hv{h0, h1}, lv{l0, l1};
-                // lane groups 0/1 (2/3): channels 0-7 (8-15) of the m-block as
-                // one 16-B hi chunk (group 0/2) and one lo chunk (group 1/3)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const auto sw = __builtin_amdgcn_permlane16_swap(hv[j], lv[j], false, false);
-                    hv[j] = sw[0];
-                    lv[j] = sw[1];
-                }
-                const u32x4 val{hv[0], hv[1], lv[0], lv[1]};
-                if constexpr (L < 2) {
-                    unsigned char* op = lds + (L == 0 ? R1_OFF : R2_OFF) + ((16 * k + li) & (RROWS - 1)) * RS1 +
-                                        64 * S + 32 * h + 256 * (g & 1) + 16 * (g >> 1);
-                    *reinterpret_cast<u32x4*>(op) = val;
-                } else if (k >= 0 && x >= 0 && x < L1) {  // U2 row of position 4x + S
+            unsigned h0, h1, l0, l1;
+            split2u(v[0], v[1], h0, l0);
+            split2u(v[2], v[3], h1, l1);
+            // lane groups 0/1 (2/3): channels 0-7 (8-15) of the m-block as
+            // one 16-B hi chunk (group 0/2) and one lo chunk (group 1/3)
+            const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
+            const u32x4 val{s0[0], s1[0], s0[1], s1[1]};
+            if constexpr (L < 2) {
+                *reinterpret_cast<u32x4*>(lds + oadr[j] + 32 * h) = val;
+            } else {
+                const int x = x0 + li;
+                if (k >= 0 && x >= 0 && x < L1)  // U2 row of position 4x + S
                     *reinterpret_cast<u32x4*>(u2row + ((size_t)4 * x + S) * 128 + 32 * h + 64 * (g & 1) +
                                               16 * (g >> 1)) = val;
-                }
             }
         }
-        step_barrier();
+    };
+    constexpr int LAST = NCH + 2;  // conv2 computes chunk NCH - 1 in step NCH + 2
+    auto step = [&](int s, auto jc) {
+        if (s <= LAST) {
+            const int k = s - (L + 1);
+            if (k >= -1 && k < NCH) work(k, jc);
+            step_barrier();
+        }
+    };
+    constexpr int J0 = (-1 - (L + 1)) & 3;  // ring phase of step -1's chunk
+#pragma unroll 1
+    for (int s = -1; s <= LAST; s += 4) {
+        step(s, ic<J0>{});
+        step(s + 1, ic<(J0 + 1) & 3>{});
+        step(s + 2, ic<(J0 + 2) & 3>{});
+        step(s + 3, ic<(J0 + 3) & 3>{});
     }
 }
 
 // U1 rows (256 B) into ring R0, two chunks ahead: chunk c = columns
 // [qa + 3 + 16c, +16), zero outside [0, L1).  Four 16-B pieces per lane per
 // chunk, loads issued unconditionally (clamped) so their waits are counted.
-template <int NCH>
+template <int NCH, bool EDGE>
 __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L1, const unsigned char* __restrict__ u1) {
     const int lane = threadIdx.x & 63, cr = lane >> 4, pc = lane & 15;
     auto fetch = [&](int c, u32x4 (&v)[4]) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int col = min(max(qa + 3 + 16 * c + 4 * j + cr, 0), L1 - 1);
+            int col = qa + 3 + 16 * c + 4 * j + cr;
+            if (EDGE) col = min(max(col, 0), L1 - 1);
             v[j] = *reinterpret_cast<const u32x4*>(u1 + (size_t)col * 256 + pc * 16);
         }
     };
@@ -178,7 +226,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L1, 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int col = qa + 3 + 16 * s + 4 * j + cr;
-                const bool in = col >= 0 && col < L1;
+                const bool in = !EDGE || (col >= 0 && col < L1);
                 const u32x4 z{0u, 0u, 0u, 0u};
                 *reinterpret_cast<u32x4*>(lds + R0_OFF + ((16 * s + 4 * j + cr) & (RROWS - 1)) * RS0 + pc * 16) =
                     in ? cur[j] : z;
@@ -224,7 +272,10 @@ __global__ __launch_bounds__(NWAVES * 64, 4) void midp_kernel(const unsigned cha
         case 9: layer_role<2, 1, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
         case 10: layer_role<2, 2, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
         case 11: layer_role<2, 3, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        default: loader_role<NCH>(lds, qa, L1, U1 + (size_t)b * L1 * 256); break;
+        default:
+            if (edge) loader_role<NCH, true>(lds, qa, L1, U1 + (size_t)b * L1 * 256);
+            else loader_role<NCH, false>(lds, qa, L1, U1 + (size_t)b * L1 * 256);
+            break;
     }
 }
 

@@ -20,9 +20,7 @@ sys.path.insert(0, str(ROOT / "m2-tts_amd" / "src"))
 import bench  # noqa: E402
 from m2amd import _lib  # noqa: E402
 
-ROLES = ["L0 convT3 mb0", "L0 convT3 mb1", "L1 rb3c1 mb0", "L1 rb3c1 mb1", "L2 rb3c2 mb0", "L2 rb3c2 mb1",
-         "L3 convT4 mb0", "L3 convT4 mb1", "L4 rb4c1 mb0", "L4 rb4c1 mb1", "L5 rb4c2 mb0", "L5 rb4c2 mb1", "L6 out",
-         "loader"]
+ROLES = ["L0 convT3", "L1 rb3c1", "L2 rb3c2 (+x)", "L3 convT4", "L4 rb4c1", "L5 rb4c2 (+x)", "L6 out", "loader"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = 500
 dev = torch.device("cuda", 0)
