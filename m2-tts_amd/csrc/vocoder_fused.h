@@ -53,6 +53,25 @@ __device__ __forceinline__ void split2u(float v0, float v1, unsigned& hi, unsign
     asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(v0));
     asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(v1));
 }
+
+// max(x, y) as a bare v_max_f32: fmaxf (and fmed3 with inf, which the
+// compiler turns back into it) adds a NaN-quieting v_max(x, x) per MFMA result.
+__device__ __forceinline__ float vmax(float x, float y) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
+// leaky_relu(x, 0.1) of four accumulator values: two packed multiplies and
+// four bare max (== x > 0 ? x : 0.1x, as act_t<ACT_LEAKY>).
+__device__ __forceinline__ void leaky4(float (&v)[4]) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 s0 = f2{v[0], v[1]} * kLeaky, s1 = f2{v[2], v[3]} * kLeaky;
+    v[0] = vmax(v[0], s0.x);
+    v[1] = vmax(v[1], s0.y);
+    v[2] = vmax(v[2], s1.x);
+    v[3] = vmax(v[3], s1.y);
+}
 struct VocX {
     const vx_u32x4* wi;
     const float* bi;

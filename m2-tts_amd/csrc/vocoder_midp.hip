@@ -55,18 +55,8 @@ __device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
 
 __device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// max(x, y) as a bare v_max_f32 (fmaxf adds a NaN-quieting v_max(x, x) per
-// MFMA result).
-__device__ __forceinline__ float vmax(float x, float y) {
-    float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
-    return r;
-}
-
 template <int V>
 using ic = std::integral_constant<int, V>;
-
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 // Layer L (0 ConvT2, 1 conv1, 2 conv2) of phase S: both m-blocks 2S, 2S+1.
 // As in vocoder_tailp.hip: one fp32 accumulator per m-block for the three
@@ -152,12 +142,10 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[h][r];
             if constexpr (L < 2) {
-                const f2 s0 = f2{acc[h][0], acc[h][1]} * kLeaky, s1 = f2{acc[h][2], acc[h][3]} * kLeaky;
-                v[0] = vmax(acc[h][0], s0.x);
-                v[1] = vmax(acc[h][1], s0.y);
-                v[2] = vmax(acc[h][2], s1.x);
-                v[3] = vmax(acc[h][3], s1.y);
+                leaky4(v);
                 if (straddle) {
                     const int x = x0 + li;
                     if (x < 0 || x >= L1) {
@@ -165,9 +153,6 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
                         for (int r = 0; r < 4; ++r) v[r] = 0.f;
                     }
                 }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[h][r];
             }
             unsigned h0, h1, l0, l1;
             split2u(v[0], v[1], h0, l0);

@@ -97,18 +97,8 @@ __device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __built
 constexpr int off_l(int l) { return l + 1; }
 constexpr int last_step(int nch) { return nch - 1 + off_l(6); }
 
-// max(x, y) as a bare v_max_f32: fmaxf (and fmed3 with inf, which the
-// compiler turns back into it) adds a NaN-quieting v_max(x, x) per MFMA result.
-__device__ __forceinline__ float vmax(float x, float y) {
-    float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
-    return r;
-}
-
 template <int V>
 using ic = std::integral_constant<int, V>;
-
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 // One wave per layer (all NMB m-blocks).  Everything lane-dependent that does
 // not change along the strip is precomputed: the weights, biases and the LDS
@@ -222,16 +212,9 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
 #pragma unroll
             for (int m = 0; m < NMB; ++m) {
                 float v[4];
-                if constexpr (ACT == ACT_LEAKY) {
-                    const f2 s0 = f2{acc[m][0], acc[m][1]} * kLeaky, s1 = f2{acc[m][2], acc[m][3]} * kLeaky;
-                    v[0] = vmax(acc[m][0], s0.x);
-                    v[1] = vmax(acc[m][1], s0.y);
-                    v[2] = vmax(acc[m][2], s1.x);
-                    v[3] = vmax(acc[m][3], s1.y);
-                } else {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = acc[m][r];
-                }
+                for (int r = 0; r < 4; ++r) v[r] = acc[m][r];
+                if constexpr (ACT == ACT_LEAKY) leaky4(v);
                 if (straddle) {
                     const int x = x0 + li;
                     if (x < 0 || x >= L2) {

@@ -76,7 +76,7 @@ __device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
 }
 
 // ---------------------------------------------------------------------------
-// acc[n] += A_hi.B_hi, cor[n] += A_hi.B_lo + A_lo.B_hi over all k-blocks, for
+// acc[n] += A_hi.B_hi + A_hi.B_lo + A_lo.B_hi over all k-blocks, for
 // NT 16-position tiles (NT compile-time: no per-tile guards, which would
 // make the MFMA chain conditional code and blow up register allocation).
 // wp: this lane's A slot of k-block 0 (u32x4 units, k-block stride 128 =
@@ -88,7 +88,7 @@ __device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
 // packed weights hold the identity there, so the GEMM itself adds x.
 template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR>
 __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
-                                       const unsigned char* xr, f32x4 (&acc)[NT], f32x4 (&cor)[NT]) {
+                                       const unsigned char* xr, f32x4 (&acc)[NT]) {
     constexpr int NOCT = CIN / 8, NK = NTAP * NOCT, NKB = (NK + 3) / 4;
     static_assert(CIN % 8 == 0 && (NOCT <= 2 || NOCT % 4 == 0), "channel count must be 8, 16 or a multiple of 32");
     static_assert(!XR || 4 * NKB - NK == NOCT, "residual fold needs exactly one row of padding octets");
@@ -128,11 +128,11 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
         __builtin_amdgcn_sched_barrier(0);
         const u32x4 ah = a[kb % PD][0], al = a[kb % PD][1];
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-            acc[n] = mfma_h(ah, bh[n], acc[n]);
-            cor[n] = mfma_h(ah, blo[n], cor[n]);
-            cor[n] = mfma_h(al, bh[n], cor[n]);
-        }
+        for (int n = 0; n < NT; ++n) acc[n] = mfma_h(ah, bh[n], acc[n]);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = mfma_h(ah, blo[n], acc[n]);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = mfma_h(al, bh[n], acc[n]);
         if (kb + PD < NKB) {
             a[kb % PD][0] = wp[(kb + PD) * 128];
             a[kb % PD][1] = wp[(kb + PD) * 128 + 64];
@@ -144,7 +144,7 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
 template <int CIN, int NTAP>
 constexpr int nkb() { return (NTAP * (CIN / 8) + 3) / 4; }
 
-// Epilogue for one tile (acc already holds the bias): v = act(acc + cor)
+// Epilogue for one tile (acc already holds the bias): v = act(acc)
 // [+ residual read back from `out`], 0 outside [0, L) (only
 // evaluated for tiles that reach past an edge), split and stored as hi/lo.
 // Executed by every lane (the permlane16 swap reads the partner lane group);
@@ -153,11 +153,13 @@ constexpr int nkb() { return (NTAP * (CIN / 8) + 3) / 4; }
 // (3) the lo halves: one ds_write_b128 per lane instead of two ds_write_b64
 // (2-way instead of 4-way bank conflicts on RS/16 = 2 mod 4 rows).
 template <int COUT, int RSO, int ACT, bool RES>
-__device__ __forceinline__ void store_tile(const f32x4& acc, const f32x4& cor, XW out, int t, int co0, int L,
+__device__ __forceinline__ void store_tile(const f32x4& acc, XW out, int t, int co0, int L,
                                            bool edge, bool store) {
     float v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[r] + cor[r]);
+    for (int r = 0; r < 4; ++r) v[r] = acc[r];
+    if constexpr (ACT == ACT_LEAKY) leaky4(v);
+    else static_assert(ACT == ACT_NONE, "x3 layers: leaky or none");
     unsigned char* rowp = out.p + (t - out.start) * RSO;
     if (RES) {
         const unsigned char* row = rowp + co0 * 2;
@@ -193,7 +195,7 @@ template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int 
 __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
                                          const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
                                          int ph, int tile0, int L) {
-    f32x4 acc[NTT], cor[NTT];
+    f32x4 acc[NTT];
     {
         f32x4 bv;
 #pragma unroll
@@ -201,10 +203,9 @@ __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const flo
 #pragma unroll
         for (int n = 0; n < NTT; ++n) {
             acc[n] = bv;
-            cor[n] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
-    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR>(wp, bp, xr, acc, cor);
+    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR>(wp, bp, xr, acc);
     const bool edge = (p0 + tile0 * 16) * RR < 0 || (p0 + (tile0 + NTT) * 16) * RR > L;
     const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
     const bool rows_ok = co0 - 4 * g + 8 * (g >> 1) < COUT;  // after the swap: this lane's 8 channels
@@ -212,7 +213,7 @@ __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const flo
     for (int n = 0; n < NTT; ++n) {
         const int j = (tile0 + n) * 16 + li;
         const bool col_ok = ((tile0 + n + 1) * 16 <= JMAX) || j < JMAX;
-        store_tile<COUT, RSO, ACT, RES>(acc[n], cor[n], out, (p0 + j) * RR + ph, co0, L, edge, rows_ok && col_ok);
+        store_tile<COUT, RSO, ACT, RES>(acc[n], out, (p0 + j) * RR + ph, co0, L, edge, rows_ok && col_ok);
     }
 }
 
