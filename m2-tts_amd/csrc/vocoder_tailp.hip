@@ -208,33 +208,44 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                 *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
             }
         } else {
-            const bool straddle = edge && (x0 < 0 || x0 + 16 > L2);  // wave-uniform
+            // Both m-blocks in one basic block (the compiler interleaves their
+            // dependent VALU chains); chunks that straddle an utterance end
+            // take the copy that zeroes columns outside [0, L2).
+            auto epilogue = [&](auto zc) {
+                constexpr bool ZERO = decltype(zc)::value;
+                float v[NMB][4];
 #pragma unroll
-            for (int m = 0; m < NMB; ++m) {
-                float v[4];
+                for (int m = 0; m < NMB; ++m) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[m][r];
-                if constexpr (ACT == ACT_LEAKY) leaky4(v);
-                if (straddle) {
-                    const int x = x0 + li;
-                    if (x < 0 || x >= L2) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = 0.f;
-                    }
+                    for (int r = 0; r < 4; ++r) v[m][r] = acc[m][r];
+                    if constexpr (ACT == ACT_LEAKY) leaky4(v[m]);
                 }
-                unsigned h0, h1, l0, l1;
-                split2u(v[0], v[1], h0, l0);
-                split2u(v[2], v[3], h1, l1);
-                // Lane groups 0/1 (and 2/3) hold channels 0-3 / 4-7 (8-11 /
-                // 12-15) of the m-block; one permlane16 swap per dword gives
-                // group 0 the hi octet of channels 0-7 and group 1 its lo
-                // octet (groups 2/3: channels 8-15), so each lane stores one
-                // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
-                // 8-B halves (ds_write_b64, 4-way).
-                const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
-                const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
-                *reinterpret_cast<u32x4*>(lds + oadr[j] + 32 * m) = u32x4{s0[0], s1[0], s0[1], s1[1]};
-            }
+                if constexpr (ZERO) {
+                    const int x = x0 + li;
+                    const bool out = x < 0 || x >= L2;
+#pragma unroll
+                    for (int m = 0; m < NMB; ++m)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[m][r] = out ? 0.f : v[m][r];
+                }
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+                    unsigned h0, h1, l0, l1;
+                    split2u(v[m][0], v[m][1], h0, l0);
+                    split2u(v[m][2], v[m][3], h1, l1);
+                    // Lane groups 0/1 (and 2/3) hold channels 0-3 / 4-7 (8-11 /
+                    // 12-15) of the m-block; one permlane16 swap per dword gives
+                    // group 0 the hi octet of channels 0-7 and group 1 its lo
+                    // octet (groups 2/3: channels 8-15), so each lane stores one
+                    // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
+                    // 8-B halves (ds_write_b64, 4-way).
+                    const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
+                    const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
+                    *reinterpret_cast<u32x4*>(lds + oadr[j] + 32 * m) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+                }
+            };
+            if (edge && (x0 < 0 || x0 + 16 > L2)) epilogue(std::true_type{});  // wave-uniform
+            else epilogue(std::false_type{});
         }
     };
     constexpr int LAST = last_step(NCH);
