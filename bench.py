@@ -51,6 +51,10 @@ STAGE1 = dict(vocab_size=256, hidden_dim=64, mel_channels=64, text_encoder_layer
               num_heads=2, dropout=0.1, vocoder_channels=128)
 
 
+# Event sampling in the timed region: one event pair around the dominant
+# kernel every PROF_STRIDE steps (each pair costs a few us of pipeline drain).
+PROF_STRIDE = 8
+
 def vocoder_flops_per_sample(C: int, M: int) -> float:
     """Algorithmic FLOPs per output audio sample of SimpleVocoder.
 
@@ -138,8 +142,11 @@ def cpu_baseline(workload: str, B: int, S: int, T: int, budget_s: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # Defaults: the GPU clocks take tens of ms of load to settle (a first
+    # 30 ms loop runs ~7 % slow: tools/probe/timing_order.py), so the default
+    # warm-up is a few hundred steps (~40 ms); both finish in well under a second.
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--workload", choices=["vocoder", "pipeline"], default="vocoder")
     ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
     ap.add_argument("--phonemes", type=int, default=100)
@@ -181,15 +188,16 @@ def main():
 
     nk = lib.m2_profile_kernel_count()
 
-    def timed(fn, steps, warmup, kernel_mask=0):
+    def timed(fn, steps, warmup, kernel_mask=0, stride=1):
         """Run `steps` of fn between barriers + syncs; with kernel_mask, HIP
         events (fence-free, on the launch stream inside m2_vocoder) around
-        the selected fused vocoder kernels of every step."""
+        the selected fused vocoder kernels of every `stride`-th step."""
         for _ in range(warmup):
             fn()
         if kernel_mask:
             _lib.check(lib.m2_profile_select(hm.handle, kernel_mask), "m2_profile_select")
-            _lib.check(lib.m2_profile_enable(hm.handle, steps), "m2_profile_enable")
+            _lib.check(lib.m2_profile_stride(hm.handle, stride), "m2_profile_stride")
+            _lib.check(lib.m2_profile_enable(hm.handle, (steps + stride - 1) // stride), "m2_profile_enable")
         torch.cuda.synchronize(dev)
         if dist:
             td.barrier()
@@ -203,12 +211,13 @@ def main():
         ms = []
         if kernel_mask:
             import ctypes
-            cap = steps * nk
+            cap = (steps + stride - 1) // stride * nk
             buf = (ctypes.c_float * cap)()
             n = ctypes.c_int32(0)
             _lib.check(lib.m2_profile_read(hm.handle, buf, cap, ctypes.byref(n)), "m2_profile_read")
             ms = list(buf[: n.value])
             lib.m2_profile_disable(hm.handle)
+            _lib.check(lib.m2_profile_stride(hm.handle, 1), "m2_profile_stride")
         if dist:
             t = torch.tensor([el], device=dev, dtype=torch.float64)
             td.all_reduce(t, op=td.ReduceOp.MAX)
@@ -234,13 +243,13 @@ def main():
     # 1) Untimed pass with events on all three kernels: per-kernel table and
     #    which kernel dominates.  Events drain the pipeline between kernels
     #    (a few us each), so 2) the timed region carries events around the
-    #    dominant kernel only: its average duration over every launch of the
-    #    timed region is the roofline's denominator.  3) the same loop with no
-    #    events at all, for the record.
+    #    dominant kernel of every PROF_STRIDE-th step only: its average
+    #    duration over those launches of the timed region is the roofline's
+    #    denominator.  3) the same loop with no events at all, for the record.
     _, all_ms = timed(step, min(args.steps, 20), args.warmup, kernel_mask=(1 << nk) - 1)
     per_kernel = kernel_table(all_ms)
     dom_i = max(per_kernel, key=lambda d: d["avg_ms"])["index"] if per_kernel else 0
-    elapsed, kern_ms = timed(step, args.steps, 2, kernel_mask=1 << dom_i)
+    elapsed, kern_ms = timed(step, args.steps, 2, kernel_mask=1 << dom_i, stride=PROF_STRIDE)
     el_ne, _ = timed(step, args.steps, 2)
     samples_per_step = B * 64 * T
     total_samples = samples_per_step * args.steps * world

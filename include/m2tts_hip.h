@@ -194,6 +194,10 @@ int32_t m2_profile_disable(m2_model* model);
  * m2_profile_read reports -1 for the others.  Every recorded event costs a
  * few microseconds of pipeline drain between kernels. */
 int32_t m2_profile_select(m2_model* model, uint32_t kernel_mask);
+/* Record on every `stride`-th m2_vocoder call only (default 1; the calls in
+ * between record nothing and take no capacity), so a timed region can carry a
+ * sample of the launches at a fraction of the event cost.  Reset by enable. */
+int32_t m2_profile_stride(m2_model* model, int32_t stride);
 int32_t m2_profile_kernel_count(void);
 const char* m2_profile_kernel_name(int32_t index);
 /* The same kernel as launched by this model (symbol prefix = rocprofv3 name). */

@@ -161,6 +161,8 @@ struct m2_model {
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
     mutable int prof_calls = 0;
     uint32_t prof_mask = ~0u;  // which kernels get an event pair (m2_profile_select)
+    int prof_stride = 1;       // record on every prof_stride-th call (m2_profile_stride)
+    mutable long prof_seen = 0;
 };
 
 using namespace m2;
@@ -719,7 +721,8 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
     int32_t rc;
     if (m->fused) {
         const int call = m->prof_calls;
-        const bool rec = (size_t)(call + 1) * kVocKernels <= m->prof_begin.size();
+        const bool rec = (size_t)(call + 1) * kVocKernels <= m->prof_begin.size() &&
+                         m->prof_seen++ % m->prof_stride == 0;
         if (rec) m->prof_calls++;
         auto mark = [&](int kidx, bool begin) {
             if (!rec || !((m->prof_mask >> kidx) & 1u)) return;
@@ -840,6 +843,7 @@ int32_t m2_profile_enable(m2_model* m, int32_t capacity) {
         m->prof_end.push_back(b);
     }
     m->prof_calls = 0;
+    m->prof_seen = 0;
     return M2_OK;
 }
 
@@ -860,6 +864,13 @@ int32_t m2_profile_read(m2_model* m, float* ms_out, int32_t capacity, int32_t* n
 int32_t m2_profile_select(m2_model* m, uint32_t kernel_mask) {
     M2_CHECK_ARG(m, "m2_profile_select: null model");
     m->prof_mask = kernel_mask;
+    return M2_OK;
+}
+
+int32_t m2_profile_stride(m2_model* m, int32_t stride) {
+    M2_CHECK_ARG(m && stride >= 1, "m2_profile_stride: bad argument");
+    m->prof_stride = stride;
+    m->prof_seen = 0;
     return M2_OK;
 }
 

@@ -60,6 +60,7 @@ _SIGNATURES = {
     "m2_profile_kernel_name": (ctypes.c_char_p, [c_i32]),
     "m2_profile_kernel_name_for": (ctypes.c_char_p, [c_vp, c_i32]),
     "m2_profile_select": (c_i32, [c_vp, ctypes.c_uint32]),
+    "m2_profile_stride": (c_i32, [c_vp, c_i32]),
     "m2_vocoder_path": (c_i32, [c_vp]),
 }
 

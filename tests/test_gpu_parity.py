@@ -363,3 +363,29 @@ def test_alternate_kernel_paths(gpu, stage, env, monkeypatch):
     mel, audio = m.inference(ids, lens)
     assert maxabs(mel, g["mel"]) <= MEL_MAXABS_TOL
     assert rms(audio, g["audio"]) <= AUDIO_RMS_TOL
+
+
+def test_profile_events_strided(gpu):
+    """bench.py's roofline events: a stride-k sample of the m2_vocoder calls
+    records one event pair per selected kernel on every k-th call only."""
+    import ctypes
+    from m2amd import _lib
+    lib = _lib.load()
+    m = build_model("s1", gpu)
+    mel = torch.randn(2, 64, 40, device=gpu)
+    h = m._hip(gpu).handle
+    nk = lib.m2_profile_kernel_count()
+    _lib.check(lib.m2_profile_select(h, 1 << 2), "select")
+    _lib.check(lib.m2_profile_stride(h, 3), "stride")
+    _lib.check(lib.m2_profile_enable(h, 3), "enable")
+    for _ in range(7):  # calls 0, 3, 6 record
+        m.vocoder(mel)
+    buf = (ctypes.c_float * (3 * nk))()
+    n = ctypes.c_int32(0)
+    _lib.check(lib.m2_profile_read(h, buf, 3 * nk, ctypes.byref(n)), "read")
+    lib.m2_profile_disable(h)
+    _lib.check(lib.m2_profile_stride(h, 1), "stride")
+    ms = list(buf[: n.value])
+    assert n.value == 3 * nk
+    assert all(v > 0 for v in ms[2::nk]) and all(v < 0 for i, v in enumerate(ms) if i % nk != 2)
+    assert lib.m2_profile_stride(h, 0) != 0  # bad stride is an error, not a crash
