@@ -31,6 +31,7 @@
 // depends on its own B column only, and layer l is valid from column
 // qa - 8 + l of chunk -1 on while later layers need it from qa - 6 + l.
 // Columns outside [0, L2) store 0 (the next conv's zero padding).
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -49,12 +50,35 @@ typedef vx_u32x4 u32x4;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int RS = 160;           // ring row stride: 128 B (hi[32] lo[32]) + pad, RS/16 = 2 mod 4
-constexpr int RROWS = 64;         // 4 chunks of 16 columns
-constexpr int RING = RROWS * RS;  // bytes per ring
-constexpr int NRING = 7;          // R0 = U2 input, R(l+1) = output of layer l (l = 0..5)
-constexpr int LDS_BYTES = NRING * RING;
-constexpr int NWAVES = 8;         // 7 layer waves (all m-blocks of a layer) + 1 loader
+// LDS rings.  R0 = U2 input, R(l+1) = output of layer l (l = 0..5); a ring
+// row is one column: 32 rows x (hi, lo) f16 kept as a hi plane and a lo plane
+// of 64-B rows (the lo plane kLoOff(n) bytes after the hi plane, so a
+// fragment's lo read is its hi read plus an immediate offset).  Within a 64-B
+// row octet o sits at 16 * (o ^ ((row >> 1) & 3)): with lane li on row r0 + li
+// that makes every B-fragment read (ds_read_b128, 16-lane groups) and every
+// epilogue store (ds_write_b128, 8 consecutive rows) bank-conflict free
+// without padding (tools/probe/tailp_banks.py).  The swizzle depends on row
+// bits 1-2 only, so it does not change from chunk to chunk.  Rings hold 4
+// chunks of 16 columns (3 for R0 and R6, whose only reader is one step behind
+// its writer; R1 and R4 also feed a residual reader two layers down), 53,248 B
+// in all: three workgroups per CU.
+constexpr int kRingRows[7] = {48, 64, 64, 64, 64, 64, 48};
+constexpr int kRingOff(int n) { return n == 0 ? 0 : kRingOff(n - 1) + kRingRows[n - 1] * 128; }
+constexpr int kLoOff(int n) { return kRingRows[n] * 64; }
+constexpr int kPeriod(int n) { return kRingRows[n] / 16; }  // chunks per ring (3 or 4)
+constexpr int LDS_BYTES = kRingOff(7);
+static_assert(LDS_BYTES * 3 <= 160 * 1024, "three workgroups per CU");
+constexpr int NWAVES = 8;  // 7 layer waves (all m-blocks of a layer) + 1 loader
+
+// Byte offset of (row, octet) in ring n's hi plane; row in [0, kRingRows[n]).
+__device__ __forceinline__ unsigned ring_at(int n, int row, int oct) {
+    return kRingOff(n) + row * 64 + 16 * (oct ^ ((row >> 1) & 3));
+}
+// Row of column offset c (-2 .. 16) of the chunk in ring phase j.
+__device__ __forceinline__ int ring_row(int n, int j, int c) {
+    const int r = 16 * j + c, R = kRingRows[n];
+    return r < 0 ? r + R : (r >= R ? r - R : r);
+}
 
 __device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
@@ -139,19 +163,25 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 32 + m * 16 + 4 * g + r];
     }
-    // input ring R(L) holds layer L-1's columns one column ahead of layer L's,
-    // the residual ring R(L-1) two columns ahead; rows wrap mod 64.
-    unsigned radr[NF][4], xadr[4], oadr[4];
+    // Input ring R(L) holds layer L-1's columns one column ahead of layer L's,
+    // the residual ring R(L-1) two columns ahead.  Addresses for each ring
+    // phase (chunk index mod the ring's chunk count).
+    constexpr int PI = kPeriod(L), PO = L < 6 ? kPeriod(L + 1) : 1, PX = RES ? kPeriod(L - 1) : 1;
+    unsigned radr[NF][PI], xadr[PX], oadr[PO];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < PI; ++j)
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
             const Slot sl = fslot(L, f, g);
-            radr[f][j] = L * RING + sl.oct * 16 + ((16 * j + li + sl.dq - 1) & (RROWS - 1)) * RS;
+            radr[f][j] = ring_at(L, ring_row(L, j, li + sl.dq - 1), sl.oct);
         }
-        xadr[j] = (L - 1) * RING + ((16 * j + li - 2) & (RROWS - 1)) * RS + 16 * g;
-        oadr[j] = (L + 1) * RING + ((16 * j + li) & (RROWS - 1)) * RS + 64 * (g & 1) + 16 * (g >> 1);
-    }
+#pragma unroll
+    for (int j = 0; j < PX; ++j) xadr[j] = RES ? ring_at(L - 1, ring_row(L - 1, j, li - 2), g) : 0u;
+    // epilogue: after the permlane16 swap lane group g stores the hi (g even)
+    // or lo (g odd) octet of channels 8(g >> 1) .. +7 of each m-block
+#pragma unroll
+    for (int j = 0; j < PO; ++j)
+        oadr[j] = L < 6 ? (g & 1) * kLoOff(L + 1) + ring_at(L + 1, ring_row(L + 1, j, li), (g >> 1)) : 0u;
     // identity A of m-block m: row li takes input row 16m + li = 8g + e
     u32x4 aid[NMB];
 #pragma unroll
@@ -163,18 +193,19 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
     }
     const int sL = qa + 6 - L;  // first column of chunk 0
     auto work = [&](int k, auto jc) {
-        constexpr int j = decltype(jc)::value;
+        constexpr int kk = decltype(jc)::value;  // k mod lcm of the ring periods
+        constexpr int ji = kk % PI, jx = kk % PX, jo = kk % PO;
         u32x4 bh[NF], bl[NF];
 #pragma unroll
         for (int f = 0; f < NF; ++f)
             if (used(f)) {
-                bh[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][j]);
-                bl[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][j] + 64);
+                bh[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][ji]);
+                bl[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][ji] + kLoOff(L));
             }
         u32x4 xh, xl;
         if constexpr (RES) {
-            xh = *reinterpret_cast<const u32x4*>(lds + xadr[j]);
-            xl = *reinterpret_cast<const u32x4*>(lds + xadr[j] + 64);
+            xh = *reinterpret_cast<const u32x4*>(lds + xadr[jx]);
+            xl = *reinterpret_cast<const u32x4*>(lds + xadr[jx] + kLoOff(L - 1));
         }
         // hi*hi, hi*lo and lo*hi into one fp32 accumulator per m-block
         f32x4 acc[NMB];
@@ -237,11 +268,10 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                     // 12-15) of the m-block; one permlane16 swap per dword gives
                     // group 0 the hi octet of channels 0-7 and group 1 its lo
                     // octet (groups 2/3: channels 8-15), so each lane stores one
-                    // 16-B chunk (ds_write_b128, 2-way on RS 160) instead of two
-                    // 8-B halves (ds_write_b64, 4-way).
+                    // 16-B chunk (ds_write_b128) instead of two 8-B halves.
                     const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
                     const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
-                    *reinterpret_cast<u32x4*>(lds + oadr[j] + 32 * m) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+                    *reinterpret_cast<u32x4*>(lds + (oadr[jo] ^ (32 * m))) = u32x4{s0[0], s1[0], s0[1], s1[1]};
                 }
             };
             if (edge && (x0 < 0 || x0 + 16 > L2)) epilogue(std::true_type{});  // wave-uniform
@@ -258,14 +288,20 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
             step_barrier();
         }
     };
-    // step s handles chunk k = s - L - 1, ring phase k & 3: (J0 + i) & 3 in copy i
-    constexpr int J0 = (-1 - off_l(L)) & 3;
+    // step s handles chunk k = s - L - 1; the loop is unrolled by U, the lcm
+    // of the periods of the rings this layer touches, so every ring phase is a
+    // compile-time index: copy i of the iteration starting at step s sees
+    // k mod U = (J0 + i) mod U.
+    constexpr int U = (PI == 3 || PO == 3 || PX == 3) ? 12 : 4;
+    constexpr int J0 = ((-1 - off_l(L)) % U + U) % U;
+    auto iter = [&](int s, auto... i) { (step(s + decltype(i)::value, ic<(J0 + decltype(i)::value) % U>{}), ...); };
 #pragma unroll 1
-    for (int s = -1; s <= LAST; s += 4) {
-        step(s, ic<J0>{});
-        step(s + 1, ic<(J0 + 1) & 3>{});
-        step(s + 2, ic<(J0 + 2) & 3>{});
-        step(s + 3, ic<(J0 + 3) & 3>{});
+    for (int s = -1; s <= LAST; s += U) {
+        if constexpr (U == 4)
+            iter(s, ic<0>{}, ic<1>{}, ic<2>{}, ic<3>{});
+        else
+            iter(s, ic<0>{}, ic<1>{}, ic<2>{}, ic<3>{}, ic<4>{}, ic<5>{}, ic<6>{}, ic<7>{}, ic<8>{}, ic<9>{},
+                 ic<10>{}, ic<11>{});
     }
 }
 
@@ -292,7 +328,16 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     // no register that a load in flight writes is ever copied (a copy would
     // wait for that load).
     u32x4 buf[3][2];
-    auto step = [&](int s, u32x4 (&cur)[2], u32x4 (&ahead)[2]) {
+    // R0 has 3 chunks: chunk s sits in ring phase s mod 3 (the loop below is
+    // unrolled by three, so copy i writes phase (i + 2) mod 3).  Lanes pc 0-3
+    // carry hi octets, 4-7 lo octets.
+    unsigned wadr[3][2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) wadr[j][h] = (pc >> 2) * kLoOff(0) + ring_at(0, ring_row(0, j, r + 8 * h), pc & 3);
+    auto step = [&](int s, auto jc, u32x4 (&cur)[2], u32x4 (&ahead)[2]) {
+        constexpr int j = decltype(jc)::value;
         fetch(min(s + 2, NCH - 1), ahead);  // past the strip: re-read the last chunk (an L2 hit)
         if (s < NCH) {
 #pragma unroll
@@ -300,8 +345,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
                 const int col = qa + 7 + 16 * s + r + 8 * h;
                 const bool in = !EDGE || (col >= 0 && col < L2);
                 const u32x4 z{0u, 0u, 0u, 0u};
-                const int row = (16 * s + r + 8 * h) & (RROWS - 1);
-                *reinterpret_cast<u32x4*>(lds + row * RS + pc * 16) = in ? cur[h] : z;
+                *reinterpret_cast<u32x4*>(lds + wadr[j][h]) = in ? cur[h] : z;
             }
         }
         step_barrier();
@@ -311,16 +355,16 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     int s = -1;
 #pragma unroll 1
     for (; s + 2 <= last_step(NCH); s += 3) {  // covers every step with work (s <= NCH - 1)
-        step(s, buf[0], buf[2]);
-        step(s + 1, buf[1], buf[0]);
-        step(s + 2, buf[2], buf[1]);
+        step(s, ic<2>{}, buf[0], buf[2]);
+        step(s + 1, ic<0>{}, buf[1], buf[0]);
+        step(s + 2, ic<1>{}, buf[2], buf[1]);
     }
 #pragma unroll 1
     for (; s <= last_step(NCH); ++s) step_barrier();
 }
 
 template <int NCH>
-__global__ __launch_bounds__(NWAVES * 64, 4) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
+__global__ __launch_bounds__(NWAVES * 64, 6) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
                                                                 const u32x4* __restrict__ W,
                                                                 const float* __restrict__ bias,
                                                                 float* __restrict__ audio) {
@@ -381,13 +425,21 @@ const char* const kVocTailpKernelName =
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                              hipStream_t st) {
     if (B == 0 || L2 == 0) return M2_OK;
-    static const int nch = [] {
+    // Strip length: the shortest instantiated NCH that covers an utterance in
+    // at most floor(768 / B) strips, so the grid is about one round of three
+    // workgroups per CU (stage1 B = 32, L2 = 8000: 24 strips of NCH 21).
+    static const int forced = [] {
         const char* e = std::getenv("M2_TAILP_NCH");
-        const int v = e ? std::atoi(e) : 32;
-        return (v == 16 || v == 64) ? v : 32;
+        const int v = e ? std::atoi(e) : 0;
+        return (v == 21 || v == 32 || v == 48) ? v : 0;
     }();
-    if (nch == 16) return tp::launch<16>(U2, L2, B, W, bias, audio, st);
-    if (nch == 64) return tp::launch<64>(U2, L2, B, W, bias, audio, st);
+    int nch = forced;
+    if (!nch) {
+        const int chunks = cdiv(L2, 16), strips = std::max(1, 3 * 256 / B), need = cdiv(chunks, strips);
+        nch = need <= 21 ? 21 : (need <= 32 ? 32 : 48);
+    }
+    if (nch == 21) return tp::launch<21>(U2, L2, B, W, bias, audio, st);
+    if (nch == 48) return tp::launch<48>(U2, L2, B, W, bias, audio, st);
     return tp::launch<32>(U2, L2, B, W, bias, audio, st);
 }
 
