@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <functional>
 
 #include "m2_common.h"
@@ -75,6 +76,9 @@ __device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
     lo = __builtin_bit_cast(h4, u32x2{l0, l1});
 }
 
+template <int CIN, int NTAP>
+constexpr int nkb_of() { return (NTAP * (CIN / 8) + 3) / 4; }
+
 // ---------------------------------------------------------------------------
 // acc[n] += A_hi.B_hi + A_hi.B_lo + A_lo.B_hi over all k-blocks, for
 // NT 16-position tiles (NT compile-time: no per-tile guards, which would
@@ -86,9 +90,20 @@ __device__ __forceinline__ void split4(const float (&v)[4], h4& hi, h4& lo) {
 // XR (residual fold, 8- and 16-channel ResBlock conv2): the padding octets
 // of the last k-block read the block input x at the output row (xr) and the
 // packed weights hold the identity there, so the GEMM itself adds x.
-template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR>
+// NMB m-blocks (weight rows WS u32x4 apart) share every B fragment read.
+// a: the weight-fragment pipeline (PD k-blocks in flight).  PRE: the caller
+// already issued the loads of k-blocks 0 .. PD-1 (the previous layer's item
+// did, before its epilogue and the barrier); wp_next (PD == 4, NMB == 1): once
+// this item's last MFMA is issued, start the next item's first PD k-blocks.
+template <int CIN, int NTAP, int NMB>
+constexpr int pd_of() {
+    constexpr int NKB = (NTAP * (CIN / 8) + 3) / 4;
+    return NKB < 4 / NMB ? NKB : 4 / NMB;
+}
+template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE>
 __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
-                                       const unsigned char* xr, f32x4 (&acc)[NT]) {
+                                       const unsigned char* xr, f32x4 (&acc)[NMB][NT],
+                                       u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2], const u32x4* wp_next) {
     constexpr int NOCT = CIN / 8, NK = NTAP * NOCT, NKB = (NK + 3) / 4;
     static_assert(CIN % 8 == 0 && (NOCT <= 2 || NOCT % 4 == 0), "channel count must be 8, 16 or a multiple of 32");
     static_assert(!XR || 4 * NKB - NK == NOCT, "residual fold needs exactly one row of padding octets");
@@ -106,16 +121,19 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
     const int o_last = 4 * (NKB - 1) + g;
     const unsigned char* b_last = o_last < NK ? bl + koff(NKB - 1)
                                               : (XR ? xr + (o_last - NK) * 16 : bp + koff(NKB - 1));
-    // Weight fragments stream PD k-blocks ahead (PD = all of them up to 4):
-    // one L2 round trip per item rather than one per k-block (a k-block is
-    // only 3*NT MFMAs, shorter than an L2 hit), at most 32 VGPRs in flight.
-    constexpr int PD = NKB < 4 ? NKB : 4;
-    u32x4 a[PD][2];
+    // Weight fragments stream PD k-blocks ahead (PD = all of them up to
+    // 4 / NMB): one L2 round trip per item rather than one per k-block (a
+    // k-block is only 3*NT*NMB MFMAs, shorter than an L2 hit), at most 32
+    // VGPRs in flight.
+    constexpr int PD = pd_of<CIN, NTAP, NMB>();
+    if (!PRE)
 #pragma unroll
-    for (int kb = 0; kb < PD; ++kb) {
-        a[kb][0] = wp[kb * 128];
-        a[kb][1] = wp[kb * 128 + 64];
-    }
+    for (int kb = 0; kb < PD; ++kb)
+#pragma unroll
+        for (int m = 0; m < NMB; ++m) {
+            a[kb][m][0] = wp[m * WS + kb * 128];
+            a[kb][m][1] = wp[m * WS + kb * 128 + 64];
+        }
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
         const unsigned char* b0 = kb == NKB - 1 ? b_last : bl + koff(kb);
@@ -126,23 +144,38 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
             blo[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
         }
         __builtin_amdgcn_sched_barrier(0);
-        const u32x4 ah = a[kb % PD][0], al = a[kb % PD][1];
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = mfma_h(ah, bh[n], acc[n]);
+        for (int m = 0; m < NMB; ++m)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = mfma_h(ah, blo[n], acc[n]);
+            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], bh[n], acc[m][n]);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = mfma_h(al, bh[n], acc[n]);
+        for (int m = 0; m < NMB; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], blo[n], acc[m][n]);
+#pragma unroll
+        for (int m = 0; m < NMB; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][1], bh[n], acc[m][n]);
         if (kb + PD < NKB) {
-            a[kb % PD][0] = wp[(kb + PD) * 128];
-            a[kb % PD][1] = wp[(kb + PD) * 128 + 64];
+#pragma unroll
+            for (int m = 0; m < NMB; ++m) {
+                a[kb % PD][m][0] = wp[m * WS + (kb + PD) * 128];
+                a[kb % PD][m][1] = wp[m * WS + (kb + PD) * 128 + 64];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (PD == 4 && NMB == 1) {
+        if (wp_next) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) {
+                a[kb][0][0] = wp_next[kb * 128];
+                a[kb][0][1] = wp_next[kb * 128 + 64];
+            }
+        }
+    }
 }
 
-template <int CIN, int NTAP>
-constexpr int nkb() { return (NTAP * (CIN / 8) + 3) / 4; }
 
 // Epilogue for one tile (acc already holds the bias): v = act(acc)
 // [+ residual read back from `out`], 0 outside [0, L) (only
@@ -187,33 +220,39 @@ __device__ __forceinline__ void store_tile(const f32x4& acc, XW out, int t, int 
 template <int C>
 constexpr bool kFold = res_fold_channels(C);
 
-// One work item: NTT tiles of one (phase, m-block) row starting at tile0.
-// Output position of column j (relative to the layer's first input q0 / a0):
-// t = (p0 + j) * RR + ph (RR = 1, ph = 0 for conv3).
+// One work item: NTT tiles of NMB (phase, m-block) rows (consecutive m-blocks
+// of one phase, co0 .. co0 + 16 NMB, sharing the B fragments) starting at
+// tile0.  Output position of column j (relative to the layer's first input
+// q0 / a0): t = (p0 + j) * RR + ph (RR = 1, ph = 0 for conv3).
 template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int ACT, bool RES, bool XR, int RR,
-          int JMAX>
+          int JMAX, int NMB, bool PRE>
 __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
                                          const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
-                                         int ph, int tile0, int L) {
-    f32x4 acc[NTT];
-    {
+                                         int ph, int tile0, int L, u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2],
+                                         const u32x4* wp_next) {
+    constexpr int WS = nkb_of<CIN, NTAP>() * 128;  // u32x4 between consecutive m-blocks' weights
+    f32x4 acc[NMB][NTT];
+#pragma unroll
+    for (int m = 0; m < NMB; ++m) {
         f32x4 bv;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = co0 + r < COUT ? bias[co0 + r] : 0.f;
+        for (int r = 0; r < 4; ++r) bv[r] = co0 + 16 * m + r < COUT ? bias[co0 + 16 * m + r] : 0.f;
 #pragma unroll
-        for (int n = 0; n < NTT; ++n) {
-            acc[n] = bv;
-        }
+        for (int n = 0; n < NTT; ++n) acc[m][n] = bv;
     }
-    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR>(wp, bp, xr, acc);
+    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR, NMB, WS, PRE>(wp, bp, xr, acc, a, wp_next);
     const bool edge = (p0 + tile0 * 16) * RR < 0 || (p0 + (tile0 + NTT) * 16) * RR > L;
     const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
-    const bool rows_ok = co0 - 4 * g + 8 * (g >> 1) < COUT;  // after the swap: this lane's 8 channels
 #pragma unroll
-    for (int n = 0; n < NTT; ++n) {
-        const int j = (tile0 + n) * 16 + li;
-        const bool col_ok = ((tile0 + n + 1) * 16 <= JMAX) || j < JMAX;
-        store_tile<COUT, RSO, ACT, RES>(acc[n], out, (p0 + j) * RR + ph, co0, L, edge, rows_ok && col_ok);
+    for (int m = 0; m < NMB; ++m) {
+        const int cm = co0 + 16 * m;
+        const bool rows_ok = cm - 4 * g + 8 * (g >> 1) < COUT;  // after the swap: this lane's 8 channels
+#pragma unroll
+        for (int n = 0; n < NTT; ++n) {
+            const int j = (tile0 + n) * 16 + li;
+            const bool col_ok = ((tile0 + n + 1) * 16 <= JMAX) || j < JMAX;
+            store_tile<COUT, RSO, ACT, RES>(acc[m][n], out, (p0 + j) * RR + ph, cm, L, edge, rows_ok && col_ok);
+        }
     }
 }
 
@@ -228,60 +267,120 @@ struct Chunks {
     __device__ static int lo(int k) { return k * NTILES / NCH; }
 };
 
+// Weight-fragment hand-off between the layers of a kernel in which every wave
+// does exactly one item per layer (the stage1 head): the loads of the next
+// layer's first four k-blocks are issued right after the current item's last
+// MFMA, so they are in flight during its epilogue and the barrier.
+typedef u32x4 APipe[4][1][2];
+
+// Work items of a layer: (m-block group, chunk) for conv3, (phase, m-block
+// group, chunk) for the transposed convs; NMB m-blocks per item share the B
+// reads.  ONE (= the wave count, one item each): the wave's item is its index, its
+// first k-blocks' weights were loaded into `ap` by the previous layer, and it
+// starts the loads of `wp_next` (the next layer's item) into `ap`.
+template <int CIN, int COUT, int NT, int NPOS, int NMB>
+struct Conv3Items {
+    static constexpr int MB = (COUT + 15) / 16, NKB = nkb_of<CIN, 3>(), MG = MB / NMB;
+    static_assert(MB % NMB == 0, "m-block groups");
+    using CH = Chunks<(NPOS + 15) / 16, NT>;
+    static constexpr int N = MG * CH::NCH;
+    __device__ static const u32x4* wp(const u32x4* Wp, int item) {
+        return Wp + (size_t)(item % MG) * NMB * NKB * 128 + (threadIdx.x & 63);
+    }
+};
+template <int CIN, int COUT, int R, int NT, int NQ, int NMB>
+struct ConvTItems {
+    static constexpr int MB = (COUT + 15) / 16, NKB = nkb_of<CIN, 2>(), MG = MB / NMB;
+    static_assert(MB % NMB == 0, "m-block groups");
+    using CH = Chunks<(NQ + 15) / 16, NT>;
+    static constexpr int N = R * MG * CH::NCH;
+    __device__ static const u32x4* wp(const u32x4* Wp, int item) {
+        const int rg = item % (R * MG), ph = rg / MG, mb = (rg - ph * MG) * NMB;
+        return Wp + (size_t)(ph * MB + mb) * NKB * 128 + (threadIdx.x & 63);
+    }
+};
+
 // Conv1d(k=3, pad=1): abs positions [a0, a0+NPOS) of `out` from `in`.
 // RES: out += conv(in) (ResBlock conv2, x = out), folded into the GEMM for
 // 8/16 channels, read back in the epilogue otherwise.
-template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS>
+template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS, int NMB = 1, int ONE = 0>
 __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
-                                       int a0, int L) {
-    constexpr int MB = (COUT + 15) / 16, NKB = nkb<CIN, 3>();
+                                       int a0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr) {
+    using IT = Conv3Items<CIN, COUT, NT, NPOS, NMB>;
+    using CH = typename IT::CH;
+    constexpr int MG = IT::MG;
     constexpr bool FOLD = RES && kFold<CIN>;
     static_assert(!FOLD || (CIN == COUT && RSI == RSO), "folded residual: x has the conv's input layout");
-    using CH = Chunks<(NPOS + 15) / 16, NT>;
+    static_assert(!ONE || (IT::N == ONE && NMB == 1 && pd_of<CIN, 3, 1>() == 4), "one item per wave");
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-#pragma unroll 1
-    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < MB * CH::NCH; item += blockDim.x >> 6) {
-        const int mb = item % MB, k = item / MB;
+    auto body = [&](int item, auto pre) {
+        constexpr bool PRE = decltype(pre)::value;
+        const int mb = (item % MG) * NMB, k = item / MG;
         const int tile0 = CH::lo(k), nt = CH::lo(k + 1) - tile0;
         const int co0 = mb * 16 + 4 * g;
         const int p = a0 + tile0 * 16 + li;  // this lane's output position in tile 0
-        const u32x4* wp = Wp + (size_t)mb * NKB * 128 + lane;
+        const u32x4* wp = IT::wp(Wp, item);
         const unsigned char* bp = in.p + (p - 1 - in.start) * RSI;
         const unsigned char* xr = out.p + (p - out.start) * RSO;
+        u32x4 al[pd_of<CIN, 3, NMB>()][NMB][2];
+        auto& a = [&]() -> auto& {
+            if constexpr (PRE) return *ap;
+            else return al;
+        }();
         if (nt == CH::QHI)
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS>(wp, bias, bp, xr, out, co0,
-                                                                                        a0, 0, tile0, L);
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE>(
+                wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next);
         else
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS>(wp, bias, bp, xr, out, co0,
-                                                                                        a0, 0, tile0, L);
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE>(
+                wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next);
+    };
+    if constexpr (ONE) {
+        body(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), std::true_type{});
+    } else {
+#pragma unroll 1
+        for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < IT::N; item += blockDim.x >> 6)
+            body(item, std::false_type{});
     }
 }
 
 // leaky(ConvTranspose1d(k=2R, stride R, pad R/2)): inputs q in [q0, q0+NQ)
 // give outputs t = q*R + ph.  Phase ph reads taps (q, q-1) if ph + R/2 < R,
 // else (q+1, q): B base row q + d0, tap k at row q + d0 - k.
-template <int CIN, int COUT, int R, int NT, int RSI, int RSO, int NQ>
+template <int CIN, int COUT, int R, int NT, int RSI, int RSO, int NQ, int NMB = 1, int ONE = 0>
 __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
-                                       int q0, int L) {
-    constexpr int MB = (COUT + 15) / 16, NKB = nkb<CIN, 2>(), PAD = R / 2;
-    using CH = Chunks<(NQ + 15) / 16, NT>;
+                                       int q0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr) {
+    using IT = ConvTItems<CIN, COUT, R, NT, NQ, NMB>;
+    using CH = typename IT::CH;
+    constexpr int MG = IT::MG, PAD = R / 2;
+    static_assert(!ONE || (IT::N == ONE && NMB == 1 && pd_of<CIN, 2, 1>() == 4), "one item per wave");
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
-#pragma unroll 1
-    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < R * MB * CH::NCH;
-         item += blockDim.x >> 6) {
-        const int row = item % (R * MB), k = item / (R * MB);  // row = ph*MB + mb
-        const int ph = row / MB, mb = row - ph * MB;
+    auto body = [&](int item, auto pre) {
+        constexpr bool PRE = decltype(pre)::value;
+        const int rg = item % (R * MG), k = item / (R * MG);  // rg = ph*MG + m-block group
+        const int ph = rg / MG, mb = (rg - ph * MG) * NMB;
         const int tile0 = CH::lo(k), nt = CH::lo(k + 1) - tile0;
         const int d0 = (ph + PAD < R) ? 0 : 1;
         const int co0 = mb * 16 + 4 * g;
-        const u32x4* wp = Wp + (size_t)row * NKB * 128 + lane;
+        const u32x4* wp = IT::wp(Wp, item);
         const unsigned char* bp = in.p + (q0 + tile0 * 16 + li + d0 - in.start) * RSI;
+        u32x4 al[pd_of<CIN, 2, NMB>()][NMB][2];
+        auto& a = [&]() -> auto& {
+            if constexpr (PRE) return *ap;
+            else return al;
+        }();
         if (nt == CH::QHI)
-            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ>(wp, bias, bp, nullptr, out,
-                                                                                        co0, q0, ph, tile0, L);
+            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, NMB, PRE>(
+                wp, bias, bp, nullptr, out, co0, q0, ph, tile0, L, a, wp_next);
         else
-            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ>(wp, bias, bp, nullptr, out,
-                                                                                        co0, q0, ph, tile0, L);
+            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, NMB, PRE>(
+                wp, bias, bp, nullptr, out, co0, q0, ph, tile0, L, a, wp_next);
+    };
+    if constexpr (ONE) {
+        body(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), std::true_type{});
+    } else {
+#pragma unroll 1
+        for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < IT::N; item += blockDim.x >> 6)
+            body(item, std::false_type{});
     }
 }
 
@@ -428,6 +527,8 @@ struct TailPlan {  // A: in | h3 | u4   B: u3 | h4
 #define X3_NT_IN 3
 #define X3_NT_T1 5
 #define X3_NT_R1 4
+#define X3_G_T1 1
+#define X3_G_R1 1
 #endif
 struct CfgS1 {
     static constexpr int M = 64, MP = 64, C = 128;
@@ -436,6 +537,8 @@ struct CfgS1 {
     static constexpr int W3 = 168, TW = 8, TMIN = 4;
     static constexpr int NT_IN = X3_NT_IN, NT_T1 = X3_NT_T1, NT_R1 = X3_NT_R1, NT_T2 = 4, NT_R2 = 4, NT_T3 = 3,
                          NT_R3 = 3, NT_T4 = 3, NT_R4 = 6;
+    // head ConvT1 / ResBlock1: m-blocks per item sharing B (2: half the B reads)
+    static constexpr int G_T1 = X3_G_T1, G_R1 = X3_G_R1;
 };
 struct CfgS2 {
     static constexpr int M = 80, MP = 96, C = 256;
@@ -443,6 +546,7 @@ struct CfgS2 {
     static constexpr int W2 = 28, MW = 8, MMIN = 2;
     static constexpr int W3 = 120, TW = 8, TMIN = 2;
     static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+    static constexpr int G_T1 = 1, G_R1 = 1;
 };
 
 // Diagnostic build only (-DM2_STAMPS): per-wave s_memtime stamps at phase
@@ -476,24 +580,68 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     XW hw{lds, 4 * f0 - 1};
     XW melw{lds + Pl::RA, f0 - 3};
     XW uw{lds + Pl::RA, 4 * f0 - 4};
+    constexpr int NW = Cfg::HW;
+    using I0 = Conv3Items<MP, C, Cfg::NT_IN, Pl::A0_N, 1>;
+    using I1 = ConvTItems<C, C1, 4, Cfg::NT_T1, Pl::NQ, Cfg::G_T1>;
+    using I2 = Conv3Items<C1, C1, Cfg::NT_R1, Pl::H_N, Cfg::G_R1>;
+    using I3 = Conv3Items<C1, C1, Cfg::NT_R1, Pl::O_N, Cfg::G_R1>;
+    // One item per wave in every layer (stage1): weight fragments handed
+    // from layer to layer across the barriers (APipe).
+    constexpr bool ONE = Cfg::G_T1 == 1 && Cfg::G_R1 == 1 && I0::N == NW && I1::N == NW && I2::N == NW &&
+                         I3::N == NW && pd_of<MP, 3, 1>() == 4 && pd_of<C, 2, 1>() == 4 && pd_of<C1, 3, 1>() == 4;
     XSTAMP(0, 0);
-    gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melw);
-    XSTAMP(0, 1);
-    __syncthreads();
-    XSTAMP(0, 2);
-    xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N>(w.wi, w.bi, melw, a0w, f0 - 2, T);
-    XSTAMP(0, 3);
-    __syncthreads();
-    XSTAMP(0, 4);
-    xconvT<C, C1, 4, Cfg::NT_T1, Pl::RS_C, Pl::RS_1, Pl::NQ>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, 4 * T);
-    XSTAMP(0, 5);
-    __syncthreads();
-    XSTAMP(0, 6);
-    xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, 4 * T);
-    XSTAMP(0, 7);
-    __syncthreads();
-    XSTAMP(0, 8);
-    xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N>(w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T);
+    if constexpr (ONE) {
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        APipe ap;
+        const u32x4* wp0 = I0::wp(w.wi, wv);
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            ap[kb][0][0] = wp0[kb * 128];
+            ap[kb][0][1] = wp0[kb * 128 + 64];
+        }
+        gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melw);
+        XSTAMP(0, 1);
+        __syncthreads();
+        XSTAMP(0, 2);
+        xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N, 1, NW>(
+            w.wi, w.bi, melw, a0w, f0 - 2, T, &ap, I1::wp(w.wt[0], wv));
+        XSTAMP(0, 3);
+        __syncthreads();
+        XSTAMP(0, 4);
+        xconvT<C, C1, 4, Cfg::NT_T1, Pl::RS_C, Pl::RS_1, Pl::NQ, 1, NW>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, 4 * T,
+                                                                     &ap, I2::wp(w.w1[0], wv));
+        XSTAMP(0, 5);
+        __syncthreads();
+        XSTAMP(0, 6);
+        xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N, 1, NW>(
+            w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, 4 * T, &ap, I3::wp(w.w2[0], wv));
+        XSTAMP(0, 7);
+        __syncthreads();
+        XSTAMP(0, 8);
+        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, NW>(w.w2[0], w.b2[0], hw, uw,
+                                                                                      4 * f0, 4 * T, &ap, nullptr);
+    } else {
+        gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melw);
+        XSTAMP(0, 1);
+        __syncthreads();
+        XSTAMP(0, 2);
+        xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N>(w.wi, w.bi, melw, a0w, f0 - 2, T);
+        XSTAMP(0, 3);
+        __syncthreads();
+        XSTAMP(0, 4);
+        xconvT<C, C1, 4, Cfg::NT_T1, Pl::RS_C, Pl::RS_1, Pl::NQ, Cfg::G_T1>(w.wt[0], w.bt[0], a0w, uw, f0 - 1,
+                                                                            4 * T);
+        XSTAMP(0, 5);
+        __syncthreads();
+        XSTAMP(0, 6);
+        xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N, Cfg::G_R1>(w.w1[0], w.b1[0], uw,
+                                                                                            hw, 4 * f0 - 1, 4 * T);
+        XSTAMP(0, 7);
+        __syncthreads();
+        XSTAMP(0, 8);
+        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, Cfg::G_R1>(w.w2[0], w.b2[0], hw, uw,
+                                                                                           4 * f0, 4 * T);
+    }
     XSTAMP(0, 9);
     __syncthreads();
     XSTAMP(0, 10);
