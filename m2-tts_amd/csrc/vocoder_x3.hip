@@ -185,9 +185,12 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
 // 0 (2) holds the hi halves of channels 0-7 (8-15) of the m-block and group 1
 // (3) the lo halves: one ds_write_b128 per lane instead of two ds_write_b64
 // (2-way instead of 4-way bank conflicts on RS/16 = 2 mod 4 rows).
-template <int COUT, int RSO, int ACT, bool RES>
+// GO: the tile goes straight to global rows of 4*COUT bytes (gout, absolute
+// position t, t < L only) instead of back into `out` (the residual is still
+// read from `out`).
+template <int COUT, int RSO, int ACT, bool RES, bool GO>
 __device__ __forceinline__ void store_tile(const f32x4& acc, XW out, int t, int co0, int L,
-                                           bool edge, bool store) {
+                                           bool edge, bool store, unsigned char* gout) {
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = acc[r];
@@ -200,7 +203,7 @@ __device__ __forceinline__ void store_tile(const f32x4& acc, XW out, int t, int 
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += (float)hi[r] + (float)lo[r];
     }
-    if (edge && (t < 0 || t >= L)) {
+    if (!GO && edge && (t < 0 || t >= L)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = 0.f;
     }
@@ -210,9 +213,13 @@ __device__ __forceinline__ void store_tile(const f32x4& acc, XW out, int t, int 
     const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
     const int g = (threadIdx.x & 63) >> 4;
-    if (store)
-        *reinterpret_cast<u32x4*>(rowp + 2 * (co0 - 4 * g + 8 * (g >> 1)) + (g & 1) * 2 * COUT) =
-            u32x4{s0[0], s1[0], s0[1], s1[1]};
+    const int off = 2 * (co0 - 4 * g + 8 * (g >> 1)) + (g & 1) * 2 * COUT;
+    if constexpr (GO) {
+        if (store && t < L)
+            *reinterpret_cast<u32x4*>(gout + (size_t)t * 4 * COUT + off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    } else if (store) {
+        *reinterpret_cast<u32x4*>(rowp + off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
 }
 
 // Does 3-tap packing fold the ResBlock residual into the GEMM (see mma_x3)?
@@ -225,11 +232,11 @@ constexpr bool kFold = res_fold_channels(C);
 // tile0.  Output position of column j (relative to the layer's first input
 // q0 / a0): t = (p0 + j) * RR + ph (RR = 1, ph = 0 for conv3).
 template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int ACT, bool RES, bool XR, int RR,
-          int JMAX, int NMB, bool PRE>
+          int JMAX, int NMB, bool PRE, bool GO = false>
 __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
                                          const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
                                          int ph, int tile0, int L, u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2],
-                                         const u32x4* wp_next) {
+                                         const u32x4* wp_next, unsigned char* gout = nullptr) {
     constexpr int WS = nkb_of<CIN, NTAP>() * 128;  // u32x4 between consecutive m-blocks' weights
     f32x4 acc[NMB][NTT];
 #pragma unroll
@@ -251,7 +258,8 @@ __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const flo
         for (int n = 0; n < NTT; ++n) {
             const int j = (tile0 + n) * 16 + li;
             const bool col_ok = ((tile0 + n + 1) * 16 <= JMAX) || j < JMAX;
-            store_tile<COUT, RSO, ACT, RES>(acc[m][n], out, (p0 + j) * RR + ph, cm, L, edge, rows_ok && col_ok);
+            store_tile<COUT, RSO, ACT, RES, GO>(acc[m][n], out, (p0 + j) * RR + ph, cm, L, edge, rows_ok && col_ok,
+                                                gout);
         }
     }
 }
@@ -303,9 +311,12 @@ struct ConvTItems {
 // Conv1d(k=3, pad=1): abs positions [a0, a0+NPOS) of `out` from `in`.
 // RES: out += conv(in) (ResBlock conv2, x = out), folded into the GEMM for
 // 8/16 channels, read back in the epilogue otherwise.
-template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS, int NMB = 1, int ONE = 0>
+// GO: store the output tiles to global rows (gout) instead of `out`.
+template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS, int NMB = 1, int ONE = 0,
+          bool GO = false>
 __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
-                                       int a0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr) {
+                                       int a0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr,
+                                       unsigned char* gout = nullptr) {
     using IT = Conv3Items<CIN, COUT, NT, NPOS, NMB>;
     using CH = typename IT::CH;
     constexpr int MG = IT::MG;
@@ -328,11 +339,11 @@ __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float
             else return al;
         }();
         if (nt == CH::QHI)
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE>(
-                wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next);
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO>(
+                wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next, gout);
         else
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE>(
-                wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next);
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO>(
+                wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next, gout);
     };
     if constexpr (ONE) {
         body(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), std::true_type{});
@@ -618,8 +629,12 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         XSTAMP(0, 7);
         __syncthreads();
         XSTAMP(0, 8);
-        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, NW>(w.w2[0], w.b2[0], hw, uw,
-                                                                                      4 * f0, 4 * T, &ap, nullptr);
+        // ResBlock1 conv2 + x straight to U1 (rows of hi[C1] lo[C1]): no LDS
+        // round trip, no last barrier, no separate store phase
+        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, NW, true>(
+            w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T, &ap, nullptr, U1 + (size_t)b * 4 * T * 4 * C1);
+        XSTAMP(0, 9);
+        return;
     } else {
         gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melw);
         XSTAMP(0, 1);
