@@ -2,6 +2,9 @@
 """LDS bank-conflict check for the pipelined tail's B-fragment reads and
 epilogue writes (vocoder_tailp.hip): every K-slot list of tp::kslot,
 ds_read_b128 / ds_write_b64 lane groups from MI355X_MICROARCH.md (LDS table).
+Padded-row layouts (the earlier RS 144..208 strides) and, with --swizzle, the
+current unpadded 64-B hi / lo planes with octet o of row r at
+16 * (o ^ ((r >> 1) & 3)).
 
     python tools/probe/tailp_banks.py
 """
@@ -72,7 +75,33 @@ def writes_b128(rs):
     return worst
 
 
+def swizzled():
+    """Current layout: every fragment read and 8-row b128 store conflict free."""
+    worst_r = worst_w = 1
+    for key, kbs in K.items():
+        for kb in kbs:
+            for r0 in range(64):
+                for grp in GROUPS:
+                    v = []
+                    for lane in grp:
+                        li, g = lane & 15, lane >> 4
+                        res, dq, oc = kb[g]
+                        r = (r0 + li + dq - (2 if res else 1)) % 64
+                        v.append((r * 64 + 16 * (oc ^ ((r >> 1) & 3))) // 16 % 16)
+                    worst_r = max(worst_r, max(v.count(x) for x in set(v)))
+    for r0 in range(64):
+        for o in range(4):
+            v = [(((r0 + li) % 64) * 64 + 16 * (o ^ ((((r0 + li) % 64) >> 1) & 3))) // 16 % 8 for li in range(8)]
+            worst_w = max(worst_w, max(v.count(x) for x in set(v)))
+    return worst_r, worst_w
+
+
 if __name__ == "__main__":
+    import sys
+    if "--swizzle" in sys.argv:
+        r, w = swizzled()
+        print(f"swizzled 64-B planes: reads {r}-way, ds_write_b128 {w}-way")
+        sys.exit(0)
     for rs in (144, 160, 176, 208):
         print(f"RS {rs}: reads {reads(rs, False)}-way, ds_write_b64 {writes_b64(rs)}-way, "
               f"ds_write_b128 {writes_b128(rs)}-way")

@@ -8,7 +8,9 @@ tag=$1; shift
 export TMPDIR=/tmp
 out=gpurun_out/prof_$tag
 mkdir -p $out
-BENCH="python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-pipeline-extra $*"
+# enough warm-up for the clocks to settle (bench.py's default), so the kernel
+# averages match the bench's own HIP-event timings
+BENCH="python3 bench.py --steps 100 --warmup 300 --no-cpu-baseline --no-pipeline-extra $*"
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 240 rocprofv3 "$@" --output-format csv -d $out/$name -o run -- $BENCH > $out/$name.log 2>&1
