@@ -7,7 +7,11 @@
 //
 // All fp32.  The GEMMs run on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32,
 // 64 FLOP/clk/SIMD = the fp32 vector peak, one rounding per product).
+#include <cstdlib>
+#include <type_traits>
+
 #include "m2_common.h"
+#include "vocoder_fused.h"  // split2u: fp32 -> (hi, lo) f16
 
 namespace m2 {
 
@@ -310,6 +314,271 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// The same attention core on split-f16 MFMA (v_mfma_f32_16x16x32_f16, 16x the
+// f32 MFMA's rate): every fp32 operand as hi = f16(x), lo = f16(x - hi) and
+// every product as hi*hi + hi*lo + lo*hi in one fp32 accumulator, the
+// vocoder's arithmetic (~2^-22 relative per product).  Same
+// tiling and transposed formulation as attention_kernel; K and V^T are split
+// once, when a chunk is stashed in LDS (hi and lo planes per row), Q once per
+// wave, P per 32-key k-step in registers.
+//   S^T = K . Q^T: A = K rows (lane: 8 head dims of one key), B = Q^T (lane:
+//     8 head dims of its query); head dims padded to 32 per k-step.
+//   O^T += V^T . P^T: a 32-key k-step takes key blocks 2j and 2j+1, whose S^T
+//     accumulators give lane group g keys {32j + 4g + e, 32j + 16 + 4g + e}
+//     (e < 4) of its query: exactly the B fragment, provided V^T's columns are
+//     stored in that order (key 32j + 16h + 4g + e at column 32j + 8g + 4h + e).
+// Row strides 160 / 288 B (RS/16 = 2 mod 4): conflict-free ds_read_b128.
+template <int V>
+using ic_ = std::integral_constant<int, V>;
+
+template <int HD>
+struct AttSplit {
+    static constexpr int KS = (HD + 31) / 32, DP = 32 * KS;  // QK^T k-steps, padded head dim
+    static constexpr int KRS = 4 * DP + 32;                    // K row: hi[DP] lo[DP] f16 + pad
+    static constexpr int VRS = 4 * ATT_KC + 32;                // V^T row: hi[64 keys] lo[64] + pad
+    static constexpr int KBUF = ATT_KC * KRS, VBUF = HD * VRS;
+    static constexpr int LDS = 2 * KBUF + 2 * VBUF + 2 * ATT_KC * 8;
+};
+
+__device__ __forceinline__ f32x4 mfma_f16(vx_u32x4 a, vx_u32x4 b, f32x4 c) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attention_split_kernel(const float* __restrict__ qkv,
+                                                              const uint8_t* __restrict__ key_mask, int N, int H,
+                                                              float scale, float* __restrict__ out) {
+    using P = AttSplit<HD>;
+    constexpr int KS = P::KS, DP = P::DP, KRS = P::KRS, VRS = P::VRS;
+    constexpr int MT = HD / 16;                  // 16-row d blocks of O^T
+    constexpr int IT = ATT_KC * (HD / 4) / 256;  // float4 of K (and of V) per thread per chunk
+    static_assert(HD % 16 == 0 && ATT_KC * (HD / 4) % 256 == 0, "head_dim");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* const Ks0 = smem;
+    unsigned char* const Vt0 = smem + 2 * P::KBUF;
+    // per key (scale, add): live (scale*log2e, 0), masked (0, -1e9*log2e),
+    // past the end (0, -inf): the base-2 score is one fma of the raw dot product
+    float2* const Mk0 = reinterpret_cast<float2*>(smem + 2 * P::KBUF + 2 * P::VBUF);
+    const int b = blockIdx.z, hh = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, g = lane >> 4;
+    const size_t row3 = (size_t)3 * H;
+    const float* base = qkv + (size_t)b * N * row3 + hh * HD;
+    const int qi = blockIdx.x * 64 + wave * 16 + li;
+    const float sl2 = scale * kLog2e;
+
+    if constexpr (DP > HD) {  // zero the padded head dims of both K buffers once
+        for (int i = tid; i < 2 * ATT_KC; i += 256) {
+            unsigned char* r = Ks0 + i * KRS;
+            for (int d = HD; d < DP; d += 4) {
+                *reinterpret_cast<uint2*>(r + 2 * d) = uint2{0u, 0u};
+                *reinterpret_cast<uint2*>(r + 2 * DP + 2 * d) = uint2{0u, 0u};
+            }
+        }
+    }
+    // Chunks stream through registers PF chunks ahead of their stash (the
+    // split kernel's compute per chunk is short next to an L2 / HBM round
+    // trip).  K: thread = (key, head-dim quad), quads fastest (128-B rows);
+    // V: thread = (key pair, quad), pairs fastest, so the transposed stores
+    // (two keys' f16 in one dword of a V^T row) hit 32 distinct banks.
+    constexpr int PF = 3;
+    constexpr int NQ4 = HD / 4, ITV = (32 * NQ4 + 255) / 256;
+    float4 kr[PF][IT], vr[PF][ITV][2];
+    float2 mkr[PF];
+    auto fetch = [&](int j0, auto sc) {
+        constexpr int sl = decltype(sc)::value;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256, key = i / NQ4, d4 = i - key * NQ4, j = j0 + key;
+            kr[sl][it] = j < N ? *reinterpret_cast<const float4*>(base + j * row3 + H + 4 * d4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int it = 0; it < ITV; ++it) {
+            const int i = tid + it * 256, pr = i & 31, d4 = i >> 5;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j = j0 + 2 * pr + h;
+                vr[sl][it][h] = (j < N && d4 < NQ4) ? *reinterpret_cast<const float4*>(base + j * row3 + 2 * H + 4 * d4)
+                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        if (tid < ATT_KC) {
+            const int j = j0 + tid;
+            // 0: live key, 1: masked (score -1e9), 2: past the end (weight 0)
+            mkr[sl] = j >= N ? make_float2(0.f, -INFINITY)
+                             : ((key_mask && key_mask[(size_t)b * N + j] == 0) ? make_float2(0.f, kMaskFill * kLog2e)
+                                                                                : make_float2(sl2, 0.f));
+        }
+    };
+    auto stash = [&](int buf, auto sc) {
+        constexpr int sl = decltype(sc)::value;
+        unsigned char* Kb = Ks0 + buf * P::KBUF;
+        unsigned char* Vb = Vt0 + buf * P::VBUF;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256, key = i / NQ4, d4 = i - key * NQ4;
+            unsigned h0, h1, l0, l1;
+            split2u(kr[sl][it].x, kr[sl][it].y, h0, l0);
+            split2u(kr[sl][it].z, kr[sl][it].w, h1, l1);
+            unsigned char* kp = Kb + key * KRS + 8 * d4;
+            *reinterpret_cast<uint2*>(kp) = uint2{h0, h1};
+            *reinterpret_cast<uint2*>(kp + 2 * DP) = uint2{l0, l1};
+        }
+#pragma unroll
+        for (int it = 0; it < ITV; ++it) {
+            const int i = tid + it * 256, pr = i & 31, d4 = i >> 5;
+            if (d4 < NQ4) {
+                // keys 2pr, 2pr + 1 sit next to each other in the permuted column order
+                const int key = 2 * pr;
+                const int pk = (key & 32) | (((key >> 2) & 3) << 3) | (((key >> 4) & 1) << 2) | (key & 3);
+                const float4 v0 = vr[sl][it][0], v1 = vr[sl][it][1];
+                const float a[4] = {v0.x, v0.y, v0.z, v0.w}, c[4] = {v1.x, v1.y, v1.z, v1.w};
+                unsigned char* vp = Vb + 4 * d4 * VRS + 2 * pk;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    unsigned hi, lo;
+                    split2u(a[e], c[e], hi, lo);
+                    *reinterpret_cast<unsigned*>(vp + e * VRS) = hi;
+                    *reinterpret_cast<unsigned*>(vp + e * VRS + 2 * ATT_KC) = lo;
+                }
+            }
+        }
+        if (tid < ATT_KC) Mk0[buf * ATT_KC + tid] = mkr[sl];
+    };
+
+    const int nch = (N + ATT_KC - 1) / ATT_KC;
+    fetch(0, ic_<0>{});
+    if (nch > 1) fetch(ATT_KC, ic_<1>{});
+    if (nch > 2) fetch(2 * ATT_KC, ic_<2>{});
+    vx_u32x4 qh[KS], ql[KS];  // B = Q^T: lane (query li, group g) holds head dims 32 ks + 8 g .. + 7
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int d = 32 * ks + 8 * g + e;
+            v[e] = (qi < N && d < HD) ? base[(size_t)qi * row3 + d] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            unsigned hi, lo;
+            split2u(v[2 * e], v[2 * e + 1], hi, lo);
+            qh[ks][e] = hi;
+            ql[ks][e] = lo;
+        }
+    }
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+    stash(0, ic_<0>{});
+    __syncthreads();
+
+    // chunk c: registers of slot c % PF; unrolled by PF so slots are compile-time
+    auto chunk = [&](int c, auto sc) {
+        constexpr int sl = decltype(sc)::value;
+        const int buf = c & 1;
+        const unsigned char* K = Ks0 + buf * P::KBUF;
+        const unsigned char* V = Vt0 + buf * P::VBUF;
+        const float2* MK = Mk0 + buf * ATT_KC;
+        float s[4][4];  // [16-key block][r]: key 16*kb + 4*g + r of query li (base-2 scores)
+        float cmax = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const unsigned char* kp = K + (16 * kb + li) * KRS + 2 * (32 * ks + 8 * g);
+                const vx_u32x4 ah = *reinterpret_cast<const vx_u32x4*>(kp);
+                const vx_u32x4 al = *reinterpret_cast<const vx_u32x4*>(kp + 2 * DP);
+                st = mfma_f16(ah, qh[ks], st);
+                st = mfma_f16(ah, ql[ks], st);
+                st = mfma_f16(al, qh[ks], st);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float2 mk = MK[16 * kb + 4 * g + r];
+                s[kb][r] = __builtin_fmaf(st[r], mk.x, mk.y);  // masked: 0 * dot + fill, exactly the fill
+                cmax = vmax(cmax, s[kb][r]);
+            }
+        }
+        cmax = vmax(cmax, __shfl_xor(cmax, 16));
+        cmax = vmax(cmax, __shfl_xor(cmax, 32));
+        const float mn = vmax(m, cmax);
+        // raw v_exp_f32 (results below 2^-126 flush to 0: weights that small
+        // vanish next to the row's maximum weight 1 anyway)
+        const float corr = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first chunk -> 0
+        lsum *= corr;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[t] *= corr;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] - mn);
+                lsum += s[kb][r];
+            }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            unsigned ph[4], pl[4];  // B = P^T: keys 32j + 4g + e (e < 4), 32j + 16 + 4g + e - 4
+            split2u(s[2 * j][0], s[2 * j][1], ph[0], pl[0]);
+            split2u(s[2 * j][2], s[2 * j][3], ph[1], pl[1]);
+            split2u(s[2 * j + 1][0], s[2 * j + 1][1], ph[2], pl[2]);
+            split2u(s[2 * j + 1][2], s[2 * j + 1][3], ph[3], pl[3]);
+            const vx_u32x4 bh{ph[0], ph[1], ph[2], ph[3]}, bl{pl[0], pl[1], pl[2], pl[3]};
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const unsigned char* vp = V + (16 * t + li) * VRS + 2 * (32 * j + 8 * g);
+                const vx_u32x4 vh = *reinterpret_cast<const vx_u32x4*>(vp);
+                const vx_u32x4 vl = *reinterpret_cast<const vx_u32x4*>(vp + 2 * ATT_KC);
+                acc[t] = mfma_f16(vh, bh, acc[t]);
+                acc[t] = mfma_f16(vh, bl, acc[t]);
+                acc[t] = mfma_f16(vl, bh, acc[t]);
+            }
+        }
+        m = mn;
+        if (c + 1 < nch) {
+            // the other buffer was last read in chunk c-1, before the previous barrier
+            stash(buf ^ 1, ic_<(sl + 1) % PF>{});
+            if (c + PF < nch) fetch((c + PF) * ATT_KC, ic_<sl>{});  // slot sl is free again
+            __syncthreads();
+        }
+    };
+#pragma unroll 1
+    for (int c = 0; c < nch; c += PF) {
+        chunk(c, ic_<0>{});
+        if (c + 1 < nch) chunk(c + 1, ic_<1>{});
+        if (c + 2 < nch) chunk(c + 2, ic_<2>{});
+    }
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    if (qi >= N) return;
+    const float inv = 1.0f / lsum;
+    float* orow = out + ((size_t)b * N + qi) * H + hh * HD;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) orow[16 * t + 4 * g + r] = acc[t][r] * inv;
+}
+
+template <int HD>
+static int32_t launch_att_split(dim3 grid, const float* qkv, const uint8_t* mask, int N, int H, float scale,
+                                float* out, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attention_split_kernel<HD>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, AttSplit<HD>::LDS));
+        attr = true;
+    }
+    hipLaunchKernelGGL(attention_split_kernel<HD>, grid, dim3(256), AttSplit<HD>::LDS, st, qkv, mask, N, H, scale,
+                       out);
+    M2_LAUNCHED("attention_split_kernel");
+    return M2_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Host launchers (used by the runtime and by the standalone C entry points).
 int32_t launch_embed_pe(const int64_t* ids, const float* emb, const float* pe, int B, int S, int H,
                         int vocab, float* out, hipStream_t st) {
@@ -386,6 +655,18 @@ int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, in
     // float4 reads of q/k/v rows: H and the head offsets must be 16-B aligned
     M2_CHECK_SHAPE(H % 4 == 0, "attention: hidden_dim must be a multiple of 4");
     dim3 grid(cdiv(N, 64), heads, B);
+    // split-f16 MFMA by default; M2_ATT_F32=1: the exact-f32 MFMA kernel
+    static const bool f32 = [] {
+        const char* e = std::getenv("M2_ATT_F32");
+        return e && *e && *e != '0';
+    }();
+    if (!f32) switch (hd) {
+            case 16: return launch_att_split<16>(grid, qkv, mask, N, H, scale, out, st);
+            case 32: return launch_att_split<32>(grid, qkv, mask, N, H, scale, out, st);
+            case 48: return launch_att_split<48>(grid, qkv, mask, N, H, scale, out, st);
+            case 64: return launch_att_split<64>(grid, qkv, mask, N, H, scale, out, st);
+            default: return fail(M2_E_SHAPE, "attention: head_dim must be 16, 32, 48 or 64");
+        }
     switch (hd) {
         case 16: hipLaunchKernelGGL(attention_kernel<16>, grid, dim3(256), 0, st, qkv, mask, N, H, scale, out); break;
         case 32: hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(256), 0, st, qkv, mask, N, H, scale, out); break;
