@@ -656,10 +656,9 @@ int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, in
     M2_CHECK_SHAPE(H % 4 == 0, "attention: hidden_dim must be a multiple of 4");
     dim3 grid(cdiv(N, 64), heads, B);
     // split-f16 MFMA by default; M2_ATT_F32=1: the exact-f32 MFMA kernel
-    static const bool f32 = [] {
-        const char* e = std::getenv("M2_ATT_F32");
-        return e && *e && *e != '0';
-    }();
+    // (read per launch, so a process can switch: tests/test_gpu_parity.py)
+    const char* env = std::getenv("M2_ATT_F32");
+    const bool f32 = env && *env && *env != '0';
     if (!f32) switch (hd) {
             case 16: return launch_att_split<16>(grid, qkv, mask, N, H, scale, out, st);
             case 32: return launch_att_split<32>(grid, qkv, mask, N, H, scale, out, st);

@@ -351,11 +351,13 @@ def test_vocoder_arithmetic_paths(gpu, stage, monkeypatch):
 
 
 @pytest.mark.parametrize("stage", STAGES)
-@pytest.mark.parametrize("env", ["M2_TF_UNFUSED", "M2_VOCODER_PERLAYER", "M2_VOC_TAIL_X3", "M2_VOC_MID_X3"])
+@pytest.mark.parametrize("env", ["M2_TF_UNFUSED", "M2_VOCODER_PERLAYER", "M2_VOC_TAIL_X3", "M2_VOC_MID_X3",
+                                 "M2_ATT_F32"])
 def test_alternate_kernel_paths(gpu, stage, env, monkeypatch):
     """The unfused transformer layer (five linears), the per-layer vocoder
-    kernels and the x3 tail / mid kernels (instead of the pipelined stage1 ones) stay
-    parity-green: inference vs the reference's fixture."""
+    kernels, the x3 tail / mid kernels (instead of the pipelined stage1 ones)
+    and the exact-f32 attention stay parity-green: inference vs the
+    reference's fixture."""
     monkeypatch.setenv(env, "1")
     g = golden(f"{stage}_small")
     m = build_model(stage, gpu)
