@@ -386,7 +386,8 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             hipError_t er = hipMemcpyAsync(w.data(), weights[idx(n)], w.size() * sizeof(float), hipMemcpyDeviceToHost, st);
             if (er == hipSuccess) er = hipStreamSynchronize(st);
             if (er != hipSuccess) return er;
-            const std::vector<float> pk = pack_bfrag(w.data(), N, K);
+            std::vector<float> pk;
+            if (!pack_bfrag_split(w.data(), N, K, &pk)) return hipErrorInvalidValue;  // |w| >= 65504
             er = hipMemcpyAsync(m->buf + o, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice, st);
             if (er == hipSuccess) er = hipStreamSynchronize(st);
             *slot = m->buf + o;
@@ -404,6 +405,10 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             if (e == hipSuccess) e = pack_up(p + ".ffn.linear2.weight", H, 2 * H, &L.ff2_p);
         }
         if (e == hipSuccess) e = pack_up("decoder.mel_projection.weight", cfg->mel_channels, H, &m->mel_p);
+        if (e == hipErrorInvalidValue) {  // a weight outside the f16 range: keep the fp32 five-linear layers
+            m->tfused = false;
+            e = hipSuccess;
+        }
         if (e != hipSuccess) return bail(e, "pack transformer weights");
     }
     m->enc_nw = P("text_encoder.norm.weight");

@@ -10,10 +10,13 @@ namespace m2 {
 bool tf_fused_supported(int H, int N_out);
 // W [N][K] row-major (nn.Linear.weight) -> B-fragment order for v_mfma_f32_16x16x4_f32.
 std::vector<float> pack_bfrag(const float* W, int N, int K);
-// y[R][N] = LN(x)[R][K] . W^T (+ bias); Wp from pack_bfrag.
+// W [N][K] -> the fused layers' split-f16 fragment order (same byte count as
+// W in fp32); false if a weight is outside the f16 range.
+bool pack_bfrag_split(const float* W, int N, int K, std::vector<float>* out);
+// y[R][N] = LN(x)[R][K] . W^T (+ bias); Wp from pack_bfrag_split.
 int32_t launch_ln_gemm(const float* x, const float* g, const float* b, const float* Wp, const float* bias, int act,
                        int R, int K, int N, float* y, hipStream_t st);
-// y = o + FFN(LN2(o)), o = x + att . Wo^T + bo (packed Wo, W1, W2); y may alias x.
+// y = o + FFN(LN2(o)), o = x + att . Wo^T + bo (Wo, W1, W2 from pack_bfrag_split); y may alias x.
 int32_t launch_post_attn(const float* att, const float* x, const float* Wo, const float* bo, const float* g2,
                          const float* b2n, const float* W1, const float* b1, const float* W2, const float* b2, int R,
                          int H, float* y, hipStream_t st);

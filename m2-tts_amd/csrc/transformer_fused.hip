@@ -1,160 +1,224 @@
-// Fused transformer-layer kernels (gfx950, exact-f32 MFMA v_mfma_f32_16x16x4_f32).
+// Fused transformer-layer kernels (gfx950, split-f16 MFMA v_mfma_f32_16x16x32_f16).
 //
 // One pre-LN layer (components.py:131-140) is three launches:
-//   ln_qkv_kernel    qkv = LN1(x) . Wqkv^T                          (components.py:55-56,135)
-//   attention_kernel (transformer.hip)
+//   ln_gemm_kernel   qkv = LN1(x) . Wqkv^T                          (components.py:55-56,135)
+//   attention_split_kernel (transformer.hip)
 //   post_attn_kernel y = o + FFN(LN2(o)),  o = x + att . Wo^T + bo   (components.py:86-90,98-103,136-140)
 // instead of five generic linears: the out-projection, LayerNorm, both FFN
 // GEMMs and both residuals of a 32-row tile run out of LDS, so the only HBM
 // traffic is att + x in and y out (12 B/row/channel instead of ~40).
 //
+// Arithmetic: the vocoder's split-f16 form: every fp32 operand
+// as hi = f16(x), lo = f16(x - hi), every product as hi*hi + hi*lo + lo*hi
+// in one fp32 accumulator (~2^-22 relative per product); LayerNorms,
+// residuals and biases stay fp32.  Weights are packed once at model creation
+// (pack_bfrag_split), activations are split when they are written to LDS.
+//
 // GEMM tiles: a workgroup (4 waves) owns 32 rows; wave w computes the
-// 16-column blocks nb = w, w+4, ... for both 16-row halves.  A = activations
-// from LDS (row stride K+2 floats: the 16 rows x 2 k-lanes of a ds_read_b32
-// half-wave hit 32 distinct banks), B = weights packed in B-fragment order
-// [n-block][k-step/4][lane][4] (one global_load_dwordx4 per lane per 4
-// k-steps, L2-resident: every workgroup reads the same few tens of KB).
+// 16-column blocks nb = w, w+4, ... for both 16-row halves, as the transposed
+// product D^T = W . X^T: A = the weights (lane: 8 k of one output column,
+// packed [n-block][k-step][hi|lo][lane][8 f16], one global_load_dwordx4 per
+// lane and k-step, L2-resident), B = the activations from LDS hi / lo planes
+// (lane: 8 k of one row, one ds_read_b128; row stride 4K + 32 B, RS/16 = 2
+// mod 4: conflict-free).  A lane of D^T then holds 4 consecutive output
+// columns of one row, so the epilogues write 16-B fp32 or 8-B f16 pieces.
+#include <cmath>
+#include <cstring>
+
 #include "m2_common.h"
 #include "transformer_fused.h"
+#include "vocoder_fused.h"  // split2u
 
 namespace m2 {
 namespace tfx {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef vx_u32x4 u32x4;
 
-__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
 }
 
 constexpr int TR = 32;  // rows per workgroup tile
 
-// acc[rb] (rows rb*16.., cols nb*16..) += X[rows][0:K] . W[nb*16 + j][0:K]^T
-// X: LDS rows of stride XS floats.  Wp: packed, this n-block, lane offset applied.
-// An n-block's weight strip: K/4 floats per lane (float4 per 4 k-steps).
+// Split activation rows in LDS: hi[K] f16, lo[K] f16, pad.
+constexpr int srs(int K) { return 4 * K + 32; }
+// fp32 rows in LDS (16-B aligned rows).
+constexpr int frs(int K) { return K + 4; }
+
+// An n-block's weight strip: hi and lo fragments of its K/32 k-steps.
 template <int K>
 struct Strip {
-    float4 w[K / 16];
-    __device__ __forceinline__ void load(const float4* __restrict__ Wp, int nb) {
-        const float4* p = Wp + (size_t)nb * (K / 16) * 64 + (threadIdx.x & 63);
+    u32x4 w[K / 32][2];
+    __device__ __forceinline__ void load(const u32x4* __restrict__ Wp, int nb) {
+        const u32x4* p = Wp + (size_t)nb * (K / 32) * 128 + (threadIdx.x & 63);
 #pragma unroll
-        for (int s4 = 0; s4 < K / 16; ++s4) w[s4] = p[s4 * 64];
+        for (int ks = 0; ks < K / 32; ++ks) {
+            w[ks][0] = p[ks * 128];
+            w[ks][1] = p[ks * 128 + 64];
+        }
     }
 };
 
-template <int K, int XS>
-__device__ __forceinline__ void gemm_strip(const float* X, const Strip<K>& st, f32x4 (&acc)[2]) {
+// acc[rb] (transposed: lane = row rb*16 + (lane&15), columns nb*16 + 4g + r)
+// += W[nb cols][0:K] . X[rows][0:K]^T, X = split LDS rows (stride srs(K)).
+template <int K>
+__device__ __forceinline__ void gemm_strip(const unsigned char* X, const Strip<K>& st, f32x4 (&acc)[2]) {
     const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-    const float* x0 = X + i * XS + g;
-    const float* x1 = x0 + 16 * XS;
 #pragma unroll
-    for (int s4 = 0; s4 < K / 16; ++s4) {
-        const float wv[4] = {st.w[s4].x, st.w[s4].y, st.w[s4].z, st.w[s4].w};
+    for (int ks = 0; ks < K / 32; ++ks) {
+        u32x4 xh[2], xl[2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = (4 * s4 + q) * 4;
-            acc[0] = mfma(x0[k], wv[q], acc[0]);
-            acc[1] = mfma(x1[k], wv[q], acc[1]);
+        for (int rb = 0; rb < 2; ++rb) {
+            const unsigned char* p = X + (rb * 16 + i) * srs(K) + 2 * (32 * ks + 8 * g);
+            xh[rb] = *reinterpret_cast<const u32x4*>(p);
+            xl[rb] = *reinterpret_cast<const u32x4*>(p + 2 * K);
         }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) acc[rb] = mfma_h(st.w[ks][0], xh[rb], acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) acc[rb] = mfma_h(st.w[ks][0], xl[rb], acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) acc[rb] = mfma_h(st.w[ks][1], xh[rb], acc[rb]);
     }
 }
 
 // Columns [nb*16, nb*16+16) of X . W^T for nb = wave, wave+4, ...: the next
 // strip is requested before the current one is consumed (and the first one
 // by the caller, before its LDS staging), so weight latency overlaps work.
-// epi(nb, acc) consumes each finished block.
-template <int K, int XS, int NB, typename Epi>
-__device__ __forceinline__ void gemm_cols(const float* X, const float4* __restrict__ Wp, Strip<K>& cur,
+// epi(nb, acc) consumes each finished block (lane: row rb*16 + (lane&15),
+// columns nb*16 + 4*(lane>>4) + r).
+template <int K, int NB, typename Epi>
+__device__ __forceinline__ void gemm_cols(const unsigned char* X, const u32x4* __restrict__ Wp, Strip<K>& cur,
                                           const float* __restrict__ bias, Epi epi) {
-    const int wave = threadIdx.x >> 6, j = threadIdx.x & 15;
+    const int wave = threadIdx.x >> 6, g = (threadIdx.x & 63) >> 4;
 #pragma unroll 1
     for (int nb = wave; nb < NB; nb += 4) {
         Strip<K> nxt;
         if (nb + 4 < NB) nxt.load(Wp, nb + 4);
         f32x4 acc[2];
-        const float bv = bias ? bias[nb * 16 + j] : 0.f;
-        acc[0] = acc[1] = f32x4{bv, bv, bv, bv};
-        gemm_strip<K, XS>(X, cur, acc);
+        f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bias[nb * 16 + 4 * g + r];
+        }
+        acc[0] = acc[1] = bv;
+        gemm_strip<K>(X, cur, acc);
         epi(nb, acc);
         if (nb + 4 < NB) cur = nxt;
     }
 }
 
-// LayerNorm of TR rows of H floats in LDS (src, stride SS) -> dst (stride DS):
-// 8 lanes per row, two-pass mean / biased variance as nn.LayerNorm.
-template <int H, int SS, int DS>
-__device__ __forceinline__ void ln_rows(const float* src, float* dst, const float* __restrict__ g,
+// Four consecutive fp32 values -> their hi and lo f16 at p, p + 2K.
+template <int K>
+__device__ __forceinline__ void put_split4(unsigned char* p, float a, float b, float c, float d) {
+    unsigned h0, h1, l0, l1;
+    split2u(a, b, h0, l0);
+    split2u(c, d, h1, l1);
+    *reinterpret_cast<uint2*>(p) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(p + 2 * K) = uint2{l0, l1};
+}
+
+// LayerNorm of TR rows of H floats in LDS (src, stride frs(H)) -> split rows
+// (dst, stride srs(H)): 8 lanes per row, each H/8 consecutive channels;
+// two-pass mean / biased variance as nn.LayerNorm.
+template <int H>
+__device__ __forceinline__ void ln_rows(const float* src, unsigned char* dst, const float* __restrict__ g,
                                         const float* __restrict__ b) {
+    constexpr int PER = H / 8;
+    static_assert(PER % 4 == 0, "H multiple of 32");
     const int row = threadIdx.x >> 3, part = threadIdx.x & 7;
-    const float* xr = src + row * SS;
+    const float* xr = src + row * frs(H) + part * PER;
+    float v[PER];
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        const float4 t = *reinterpret_cast<const float4*>(xr + 4 * q);
+        v[4 * q] = t.x;
+        v[4 * q + 1] = t.y;
+        v[4 * q + 2] = t.z;
+        v[4 * q + 3] = t.w;
+    }
     float s = 0.f;
 #pragma unroll
-    for (int kk = 0; kk < H / 8; ++kk) s += xr[part + 8 * kk];
+    for (int k = 0; k < PER; ++k) s += v[k];
     s += __shfl_xor(s, 1);
     s += __shfl_xor(s, 2);
     s += __shfl_xor(s, 4);
     const float mean = s / (float)H;
-    float v = 0.f;
+    float var = 0.f;
 #pragma unroll
-    for (int kk = 0; kk < H / 8; ++kk) {
-        const float d = xr[part + 8 * kk] - mean;
-        v += d * d;
+    for (int k = 0; k < PER; ++k) {
+        const float d = v[k] - mean;
+        var += d * d;
     }
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 4);
-    const float rstd = 1.0f / sqrtf(v / (float)H + kLnEps);
-    float* yr = dst + row * DS;
+    var += __shfl_xor(var, 1);
+    var += __shfl_xor(var, 2);
+    var += __shfl_xor(var, 4);
+    const float rstd = 1.0f / sqrtf(var / (float)H + kLnEps);
+    unsigned char* yr = dst + row * srs(H) + 2 * part * PER;
 #pragma unroll
-    for (int kk = 0; kk < H / 8; ++kk) {
-        const int k = part + 8 * kk;
-        yr[k] = (xr[k] - mean) * rstd * g[k] + b[k];
+    for (int q = 0; q < PER / 4; ++q) {
+        float y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = part * PER + 4 * q + e;
+            y[e] = (v[4 * q + e] - mean) * rstd * g[k] + b[k];
+        }
+        put_split4<H>(yr + 8 * q, y[0], y[1], y[2], y[3]);
     }
 }
 
-// Global rows [r0, r0+TR) of width H (zero past R) -> LDS (stride S).
-template <int H, int S>
+// Global rows [r0, r0+TR) of width H (zero past R) -> LDS fp32 rows (stride frs(H)).
+template <int H>
 __device__ __forceinline__ void load_rows(const float* __restrict__ x, int r0, int R, float* dst) {
     constexpr int H4 = H / 4;
     for (int i = threadIdx.x; i < TR * H4; i += 256) {
         const int r = i / H4, c = (i - r * H4) * 4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (r0 + r < R) v = *reinterpret_cast<const float4*>(x + (size_t)(r0 + r) * H + c);
-        float* d = dst + r * S + c;
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
+        *reinterpret_cast<float4*>(dst + r * frs(H) + c) = v;
+    }
+}
+// ... -> LDS split rows (stride srs(H)).
+template <int H>
+__device__ __forceinline__ void load_rows_split(const float* __restrict__ x, int r0, int R, unsigned char* dst) {
+    constexpr int H4 = H / 4;
+    for (int i = threadIdx.x; i < TR * H4; i += 256) {
+        const int r = i / H4, c = (i - r * H4) * 4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r0 + r < R) v = *reinterpret_cast<const float4*>(x + (size_t)(r0 + r) * H + c);
+        put_split4<H>(dst + r * srs(H) + 2 * c, v.x, v.y, v.z, v.w);
     }
 }
 
 // y[R][N] = act(LN?(x)[R][K] . W^T + b) for N % 16 == 0.
 template <int K, int N, bool LN, int ACT>
 __global__ __launch_bounds__(256) void ln_gemm_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                      const float* __restrict__ bln, const float4* __restrict__ Wp,
+                                                      const float* __restrict__ bln, const u32x4* __restrict__ Wp,
                                                       const float* __restrict__ bias, int R, float* __restrict__ y) {
-    constexpr int XS = K + 2;
-    __shared__ float X[TR * XS];
-    __shared__ float Xn[LN ? TR * XS : 1];
+    static_assert(LN, "ln_gemm: LN form only");
+    __shared__ __attribute__((aligned(16))) float X[TR * frs(K)];
+    __shared__ __attribute__((aligned(16))) unsigned char Xn[TR * srs(K)];
     const int r0 = blockIdx.x * TR;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, gq = lane >> 4;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     Strip<K> st;
     if (wave < N / 16) st.load(Wp, wave);
-    load_rows<K, XS>(x, r0, R, X);
+    load_rows<K>(x, r0, R, X);
     __syncthreads();
-    const float* A = X;
-    if (LN) {
-        ln_rows<K, XS, XS>(X, Xn, g, bln);
-        __syncthreads();
-        A = Xn;
-    }
-    gemm_cols<K, XS, N / 16>(A, Wp, st, bias, [&](int nb, const f32x4 (&acc)[2]) {
+    ln_rows<K>(X, Xn, g, bln);
+    __syncthreads();
+    gemm_cols<K, N / 16>(Xn, Wp, st, bias, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
+        for (int rb = 0; rb < 2; ++rb) {
+            const int row = r0 + rb * 16 + i;
+            if (row < R) {
+                f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = r0 + rb * 16 + 4 * gq + r;
-                if (row < R) y[(size_t)row * N + nb * 16 + j] = act_t<ACT>(acc[rb][r]);
+                for (int r = 0; r < 4; ++r) v[r] = act_t<ACT>(acc[rb][r]);
+                *reinterpret_cast<f32x4*>(y + (size_t)row * N + nb * 16 + 4 * gq) = v;
             }
+        }
     });
 }
 
@@ -162,56 +226,55 @@ __global__ __launch_bounds__(256) void ln_gemm_kernel(const float* __restrict__ 
 // y may alias x (each tile reads its rows before writing them).
 template <int H>
 __global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict__ att, const float* x,
-                                                        const float4* __restrict__ Wo, const float* __restrict__ bo,
+                                                        const u32x4* __restrict__ Wo, const float* __restrict__ bo,
                                                         const float* __restrict__ g2, const float* __restrict__ b2n,
-                                                        const float4* __restrict__ W1, const float* __restrict__ b1,
-                                                        const float4* __restrict__ W2, const float* __restrict__ b2,
+                                                        const u32x4* __restrict__ W1, const float* __restrict__ b1,
+                                                        const u32x4* __restrict__ W2, const float* __restrict__ b2,
                                                         int R, float* y) {
-    constexpr int F = 2 * H, HS = H + 2, FS = F + 2;
-    __shared__ float A[TR * HS];  // att tile, then LN2(o)
-    __shared__ float O[TR * HS];  // o
-    __shared__ float Hd[TR * FS]; // relu(FFN1)
+    constexpr int F = 2 * H;
+    __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att tile, then LN2(o) (split)
+    __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];           // o (fp32)
+    __shared__ __attribute__((aligned(16))) unsigned char Hd[TR * srs(F)];  // relu(FFN1) (split)
     const int r0 = blockIdx.x * TR;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, gq = lane >> 4;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     Strip<H> so;
     if (wave < H / 16) so.load(Wo, wave);
-    load_rows<H, HS>(att, r0, R, A);
+    load_rows_split<H>(att, r0, R, A);
     __syncthreads();
     // o = x + att . Wo^T + bo   (components.py:86, 137: x + dropout(attn(...)))
-    gemm_cols<H, HS, H / 16>(A, Wo, so, bo, [&](int nb, const f32x4 (&acc)[2]) {
+    gemm_cols<H, H / 16>(A, Wo, so, bo, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rr = rb * 16 + 4 * gq + r, row = r0 + rr, col = nb * 16 + j;
-                O[rr * HS + col] = row < R ? x[(size_t)row * H + col] + acc[rb][r] : 0.f;
-            }
+        for (int rb = 0; rb < 2; ++rb) {
+            const int rr = rb * 16 + i, row = r0 + rr, col = nb * 16 + 4 * gq;
+            f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (row < R) o = *reinterpret_cast<const f32x4*>(x + (size_t)row * H + col) + acc[rb];
+            *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = o;
+        }
     });
     Strip<H> s1;
     s1.load(W1, wave);  // F/16 >= 4 blocks: every wave has one
     __syncthreads();
-    ln_rows<H, HS, HS>(O, A, g2, b2n);
+    ln_rows<H>(O, A, g2, b2n);
     __syncthreads();
-    gemm_cols<H, HS, F / 16>(A, W1, s1, b1, [&](int nb, const f32x4 (&acc)[2]) {
+    gemm_cols<H, F / 16>(A, W1, s1, b1, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float v = acc[rb][r];
-                Hd[(rb * 16 + 4 * gq + r) * FS + nb * 16 + j] = v > 0.f ? v : 0.f;
-            }
+        for (int rb = 0; rb < 2; ++rb) {
+            const f32x4 v = acc[rb];
+            put_split4<F>(Hd + (rb * 16 + i) * srs(F) + 2 * (nb * 16 + 4 * gq), v[0] > 0.f ? v[0] : 0.f,
+                          v[1] > 0.f ? v[1] : 0.f, v[2] > 0.f ? v[2] : 0.f, v[3] > 0.f ? v[3] : 0.f);
+        }
     });
     Strip<F> s2;
     if (wave < H / 16) s2.load(W2, wave);
     __syncthreads();
-    gemm_cols<F, FS, H / 16>(Hd, W2, s2, b2, [&](int nb, const f32x4 (&acc)[2]) {
+    gemm_cols<F, H / 16>(Hd, W2, s2, b2, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rr = rb * 16 + 4 * gq + r, row = r0 + rr, col = nb * 16 + j;
-                if (row < R) y[(size_t)row * H + col] = O[rr * HS + col] + acc[rb][r];
-            }
+        for (int rb = 0; rb < 2; ++rb) {
+            const int rr = rb * 16 + i, row = r0 + rr, col = nb * 16 + 4 * gq;
+            if (row < R)
+                *reinterpret_cast<f32x4*>(y + (size_t)row * H + col) =
+                    *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
+        }
     });
 }
 
@@ -235,11 +298,34 @@ std::vector<float> pack_bfrag(const float* W, int N, int K) {
     return out;
 }
 
+// Split-f16 A-fragment packing for the fused layers' v_mfma_f32_16x16x32_f16
+// (D^T = W . X^T): element (n-block nb, k-step ks, half, lane, e) =
+// half(W[nb*16 + (lane&15)][32*ks + 8*(lane>>4) + e]), layout
+// [nb][ks][hi|lo][lane][8 f16] - as many bytes as W in fp32.  False if a
+// weight is outside the f16 range (the caller then keeps the fp32 layers).
+bool pack_bfrag_split(const float* W, int N, int K, std::vector<float>* out) {
+    out->assign((size_t)N * K, 0.f);
+    uint16_t* o = reinterpret_cast<uint16_t*>(out->data());
+    const int KS = K / 32;
+    for (int nb = 0; nb < N / 16; ++nb)
+        for (int ks = 0; ks < KS; ++ks)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                    const float v = W[(size_t)(nb * 16 + (lane & 15)) * K + 32 * ks + 8 * (lane >> 4) + e];
+                    if (!(std::fabs(v) < 65504.f)) return false;
+                    const _Float16 h = (_Float16)v, l = (_Float16)(v - (float)h);
+                    const size_t base = (((size_t)nb * KS + ks) * 2 * 64 + lane) * 8 + e;
+                    std::memcpy(&o[base], &h, 2);
+                    std::memcpy(&o[base + 64 * 8], &l, 2);
+                }
+    return true;
+}
+
 int32_t launch_ln_gemm(const float* x, const float* g, const float* b, const float* Wp, const float* bias, int act,
                        int R, int K, int N, float* y, hipStream_t st) {
     if (R == 0) return M2_OK;
     const dim3 grid(cdiv(R, tfx::TR)), blk(256);
-    const float4* W = reinterpret_cast<const float4*>(Wp);
+    const vx_u32x4* W = reinterpret_cast<const vx_u32x4*>(Wp);
 #define M2_LNG(KK, NN)                                                                                           \
     if (K == KK && N == NN) {                                                                                    \
         if (g && act == ACT_NONE)                                                                                \
@@ -268,7 +354,7 @@ int32_t launch_post_attn(const float* att, const float* x, const float* Wo, cons
                          int H, float* y, hipStream_t st) {
     if (R == 0) return M2_OK;
     const dim3 grid(cdiv(R, tfx::TR)), blk(256);
-    auto f4 = [](const float* p) { return reinterpret_cast<const float4*>(p); };
+    auto f4 = [](const float* p) { return reinterpret_cast<const vx_u32x4*>(p); };
     switch (H) {
         case 32: hipLaunchKernelGGL((tfx::post_attn_kernel<32>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n, f4(W1), b1, f4(W2), b2, R, y); break;
         case 64: hipLaunchKernelGGL((tfx::post_attn_kernel<64>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n, f4(W1), b1, f4(W2), b2, R, y); break;
