@@ -331,13 +331,20 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
 template <int V>
 using ic_ = std::integral_constant<int, V>;
 
+// Key split: a workgroup is 8 waves = 4 query groups x 2 key halves; the
+// key-half-0 waves take the even 64-key chunks, the key-half-1 waves the odd
+// ones, each with its own online-softmax state, merged through LDS at the end
+// (flash-decoding inside the workgroup).  Twice the waves per query of the
+// 4-wave form at the same LDS per wave: the per-chunk latency chain (LDS ->
+// MFMA -> softmax -> MFMA) is what bounds this kernel.
 template <int HD>
 struct AttSplit {
     static constexpr int KS = (HD + 31) / 32, DP = 32 * KS;  // QK^T k-steps, padded head dim
     static constexpr int KRS = 4 * DP + 32;                    // K row: hi[DP] lo[DP] f16 + pad
     static constexpr int VRS = 4 * ATT_KC + 32;                // V^T row: hi[64 keys] lo[64] + pad
-    static constexpr int KBUF = ATT_KC * KRS, VBUF = HD * VRS;
-    static constexpr int LDS = 2 * KBUF + 2 * VBUF + 2 * ATT_KC * 8;
+    static constexpr int KBUF = ATT_KC * KRS, VBUF = HD * VRS, MBUF = ATT_KC * 8;
+    static constexpr int NBUF = 4;                             // 2 chunk pairs: one read, one being stashed
+    static constexpr int LDS = NBUF * (KBUF + VBUF + MBUF);
 };
 
 __device__ __forceinline__ f32x4 mfma_f16(vx_u32x4 a, vx_u32x4 b, f32x4 c) {
@@ -346,30 +353,39 @@ __device__ __forceinline__ f32x4 mfma_f16(vx_u32x4 a, vx_u32x4 b, f32x4 c) {
 }
 
 template <int HD>
-__global__ __launch_bounds__(256) void attention_split_kernel(const float* __restrict__ qkv,
-                                                              const uint8_t* __restrict__ key_mask, int N, int H,
-                                                              float scale, float* __restrict__ out) {
+__global__ __launch_bounds__(512, HD <= 32 ? 4 : 2) void attention_split_kernel(const float* __restrict__ qkv,
+                                                                 const uint8_t* __restrict__ key_mask, int N, int H,
+                                                                 float scale, float* __restrict__ out, int nqb,
+                                                                 int heads, int ngroups) {
     using P = AttSplit<HD>;
     constexpr int KS = P::KS, DP = P::DP, KRS = P::KRS, VRS = P::VRS;
     constexpr int MT = HD / 16;                  // 16-row d blocks of O^T
-    constexpr int IT = ATT_KC * (HD / 4) / 256;  // float4 of K (and of V) per thread per chunk
+    constexpr int IT = ATT_KC * (HD / 4) / 256;  // float4 of K per thread per chunk (256 threads per chunk)
     static_assert(HD % 16 == 0 && ATT_KC * (HD / 4) % 256 == 0, "head_dim");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* const Ks0 = smem;
-    unsigned char* const Vt0 = smem + 2 * P::KBUF;
+    unsigned char* const Vt0 = smem + P::NBUF * P::KBUF;
     // per key (scale, add): live (scale*log2e, 0), masked (0, -1e9*log2e),
     // past the end (0, -inf): the base-2 score is one fma of the raw dot product
-    float2* const Mk0 = reinterpret_cast<float2*>(smem + 2 * P::KBUF + 2 * P::VBUF);
-    const int b = blockIdx.z, hh = blockIdx.y;
+    float2* const Mk0 = reinterpret_cast<float2*>(smem + P::NBUF * (P::KBUF + P::VBUF));
+    // XCD-aware workgroup order: workgroup L runs on XCD L % 8 (each XCD has
+    // its own L2), so the nqb query blocks of one (utterance, head) - which
+    // all stream the same K and V - are given ids on the same XCD.
+    const int L = blockIdx.x, xcd = L & 7, r = L >> 3;
+    const int grp = xcd + 8 * (r / nqb), qb = r - (r / nqb) * nqb;
+    if (grp >= ngroups) return;  // padding of the last round (ngroups % 8 != 0)
+    const int b = grp / heads, hh = grp - b * heads;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, g = lane >> 4;
+    const int qg = wave & 3, kh = wave >> 2;  // query group, key half
+    const int ct = tid & 255, ch = tid >> 8;  // fetch / stash: thread within a chunk, chunk of the pair
     const size_t row3 = (size_t)3 * H;
     const float* base = qkv + (size_t)b * N * row3 + hh * HD;
-    const int qi = blockIdx.x * 64 + wave * 16 + li;
+    const int qi = qb * 64 + qg * 16 + li;
     const float sl2 = scale * kLog2e;
 
-    if constexpr (DP > HD) {  // zero the padded head dims of both K buffers once
-        for (int i = tid; i < 2 * ATT_KC; i += 256) {
+    if constexpr (DP > HD) {  // zero the padded head dims of every K buffer once
+        for (int i = tid; i < P::NBUF * ATT_KC; i += 512) {
             unsigned char* r = Ks0 + i * KRS;
             for (int d = HD; d < DP; d += 4) {
                 *reinterpret_cast<uint2*>(r + 2 * d) = uint2{0u, 0u};
@@ -377,26 +393,27 @@ __global__ __launch_bounds__(256) void attention_split_kernel(const float* __res
             }
         }
     }
-    // Chunks stream through registers PF chunks ahead of their stash (the
-    // split kernel's compute per chunk is short next to an L2 / HBM round
-    // trip).  K: thread = (key, head-dim quad), quads fastest (128-B rows);
-    // V: thread = (key pair, quad), pairs fastest, so the transposed stores
-    // (two keys' f16 in one dword of a V^T row) hit 32 distinct banks.
-    constexpr int PF = 3;
+    // Chunk pairs stream through registers PF pairs ahead of their stash.
+    // K: thread = (key, head-dim quad), quads fastest (128-B rows); V: thread
+    // = (key pair, quad), pairs fastest, so the transposed stores (two keys'
+    // f16 in one dword of a V^T row) hit 32 distinct banks.
+    constexpr int PF = 2;
     constexpr int NQ4 = HD / 4, ITV = (32 * NQ4 + 255) / 256;
     float4 kr[PF][IT], vr[PF][ITV][2];
     float2 mkr[PF];
-    auto fetch = [&](int j0, auto sc) {
+    const int nch = (N + ATT_KC - 1) / ATT_KC, npair = (nch + 1) / 2;
+    auto fetch = [&](int pr_, auto sc) {  // chunk 2 pr_ + ch
         constexpr int sl = decltype(sc)::value;
+        const int j0 = (2 * pr_ + ch) * ATT_KC;
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256, key = i / NQ4, d4 = i - key * NQ4, j = j0 + key;
+            const int i = ct + it * 256, key = i / NQ4, d4 = i - key * NQ4, j = j0 + key;
             kr[sl][it] = j < N ? *reinterpret_cast<const float4*>(base + j * row3 + H + 4 * d4)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int it = 0; it < ITV; ++it) {
-            const int i = tid + it * 256, pr = i & 31, d4 = i >> 5;
+            const int i = ct + it * 256, pr = i & 31, d4 = i >> 5;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int j = j0 + 2 * pr + h;
@@ -404,21 +421,20 @@ __global__ __launch_bounds__(256) void attention_split_kernel(const float* __res
                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-        if (tid < ATT_KC) {
-            const int j = j0 + tid;
-            // 0: live key, 1: masked (score -1e9), 2: past the end (weight 0)
+        if (ct < ATT_KC) {
+            const int j = j0 + ct;
             mkr[sl] = j >= N ? make_float2(0.f, -INFINITY)
                              : ((key_mask && key_mask[(size_t)b * N + j] == 0) ? make_float2(0.f, kMaskFill * kLog2e)
                                                                                 : make_float2(sl2, 0.f));
         }
     };
-    auto stash = [&](int buf, auto sc) {
+    auto stash = [&](int buf, auto sc) {  // this thread's chunk of the pair into buffer buf
         constexpr int sl = decltype(sc)::value;
         unsigned char* Kb = Ks0 + buf * P::KBUF;
         unsigned char* Vb = Vt0 + buf * P::VBUF;
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256, key = i / NQ4, d4 = i - key * NQ4;
+            const int i = ct + it * 256, key = i / NQ4, d4 = i - key * NQ4;
             unsigned h0, h1, l0, l1;
             split2u(kr[sl][it].x, kr[sl][it].y, h0, l0);
             split2u(kr[sl][it].z, kr[sl][it].w, h1, l1);
@@ -428,7 +444,7 @@ __global__ __launch_bounds__(256) void attention_split_kernel(const float* __res
         }
 #pragma unroll
         for (int it = 0; it < ITV; ++it) {
-            const int i = tid + it * 256, pr = i & 31, d4 = i >> 5;
+            const int i = ct + it * 256, pr = i & 31, d4 = i >> 5;
             if (d4 < NQ4) {
                 // keys 2pr, 2pr + 1 sit next to each other in the permuted column order
                 const int key = 2 * pr;
@@ -445,13 +461,11 @@ __global__ __launch_bounds__(256) void attention_split_kernel(const float* __res
                 }
             }
         }
-        if (tid < ATT_KC) Mk0[buf * ATT_KC + tid] = mkr[sl];
+        if (ct < ATT_KC) Mk0[buf * ATT_KC + ct] = mkr[sl];
     };
 
-    const int nch = (N + ATT_KC - 1) / ATT_KC;
     fetch(0, ic_<0>{});
-    if (nch > 1) fetch(ATT_KC, ic_<1>{});
-    if (nch > 2) fetch(2 * ATT_KC, ic_<2>{});
+    if (npair > 1) fetch(1, ic_<1>{});
     vx_u32x4 qh[KS], ql[KS];  // B = Q^T: lane (query li, group g) holds head dims 32 ks + 8 g .. + 7
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -473,13 +487,11 @@ __global__ __launch_bounds__(256) void attention_split_kernel(const float* __res
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
-    stash(0, ic_<0>{});
+    stash(ch, ic_<0>{});
     __syncthreads();
 
-    // chunk c: registers of slot c % PF; unrolled by PF so slots are compile-time
-    auto chunk = [&](int c, auto sc) {
-        constexpr int sl = decltype(sc)::value;
-        const int buf = c & 1;
+    // chunk 2p + kh of this wave from buffer 2 (p & 1) + kh
+    auto process = [&](int buf) {
         const unsigned char* K = Ks0 + buf * P::KBUF;
         const unsigned char* V = Vt0 + buf * P::VBUF;
         const float2* MK = Mk0 + buf * ATT_KC;
@@ -539,19 +551,42 @@ __global__ __launch_bounds__(256) void attention_split_kernel(const float* __res
             }
         }
         m = mn;
-        if (c + 1 < nch) {
-            // the other buffer was last read in chunk c-1, before the previous barrier
-            stash(buf ^ 1, ic_<(sl + 1) % PF>{});
-            if (c + PF < nch) fetch((c + PF) * ATT_KC, ic_<sl>{});  // slot sl is free again
-            __syncthreads();
+    };
+    // pair p: buffers 2 (p & 1) + {0, 1}; registers of slot p % PF (unrolled by PF)
+    auto pair = [&](int p, auto sc) {
+        constexpr int sl = decltype(sc)::value;
+        if (2 * p + kh < nch) process(2 * (p & 1) + kh);  // wave-uniform
+        if (p + 1 < npair) {
+            // the other buffer pair was last read in pair p-1, before the previous barrier
+            stash(2 * ((p + 1) & 1) + ch, ic_<(sl + 1) % PF>{});
+            if (p + PF < npair) fetch(p + PF, ic_<sl>{});  // slot sl is free again
         }
+        __syncthreads();
     };
 #pragma unroll 1
-    for (int c = 0; c < nch; c += PF) {
-        chunk(c, ic_<0>{});
-        if (c + 1 < nch) chunk(c + 1, ic_<1>{});
-        if (c + 2 < nch) chunk(c + 2, ic_<2>{});
+    for (int p = 0; p < npair; p += PF) {
+        pair(p, ic_<0>{});
+        if (p + 1 < npair) pair(p + 1, ic_<1>{});
     }
+    // merge the two key halves: kh 1 hands (m, lsum partial, acc) to kh 0 via LDS
+    float* xs = reinterpret_cast<float*>(smem) + (qg * 64 + lane) * (2 + 4 * MT);
+    if (kh == 1) {
+        xs[0] = m;
+        xs[1] = lsum;
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xs[2 + 4 * t + r] = acc[t][r];
+    }
+    __syncthreads();
+    if (kh == 1) return;
+    const float mb = xs[0], mt = vmax(m, mb);
+    const float fa = __builtin_amdgcn_exp2f(m - mt), fb = __builtin_amdgcn_exp2f(mb - mt);
+    lsum = lsum * fa + xs[1] * fb;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][r] = acc[t][r] * fa + xs[2 + 4 * t + r] * fb;
     lsum += __shfl_xor(lsum, 16);
     lsum += __shfl_xor(lsum, 32);
     if (qi >= N) return;
@@ -566,14 +601,16 @@ __global__ __launch_bounds__(256) void attention_split_kernel(const float* __res
 template <int HD>
 static int32_t launch_att_split(dim3 grid, const float* qkv, const uint8_t* mask, int N, int H, float scale,
                                 float* out, hipStream_t st) {
+    const int nqb = (int)grid.x, heads = (int)grid.y, ngroups = (int)(grid.y * grid.z);
+    const dim3 g1(8 * nqb * ((ngroups + 7) / 8));
     static bool attr = false;
     if (!attr) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attention_split_kernel<HD>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, AttSplit<HD>::LDS));
         attr = true;
     }
-    hipLaunchKernelGGL(attention_split_kernel<HD>, grid, dim3(256), AttSplit<HD>::LDS, st, qkv, mask, N, H, scale,
-                       out);
+    hipLaunchKernelGGL(attention_split_kernel<HD>, g1, dim3(512), AttSplit<HD>::LDS, st, qkv, mask, N, H, scale, out,
+                       nqb, heads, ngroups);
     M2_LAUNCHED("attention_split_kernel");
     return M2_OK;
 }
