@@ -11,10 +11,16 @@ mkdir -p $out
 # enough warm-up for the clocks to settle (bench.py's default), so the kernel
 # averages match the bench's own HIP-event timings
 BENCH="python3 bench.py --steps 100 --warmup 300 --no-cpu-baseline --no-pipeline-extra $*"
+# PMC passes: counters per dispatch, so a few timed steps are enough
+PMCBENCH="python3 bench.py --steps 4 --warmup 300 --no-cpu-baseline --no-pipeline-extra $*"
 run() {  # name, rocprof args...
   local name=$1; shift
-  timeout -k 10 240 rocprofv3 "$@" --output-format csv -d $out/$name -o run -- $BENCH > $out/$name.log 2>&1
+  local cmd=$PMCBENCH
+  [ "$name" = trace ] && cmd=$BENCH
+  timeout -k 10 240 rocprofv3 "$@" --output-format csv -d $out/$name -o run -- $cmd > $out/$name.log 2>&1
   local rc=$?
+  # the per-dispatch trace is large; the stats csv is what gets summarised
+  rm -f $out/$name/run_kernel_trace.csv
   echo "pass $name rc=$rc"
   return $rc
 }
