@@ -160,27 +160,52 @@ __global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ 
     }
 }
 
-// One wave per output frame; binary search of the frame in cum[b].
+// Frame gather: a workgroup owns LR_TF frames of one utterance.  The
+// utterance's prefix sums go to LDS once, one thread per frame finds its
+// phoneme there (binary search: smallest s with cum[s+1] > t; frames at or
+// past cum[S] are zero padding), then the whole workgroup copies the rows in
+// 16-B pieces.  (Was one wave per frame searching global memory: 7 dependent
+// L2 round trips per frame.)
+constexpr int LR_TF = 64;
+
 __global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict__ enc,
                                                         const int32_t* __restrict__ cum, int S,
                                                         int H, int T_out, float* __restrict__ out) {
-    const int b = blockIdx.y;
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (t >= T_out) return;
+    extern __shared__ int32_t cs[];  // [S + 1] prefix sums, then [LR_TF] source phoneme per frame
+    int32_t* src = cs + S + 1;
+    const int b = blockIdx.y, t0 = blockIdx.x * LR_TF, tid = threadIdx.x;
     const int32_t* c = cum + (size_t)b * (S + 1);
-    float* o = out + ((size_t)b * T_out + t) * H;
-    if (t >= c[S]) {
-        for (int h = lane; h < H; h += 64) o[h] = 0.f;
-        return;
+    for (int i = tid; i <= S; i += 256) cs[i] = c[i];
+    __syncthreads();
+    if (tid < LR_TF) {
+        const int t = t0 + tid;
+        int sp = -1;
+        if (t < T_out && t < cs[S]) {
+            int lo = 0, hi = S - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (cs[mid + 1] > t) hi = mid; else lo = mid + 1;
+            }
+            sp = lo;
+        }
+        src[tid] = sp;
     }
-    int lo = 0, hi = S - 1;  // smallest s with c[s+1] > t
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (c[mid + 1] > t) hi = mid; else lo = mid + 1;
+    __syncthreads();
+    const int nf = min(LR_TF, T_out - t0);
+    if ((H & 3) == 0) {
+        const int H4 = H / 4;
+        for (int i = tid; i < nf * H4; i += 256) {
+            const int f = i / H4, c4 = i - f * H4, sp = src[f];
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (sp >= 0) v = *reinterpret_cast<const float4*>(enc + ((size_t)b * S + sp) * H + 4 * c4);
+            *reinterpret_cast<float4*>(out + ((size_t)b * T_out + t0 + f) * H + 4 * c4) = v;
+        }
+    } else {
+        for (int i = tid; i < nf * H; i += 256) {
+            const int f = i / H, h = i - f * H, sp = src[f];
+            out[((size_t)b * T_out + t0 + f) * H + h] = sp >= 0 ? enc[((size_t)b * S + sp) * H + h] : 0.f;
+        }
     }
-    const float* e = enc + ((size_t)b * S + lo) * H;
-    for (int h = lane; h < H; h += 64) o[h] = e[h];
 }
 
 // ---------------------------------------------------------------------------
@@ -219,7 +244,9 @@ int32_t launch_lr_count(const void* dur, int is_int, float scale, int B, int S, 
 int32_t launch_lr_expand(const float* enc, const int32_t* cum, int B, int S, int H, int T_out,
                          float* out, hipStream_t st) {
     if (B == 0 || T_out == 0) return M2_OK;
-    hipLaunchKernelGGL(lr_expand_kernel, dim3(cdiv(T_out, 4), B), dim3(256), 0, st, enc, cum, S, H,
+    const size_t lds = ((size_t)S + 1 + LR_TF) * sizeof(int32_t);
+    M2_CHECK_SHAPE(lds <= 64 * 1024, "length_regulator: too many phonemes per utterance");
+    hipLaunchKernelGGL(lr_expand_kernel, dim3(cdiv(T_out, LR_TF), B), dim3(256), lds, st, enc, cum, S, H,
                        T_out, out);
     M2_LAUNCHED("lr_expand_kernel");
     return M2_OK;
