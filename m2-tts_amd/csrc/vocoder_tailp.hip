@@ -21,9 +21,10 @@
 // with their weights (2 KB per (m-block, k-block) fragment pair) and biases
 // held in VGPRs for the whole strip.  In step s the wave of layer l computes
 // chunk k = s - l - 1 (16 columns) from the ring its producer wrote in steps
-// s-1 and s-2; one s_barrier per step.  Rings hold 4 chunks (64 columns), so
-// a producer writing chunk k+1 never meets its consumer reading chunks k and
-// k-1 (or a residual reader two chunks behind).  Layer l's chunk k covers
+// s-1 and s-2; one s_barrier per step.  Rings hold 3 chunks where the only
+// reader is one layer down (a producer writing chunk k+1 never meets its
+// consumer reading chunks k and k-1) and 4 where a residual reader two layers
+// down also reads them (R1, R4).  Layer l's chunk k covers
 // columns [qa + 6 - l + 16k, +16): each layer lags its input by one column,
 // the receptive field of its k3 taps, so chunk k of layer l+1 needs exactly
 // chunks k and k-1 of layer l.  Chunk -1 is the warm-up: its leftmost columns
