@@ -100,10 +100,13 @@ constexpr int pd_of() {
     constexpr int NKB = (NTAP * (CIN / 8) + 3) / 4;
     return NKB < 4 / NMB ? NKB : 4 / NMB;
 }
-template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE>
+// TB: tap k's rows start at tb[k] (this lane's row, before the lane-group
+// offset) instead of bp + k*STEP*RSI - the phase-planar layouts of the head.
+template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE, bool TB = false>
 __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
                                        const unsigned char* xr, f32x4 (&acc)[NMB][NT],
-                                       u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2], const u32x4* wp_next) {
+                                       u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2], const u32x4* wp_next,
+                                       const unsigned char* const* tb = nullptr) {
     constexpr int NOCT = CIN / 8, NK = NTAP * NOCT, NKB = (NK + 3) / 4;
     static_assert(CIN % 8 == 0 && (NOCT <= 2 || NOCT % 4 == 0), "channel count must be 8, 16 or a multiple of 32");
     static_assert(!XR || 4 * NKB - NK == NOCT, "residual fold needs exactly one row of padding octets");
@@ -136,7 +139,13 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
         }
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-        const unsigned char* b0 = kb == NKB - 1 ? b_last : bl + koff(kb);
+        const unsigned char* b0;
+        if constexpr (TB) {
+            static_assert(NOCT >= 4 && !XR, "tap bases: whole octet rows only");
+            b0 = tb[kb / (NOCT / 4)] + g * 16 + (kb % (NOCT / 4)) * 64;
+        } else {
+            b0 = kb == NKB - 1 ? b_last : bl + koff(kb);
+        }
         u32x4 bh[NT], blo[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
@@ -396,6 +405,124 @@ __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float
 }
 
 // ---------------------------------------------------------------------------
+// Phase-planar head (stage1, one item per wave).  ConvT1's output u (x4) and
+// ResBlock1's hidden h are kept as 4 planes of 64 rows, plane p = positions
+// t = 4q + p for q in [qs(p), qs(p) + 64): u: qs = f0 - 1 for p >= 2, else
+// f0; h: qs = f0 - 1 for p = 3, else f0 - exactly the positions the next
+// layer reads.  Against the position-major layout (ConvT1 NQ = 65 inputs =
+// 5 tiles per phase, outputs 4 rows apart) this is 4 tiles per phase (20 %
+// fewer ConvT1 MFMAs) and conflict-free epilogue stores (consecutive lanes,
+// consecutive rows); the ResBlock1 convs become per-phase GEMMs whose three
+// taps read rows of the neighbouring planes (mma_x3 with tap bases).
+__device__ __forceinline__ int qs_u(int p, int f0) { return f0 - (p >= 2 ? 1 : 0); }
+__device__ __forceinline__ int qs_h(int p, int f0) { return f0 - (p == 3 ? 1 : 0); }
+constexpr int kPlane = 64;
+
+// Epilogue of one tile into an explicit LDS row (rowp) or straight to global
+// (GO); the residual, if any, is read from xrow.
+template <int COUT, int ACT, bool RES, bool GO>
+__device__ __forceinline__ void store_row(const f32x4& acc, unsigned char* rowp, const unsigned char* xrow, int co0,
+                                          bool zero, bool store, unsigned char* gout, int t) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[r];
+    if constexpr (ACT == ACT_LEAKY) leaky4(v);
+    if constexpr (RES) {
+        const unsigned char* row = xrow + co0 * 2;
+        const h4 hi = *reinterpret_cast<const h4*>(row), lo = *reinterpret_cast<const h4*>(row + 2 * COUT);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)hi[r] + (float)lo[r];
+    }
+    if (zero) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = 0.f;
+    }
+    unsigned h0, h1, l0, l1;
+    split2u(v[0], v[1], h0, l0);
+    split2u(v[2], v[3], h1, l1);
+    const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
+    const int g = (threadIdx.x & 63) >> 4;
+    const int off = 2 * (co0 - 4 * g + 8 * (g >> 1)) + (g & 1) * 2 * COUT;
+    if (store) {
+        if constexpr (GO)
+            *reinterpret_cast<u32x4*>(gout + (size_t)t * 4 * COUT + off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+        else
+            *reinterpret_cast<u32x4*>(rowp + off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
+}
+
+// ConvT1 (x4, k 8, pad 2) + leaky from the position-major inconv output (in,
+// frames f0-2 ..) into the u planes; item = wave = (phase, m-block).
+template <int CIN, int COUT, int RSI, int RSO>
+__device__ __forceinline__ void head_convT1_planar(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
+                                                   XW in, unsigned char* u, int f0, int L, APipe* ap,
+                                                   const u32x4* wp_next) {
+    constexpr int MB = COUT / 16, NKB = nkb_of<CIN, 2>(), NT = 4;
+    const int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ph = item / MB, mb = item - ph * MB;
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4, co0 = mb * 16 + 4 * g;
+    const int qs = qs_u(ph, f0), d0 = ph < 2 ? 0 : 1;  // taps (q + d0, q + d0 - 1)
+    const u32x4* wp = Wp + (size_t)(ph * MB + mb) * NKB * 128 + lane;
+    const unsigned char* bp = in.p + (qs + li + d0 - in.start) * RSI;
+    f32x4 acc[1][NT];
+    f32x4 bv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = bias[co0 + r];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[0][n] = bv;
+    mma_x3<CIN, 2, -1, RSI, NT, false, 1, NKB * 128, true>(wp, bp, nullptr, acc, *ap, wp_next);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int t = 4 * (qs + 16 * n + li) + ph;
+        store_row<COUT, ACT_LEAKY, false, false>(acc[0][n], u + (ph * kPlane + 16 * n + li) * RSO, nullptr, co0,
+                                                 t < 0 || t >= L, true, nullptr, t);
+    }
+}
+
+// ResBlock1 conv (k3, pad 1) between planes: input planes start at qsi(p),
+// output plane p covers q in [qso(p), +64).  CONV2: + x from the u planes,
+// stored straight to U1 (t < L and q < f0 + tf only); else leaky into the
+// h planes (0 outside [0, L)).
+template <int C, int RS, bool CONV2>
+__device__ __forceinline__ void head_rb1_planar(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
+                                                const unsigned char* in, unsigned char* out,
+                                                const unsigned char* x, int f0, int tf, int L, APipe* ap,
+                                                const u32x4* wp_next, unsigned char* gout) {
+    constexpr int MB = C / 16, NKB = nkb_of<C, 3>(), NT = 4;
+    const int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p = item / MB, mb = item - p * MB;
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4, co0 = mb * 16 + 4 * g;
+    const int qo = CONV2 ? f0 : qs_h(p, f0);
+    const unsigned char* tb[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const int pd = p + d - 1, dq = pd < 0 ? -1 : (pd > 3 ? 1 : 0), pi = pd - 4 * dq;
+        const int qsi = CONV2 ? qs_h(pi, f0) : qs_u(pi, f0);
+        tb[d] = in + (pi * kPlane + qo + dq - qsi + li) * RS;
+    }
+    const u32x4* wp = Wp + (size_t)mb * NKB * 128 + lane;
+    f32x4 acc[1][NT];
+    f32x4 bv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = bias[co0 + r];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[0][n] = bv;
+    mma_x3<C, 3, 1, RS, NT, false, 1, NKB * 128, true, true>(wp, nullptr, nullptr, acc, *ap, wp_next, tb);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int q = qo + 16 * n + li, t = 4 * q + p;
+        if constexpr (CONV2) {
+            const unsigned char* xrow = x + (p * kPlane + q - qs_u(p, f0)) * RS;
+            store_row<C, ACT_NONE, true, true>(acc[0][n], nullptr, xrow, co0, false, q < f0 + tf && t < L, gout, t);
+        } else {
+            store_row<C, ACT_LEAKY, false, false>(acc[0][n], out + (p * kPlane + 16 * n + li) * RS, nullptr, co0,
+                                                  t < 0 || t >= L, true, nullptr, t);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Global <-> LDS.  Trip counts are compile-time (NTHR threads, N rows) so
 // every thread issues all its global loads before the first LDS store.
 // mel -> window rows [0, N) (abs start + r), MP channels (zero past M).
@@ -493,15 +620,16 @@ __device__ __forceinline__ void gstore_rows(unsigned char* __restrict__ g, int L
 // columns of a partial 16-wide tile may read past them into region B, which
 // only feeds columns that are never stored (an MFMA output column depends
 // on its own B column only).  Region-B buffers keep the full read extent.
-template <int MP, int C, int TF>
+template <int MP, int C, int TF, bool PL = false>
 struct HeadPlan {  // A: a0 | h   B: mel | u
     static constexpr int C1 = C / 2;
     static constexpr int RS_M = rs_for(MP), RS_C = rs_for(C), RS_1 = rs_for(C1);
     static constexpr int MEL_N = TF + 6, A0_N = TF + 4, NQ = TF + 2, H_N = 4 * TF + 2, O_N = 4 * TF;
     static constexpr int CAP_MEL = cmax(MEL_N, rup16(A0_N) + 2);
     static constexpr int CAP_U = cmax(4 * NQ, rup16(H_N) + 4);
-    static constexpr int RA = cmax(A0_N * RS_C, H_N * RS_1);
-    static constexpr int LDS_BYTES = RA + cmax(CAP_MEL * RS_M, CAP_U * RS_1);
+    // PL: the phase-planar path keeps h and u as 4 planes of 64 rows
+    static constexpr int RA = cmax(A0_N * RS_C, cmax(H_N, PL ? 4 * 64 : 0) * RS_1);
+    static constexpr int LDS_BYTES = RA + cmax(CAP_MEL * RS_M, cmax(CAP_U, PL ? 4 * 64 + 4 : 0) * RS_1);
 };
 
 template <int CI, int W>
@@ -541,6 +669,9 @@ struct TailPlan {  // A: in | h3 | u4   B: u3 | h4
 #define X3_G_T1 1
 #define X3_G_R1 1
 #endif
+#ifndef X3_PLANAR  // stage1 head: phase-planar ConvT1 / ResBlock1 (0: position-major x3 layers)
+#define X3_PLANAR 1
+#endif
 struct CfgS1 {
     static constexpr int M = 64, MP = 64, C = 128;
     static constexpr int TF = X3_HEAD_TF, HW = X3_HEAD_HW, HMIN = 4;
@@ -579,11 +710,19 @@ __device__ unsigned long long g_x3_stamps[3][4096][16][16];
     } while (0)
 #endif
 
+// The stage1 head runs ConvT1 / ResBlock1 phase-planar when one item per wave
+// covers them: planes of 64 rows hold TF + 2 <= 65 input columns and the
+// (phase, m-block) items of the C/2-channel layers number exactly HW.
+template <class Cfg>
+constexpr bool head_planar() {
+    return X3_PLANAR && Cfg::TF + 1 <= 64 && 4 * (Cfg::C / 2 / 16) == Cfg::HW && Cfg::G_T1 == 1 && Cfg::G_R1 == 1;
+}
+
 template <class Cfg, bool TRANS>
 __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const float* __restrict__ mel, int T,
                                                                             VocX w, unsigned char* __restrict__ U1) {
     constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
-    using Pl = HeadPlan<MP, C, TF>;
+    using Pl = HeadPlan<MP, C, TF, head_planar<Cfg>()>;
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, f0 = blockIdx.x * TF;
@@ -600,6 +739,9 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     // from layer to layer across the barriers (APipe).
     constexpr bool ONE = Cfg::G_T1 == 1 && Cfg::G_R1 == 1 && I0::N == NW && I1::N == NW && I2::N == NW &&
                          I3::N == NW && pd_of<MP, 3, 1>() == 4 && pd_of<C, 2, 1>() == 4 && pd_of<C1, 3, 1>() == 4;
+    // phase-planar ConvT1 / ResBlock1: planes of 64 rows hold TF + 2 <= 65
+    // input columns, one item per wave = (phase, m-block)
+    constexpr bool PLANAR = ONE && head_planar<Cfg>();
     XSTAMP(0, 0);
     if constexpr (ONE) {
         const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -614,6 +756,34 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         XSTAMP(0, 1);
         __syncthreads();
         XSTAMP(0, 2);
+        if constexpr (PLANAR) {
+            // phase-planar ConvT1 / ResBlock1 (u planes in region B, h planes in region A)
+            unsigned char* up = lds + Pl::RA;
+            unsigned char* hp = lds;
+            xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N, 1, NW>(
+                w.wi, w.bi, melw, a0w, f0 - 2, T, &ap, w.wt[0] + (size_t)wv * nkb_of<C, 2>() * 128 + (threadIdx.x & 63));
+            XSTAMP(0, 3);
+            __syncthreads();
+            XSTAMP(0, 4);
+            constexpr int MB1 = C1 / 16;
+            head_convT1_planar<C, C1, Pl::RS_C, Pl::RS_1>(w.wt[0], w.bt[0], a0w, up, f0, 4 * T, &ap,
+                                                        w.w1[0] + (size_t)(wv % MB1) * nkb_of<C1, 3>() * 128 +
+                                                            (threadIdx.x & 63));
+            XSTAMP(0, 5);
+            __syncthreads();
+            XSTAMP(0, 6);
+            head_rb1_planar<C1, Pl::RS_1, false>(w.w1[0], w.b1[0], up, hp, nullptr, f0, TF, 4 * T, &ap,
+                                                 w.w2[0] + (size_t)(wv % MB1) * nkb_of<C1, 3>() * 128 +
+                                                     (threadIdx.x & 63),
+                                                 nullptr);
+            XSTAMP(0, 7);
+            __syncthreads();
+            XSTAMP(0, 8);
+            head_rb1_planar<C1, Pl::RS_1, true>(w.w2[0], w.b2[0], hp, nullptr, up, f0, TF, 4 * T, &ap, nullptr,
+                                                U1 + (size_t)b * 4 * T * 4 * C1);
+            XSTAMP(0, 9);
+            return;
+        }
         xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N, 1, NW>(
             w.wi, w.bi, melw, a0w, f0 - 2, T, &ap, I1::wp(w.wt[0], wv));
         XSTAMP(0, 3);
@@ -776,7 +946,7 @@ int32_t set_lds(K kernel, size_t bytes) {
 template <class Cfg>
 int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1, void* U2, float* audio,
             hipStream_t st, const std::function<void(int, bool)>& mark) {
-    using HP = HeadPlan<Cfg::MP, Cfg::C, Cfg::TF>;
+    using HP = HeadPlan<Cfg::MP, Cfg::C, Cfg::TF, head_planar<Cfg>()>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
     static bool attr = false;
