@@ -107,6 +107,12 @@ struct Slot {
 constexpr int kLayers = 7, kUnits = 22;
 constexpr int nmb(int l) { return l == 6 ? 1 : 2; }
 constexpr int nkb(int l) { return (l == 4 || l == 5) ? 1 : 2; }
+// ConvT4 (layer 3): output phases 1 and 2 read column q only (t3 = 2q, 2q + 1),
+// phases 0 and 3 also its neighbours, so its m-block 0 holds phases 1, 2 (one
+// k-block) and m-block 1 phases 0, 3 (two); MFMA row R holds the dense
+// (phase, channel) row prow(l, R).  Weight units keep nkb(l) per m-block.
+constexpr int nkbm(int l, int mb) { return l == 3 && mb == 0 ? 1 : nkb(l); }
+constexpr int prow(int l, int R) { return l != 3 ? R : (R < 16 ? R + 8 : (R < 24 ? R - 16 : R)); }
 constexpr int nfrag(int l) { return l == 0 ? 3 : 2; }
 constexpr int unit0(int l) { return l <= 4 ? 4 * l : (l == 5 ? 18 : 20); }
 // ConvT3: phase 0 reads columns q, q-1 (fragments 0, 1), phase 1 q+1, q (2, 0);

@@ -12,7 +12,9 @@
 // rows = two 16-row m-blocks, whose K is a list of (dq, input octet) slots
 // (tp::kslot): a k=3 conv on a P-phase signal reads tap t+d at column
 // q + floor((p+d)/P), phase (p+d) mod P.  The 8-channel layers fill all 16
-// rows of an m-block (two phases), where the natural layout fills 8.
+// rows of an m-block (two phases), where the natural layout fills 8;
+// ConvT4 pairs phases 1, 2 (which read column q only: one k-block) and 0, 3
+// (tp::prow), 9 MFMAs per step instead of 12.
 //
 // Systolic pipeline.  One workgroup owns a strip of 16*NCH columns of one
 // utterance and runs 8 waves with fixed roles: a loader wave streams U2 into
@@ -148,7 +150,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
     auto used = [](int f) {
         bool u = false;
         for (int m = 0; m < NMB; ++m)
-            for (int kb = 0; kb < NKB; ++kb) u = u || frag(L, m, kb) == f;
+            for (int kb = 0; kb < nkbm(L, m); ++kb) u = u || frag(L, m, kb) == f;
         return u;
     };
     u32x4 a[NMB][NKB][2];
@@ -156,13 +158,13 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
 #pragma unroll
     for (int m = 0; m < NMB; ++m) {
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
+        for (int kb = 0; kb < nkbm(L, m); ++kb) {
             const int u = unit0(L) + m * NKB + kb;
             a[m][kb][0] = W[u * 128 + lane];
             a[m][kb][1] = W[u * 128 + 64 + lane];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 32 + m * 16 + 4 * g + r];
+        for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 32 + m * 16 + 4 * g + r];  // packed in MFMA row order
     }
     // Input ring R(L) holds layer L-1's columns one column ahead of layer L's,
     // the residual ring R(L-1) two columns ahead.  Addresses for each ring
@@ -179,10 +181,14 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
 #pragma unroll
     for (int j = 0; j < PX; ++j) xadr[j] = RES ? ring_at(L - 1, ring_row(L - 1, j, li - 2), g) : 0u;
     // epilogue: after the permlane16 swap lane group g stores the hi (g even)
-    // or lo (g odd) octet of channels 8(g >> 1) .. +7 of each m-block
+    // or lo (g odd) octet of rows 8(g >> 1) .. +7 of each m-block: ring octet
+    // 2m + (g >> 1) (address oadr ^ 32m); ConvT4's permuted m-blocks hold
+    // octets 1, 2 (phases 1, 2) and 0, 3 (address oadr ^ 16)
+    constexpr unsigned MX = L == 3 ? 16u : 32u;
+    const int obase = L == 3 ? 1 + (g >> 1) : (g >> 1);
 #pragma unroll
     for (int j = 0; j < PO; ++j)
-        oadr[j] = L < 6 ? (g & 1) * kLoOff(L + 1) + ring_at(L + 1, ring_row(L + 1, j, li), (g >> 1)) : 0u;
+        oadr[j] = L < 6 ? (g & 1) * kLoOff(L + 1) + ring_at(L + 1, ring_row(L + 1, j, li), obase) : 0u;
     // identity A of m-block m: row li takes input row 16m + li = 8g + e
     u32x4 aid[NMB];
 #pragma unroll
@@ -217,10 +223,11 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
 #pragma unroll
             for (int pr = 0; pr < 3; ++pr)
 #pragma unroll
-                for (int m = 0; m < NMB; ++m) {
-                    const int f = frag(L, m, kb);
-                    acc[m] = mfma_h(a[m][kb][pr == 2], pr == 1 ? bl[f] : bh[f], acc[m]);
-                }
+                for (int m = 0; m < NMB; ++m)
+                    if (kb < nkbm(L, m)) {
+                        const int f = frag(L, m, kb);
+                        acc[m] = mfma_h(a[m][kb][pr == 2], pr == 1 ? bl[f] : bh[f], acc[m]);
+                    }
         if constexpr (RES) {
 #pragma unroll
             for (int m = 0; m < NMB; ++m) acc[m] = mfma_h(aid[m], xh, acc[m]);
@@ -272,7 +279,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                     // 16-B chunk (ds_write_b128) instead of two 8-B halves.
                     const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
                     const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
-                    *reinterpret_cast<u32x4*>(lds + (oadr[jo] ^ (32 * m))) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+                    *reinterpret_cast<u32x4*>(lds + (oadr[jo] ^ (MX * m))) = u32x4{s0[0], s1[0], s0[1], s1[1]};
                 }
             };
             if (edge && (x0 < 0 || x0 + 16 > L2)) epilogue(std::true_type{});  // wave-uniform
@@ -378,6 +385,8 @@ __global__ __launch_bounds__(NWAVES * 64, 6) void tailp_kernel(const unsigned ch
     // Later layers get higher issue priority: they are the younger waves of
     // the workgroup and lose VALU arbitration on age (MI355X_MICROARCH.md, two
     // waves per SIMD), while the step waits for the slowest role (-1.5 %).
+    // (Pairing the roles so that waves w and w + 4, which share a SIMD, carry
+    // equal MFMA counts measured the same: the step is latency-bound.)
     if (w >= 5) __builtin_amdgcn_s_setprio(3);
     else if (w >= 3) __builtin_amdgcn_s_setprio(2);
     else if (w >= 1) __builtin_amdgcn_s_setprio(1);
@@ -508,14 +517,15 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
     dense_conv3(d[6], s.wo, 4, 8, 1);
     const int nrows[tp::kLayers] = {32, 32, 32, 32, 32, 32, 4};
     for (int l = 0; l < tp::kLayers; ++l)
-        for (int row = 0; row < 32; ++row)
+        for (int R = 0; R < 32; ++R)  // MFMA row R computes dense row prow(l, R)
             for (int dq = -1; dq <= 1; ++dq)
                 for (int in = 0; in < 32; ++in) {
+                    const int row = tp::prow(l, R);
                     if (d[l].at(row, dq, in) == 0.f) continue;
                     bool missing = row < nrows[l];
-                    for (int kb = 0; missing && kb < tp::nkb(l); ++kb)
+                    for (int kb = 0; missing && kb < tp::nkbm(l, R / 16); ++kb)
                         for (int g = 0; g < 4; ++g) {
-                            const tp::Slot sl = tp::kslot(l, row / 16, kb, g);
+                            const tp::Slot sl = tp::kslot(l, R / 16, kb, g);
                             if (sl.dq == dq && sl.oct == in / 8) missing = false;
                         }
                     if (missing) return false;  // a non-zero weight that no slot reads
@@ -523,10 +533,10 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
     wout->assign((size_t)tp::kUnits * 2 * 64 * 8, 0);
     for (int l = 0; l < tp::kLayers; ++l)
         for (int mb = 0; mb < tp::nmb(l); ++mb)
-            for (int kb = 0; kb < tp::nkb(l); ++kb) {
+            for (int kb = 0; kb < tp::nkbm(l, mb); ++kb) {
                 const int u = tp::unit0(l) + mb * tp::nkb(l) + kb;
                 for (int lane = 0; lane < 64; ++lane) {
-                    const int row = mb * 16 + (lane & 15), g = lane >> 4;
+                    const int row = tp::prow(l, mb * 16 + (lane & 15)), g = lane >> 4;
                     const tp::Slot sl = tp::kslot(l, mb, kb, g);
                     // a (dq, octet) the m-block already reads in an earlier slot gets zeros
                     bool dup = false;
@@ -545,7 +555,7 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
     const float* bsrc[tp::kLayers] = {s.bt3, s.b31, s.b32, s.bt4, s.b41, s.b42, s.bo};
     const int cper[tp::kLayers] = {16, 16, 16, 8, 8, 8, 1};
     for (int l = 0; l < tp::kLayers; ++l)
-        for (int row = 0; row < nrows[l]; ++row) (*bout)[l * 32 + row] = bsrc[l][row % cper[l]];
+        for (int R = 0; R < nrows[l]; ++R) (*bout)[l * 32 + R] = bsrc[l][tp::prow(l, R) % cper[l]];
     return true;
 }
 
