@@ -37,6 +37,7 @@ extern "C" {
 #define M2_E_SHAPE (-2)       /* shape outside what the kernels support       */
 #define M2_E_WORKSPACE (-3)   /* workspace smaller than m2_workspace_bytes()  */
 #define M2_E_WEIGHTS (-4)     /* weight table incomplete                      */
+#define M2_E_INTERNAL (-5)    /* internal protocol failure (see m2_last_error) */
 
 /* M2TTSModel.__init__ hyper-parameters (tts_model.py:303-313), plus the
  * positional-encoding table length (TextEncoder max_seq_len, tts_model.py:29). */
@@ -100,6 +101,17 @@ int32_t m2_duration_predictor(const m2_model* model, const float* enc, int32_t B
 int32_t m2_length_regulator_count(const void* dur, int32_t dur_is_int, float scale,
                                   int32_t B, int32_t S, int32_t* out_cum, int32_t* out_T,
                                   int32_t* out_Tmax, void* stream);
+
+/* m2_length_regulator_count, plus the one host read the regulator needs
+ * (tts_model.py:163-166: the batch maximum sizes the output): also stores
+ * T_max into *host_Tmax (host memory) before returning, by a mailbox the
+ * count kernel posts to coherent host-mapped memory, polled by this call -
+ * in place of a device->host copy and a stream synchronisation.  Blocks the
+ * calling thread until the work queued on `stream` before it and the count
+ * kernel are done.  One calling thread per device. */
+int32_t m2_length_regulator_count_sync(const void* dur, int32_t dur_is_int, float scale,
+                                       int32_t B, int32_t S, int32_t* out_cum, int32_t* out_T,
+                                       int32_t* out_Tmax, int32_t* host_Tmax, void* stream);
 
 /* LengthRegulator.forward, expanding half (tts_model.py:146-178): frame t of
  * utterance b copies enc[b, s] for cum[b,s] <= t < cum[b,s+1]; frames past

@@ -127,10 +127,17 @@ __device__ __forceinline__ int frames_of(const void* dur, int is_int, float scal
     return v >= 1073741824.f ? 1073741824 : (int)v;               // int() truncates toward zero
 }
 
+// SYNC: no pre-zeroed Tmax / atomicMax: the last workgroup to finish (a
+// ticket counter, reset by that workgroup for the next call) reduces the
+// totals, stores Tmax and posts (seq, Tmax) to a host-mapped mailbox with
+// system-scope stores (Tmax first, then seq with release order), which the
+// host polls instead of a device->host copy and a stream synchronisation.
+template <bool SYNC>
 __global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ dur, int is_int,
                                                        float scale, int S, int32_t* __restrict__ cum,
                                                        int32_t* __restrict__ T,
-                                                       int32_t* __restrict__ Tmax) {
+                                                       int32_t* __restrict__ Tmax, unsigned* __restrict__ ticket,
+                                                       int32_t* __restrict__ mbox, int32_t seq) {
     __shared__ int part[256];
     const int b = blockIdx.x, tid = threadIdx.x;
     const int chunk = (S + 255) / 256;
@@ -154,9 +161,36 @@ __global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ 
         run += frames_of(dur, is_int, scale, base + s);
         c[s + 1] = run;
     }
-    if (tid == 255) {
-        T[b] = part[255];
-        atomicMax(Tmax, part[255]);
+    if constexpr (!SYNC) {
+        if (tid == 255) {
+            T[b] = part[255];
+            atomicMax(Tmax, part[255]);
+        }
+    } else {
+        __shared__ bool last;
+        if (tid == 255) {
+            __hip_atomic_store(T + b, part[255], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __atomic_thread_fence(__ATOMIC_RELEASE);  // totals before the ticket
+            last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last) {  // every other workgroup's total is visible
+            int m = 0;
+            for (int i = tid; i < (int)gridDim.x; i += 256)
+                m = max(m, __hip_atomic_load(T + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            part[tid] = m;
+            __syncthreads();
+            for (int off = 128; off > 0; off >>= 1) {
+                if (tid < off) part[tid] = max(part[tid], part[tid + off]);
+                __syncthreads();
+            }
+            if (tid == 0) {
+                *Tmax = part[0];
+                __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(mbox + 1, part[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(mbox, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
     }
 }
 
@@ -235,8 +269,16 @@ int32_t launch_lr_count(const void* dur, int is_int, float scale, int B, int S, 
                         int32_t* T, int32_t* Tmax, hipStream_t st) {
     M2_HIP(hipMemsetAsync(Tmax, 0, sizeof(int32_t), st));
     if (B == 0) return M2_OK;
-    hipLaunchKernelGGL(lr_count_kernel, dim3(B), dim3(256), 0, st, dur, is_int, scale, S, cum, T,
-                       Tmax);
+    hipLaunchKernelGGL(lr_count_kernel<false>, dim3(B), dim3(256), 0, st, dur, is_int, scale, S, cum, T,
+                       Tmax, nullptr, nullptr, 0);
+    M2_LAUNCHED("lr_count_kernel");
+    return M2_OK;
+}
+
+int32_t launch_lr_count_sync(const void* dur, int is_int, float scale, int B, int S, int32_t* cum, int32_t* T,
+                             int32_t* Tmax, unsigned* ticket, int32_t* mbox, int32_t seq, hipStream_t st) {
+    hipLaunchKernelGGL(lr_count_kernel<true>, dim3(B), dim3(256), 0, st, dur, is_int, scale, S, cum, T, Tmax,
+                       ticket, mbox, seq);
     M2_LAUNCHED("lr_count_kernel");
     return M2_OK;
 }

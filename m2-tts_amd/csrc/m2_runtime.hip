@@ -1,8 +1,12 @@
 // C-ABI runtime: weight table, model handle, stage orchestration.
 // See include/m2tts_hip.h for the contract of every entry point.
+#include <immintrin.h>
+
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -20,6 +24,8 @@ int32_t launch_linear(const float*, const float*, const float*, const float*, co
 int32_t launch_attention(const float*, const uint8_t*, int, int, int, int, float*, hipStream_t);
 int32_t launch_duration(const float*, int, int, int, const float* const*, float*, hipStream_t);
 int32_t launch_lr_count(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
+int32_t launch_lr_count_sync(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, unsigned*, int32_t*,
+                             int32_t, hipStream_t);
 int32_t launch_lr_expand(const float*, const int32_t*, int, int, int, int, float*, hipStream_t);
 int32_t launch_conv(const float*, const float*, const float*, const float*, const float*,
                     const float*, int, int, bool, int, int, int, int, float*, hipStream_t);
@@ -682,6 +688,86 @@ int32_t m2_length_regulator_count(const void* dur, int32_t dur_is_int, float sca
                                   void* stream) {
     M2_CHECK_ARG(dur && out_cum && out_T && out_Tmax && B >= 0 && S >= 0, "m2_length_regulator_count: bad argument");
     return launch_lr_count(dur, dur_is_int, scale, B, S, out_cum, out_T, out_Tmax, static_cast<hipStream_t>(stream));
+}
+
+// Per-device mailbox of m2_length_regulator_count_sync: [seq, Tmax] in
+// coherent host-mapped memory plus the count kernel's ticket counter.
+namespace {
+struct LrMailbox {
+    int32_t* host = nullptr;
+    int32_t* dev = nullptr;
+    unsigned* ticket = nullptr;
+    int32_t seq = 0;
+};
+constexpr int kMaxDevices = 64;
+std::mutex g_mb_mu;
+LrMailbox g_mb[kMaxDevices];
+
+int32_t mailbox_for(int dev, LrMailbox** out) {
+    LrMailbox& mb = g_mb[dev];
+    if (!mb.host) {
+        int cur = 0;
+        M2_HIP(hipGetDevice(&cur));
+        M2_HIP(hipSetDevice(dev));
+        void* h = nullptr;
+        hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
+        void* d = nullptr;
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
+        void* t = nullptr;
+        if (e == hipSuccess) e = hipMalloc(&t, sizeof(unsigned));
+        if (e == hipSuccess) e = hipMemset(t, 0, sizeof(unsigned));
+        (void)hipSetDevice(cur);
+        if (e != hipSuccess) return hip_status(e, "m2_length_regulator_count_sync: mailbox allocation");
+        std::memset(h, 0, 64);
+        mb.host = static_cast<int32_t*>(h);
+        mb.dev = static_cast<int32_t*>(d);
+        mb.ticket = static_cast<unsigned*>(t);
+    }
+    *out = &mb;
+    return M2_OK;
+}
+}  // namespace
+
+int32_t m2_length_regulator_count_sync(const void* dur, int32_t dur_is_int, float scale, int32_t B, int32_t S,
+                                       int32_t* out_cum, int32_t* out_T, int32_t* out_Tmax, int32_t* host_Tmax,
+                                       void* stream) {
+    M2_CHECK_ARG(out_Tmax && host_Tmax && B >= 0 && S >= 0, "m2_length_regulator_count_sync: bad argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (B == 0) {  // empty batch: the [0, ...] tensors have no storage
+        M2_HIP(hipMemsetAsync(out_Tmax, 0, sizeof(int32_t), st));
+        *host_Tmax = 0;
+        return M2_OK;
+    }
+    M2_CHECK_ARG(dur && out_cum && out_T, "m2_length_regulator_count_sync: bad argument");
+    int dev = 0;
+    if (st) M2_HIP(hipStreamGetDevice(st, &dev));
+    else M2_HIP(hipGetDevice(&dev));
+    M2_CHECK_ARG(dev >= 0 && dev < kMaxDevices, "m2_length_regulator_count_sync: device index");
+    std::lock_guard<std::mutex> lk(g_mb_mu);
+    LrMailbox* mb = nullptr;
+    int32_t rc = mailbox_for(dev, &mb);
+    if (rc) return rc;
+    mb->seq = mb->seq == INT_MAX ? 1 : mb->seq + 1;
+    const int32_t seq = mb->seq;
+    if ((rc = launch_lr_count_sync(dur, dur_is_int, scale, B, S, out_cum, out_T, out_Tmax, mb->ticket, mb->dev, seq,
+                                   st)))
+        return rc;
+    // Spin on the mailbox; every 1024 polls ask the stream whether it failed
+    // (or finished without posting, which would be a bug).
+    for (unsigned i = 1;; ++i) {
+        if (__atomic_load_n(mb->host, __ATOMIC_ACQUIRE) == seq) break;
+        if ((i & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(mb->host, __ATOMIC_ACQUIRE) == seq) break;
+                return fail(M2_E_INTERNAL, "m2_length_regulator_count_sync: stream idle but T_max not posted");
+            }
+            if (e != hipErrorNotReady) return hip_status(e, "m2_length_regulator_count_sync");
+        }
+        _mm_pause();
+    }
+    *host_Tmax = __atomic_load_n(mb->host + 1, __ATOMIC_RELAXED);
+    return M2_OK;
 }
 
 int32_t m2_length_regulator_expand(const float* enc, const int32_t* cum, int32_t B, int32_t S,

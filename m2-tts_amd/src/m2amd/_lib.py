@@ -41,6 +41,7 @@ _SIGNATURES = {
     "m2_text_encoder": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_size, c_vp]),
     "m2_duration_predictor": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
     "m2_length_regulator_count": (c_i32, [c_vp, c_i32, c_f32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "m2_length_regulator_count_sync": (c_i32, [c_vp, c_i32, c_f32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "m2_length_regulator_expand": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "m2_mel_decoder": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
     "m2_vocoder": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),

@@ -6,6 +6,7 @@ stream.  Nothing here computes on the CPU: a CPU tensor is an error.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Optional
 
@@ -157,6 +158,23 @@ def frame_counts(durations: Tensor, scale: float = 1.0):
     return cum, tot, tmax
 
 
+def frame_counts_sync(durations: Tensor, scale: float = 1.0):
+    """frame_counts plus the host read of T_max (m2_length_regulator_count_sync:
+    a host-mapped mailbox the count kernel posts to, polled in C with the GIL
+    released): returns (cum, T, Tmax device tensors, Tmax as an int)."""
+    require_device(durations, what="length_regulator")
+    B, S = durations.shape
+    d, is_int = durations_for_regulator(durations)
+    dev = durations.device
+    cum = torch.empty(B, S + 1, device=dev, dtype=torch.int32)
+    tot = torch.empty(B, device=dev, dtype=torch.int32)
+    tmax = torch.empty(1, device=dev, dtype=torch.int32)
+    host = ctypes.c_int32(0)
+    _lib.call("m2_length_regulator_count_sync", _ptr(d), is_int, float(scale), B, S, _ptr(cum), _ptr(tot), _ptr(tmax),
+              ctypes.addressof(host), stream_handle(dev))
+    return cum, tot, tmax, int(host.value)
+
+
 def expand_frames(enc: Tensor, cum: Tensor, T_out: int) -> Tensor:
     """Expanding half (m2_length_regulator_expand): [B,S,H] -> [B,T_out,H]."""
     enc = f32c(enc)
@@ -172,11 +190,12 @@ def regulate(enc: Tensor, durations: Tensor, max_length: Optional[int] = None, s
     One device->host read of the batch maximum frame count, only when
     max_length is not given (it sizes the output)."""
     require_device(enc, durations, what="length_regulator")
-    cum, _, tmax = frame_counts(durations, scale)
-    if max_length is None:
-        # an utterance with no frames becomes one zero frame (tts_model.py:158-160)
-        max_length = max(1, int(tmax.item()))
-    return expand_frames(enc, cum, max_length)
+    if max_length is not None:
+        cum, _, _ = frame_counts(durations, scale)
+        return expand_frames(enc, cum, max_length)
+    cum, _, _, t_max = frame_counts_sync(durations, scale)
+    # an utterance with no frames becomes one zero frame (tts_model.py:158-160)
+    return expand_frames(enc, cum, max(1, t_max))
 
 
 def batchnorm_eval_affine(weight: Tensor, bias: Tensor, mean: Tensor, var: Tensor, eps: float):

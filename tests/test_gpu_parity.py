@@ -391,3 +391,36 @@ def test_profile_events_strided(gpu):
     assert n.value == 3 * nk
     assert all(v > 0 for v in ms[2::nk]) and all(v < 0 for i, v in enumerate(ms) if i % nk != 2)
     assert lib.m2_profile_stride(h, 0) != 0  # bad stride is an error, not a crash
+
+
+@pytest.mark.parametrize("B,S", [(1, 7), (3, 100), (300, 40)])
+def test_frame_counts_sync_mailbox(gpu, B, S):
+    """m2_length_regulator_count_sync (the host-mapped T_max mailbox) against
+    the plain count kernel and the reference's int(d.item()) loop (oracle),
+    over repeated calls (the mailbox sequence and the ticket reset), B > 256
+    (the last workgroup's reduction loop), zero / negative / fractional
+    durations and a duration scale."""
+    from m2amd import ops
+    g = torch.Generator().manual_seed(B * 1000 + S)
+    for it in range(3):
+        d = (torch.rand(B, S, generator=g) * 12 - 2).to(torch.float32)
+        if it == 1:
+            d[0] = 0.0  # an utterance with no frames
+        scale = 1.0 if it < 2 else 1.3
+        dg = d.to(gpu)
+        cum, tot, tmax, t_host = ops.frame_counts_sync(dg, scale)
+        cum0, tot0, tmax0 = ops.frame_counts(dg, scale)
+        assert torch.equal(cum, cum0) and torch.equal(tot, tot0)
+        assert int(tmax.item()) == int(tmax0.item()) == t_host
+        n = [[max(0, int(float(np.float32(v) * np.float32(scale)))) for v in row] for row in d.numpy()]
+        assert t_host == max(sum(r) for r in n)
+        enc = torch.randn(B, S, 8, generator=g)
+        ref = orc.length_regulator(enc, d * scale if scale != 1.0 else d)
+        out = ops.regulate(enc.to(gpu), dg, None, scale=scale)
+        assert out.shape == ref.shape and torch.equal(out.cpu(), ref)
+
+
+def test_frame_counts_sync_empty_batch(gpu):
+    from m2amd import ops
+    cum, tot, tmax, t_host = ops.frame_counts_sync(torch.zeros(0, 5, device=gpu), 1.0)
+    assert t_host == 0 and int(tmax.item()) == 0
