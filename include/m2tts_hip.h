@@ -134,6 +134,41 @@ int32_t m2_vocoder(const m2_model* model, const float* mel, int32_t mel_layout, 
                    int32_t T, float* out_audio, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* ---- whole-inference entry points (M2TTSModel.inference, tts_model.py:402-438)
+ * Two calls split at the one host read the path needs (T_max sizes the
+ * outputs), so a step costs two host->library crossings instead of six:
+ *   m2_inference_front: text encoder (+ padding mask when lengths != NULL),
+ *     duration predictor, frame counts; blocks until T_max is posted
+ *     (as m2_length_regulator_count_sync) and stores it in *host_Tmax.
+ *   m2_inference_back: length-regulator expansion to T frames (the caller
+ *     passes max(1, T_max), tts_model.py:158-160), mel decoder, vocoder.
+ *     out_mel [B,T,M], out_audio [B,1,64T].
+ * `front` (m2_front_bytes(B,S)) carries the encoder output, durations and
+ * frame counts from the first call to the second; `workspace` is sized by
+ * m2_inference_workspace_bytes(B,S,T) (T = 0 for the front call). */
+size_t m2_front_bytes(const m2_model* model, int32_t B, int32_t S);
+size_t m2_inference_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T);
+int32_t m2_inference_front(const m2_model* model, const int64_t* ids, const int64_t* lengths,
+                           int32_t B, int32_t S, float scale, void* front, size_t front_bytes,
+                           void* workspace, size_t workspace_bytes, int32_t* host_Tmax,
+                           void* stream);
+int32_t m2_inference_back(const m2_model* model, int32_t B, int32_t S, int32_t T,
+                          const void* front, size_t front_bytes, float* out_mel,
+                          float* out_audio, void* workspace, size_t workspace_bytes,
+                          void* stream);
+
+/* Both halves in ONE call when the outputs fit: after T = max(1, T_max) is
+ * known, the back half runs straight away if mel_buf (mel_cap floats) holds
+ * B*T*M, audio_buf (audio_cap floats) holds B*64*T and the workspace holds
+ * m2_inference_workspace_bytes(B,S,T); the outputs are written contiguously
+ * from the start of the buffers ([B,T,M] and [B,1,64T]) and *launched = 1.
+ * Otherwise *launched = 0 and the caller allocates for *host_T and calls
+ * m2_inference_back (the front buffer holds the hand-off). */
+int32_t m2_inference(const m2_model* model, const int64_t* ids, const int64_t* lengths, int32_t B,
+                     int32_t S, float scale, void* front, size_t front_bytes, void* workspace,
+                     size_t workspace_bytes, float* mel_buf, size_t mel_cap, float* audio_buf,
+                     size_t audio_cap, int32_t* host_T, int32_t* launched, void* stream);
+
 /* ---- kernel-level entry points (for the components API and tests) ---------*/
 
 /* LightweightResBlock.forward (components.py:196-200) of vocoder stage k

@@ -228,6 +228,25 @@ void carve_voc(A& a, const m2_config& c, int B, int T, float** bufs) {
     }
 }
 
+// Stage hand-off of m2_inference_front -> m2_inference_back: the encoder
+// output, durations, frame prefix sums / totals / maximum and the padding mask.
+struct FrontBufs {
+    float *enc, *dur;
+    int32_t *cum, *tot, *tmax;
+    uint8_t* mask;
+};
+
+template <typename A>
+void carve_front(A& a, int B, int S, int H, FrontBufs* out) {
+    float* enc = a.template take<float>((size_t)B * S * H);
+    float* dur = a.template take<float>((size_t)B * S);
+    int32_t* cum = a.template take<int32_t>((size_t)B * (S + 1));
+    int32_t* tot = a.template take<int32_t>((size_t)B);
+    int32_t* tmax = a.template take<int32_t>(1);
+    uint8_t* mask = a.template take<uint8_t>((size_t)B * S);
+    if (out) *out = FrontBufs{enc, dur, cum, tot, tmax, mask};
+}
+
 // One pre-LN transformer layer (components.py:131-140), x updated in place;
 // for the first decoder layer the residual source is the caller's input.
 int32_t run_layer(const m2_model* m, const m2_layer_w& L, const float* x_in, float* x, TfBufs& wb,
@@ -914,6 +933,92 @@ const char* m2_profile_kernel_name_for(const m2_model* m, int32_t index) {
     if (m->tailp && index == 2) return kVocTailpKernelName;
     if (m->midp && index == 1) return kVocMidpKernelName;
     return m->x3 ? kVocX3KernelNames[index] : kVocKernelNames[index];
+}
+
+size_t m2_front_bytes(const m2_model* model, int32_t B, int32_t S) {
+    if (!model || B < 0 || S < 0) return 0;
+    Sizer a;
+    carve_front(a, B, S, model->cfg.hidden_dim, nullptr);
+    return a.off + 256;
+}
+
+int32_t m2_inference_front(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S,
+                           float scale, void* front, size_t front_bytes, void* workspace, size_t workspace_bytes,
+                           int32_t* host_Tmax, void* stream) {
+    M2_CHECK_ARG(m && host_Tmax && B >= 0 && S >= 0, "m2_inference_front: bad argument");
+    M2_CHECK_ARG(ids || B * S == 0, "m2_inference_front: null ids");
+    Carve a(front, front_bytes);
+    FrontBufs f;
+    carve_front(a, B, S, m->cfg.hidden_dim, &f);
+    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_inference_front: front buffer too small");
+    int32_t rc;
+    if (B > 0 && S > 0) {
+        if ((rc = m2_text_encoder(m, ids, lengths, B, S, f.enc, lengths ? f.mask : nullptr, workspace,
+                                  workspace_bytes, stream)))
+            return rc;
+        if ((rc = m2_duration_predictor(m, f.enc, B, S, f.dur, nullptr, 0, stream))) return rc;
+    }
+    return m2_length_regulator_count_sync(f.dur, 0, scale, B, S, f.cum, f.tot, f.tmax, host_Tmax, stream);
+}
+
+int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, const void* front, size_t front_bytes,
+                          float* out_mel, float* out_audio, void* workspace, size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && B >= 0 && S >= 0 && T >= 0, "m2_inference_back: bad argument");
+    if (B == 0 || T == 0) return M2_OK;
+    M2_CHECK_ARG(out_mel && out_audio, "m2_inference_back: null output");
+    const int H = m->cfg.hidden_dim;
+    Carve a(const_cast<void*>(front), front_bytes);
+    FrontBufs f;
+    carve_front(a, B, S, H, &f);
+    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_inference_back: front buffer too small");
+    // the regulated frames live after the decoder / vocoder scratch
+    Carve w(workspace, workspace_bytes);
+    Sizer sz_tf, sz_voc;
+    carve_tf(sz_tf, B, T, H, nullptr);
+    carve_voc(sz_voc, m->cfg, B, T, nullptr);
+    const size_t scratch = std::max(sz_tf.off, sz_voc.off);
+    (void)w.take<char>(scratch);
+    float* reg = w.take<float>((size_t)B * T * H);
+    if (!w.ok) return fail(M2_E_WORKSPACE, "m2_inference_back: workspace too small");
+    int32_t rc;
+    if ((rc = m2_length_regulator_expand(f.enc, f.cum, B, S, H, T, reg, stream))) return rc;
+    if ((rc = m2_mel_decoder(m, reg, B, T, out_mel, workspace, scratch, stream))) return rc;
+    return m2_vocoder(m, out_mel, 1, B, T, out_audio, workspace, scratch, stream);
+}
+
+int32_t m2_inference(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S, float scale,
+                     void* front, size_t front_bytes, void* workspace, size_t workspace_bytes, float* mel_buf,
+                     size_t mel_cap, float* audio_buf, size_t audio_cap, int32_t* host_T, int32_t* launched,
+                     void* stream) {
+    M2_CHECK_ARG(m && host_T && launched, "m2_inference: bad argument");
+    *launched = 0;
+    int32_t tmax = 0, rc;
+    if ((rc = m2_inference_front(m, ids, lengths, B, S, scale, front, front_bytes, workspace, workspace_bytes, &tmax,
+                                 stream)))
+        return rc;
+    const int32_t T = std::max(1, tmax);  // tts_model.py:158-160
+    *host_T = T;
+    const size_t need_mel = (size_t)B * T * m->cfg.mel_channels, need_audio = (size_t)B * 64 * T;
+    if (!mel_buf || !audio_buf || need_mel > mel_cap || need_audio > audio_cap ||
+        m2_inference_workspace_bytes(m, B, S, T) > workspace_bytes)
+        return M2_OK;  // the caller allocates for T and calls m2_inference_back
+    if ((rc = m2_inference_back(m, B, S, T, front, front_bytes, mel_buf, audio_buf, workspace, workspace_bytes,
+                                stream)))
+        return rc;
+    *launched = 1;
+    return M2_OK;
+}
+
+size_t m2_inference_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T) {
+    if (!model || B < 0 || S < 0 || T < 0) return 0;
+    const int H = model->cfg.hidden_dim;
+    Sizer a, b, c, d;
+    carve_tf(a, B, S, H, nullptr);
+    carve_tf(b, B, T, H, nullptr);
+    carve_voc(c, model->cfg, B, T, nullptr);
+    d.off = std::max(b.off, c.off);
+    (void)d.take<float>((size_t)B * T * H);
+    return std::max(a.off, d.off) + 256;
 }
 
 int32_t m2_vocoder_path(const m2_model* m) {

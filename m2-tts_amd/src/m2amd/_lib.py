@@ -63,6 +63,12 @@ _SIGNATURES = {
     "m2_profile_select": (c_i32, [c_vp, ctypes.c_uint32]),
     "m2_profile_stride": (c_i32, [c_vp, c_i32]),
     "m2_vocoder_path": (c_i32, [c_vp]),
+    "m2_front_bytes": (c_size, [c_vp, c_i32, c_i32]),
+    "m2_inference_workspace_bytes": (c_size, [c_vp, c_i32, c_i32, c_i32]),
+    "m2_inference_front": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, c_vp, c_size, c_vp, c_vp]),
+    "m2_inference": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, c_vp, c_size, c_vp, c_size, c_vp,
+                             c_size, c_vp, c_vp, c_vp]),
+    "m2_inference_back": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_size, c_vp, c_vp, c_vp, c_size, c_vp]),
 }
 
 # act codes (m2_common.h Act)

@@ -93,14 +93,77 @@ class HipModel:
                                            ctypes.byref(handle)), "m2_model_create")
         self.handle = handle
         self._ws: Optional[Tensor] = None
+        self._front: Optional[Tensor] = None
+        self._sizes: Dict[Tuple, int] = {}
+        self._tcap: Dict[Tuple[int, int], int] = {}
         self._finalizer = weakref.finalize(self, lib.m2_model_destroy, handle)
 
     # ------------------------------------------------------------------ scratch
     def workspace(self, B: int, S: int, T: int) -> Tensor:
-        need = int(_lib.load().m2_workspace_bytes(self.handle, B, S, T))
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=self.device)
-        return self._ws
+        return self._scratch("_ws", self._size("m2_workspace_bytes", B, S, T))
+
+    def _size(self, fn: str, *args) -> int:
+        key = (fn,) + args
+        n = self._sizes.get(key)
+        if n is None:
+            n = self._sizes[key] = int(getattr(_lib.load(), fn)(self.handle, *args))
+        return n
+
+    def _scratch(self, attr: str, need: int) -> Tensor:
+        buf = getattr(self, attr)
+        if buf is None or buf.numel() < need:
+            buf = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=self.device)
+            setattr(self, attr, buf)
+        return buf
+
+    # ------------------------------------------------------------------ whole path
+    def inference(self, ids: Tensor, lengths: Optional[Tensor], scale: float) -> Tuple[Tensor, Tensor]:
+        """M2TTSModel.inference (tts_model.py:402-438), normally ONE library call
+        (m2_inference): encoder, durations, frame counts, the T_max read, then
+        expansion, decoder and vocoder enqueued from C right after the read.
+
+        The outputs are allocated before T is known, for a frame capacity per
+        (B, S) learnt from earlier calls (T rounded up to 32 frames; shrunk
+        when T falls under half of it); the result is the contiguous [B,T,M] /
+        [B,1,64T] prefix of those buffers.  A call whose T exceeds the capacity
+        allocates exactly and finishes with m2_inference_back."""
+        require_device(ids, lengths, what="M2TTSModel")
+        if ids.dtype != torch.int64 or not ids.is_contiguous():
+            ids = ids.to(torch.int64).contiguous()
+        B, S = ids.shape
+        if S > self.cfg.max_positions:
+            raise RuntimeError(f"sequence length {S} exceeds the positional table ({self.cfg.max_positions})")
+        lens = None
+        if lengths is not None:
+            lens = lengths if lengths.dtype == torch.int64 and lengths.is_contiguous() else \
+                lengths.to(torch.int64).contiguous()
+        lib = _lib.load()
+        st = stream_handle(self.device)
+        M, dev, f32 = self.M, self.device, torch.float32
+        cap = self._tcap.get((B, S), 0)
+        front = self._scratch("_front", self._size("m2_front_bytes", B, S))
+        ws = self._scratch("_ws", self._size("m2_inference_workspace_bytes", B, S, cap))
+        mel_buf = torch.empty(B * cap * M, device=dev, dtype=f32)
+        audio_buf = torch.empty(B * 64 * cap, device=dev, dtype=f32)
+        T = ctypes.c_int32(0)
+        done = ctypes.c_int32(0)
+        _lib.check(lib.m2_inference(self.handle, ids.data_ptr(), None if lens is None else lens.data_ptr(), B, S,
+                                    float(scale), front.data_ptr(), front.numel(), ws.data_ptr(), ws.numel(),
+                                    mel_buf.data_ptr(), mel_buf.numel(), audio_buf.data_ptr(), audio_buf.numel(),
+                                    ctypes.byref(T), ctypes.byref(done), st), "m2_inference")
+        T = T.value
+        if done.value:
+            mel = mel_buf[:B * T * M].view(B, T, M)
+            audio = audio_buf[:B * 64 * T].view(B, 1, 64 * T)
+        else:
+            mel = torch.empty(B, T, M, device=dev, dtype=f32)
+            audio = torch.empty(B, 1, 64 * T, device=dev, dtype=f32)
+            ws = self._scratch("_ws", self._size("m2_inference_workspace_bytes", B, S, T))
+            _lib.check(lib.m2_inference_back(self.handle, B, S, T, front.data_ptr(), front.numel(), mel.data_ptr(),
+                                             audio.data_ptr(), ws.data_ptr(), ws.numel(), st), "m2_inference_back")
+        if T > cap or 2 * T < cap:
+            self._tcap[(B, S)] = (T + 31) // 32 * 32
+        return mel, audio
 
     # ------------------------------------------------------------------ stages
     def text_encoder(self, ids: Tensor, lengths: Optional[Tensor]):

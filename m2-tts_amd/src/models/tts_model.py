@@ -28,7 +28,7 @@ from typing import Any, Dict, Optional, Tuple
 import torch
 import torch.nn as nn
 
-from m2amd import ops
+from m2amd import ops, runtime
 from m2amd.runtime import HandleCache, make_config
 
 from .components import (LightweightResBlock, PositionalEncoding, TransformerEncoderLayer, VariancePredictor,
@@ -187,6 +187,19 @@ class M2TTSModel(nn.Module):
                     f"{total * 4 / (1024 * 1024):.1f} MB fp32")
 
     # -------------------------------------------------------------- handle
+    def _eval_if_training(self):
+        """self.eval() (tts_model.py:404) without the recursive train(False)
+        walk when every module is already in eval mode (~35 us of host time per
+        call at stage1, more than the length regulator's GPU time)."""
+        mods = self.__dict__.get("_m2_modules")
+        if mods is None or mods[0] != runtime._GEN[0]:
+            mods = (runtime._GEN[0], list(self.modules()))
+            self.__dict__["_m2_modules"] = mods
+        for mod in mods[1]:
+            if mod.training:
+                self.eval()
+                return
+
     def _hip(self, device: torch.device):
         cache = _HANDLES.get(self)
         if cache is None:
@@ -214,15 +227,10 @@ class M2TTSModel(nn.Module):
     def inference(self, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor] = None,
                   duration_scale: float = 1.0) -> Tuple[Tensor, Tensor]:
         """(mel [B,T,M], audio [B,1,64T]) - reference tts_model.py:402-438."""
-        self.eval()
+        self._eval_if_training()
         ops.require_device(phoneme_ids, what="M2TTSModel")
         with torch.no_grad():
-            hm = self._hip(phoneme_ids.device)
-            enc, _ = hm.text_encoder(phoneme_ids, phoneme_lengths)
-            dur = hm.duration(enc)
-            reg = ops.regulate(enc, dur, None, scale=duration_scale)
-            mel = hm.decoder(reg)
-            audio = hm.vocoder(mel, layout_btm=True)
+            mel, audio = self._hip(phoneme_ids.device).inference(phoneme_ids, phoneme_lengths, duration_scale)
         return mel, audio
 
     def get_model_size(self) -> Dict[str, Any]:

@@ -424,3 +424,50 @@ def test_frame_counts_sync_empty_batch(gpu):
     from m2amd import ops
     cum, tot, tmax, t_host = ops.frame_counts_sync(torch.zeros(0, 5, device=gpu), 1.0)
     assert t_host == 0 and int(tmax.item()) == 0
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_inference_single_call_capacity(gpu, stage):
+    """M2TTSModel.inference through m2_inference: the first call for a (B, S)
+    has no frame capacity (front call + m2_inference_back), later calls with
+    the same or fewer frames run in one call into capacity-sized buffers, a
+    longer request (duration_scale) overflows the capacity and falls back.
+    Every result matches the fixtures and the staged six-call path bit for bit,
+    and earlier results are not overwritten by later calls."""
+    from m2amd import ops
+    gs, gc = golden(f"{stage}_small"), golden(f"{stage}_scale")
+    m = build_model(stage, gpu)
+    g = gs
+    ids, lens = _ids(g, gpu)
+    hm = m._hip(gpu)
+
+    def staged(scale):
+        enc, _ = hm.text_encoder(ids, lens)
+        reg = ops.regulate(enc, hm.duration(enc), None, scale=scale)
+        mel = hm.decoder(reg)
+        return mel, hm.vocoder(mel, layout_btm=True)
+
+    plan = [(g, 1.0), (g, 1.0), (gc, float(gc["duration_scale"])), (g, 1.0), (gc, float(gc["duration_scale"]))]
+    kept = []
+    for fx, scale in plan:
+        fids, flens = _ids(fx, gpu)
+        assert torch.equal(fids, ids) and torch.equal(flens, lens)
+        mel, audio = m.inference(ids, lens, duration_scale=scale)
+        assert mel.is_contiguous() and audio.is_contiguous()
+        assert mel.shape == tuple(fx["mel"].shape) and audio.shape == tuple(fx["audio"].shape)
+        assert maxabs(mel, fx["mel"]) <= MEL_MAXABS_TOL
+        assert rms(audio, fx["audio"]) <= AUDIO_RMS_TOL
+        smel, saudio = staged(scale)
+        assert torch.equal(mel, smel) and torch.equal(audio, saudio)
+        kept.append((mel, audio, mel.clone(), audio.clone()))
+    for mel, audio, mel0, audio0 in kept:
+        assert torch.equal(mel, mel0) and torch.equal(audio, audio0)
+    caps = hm._tcap[tuple(ids.shape)]
+    assert caps >= max(k[0].shape[1] for k in kept)
+
+
+def test_inference_single_call_empty(gpu):
+    """B = 0 and all-zero durations (one zero frame) through m2_inference."""
+    m = build_model("s1", gpu)
+    mel, audio = m.inference(torch.zeros(0, 7, dtype=torch.long, device=gpu))
+    assert mel.shape == (0, 1, stage_config("s1").mel_channels) and audio.shape == (0, 1, 64)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Host-side time of one pipeline step (M2TTSModel.inference, B=32 S=100),
-split at the T_max read: enqueue before it, the wait inside it, enqueue after.
+split at the T_max read: enqueue before it, the wait inside it, enqueue after;
+then the staged path against M2TTSModel.inference (two library calls).
     python tools/probe/host_phases.py
 """
 import sys
@@ -61,28 +62,30 @@ for _ in range(300):
 torch.cuda.synchronize()
 print(f"inference() {(time.perf_counter() - t0) / 300 * 1e6:.1f} us/step")
 
-# A/B in one process: regulate through .item() vs the mailbox, alternated
-new_regulate = ops.regulate
+# A/B in one process: six stage calls from Python (the staged path above) vs
+# the two-call m2_inference_front / m2_inference_back path, alternated
 
 
-def old_regulate(enc, durations, max_length=None, scale=1.0):
-    cum, _, tmax = ops.frame_counts(durations, scale)
-    if max_length is None:
-        max_length = max(1, int(tmax.item()))
-    return ops.expand_frames(enc, cum, max_length)
+def staged(ids, lens):
+    with torch.no_grad():
+        hm = model._hip(dev)
+        enc, _ = hm.text_encoder(ids, lens)
+        dur = hm.duration(enc)
+        reg = ops.regulate(enc, dur, None)
+        mel = hm.decoder(reg)
+        return mel, hm.vocoder(mel, layout_btm=True)
 
 
-res = {"item": [], "mailbox": []}
+res = {"staged": [], "front_back": []}
 for rep in range(6):
-    for name, fn in (("item", old_regulate), ("mailbox", new_regulate)):
-        ops.regulate = fn
+    for name, fn in (("staged", staged), ("front_back", model.inference)):
         for _ in range(50):
-            model.inference(ids, lens)
+            fn(ids, lens)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(300):
-            model.inference(ids, lens)
+            fn(ids, lens)
         torch.cuda.synchronize()
         res[name].append((time.perf_counter() - t0) / 300 * 1e6)
 for k, v in res.items():
-    print(f"inference() via {k:8s}: " + " ".join(f"{x:.1f}" for x in v))
+    print(f"inference() via {k:10s}: " + " ".join(f"{x:.1f}" for x in v))
