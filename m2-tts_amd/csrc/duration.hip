@@ -17,22 +17,39 @@
 namespace m2 {
 
 // ---------------------------------------------------------------------------
-// One workgroup (4 waves) per (utterance, 30-phoneme tile).  Both k=3 convs
-// are GEMMs on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32): rows = 32
-// positions (two 16-row blocks), columns = 16 output channels per wave
-// (n-blocks nb = wave, wave+4, ...), K = (tap, channel) = 3H.  A = activation
-// rows in LDS (stride H+2: a ds_read_b32 half-wave of 16 rows x 2 k-lanes hits
-// 32 banks), B = conv weights packed in B-fragment order (m2_model_create;
-// L2-resident).  conv1 covers positions [s0-1, s0+31) so conv2 can produce
-// [s0, s0+30) (30 of its 32 rows; outside [0,S) conv1 stores the zero padding
-// conv2 sees).  Epilogue: +bias, BatchNorm (alpha = gamma/sqrt(var+eps),
-// beta' = beta - mean*alpha, the inference form PyTorch's CPU batch_norm
-// evaluates), ReLU.  Then the k=1 projection (one wave per phoneme) and
-// softplus.  The encoder output is read in its [B,S,H] layout (the
-// reference's transpose(1,2) is a view).
-constexpr int DUR_TS = 30;
+// One workgroup (8 waves) per (utterance, 14-phoneme tile): 8 x 32 = 256
+// workgroups at B=32, S=100, one per CU.  Both k=3 convs are GEMMs on the
+// exact-f32 MFMA (v_mfma_f32_16x16x4_f32): rows = 16 positions (one 16-row
+// block), columns = 16 output channels per wave (n-block nb = wave; H=128
+// has 8), K = (tap, channel) = 3H.  A = activation rows in LDS (stride H+2:
+// a ds_read_b32 half-wave of 16 rows x 2 k-lanes hits 32 banks), B = conv
+// weights packed in B-fragment order (m2_model_create; L2-resident).  conv1
+// covers positions [s0-1, s0+15) so conv2 can produce [s0, s0+14) (14 of its
+// 16 rows; outside [0,S) conv1 stores the zero padding conv2 sees).
+// Epilogue: +bias, BatchNorm (alpha = gamma/sqrt(var+eps), beta' = beta -
+// mean*alpha, the inference form PyTorch's CPU batch_norm evaluates), ReLU.
+// Then the k=1 projection (one wave per phoneme) and softplus.  The encoder
+// output is read in its [B,S,H] layout (the reference's transpose(1,2) is a
+// view).  (Was 4 waves x 30-phoneme tiles, two row blocks per wave: 128
+// workgroups with 2x longer per-wave MFMA chains, 15.5 us at B=32.)
+constexpr int DUR_TS = 14;
+constexpr int DUR_WAVES = 8;
 
 typedef float dur_f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int frames_from(float d, float scale) {
+    const float v = d * scale;                       // fp32 product, as dur*scale
+    if (!(v >= 1.0f)) return 0;                      // also NaN -> 0
+    return v >= 1073741824.f ? 1073741824 : (int)v;  // int() truncates toward zero
+}
+
+__device__ __forceinline__ int frames_of(const void* dur, int is_int, float scale, size_t i) {
+    if (is_int) {
+        const int v = static_cast<const int32_t*>(dur)[i];
+        return v > 0 ? v : 0;
+    }
+    return frames_from(static_cast<const float*>(dur)[i], scale);
+}
 
 template <int H>
 __device__ __forceinline__ void dur_conv_mfma(const float* in, const float4* __restrict__ Wp,
@@ -40,59 +57,53 @@ __device__ __forceinline__ void dur_conv_mfma(const float* in, const float4* __r
                                               const float* __restrict__ c, float* out, int pos0, int S) {
     constexpr int XS = H + 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-    for (int nb = wave; nb < H / 16; nb += 4) {
+    for (int nb = wave; nb < H / 16; nb += DUR_WAVES) {
         const float4* wp = Wp + (size_t)nb * (3 * H / 16) * 64 + lane;
-        dur_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+        dur_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int tap = 0; tap < 3; ++tap) {
             const float* x0 = in + (i + tap) * XS + g;
-            const float* x1 = x0 + 16 * XS;
 #pragma unroll
             for (int s4 = 0; s4 < H / 16; ++s4) {
                 const float4 w = wp[(tap * (H / 16) + s4) * 64];
                 const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int k = (4 * s4 + q) * 4;
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[k], wv[q], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[k], wv[q], acc1, 0, 0, 0);
-                }
+                for (int q = 0; q < 4; ++q)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[(4 * s4 + q) * 4], wv[q], acc, 0, 0, 0);
             }
         }
         const int co = nb * 16 + i;
         const float bb = b[co], aa = a[co], cc = c[co];
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = rb * 16 + 4 * g + r, s = pos0 + row;
-                float v = ((rb ? acc1[r] : acc0[r]) + bb) * aa + cc;
-                v = v > 0.f ? v : 0.f;
-                out[row * XS + co] = (s >= 0 && s < S) ? v : 0.f;
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * g + r, s = pos0 + row;
+            float v = (acc[r] + bb) * aa + cc;
+            v = v > 0.f ? v : 0.f;
+            out[row * XS + co] = (s >= 0 && s < S) ? v : 0.f;
+        }
     }
 }
 
 template <int H>
-__global__ __launch_bounds__(256) void duration_kernel(
+__global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ enc, int S, const float4* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ a1, const float* __restrict__ c1, const float4* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ a2, const float* __restrict__ c2,
     const float* __restrict__ pw, const float* __restrict__ pb, float* __restrict__ dur) {
-    constexpr int XS = H + 2;
-    __shared__ float X[34 * XS];   // positions s0-2 .. s0+31
-    __shared__ float Y1[34 * XS];  // s0-1 .. s0+30 (+2 spare rows read by conv2's unused rows)
-    __shared__ float Y2[32 * XS];  // s0 .. s0+29 (+2 unused)
+    constexpr int XS = H + 2, NT = 64 * DUR_WAVES;
+    __shared__ float X[18 * XS];   // positions s0-2 .. s0+15
+    __shared__ float Y1[18 * XS];  // s0-1 .. s0+14 (+2 zero rows read by conv2's unused rows)
+    __shared__ float Y2[16 * XS];  // s0 .. s0+13 (+2 unused)
     const int b = blockIdx.y, s0 = blockIdx.x * DUR_TS, tid = threadIdx.x;
     const float* e = enc + (size_t)b * S * H;
-    for (int idx = tid; idx < 34 * (H / 4); idx += 256) {
+    for (int idx = tid; idx < 18 * (H / 4); idx += NT) {
         const int p = idx / (H / 4), c4 = (idx - p * (H / 4)) * 4, s = s0 - 2 + p;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (s >= 0 && s < S) v = *reinterpret_cast<const float4*>(e + (size_t)s * H + c4);
         float* d = X + p * XS + c4;
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
-    for (int idx = tid; idx < 2 * XS; idx += 256) Y1[32 * XS + idx] = 0.f;
+    for (int idx = tid; idx < 2 * XS; idx += NT) Y1[16 * XS + idx] = 0.f;
     __syncthreads();
     dur_conv_mfma<H>(X, w1, b1, a1, c1, Y1, s0 - 1, S);
     __syncthreads();
@@ -100,7 +111,7 @@ __global__ __launch_bounds__(256) void duration_kernel(
     __syncthreads();
     // k=1 projection H -> 1: one wave per phoneme, shuffle reduction.
     const int lane = tid & 63, wave = tid >> 6;
-    for (int p = wave; p < DUR_TS; p += 4) {
+    for (int p = wave; p < DUR_TS; p += DUR_WAVES) {
         const int s = s0 + p;
         float acc = 0.f;
         for (int ci = lane; ci < H; ci += 64) acc = fmaf(pw[ci], Y2[p * XS + ci], acc);
@@ -108,7 +119,8 @@ __global__ __launch_bounds__(256) void duration_kernel(
         if (lane == 0 && s < S) {
             const float x = acc + pb[0];
             // F.softplus(beta=1, threshold=20)
-            dur[(size_t)b * S + s] = x > 20.f ? x : log1pf(expf(x));
+            const float d = x > 20.f ? x : log1pf(expf(x));
+            dur[(size_t)b * S + s] = d;
         }
     }
 }
@@ -117,15 +129,7 @@ __global__ __launch_bounds__(256) void duration_kernel(
 // One workgroup per utterance: n[s] = max(0, trunc(d[s]*scale)); exclusive
 // scan into cum[b, 0..S]; T[b] = cum[b,S]; atomicMax into Tmax (zeroed by the
 // launcher's memset node).
-__device__ __forceinline__ int frames_of(const void* dur, int is_int, float scale, size_t i) {
-    if (is_int) {
-        const int v = static_cast<const int32_t*>(dur)[i];
-        return v > 0 ? v : 0;
-    }
-    const float v = static_cast<const float*>(dur)[i] * scale;  // fp32 product, as dur*scale
-    if (!(v >= 1.0f)) return 0;                                   // also NaN -> 0
-    return v >= 1073741824.f ? 1073741824 : (int)v;               // int() truncates toward zero
-}
+
 
 // SYNC: no pre-zeroed Tmax / atomicMax: the last workgroup to finish (a
 // ticket counter, reset by that workgroup for the next call) reduces the
@@ -246,7 +250,7 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict_
 // p: w1 (packed), b1, alpha1, beta1, w2 (packed), b2, alpha2, beta2, proj_w, proj_b
 int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st) {
     if (B == 0 || S == 0) return M2_OK;
-    const dim3 grid(cdiv(S, DUR_TS), B), blk(256);
+    const dim3 grid(cdiv(S, DUR_TS), B), blk(64 * DUR_WAVES);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
 #define M2_DUR(HH)                                                                                              \
     case HH:                                                                                                    \

@@ -17,7 +17,8 @@
 namespace m2 {
 
 // ---- launchers defined in the kernel translation units ---------------------
-int32_t launch_embed_pe(const int64_t*, const float*, const float*, int, int, int, int, float*, hipStream_t);
+int32_t launch_embed_pe(const int64_t*, const float*, const float*, int, int, int, int, float*, const int64_t*,
+                        uint8_t*, hipStream_t);
 int32_t launch_layer_norm(const float*, const float*, const float*, int, int, float*, hipStream_t);
 int32_t launch_linear(const float*, const float*, const float*, const float*, const float*,
                       const float*, int, int, int, int, float*, hipStream_t);
@@ -683,12 +684,10 @@ int32_t m2_text_encoder(const m2_model* m, const int64_t* ids, const int64_t* le
     if (B == 0 || S == 0) return M2_OK;
     int32_t rc;
     const uint8_t* mask = nullptr;
-    if (lengths) {
-        uint8_t* mk = out_mask ? out_mask : wb.mask;
-        if ((rc = mask_kernel_launch(lengths, B, S, mk, st))) return rc;
-        mask = mk;
-    }
-    if ((rc = launch_embed_pe(ids, m->emb, m->pe, B, S, H, m->cfg.vocab_size, wb.x, st))) return rc;
+    if (lengths) mask = out_mask ? out_mask : wb.mask;  // written by the embedding launch
+    if ((rc = launch_embed_pe(ids, m->emb, m->pe, B, S, H, m->cfg.vocab_size, wb.x, lengths,
+                              const_cast<uint8_t*>(mask), st)))
+        return rc;
     for (const auto& L : m->enc)
         if ((rc = run_layer(m, L, wb.x, wb.x, wb, mask, B, S, st))) return rc;
     return launch_layer_norm(wb.x, m->enc_nw, m->enc_nb, B * S, H, out_enc, st);
@@ -745,6 +744,32 @@ int32_t mailbox_for(int dev, LrMailbox** out) {
     *out = &mb;
     return M2_OK;
 }
+
+// Spin on the mailbox until `seq` is posted; every 1024 polls ask the stream
+// whether it failed (or finished without posting, which would be a bug).
+int32_t mailbox_wait(const LrMailbox* mb, int32_t seq, hipStream_t st, int32_t* host_Tmax, const char* what) {
+    for (unsigned i = 1;; ++i) {
+        if (__atomic_load_n(mb->host, __ATOMIC_ACQUIRE) == seq) break;
+        if ((i & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(mb->host, __ATOMIC_ACQUIRE) == seq) break;
+                return fail(M2_E_INTERNAL, (std::string(what) + ": stream idle but T_max not posted").c_str());
+            }
+            if (e != hipErrorNotReady) return hip_status(e, what);
+        }
+        _mm_pause();
+    }
+    *host_Tmax = __atomic_load_n(mb->host + 1, __ATOMIC_RELAXED);
+    return M2_OK;
+}
+
+int32_t stream_device(hipStream_t st, int* dev) {
+    if (st) M2_HIP(hipStreamGetDevice(st, dev));
+    else M2_HIP(hipGetDevice(dev));
+    M2_CHECK_ARG(*dev >= 0 && *dev < kMaxDevices, "T_max mailbox: device index");
+    return M2_OK;
+}
 }  // namespace
 
 int32_t m2_length_regulator_count_sync(const void* dur, int32_t dur_is_int, float scale, int32_t B, int32_t S,
@@ -759,9 +784,8 @@ int32_t m2_length_regulator_count_sync(const void* dur, int32_t dur_is_int, floa
     }
     M2_CHECK_ARG(dur && out_cum && out_T, "m2_length_regulator_count_sync: bad argument");
     int dev = 0;
-    if (st) M2_HIP(hipStreamGetDevice(st, &dev));
-    else M2_HIP(hipGetDevice(&dev));
-    M2_CHECK_ARG(dev >= 0 && dev < kMaxDevices, "m2_length_regulator_count_sync: device index");
+    int32_t rc0 = stream_device(st, &dev);
+    if (rc0) return rc0;
     std::lock_guard<std::mutex> lk(g_mb_mu);
     LrMailbox* mb = nullptr;
     int32_t rc = mailbox_for(dev, &mb);
@@ -771,22 +795,7 @@ int32_t m2_length_regulator_count_sync(const void* dur, int32_t dur_is_int, floa
     if ((rc = launch_lr_count_sync(dur, dur_is_int, scale, B, S, out_cum, out_T, out_Tmax, mb->ticket, mb->dev, seq,
                                    st)))
         return rc;
-    // Spin on the mailbox; every 1024 polls ask the stream whether it failed
-    // (or finished without posting, which would be a bug).
-    for (unsigned i = 1;; ++i) {
-        if (__atomic_load_n(mb->host, __ATOMIC_ACQUIRE) == seq) break;
-        if ((i & 1023) == 0) {
-            const hipError_t e = hipStreamQuery(st);
-            if (e == hipSuccess) {
-                if (__atomic_load_n(mb->host, __ATOMIC_ACQUIRE) == seq) break;
-                return fail(M2_E_INTERNAL, "m2_length_regulator_count_sync: stream idle but T_max not posted");
-            }
-            if (e != hipErrorNotReady) return hip_status(e, "m2_length_regulator_count_sync");
-        }
-        _mm_pause();
-    }
-    *host_Tmax = __atomic_load_n(mb->host + 1, __ATOMIC_RELAXED);
-    return M2_OK;
+    return mailbox_wait(mb, seq, st, host_Tmax, "m2_length_regulator_count_sync");
 }
 
 int32_t m2_length_regulator_expand(const float* enc, const int32_t* cum, int32_t B, int32_t S,
@@ -958,6 +967,9 @@ int32_t m2_inference_front(const m2_model* m, const int64_t* ids, const int64_t*
             return rc;
         if ((rc = m2_duration_predictor(m, f.enc, B, S, f.dur, nullptr, 0, stream))) return rc;
     }
+    // A frame-count epilogue fused into the duration kernel (per-utterance
+    // tickets, one L2 write-back per workgroup) measured 5 us slower than
+    // this separate count kernel (tools/probe/count_fusion_ab.py, r17).
     return m2_length_regulator_count_sync(f.dur, 0, scale, B, S, f.cum, f.tot, f.tmax, host_Tmax, stream);
 }
 

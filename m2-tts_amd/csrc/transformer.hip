@@ -20,15 +20,21 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // ---------------------------------------------------------------------------
 // x[b,s,:] = E[ids[b,s],:] * sqrt(H) + pe[s,:]
 // Out-of-range ids read a zero row (the reference would raise in nn.Embedding).
+// With lengths != nullptr the same launch writes the padding mask
+// mask[b,s] = s < lengths[b] (components.py:236-240; the encoder's first
+// kernel, one launch fewer per inference).
 __global__ void embed_pe_kernel(const int64_t* __restrict__ ids, const float* __restrict__ emb,
                                 const float* __restrict__ pe, int R, int S, int H, int vocab,
-                                float emb_scale, float* __restrict__ out) {
+                                float emb_scale, float* __restrict__ out, const int64_t* __restrict__ lengths,
+                                uint8_t* __restrict__ mask) {
     const int total = R * H;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
         const int r = i / H, h = i - r * H;
         const int64_t id = ids[r];
         const float e = (id >= 0 && id < vocab) ? emb[id * H + h] : 0.f;
-        out[i] = e * emb_scale + pe[(r % S) * H + h];
+        const int s = r % S;
+        out[i] = e * emb_scale + pe[s * H + h];
+        if (lengths && h == 0) mask[r] = (int64_t)s < lengths[r / S] ? 1 : 0;
     }
 }
 
@@ -618,12 +624,12 @@ static int32_t launch_att_split(dim3 grid, const float* qkv, const uint8_t* mask
 // ---------------------------------------------------------------------------
 // Host launchers (used by the runtime and by the standalone C entry points).
 int32_t launch_embed_pe(const int64_t* ids, const float* emb, const float* pe, int B, int S, int H,
-                        int vocab, float* out, hipStream_t st) {
+                        int vocab, float* out, const int64_t* lengths, uint8_t* mask, hipStream_t st) {
     const int total = B * S * H;
     const int grid = std::min(cdiv(total, 256), 4096);
     const float scale = (float)std::sqrt((double)H);  // python float H**0.5, cast to fp32 by the mul
     hipLaunchKernelGGL(embed_pe_kernel, dim3(grid), dim3(256), 0, st, ids, emb, pe, B * S, S, H,
-                       vocab, scale, out);
+                       vocab, scale, out, lengths, mask);
     M2_LAUNCHED("embed_pe_kernel");
     return M2_OK;
 }
@@ -634,7 +640,7 @@ int32_t launch_embed_pe_scaled(const int64_t* ids, const float* emb, const float
     if (total == 0) return M2_OK;
     const int grid = std::min(cdiv(total, 256), 4096);
     hipLaunchKernelGGL(embed_pe_kernel, dim3(grid), dim3(256), 0, st, ids, emb, pe, B * S, S, H,
-                       vocab, scale, out);
+                       vocab, scale, out, nullptr, nullptr);
     M2_LAUNCHED("embed_pe_kernel");
     return M2_OK;
 }

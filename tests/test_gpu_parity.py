@@ -471,3 +471,22 @@ def test_inference_single_call_empty(gpu):
     m = build_model("s1", gpu)
     mel, audio = m.inference(torch.zeros(0, 7, dtype=torch.long, device=gpu))
     assert mel.shape == (0, 1, stage_config("s1").mel_channels) and audio.shape == (0, 1, 64)
+
+
+def test_inference_many_utterances(gpu):
+    """m2_inference against the staged six-call path, bit for bit, for B > 256
+    (several count workgroups per ticket round, 14-phoneme duration tiles with
+    a ragged last tile), repeated calls, ragged lengths, a duration scale."""
+    from m2amd import ops
+    m = build_model("s1", gpu)
+    hm = m._hip(gpu)
+    g = torch.Generator().manual_seed(7)
+    for B, S, scale in ((300, 20, 1.0), (300, 20, 1.7), (5, 37, 1.0), (300, 20, 1.0)):
+        ids = torch.randint(0, 42, (B, S), generator=g).to(gpu)
+        lens = torch.randint(1, S + 1, (B,), generator=g).to(gpu)
+        mel, audio = m.inference(ids, lens, duration_scale=scale)
+        enc, _ = hm.text_encoder(ids, lens)
+        reg = ops.regulate(enc, hm.duration(enc), None, scale=scale)
+        smel = hm.decoder(reg)
+        assert torch.equal(mel, smel)
+        assert torch.equal(audio, hm.vocoder(smel, layout_btm=True))
