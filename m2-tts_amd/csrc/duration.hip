@@ -84,24 +84,51 @@ __device__ __forceinline__ void dur_conv_mfma(const float* in, const float4* __r
     }
 }
 
-template <int H>
+// LN: `enc` is the encoder's last layer output BEFORE its final LayerNorm
+// (tts_model.py:87); each workgroup normalises its rows while loading them
+// (one wave per row, the halo rows redundantly) and stores its own 14
+// normalised rows to enc_out - the encoder output the length regulator
+// expands - in place of a separate layer_norm_kernel launch.
+template <int H, bool LN>
 __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ enc, int S, const float4* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ a1, const float* __restrict__ c1, const float4* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ a2, const float* __restrict__ c2,
-    const float* __restrict__ pw, const float* __restrict__ pb, float* __restrict__ dur) {
+    const float* __restrict__ pw, const float* __restrict__ pb, float* __restrict__ dur,
+    const float* __restrict__ lng, const float* __restrict__ lnb, float* __restrict__ enc_out) {
     constexpr int XS = H + 2, NT = 64 * DUR_WAVES;
     __shared__ float X[18 * XS];   // positions s0-2 .. s0+15
     __shared__ float Y1[18 * XS];  // s0-1 .. s0+14 (+2 zero rows read by conv2's unused rows)
     __shared__ float Y2[16 * XS];  // s0 .. s0+13 (+2 unused)
     const int b = blockIdx.y, s0 = blockIdx.x * DUR_TS, tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
     const float* e = enc + (size_t)b * S * H;
-    for (int idx = tid; idx < 18 * (H / 4); idx += NT) {
-        const int p = idx / (H / 4), c4 = (idx - p * (H / 4)) * 4, s = s0 - 2 + p;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (s >= 0 && s < S) v = *reinterpret_cast<const float4*>(e + (size_t)s * H + c4);
-        float* d = X + p * XS + c4;
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    if constexpr (LN) {
+        for (int p = wave; p < 18; p += DUR_WAVES) {
+            const int s = s0 - 2 + p;
+            float* d = X + p * XS;
+            if (s >= 0 && s < S) {
+                const float* xr = e + (size_t)s * H;
+                float mean, rstd;
+                ln_row_stats(xr, H, lane, mean, rstd);
+                float* yo = (p >= 2 && p < 2 + DUR_TS) ? enc_out + ((size_t)b * S + s) * H : nullptr;
+                for (int k = lane; k < H; k += 64) {
+                    const float y = ln_apply(xr[k], mean, rstd, lng[k], lnb[k]);
+                    d[k] = y;
+                    if (yo) yo[k] = y;
+                }
+            } else {
+                for (int k = lane; k < H; k += 64) d[k] = 0.f;
+            }
+        }
+    } else {
+        for (int idx = tid; idx < 18 * (H / 4); idx += NT) {
+            const int p = idx / (H / 4), c4 = (idx - p * (H / 4)) * 4, s = s0 - 2 + p;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (s >= 0 && s < S) v = *reinterpret_cast<const float4*>(e + (size_t)s * H + c4);
+            float* d = X + p * XS + c4;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
     }
     for (int idx = tid; idx < 2 * XS; idx += NT) Y1[16 * XS + idx] = 0.f;
     __syncthreads();
@@ -110,7 +137,6 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     dur_conv_mfma<H>(Y1, w2, b2, a2, c2, Y2, s0, S);
     __syncthreads();
     // k=1 projection H -> 1: one wave per phoneme, shuffle reduction.
-    const int lane = tid & 63, wave = tid >> 6;
     for (int p = wave; p < DUR_TS; p += DUR_WAVES) {
         const int s = s0 + p;
         float acc = 0.f;
@@ -248,14 +274,19 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict_
 
 // ---------------------------------------------------------------------------
 // p: w1 (packed), b1, alpha1, beta1, w2 (packed), b2, alpha2, beta2, proj_w, proj_b
-int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st) {
+int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st,
+                        const float* ln_g, const float* ln_b, float* enc_out) {
     if (B == 0 || S == 0) return M2_OK;
     const dim3 grid(cdiv(S, DUR_TS), B), blk(64 * DUR_WAVES);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
-#define M2_DUR(HH)                                                                                              \
-    case HH:                                                                                                    \
-        hipLaunchKernelGGL(duration_kernel<HH>, grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], p[3], f4(p[4]), \
-                           p[5], p[6], p[7], p[8], p[9], dur);                                                  \
+#define M2_DUR(HH)                                                                                           \
+    case HH:                                                                                                 \
+        if (enc_out)                                                                                         \
+            hipLaunchKernelGGL((duration_kernel<HH, true>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], \
+                               p[3], f4(p[4]), p[5], p[6], p[7], p[8], p[9], dur, ln_g, ln_b, enc_out);     \
+        else                                                                                                 \
+            hipLaunchKernelGGL((duration_kernel<HH, false>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], \
+                               p[3], f4(p[4]), p[5], p[6], p[7], p[8], p[9], dur, nullptr, nullptr, nullptr); \
         break;
     switch (H) {
         M2_DUR(32)

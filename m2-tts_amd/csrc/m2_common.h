@@ -85,4 +85,28 @@ struct Sizer {
     T* take(size_t count) { off = align_up(off, 256) + count * sizeof(T); return nullptr; }
 };
 
+// nn.LayerNorm statistics of one row, one wave per row: two-pass mean and
+// biased variance, lane-strided sums, xor-shuffle reductions.  Shared by
+// layer_norm_kernel and the duration kernel's fused encoder LayerNorm so the
+// two give identical bits.
+__device__ __forceinline__ void ln_row_stats(const float* xr, int K, int lane, float& mean, float& rstd) {
+    // explicit roundings: no context-dependent fma contraction between the
+    // two kernels that use this
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s = __fadd_rn(s, xr[k]);
+    for (int o = 32; o > 0; o >>= 1) s = __fadd_rn(s, __shfl_xor(s, o));
+    mean = __fdiv_rn(s, (float)K);
+    float v = 0.f;
+    for (int k = lane; k < K; k += 64) {
+        const float d = __fsub_rn(xr[k], mean);
+        v = __fmaf_rn(d, d, v);
+    }
+    for (int o = 32; o > 0; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o));
+    rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(v, (float)K), kLnEps)));
+}
+
+__device__ __forceinline__ float ln_apply(float x, float mean, float rstd, float g, float b) {
+    return __fmaf_rn(__fmul_rn(__fsub_rn(x, mean), rstd), g, b);
+}
+
 }  // namespace m2

@@ -23,7 +23,8 @@ int32_t launch_layer_norm(const float*, const float*, const float*, int, int, fl
 int32_t launch_linear(const float*, const float*, const float*, const float*, const float*,
                       const float*, int, int, int, int, float*, hipStream_t);
 int32_t launch_attention(const float*, const uint8_t*, int, int, int, int, float*, hipStream_t);
-int32_t launch_duration(const float*, int, int, int, const float* const*, float*, hipStream_t);
+int32_t launch_duration(const float*, int, int, int, const float* const*, float*, hipStream_t,
+                        const float* ln_g = nullptr, const float* ln_b = nullptr, float* enc_out = nullptr);
 int32_t launch_lr_count(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int32_t launch_lr_count_sync(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, unsigned*, int32_t*,
                              int32_t, hipStream_t);
@@ -670,17 +671,20 @@ size_t m2_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T
     return std::max(a.off, std::max(b.off, c.off)) + 256;
 }
 
-int32_t m2_text_encoder(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B,
-                        int32_t S, float* out_enc, uint8_t* out_mask, void* workspace,
-                        size_t workspace_bytes, void* stream) {
-    M2_CHECK_ARG(m && ids && out_enc && B >= 0 && S >= 0, "m2_text_encoder: bad argument");
-    M2_CHECK_SHAPE(S <= m->cfg.max_positions, "m2_text_encoder: sequence longer than the positional table");
-    hipStream_t st = static_cast<hipStream_t>(stream);
+}  // extern "C"
+
+namespace {
+// TextEncoder.forward up to (not including) the final LayerNorm; *x_pre = the
+// last layer's output in the workspace.
+int32_t text_encoder_layers(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S,
+                            uint8_t* out_mask, void* workspace, size_t workspace_bytes, hipStream_t st,
+                            float** x_pre) {
     const int H = m->cfg.hidden_dim;
     Carve a(workspace, workspace_bytes);
     TfBufs wb;
     carve_tf(a, B, S, H, &wb);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_text_encoder: workspace too small");
+    *x_pre = wb.x;
     if (B == 0 || S == 0) return M2_OK;
     int32_t rc;
     const uint8_t* mask = nullptr;
@@ -690,7 +694,22 @@ int32_t m2_text_encoder(const m2_model* m, const int64_t* ids, const int64_t* le
         return rc;
     for (const auto& L : m->enc)
         if ((rc = run_layer(m, L, wb.x, wb.x, wb, mask, B, S, st))) return rc;
-    return launch_layer_norm(wb.x, m->enc_nw, m->enc_nb, B * S, H, out_enc, st);
+    return M2_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t m2_text_encoder(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B,
+                        int32_t S, float* out_enc, uint8_t* out_mask, void* workspace,
+                        size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && ids && out_enc && B >= 0 && S >= 0, "m2_text_encoder: bad argument");
+    M2_CHECK_SHAPE(S <= m->cfg.max_positions, "m2_text_encoder: sequence longer than the positional table");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    float* x = nullptr;
+    int32_t rc = text_encoder_layers(m, ids, lengths, B, S, out_mask, workspace, workspace_bytes, st, &x);
+    if (rc || B == 0 || S == 0) return rc;
+    return launch_layer_norm(x, m->enc_nw, m->enc_nb, B * S, m->cfg.hidden_dim, out_enc, st);
 }
 
 int32_t m2_duration_predictor(const m2_model* m, const float* enc, int32_t B, int32_t S,
@@ -962,10 +981,16 @@ int32_t m2_inference_front(const m2_model* m, const int64_t* ids, const int64_t*
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_inference_front: front buffer too small");
     int32_t rc;
     if (B > 0 && S > 0) {
-        if ((rc = m2_text_encoder(m, ids, lengths, B, S, f.enc, lengths ? f.mask : nullptr, workspace,
-                                  workspace_bytes, stream)))
+        M2_CHECK_SHAPE(S <= m->cfg.max_positions, "m2_inference: sequence longer than the positional table");
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        float* x = nullptr;
+        if ((rc = text_encoder_layers(m, ids, lengths, B, S, lengths ? f.mask : nullptr, workspace, workspace_bytes,
+                                      st, &x)))
             return rc;
-        if ((rc = m2_duration_predictor(m, f.enc, B, S, f.dur, nullptr, 0, stream))) return rc;
+        // the encoder's final LayerNorm runs inside the duration kernel, which
+        // also stores the normalised encoder output (f.enc)
+        if ((rc = launch_duration(x, B, S, m->cfg.hidden_dim, m->dur, f.dur, st, m->enc_nw, m->enc_nb, f.enc)))
+            return rc;
     }
     // A frame-count epilogue fused into the duration kernel (per-utterance
     // tickets, one L2 write-back per workgroup) measured 5 us slower than

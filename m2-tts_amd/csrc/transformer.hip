@@ -48,16 +48,10 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= R) return;
     const float* xr = x + (size_t)row * K;
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s += xr[k];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    const float mean = s / (float)K;
-    float v = 0.f;
-    for (int k = lane; k < K; k += 64) { float d = xr[k] - mean; v += d * d; }
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const float rstd = 1.0f / sqrtf(v / (float)K + kLnEps);
+    float mean, rstd;
+    ln_row_stats(xr, K, lane, mean, rstd);
     float* yr = y + (size_t)row * K;
-    for (int k = lane; k < K; k += 64) yr[k] = (xr[k] - mean) * rstd * g[k] + b[k];
+    for (int k = lane; k < K; k += 64) yr[k] = ln_apply(xr[k], mean, rstd, g[k], b[k]);
 }
 
 // ---------------------------------------------------------------------------
