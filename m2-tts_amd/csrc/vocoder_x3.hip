@@ -528,27 +528,37 @@ __device__ __forceinline__ void head_rb1_planar(const u32x4* __restrict__ Wp, co
 // mel -> window rows [0, N) (abs start + r), MP channels (zero past M).
 template <bool TRANS, int M, int MP, int RS, int N, int NTHR>
 __device__ __forceinline__ void gload_mel(const float* __restrict__ g, int T, XW dst) {
-    if (TRANS) {  // [T][M]: a row of M contiguous floats per frame
-        constexpr int C4 = MP / 4, TOT = N * C4, IT = (TOT + NTHR - 1) / NTHR;
-        float4 x[IT];
+    if (TRANS) {  // [T][M]: an item = 8 channels of one frame (two 16-B loads); consecutive threads take
+                  // consecutive frames, so the LDS stores are the [M][T] branch's b128 pattern (was 16
+                  // threads per frame row with 8-B hi / lo stores: [B,T,M] 0.2 us/step behind [B,M,T] in
+                  // tools/probe/mel_layout_ab.py, now level)
+        constexpr int OCT = MP / 8, TOT = N * OCT, IT = (TOT + NTHR - 1) / NTHR;
+        float4 x[IT][2];
 #pragma unroll
         for (int k = 0; k < IT; ++k) {
             const int i = threadIdx.x + k * NTHR;
-            const int r = i / C4, c = (i - r * C4) * 4, t = dst.start + r;
-            x[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (i < TOT && t >= 0 && t < T && c < M) x[k] = *reinterpret_cast<const float4*>(g + (size_t)t * M + c);
+            const int o = i / N, r = i - o * N, t = dst.start + r;
+            const bool in = i < TOT && t >= 0 && t < T;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = 8 * o + 4 * h;
+                x[k][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (in && c < M) x[k][h] = *reinterpret_cast<const float4*>(g + (size_t)t * M + c);
+            }
         }
 #pragma unroll
         for (int k = 0; k < IT; ++k) {
             const int i = threadIdx.x + k * NTHR;
             if (i < TOT) {
-                const int r = i / C4, c = (i - r * C4) * 4;
-                const float v[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
-                h4 hi, lo;
-                split4(v, hi, lo);
-                unsigned char* row = dst.p + r * RS + c * 2;
-                *reinterpret_cast<h4*>(row) = hi;
-                *reinterpret_cast<h4*>(row + 2 * MP) = lo;
+                const int o = i / N, r = i - o * N;
+                unsigned hh[4], ll[4];
+                split2u(x[k][0].x, x[k][0].y, hh[0], ll[0]);
+                split2u(x[k][0].z, x[k][0].w, hh[1], ll[1]);
+                split2u(x[k][1].x, x[k][1].y, hh[2], ll[2]);
+                split2u(x[k][1].z, x[k][1].w, hh[3], ll[3]);
+                unsigned char* row = dst.p + r * RS + 16 * o;
+                *reinterpret_cast<u32x4*>(row) = u32x4{hh[0], hh[1], hh[2], hh[3]};
+                *reinterpret_cast<u32x4*>(row + 2 * MP) = u32x4{ll[0], ll[1], ll[2], ll[3]};
             }
         }
     } else {  // [M][T]: an item = 8 channels of one frame; consecutive threads take consecutive frames

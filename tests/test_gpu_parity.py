@@ -490,3 +490,18 @@ def test_inference_many_utterances(gpu):
         smel = hm.decoder(reg)
         assert torch.equal(mel, smel)
         assert torch.equal(audio, hm.vocoder(smel, layout_btm=True))
+
+
+@pytest.mark.parametrize("stage", STAGES)
+@pytest.mark.parametrize("T", [1, 37, 500])
+def test_vocoder_mel_layouts_identical(gpu, stage, T):
+    """The vocoder reading the decoder's [B,T,M] mel in place (inference path)
+    and the module's own [B,M,T] input give identical audio, including ragged
+    tiles (T not a multiple of the head's frame window) and T = 1."""
+    m = build_model(stage, gpu)
+    hm = m._hip(gpu)
+    g = torch.Generator().manual_seed(T)
+    mel_btm = torch.randn(3, T, stage_config(stage).mel_channels, generator=g).to(gpu)
+    a = hm.vocoder(mel_btm, layout_btm=True)
+    b = hm.vocoder(mel_btm.transpose(1, 2).contiguous(), layout_btm=False)
+    assert torch.equal(a, b)
