@@ -2,28 +2,44 @@
 """Benchmark: audio samples/s (22.05 kHz) + real-time factor of the m2-tts
 mel-synthesis + vocoder path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vocoder|pipeline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 
-One process per GPU (torchrun for N>1, RCCL backend); every rank processes
-its own batch of B utterances (weak scaling: utterances are independent, no
-collective in the data path).  Timed region: barrier + synchronize, K steps,
-synchronize + barrier; the max elapsed over ranks is the job time.
+One process per GPU, RCCL (torch.distributed "nccl") between them.  With
+``--gpus N > 1`` and no WORLD_SIZE in the environment, this process starts N
+fresh rank processes (spawn, before anything touches the GPU) and waits for
+them; under ``torch.distributed.run`` the ranks come from the environment.
+Timed region of every line: barrier + synchronize, K steps, synchronize +
+barrier; the job time is the max over ranks.  Before the first timed region
+every rank runs the workload untimed for ``--settle-ms`` (the GPU clocks need
+tens of ms of load to settle; a 1.6 ms timed loop right after launch runs
+~20 % slow, tools/probe/timing_order.py).
 
-Workloads:
-  vocoder  (default, BASELINE.json configs[1]) stage1_poc SimpleVocoder, B=32,
-           mel [32, 64, 500] ~ N(0,1) resident in HBM -> audio [32, 1, 32000]
-  pipeline (configs[2]) stage1_poc M2TTSModel.inference, B=32, 100 phonemes,
-           fixture weights with durations pinned to 5 frames -> T=500
-
-Extra fields: ``roofline`` for the dominant kernel (HIP events on its launch
-stream, around every launch of the timed region), ``cpu_baseline`` (the CPU
-oracle = the reference's op sequence, timed on this host, rank 0, N=1 only).
+Workloads (BASELINE.json configs):
+  vocoder      configs[1] (headline): stage1 SimpleVocoder, B=32 utterances
+               PER GPU, mel [32, 64, 500] ~ N(0,1) resident in HBM -> audio
+               [32, 1, 32000]; weak scaling (independent replicas, no collective)
+  pipeline     configs[2]: stage1 M2TTSModel.inference, B=32 per GPU, 100
+               phonemes, fixture weights (durations pinned to 5 frames) -> T=500
+  s2_b64       configs[3]: stage2 M2TTSModel.inference over a GLOBAL batch of 64
+               utterances (100 phonemes -> T=500) sharded by utterance across
+               the N ranks (m2amd.parallel.sharded_inference: RCCL all_reduce(MAX)
+               of the frame count + all_gather of mel/audio); strong scaling
+  s2_longform  configs[4]: the same with a global batch of 128 utterances of
+               520 phonemes -> T=2600 mel frames (30.2 s at hop 256), vocoder
+               streamed in 256-frame chunks (3-frame halo)
+  s2_vocoder   stage2 SimpleVocoder at the per-GPU shape of configs[3] on 8
+               GPUs: B=8, T=500 (per-kernel roofline table)
+The default run measures ``vocoder`` as the headline ``value`` and adds the
+other workloads, the exact-f32 vocoder, and (rank 0, N=1) the CPU oracle as
+sub-objects of the same JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
+import socket
 import sys
 import time
 from pathlib import Path
@@ -36,6 +52,7 @@ sys.path.insert(0, str(ROOT / "m2-tts_amd" / "src"))
 SAMPLE_RATE = 22050
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 vector = f32 MFMA peak
 F16_PEAK_TFLOPS = 2516.8     # MI355X_MICROARCH.md: f16/bf16 dense MFMA = 16 x the f32 MFMA rate
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E
 # Vocoder arithmetic paths (m2_vocoder_path): peak for ALGORITHMIC fp32 FLOP/s and what it means.
 VOC_PATHS = {
     0: ("f32", FP32_PEAK_TFLOPS, "per-layer fp32 kernels; fp32 peak 157.3 TF"),
@@ -44,17 +61,16 @@ VOC_PATHS = {
         "fp32 operands as f16 hi/lo pairs, 3 v_mfma_f32_16x16x32_f16 per fp32 product: "
         "effective fp32 peak = 2516.8 / 3 = 838.9 TF"),
 }
-HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec
 METRIC = "audio samples/sec (22.05 kHz) + RTF, stage1_poc batch=32 @1/2/4/8 MI355X"
 
 STAGE1 = dict(vocab_size=256, hidden_dim=64, mel_channels=64, text_encoder_layers=2, decoder_layers=2,
               num_heads=2, dropout=0.1, vocoder_channels=128)
+STAGE2 = dict(vocab_size=256, hidden_dim=96, mel_channels=80, text_encoder_layers=3, decoder_layers=3,
+              num_heads=2, dropout=0.1, vocoder_channels=256)
+RATES = (4, 4, 2, 2)
 
 
-# Event sampling in the timed region: one event pair around the dominant
-# kernel every PROF_STRIDE steps (each pair costs a few us of pipeline drain).
-PROF_STRIDE = 8
-
+# ---------------------------------------------------------------------------- work models
 def vocoder_flops_per_sample(C: int, M: int) -> float:
     """Algorithmic FLOPs per output audio sample of SimpleVocoder.
 
@@ -63,7 +79,7 @@ def vocoder_flops_per_sample(C: int, M: int) -> float:
     output conv 2*c_last*3 per sample.  Divided by 64 samples per frame."""
     f = 2 * M * C * 3
     c, n = C, 1
-    for r in (4, 4, 2, 2):
+    for r in RATES:
         n *= r
         co = c // 2
         f += n * (2 * 2 * c * co + 2 * 2 * co * co * 3)
@@ -84,12 +100,24 @@ def vocoder_kernel_flops_per_frame(C: int, M: int):
     return [head, mid, tail]
 
 
-def fixture_model(dev):
-    """Random-init stage1 weights (seed 1234) with durations pinned
-    to 5 frames/phoneme: projection weight * 0.01, bias 5.5."""
+def mrf_bytes(C: int, B: int, T: int) -> float:
+    """SURVEY.md 8d per-kernel bytes of the four LightweightResBlocks ("MRF"):
+    each reads its input once and writes its output once (8*c*L per
+    utterance) plus its weights once (4*(6c^2+2c))."""
+    tot, c, L = 0.0, C, T
+    for r in RATES:
+        c //= 2
+        L *= r
+        tot += B * 8.0 * c * L + 4.0 * (6 * c * c + 2 * c)
+    return tot
+
+
+def fixture_model(cfg: dict, dev):
+    """Random-init weights (seed 1234) with durations pinned to 5
+    frames/phoneme: projection weight * 0.01, bias 5.5."""
     from models.tts_model import M2TTSModel
     torch.manual_seed(1234)
-    m = M2TTSModel(**STAGE1)
+    m = M2TTSModel(**cfg)
     with torch.no_grad():
         p = m.duration_predictor.predictor.projection
         p.weight.mul_(0.01)
@@ -97,8 +125,25 @@ def fixture_model(dev):
     return m.to(dev).eval()
 
 
+# ---------------------------------------------------------------------------- host / CPU baseline
+def host_info():
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return cpu_model, os.cpu_count(), affinity
+
+
 def cpu_baseline(workload: str, B: int, S: int, T: int, budget_s: float):
-    """Time the CPU oracle (reference op order) on a bounded sample of the workload."""
+    """Time the CPU oracle (the reference's op sequence) on a bounded sample of the workload."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import m2tts_oracle as orc
     threads = torch.get_num_threads()
@@ -126,35 +171,298 @@ def cpu_baseline(workload: str, B: int, S: int, T: int, budget_s: float):
             el = time.perf_counter() - t0
             if el >= budget_s or n >= 200:
                 break
-    samples = n * B * 64 * T
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": samples / el, "unit": "audio samples/s", "cores": threads, "kind": "port",
-            "sample": f"{desc}; {n} runs in {el:.1f} s; torch {torch.__version__} CPU, {threads} threads, {cpu_model}"}
+    cpu_model, ncpu, aff = host_info()
+    return {"value": samples_per(B, T) * n / el, "unit": "audio samples/s", "cores": threads, "kind": "port",
+            "host_logical_cpus": ncpu, "affinity_cpus": aff, "torch_threads": threads, "cpu_model": cpu_model,
+            "sample": f"{desc}; {n} runs in {el:.1f} s; torch {torch.__version__} CPU ops, {threads} intra-op "
+                      f"threads on {cpu_model} ({ncpu} logical CPUs on the host, {aff} in this process's "
+                      f"affinity mask)"}
 
 
-def main():
+def samples_per(B: int, T: int) -> int:
+    return B * 64 * T
+
+
+# ---------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_entry(rank: int, world: int, port: int, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse_args(argv))
+
+
+def launch_ranks(args, argv):
+    """Start args.gpus fresh rank processes (this process has not touched the GPU)."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_entry, args=(args.gpus, _free_port(), argv), nprocs=args.gpus, join=True,
+                       start_method="spawn")
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # Defaults: the GPU clocks take tens of ms of load to settle (a first
-    # 30 ms loop runs ~7 % slow: tools/probe/timing_order.py), so the default
-    # warm-up is a few hundred steps (~40 ms); both finish in well under a second.
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--workload", choices=["vocoder", "pipeline"], default="vocoder")
-    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=400.0,
+                    help="untimed, time-based run of the workload before the first timed region")
+    ap.add_argument("--workload", choices=["vocoder", "pipeline", "s2_b64", "s2_longform", "s2_vocoder"],
+                    default="vocoder")
+    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU (vocoder / pipeline)")
     ap.add_argument("--phonemes", type=int, default=100)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline-extra", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--no-extras", action="store_true", help="headline line only")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks join a gloo group, all-reduce, print one line")
+    return ap.parse_args(argv)
 
+
+def dry_run(args):
+    """CPU check of the launch path (tests/test_bench_launcher.py): every rank
+    joins a gloo group with the rendezvous the launcher set up and
+    all-reduces its rank; rank 0 prints n_gpus = world size seen."""
+    import torch.distributed as td
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        td.init_process_group("gloo", rank=rank, world_size=world)
+        t = torch.tensor([rank + 1.0])
+        td.all_reduce(t)
+        total = float(t.item())
+        td.destroy_process_group()
+    else:
+        total = 1.0
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "rank_sum": total, "gpus_flag": args.gpus}), flush=True)
+
+
+# ---------------------------------------------------------------------------- measurement
+class Ctx:
+    def __init__(self, dev, world, rank, dist):
+        self.dev, self.world, self.rank, self.dist = dev, world, rank, dist
+        from m2amd import _lib
+        self.lib = _lib.load()
+        self._lib = _lib
+        self.nk = self.lib.m2_profile_kernel_count()
+        self.models = {}
+
+    def model(self, stage: str):
+        if stage not in self.models:
+            self.models[stage] = fixture_model(STAGE1 if stage == "s1" else STAGE2, self.dev)
+        return self.models[stage]
+
+    def barrier(self):
+        if self.dist:
+            import torch.distributed as td
+            td.barrier()
+
+    def max_over_ranks(self, v: float) -> float:
+        if not self.dist:
+            return v
+        import torch.distributed as td
+        t = torch.tensor([v], device=self.dev, dtype=torch.float64)
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        return float(t.item())
+
+    def settle(self, fn, ms: float) -> float:
+        """Run fn untimed for about `ms` milliseconds of wall time (clock settling)."""
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < ms:
+            fn()
+            torch.cuda.synchronize(self.dev)
+        return (time.perf_counter() - t0) * 1e3
+
+    def timed(self, fn, steps: int, warmup: int, hm=None, kernel_mask: int = 0, stride: int = 1):
+        """Run `steps` of fn between barriers + syncs (max over ranks); with
+        kernel_mask, fence-free HIP events on the launch stream inside
+        m2_vocoder around the selected vocoder kernels of every stride-th call."""
+        lib, chk = self.lib, self._lib.check
+        for _ in range(warmup):
+            fn()
+        if kernel_mask:
+            chk(lib.m2_profile_select(hm.handle, kernel_mask), "m2_profile_select")
+            chk(lib.m2_profile_stride(hm.handle, stride), "m2_profile_stride")
+            chk(lib.m2_profile_enable(hm.handle, (steps + stride - 1) // stride), "m2_profile_enable")
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        el = time.perf_counter() - t0
+        ms = []
+        if kernel_mask:
+            cap = (steps + stride - 1) // stride * self.nk
+            buf = (ctypes.c_float * cap)()
+            n = ctypes.c_int32(0)
+            chk(lib.m2_profile_read(hm.handle, buf, cap, ctypes.byref(n)), "m2_profile_read")
+            ms = list(buf[: n.value])
+            lib.m2_profile_disable(hm.handle)
+            chk(lib.m2_profile_stride(hm.handle, 1), "m2_profile_stride")
+        return self.max_over_ranks(el), ms
+
+    def kernel_table(self, hm, kern_ms, C, M, B, T):
+        fl = vocoder_kernel_flops_per_frame(C, M)
+        _, peak, _ = VOC_PATHS[self.lib.m2_vocoder_path(hm.handle)]
+        rows = []
+        for i in range(self.nk):
+            vals = [v for v in kern_ms[i::self.nk] if v >= 0]
+            if not vals:
+                continue
+            avg = sum(vals) / len(vals)
+            flops = fl[i] * B * T
+            tf = flops / (avg * 1e-3) / 1e12
+            rows.append({"index": i, "kernel": self.lib.m2_profile_kernel_name_for(hm.handle, i).decode(),
+                         "avg_ms": round(avg, 5), "launches": len(vals), "algorithmic_flop_per_launch": flops,
+                         "tflops": round(tf, 3), "frac_of_peak": round(tf / peak, 4)})
+        return rows
+
+
+def traffic_for(kernel_name: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (not measured in this run)."""
+    tf = ROOT / "profiles" / "traffic.json"
+    if not tf.exists():
+        return None, None
+    try:
+        d = json.loads(tf.read_text())
+    except ValueError:
+        return None, None
+    v = d.get(kernel_name.split()[0])
+    return v, d.get("_source", "profiles/traffic.json")
+
+
+def vocoder_line(cx: Ctx, stage: str, B: int, T: int, args, settle_ms: float, seed: int, f32: bool = False):
+    """SimpleVocoder throughput on mel [B, M, T] per rank (weak scaling), the
+    per-kernel HIP-event table, and the dominant kernel's roofline sampled
+    live inside the timed region."""
+    cfg = STAGE1 if stage == "s1" else STAGE2
+    m = cx.model(stage)
+    hm = m._hip(cx.dev)
+    hm.vocoder_select(1 if f32 else 2)
+    try:
+        g = torch.Generator().manual_seed(seed + cx.rank)
+        mel = torch.randn(B, cfg["mel_channels"], T, generator=g).to(cx.dev)
+        step = lambda: m.vocoder(mel)  # noqa: E731
+        settled = cx.settle(step, settle_ms)
+        # untimed pass with events on all three kernels -> per-kernel table + dominant kernel
+        _, all_ms = cx.timed(step, min(args.steps, 20), 2, hm, kernel_mask=(1 << cx.nk) - 1)
+        per_kernel = cx.kernel_table(hm, all_ms, cfg["vocoder_channels"], cfg["mel_channels"], B, T)
+        dom_i = max(per_kernel, key=lambda d: d["avg_ms"])["index"] if per_kernel else 0
+        stride = max(1, args.steps // 32)
+        elapsed, kern_ms = cx.timed(step, args.steps, args.warmup, hm, kernel_mask=1 << dom_i, stride=stride)
+        path = cx.lib.m2_vocoder_path(hm.handle)
+    finally:
+        hm.vocoder_select(2)
+    dtype, peak, note = VOC_PATHS[path]
+    value = samples_per(B, T) * args.steps * cx.world / elapsed
+    ms = elapsed / args.steps * 1e3
+    live = cx.kernel_table(hm, kern_ms, cfg["vocoder_channels"], cfg["mel_channels"], B, T)
+    roof = None
+    if live:
+        d = live[0]
+        traffic, src = traffic_for(d["kernel"]) if (stage == "s1" and path == 2) else (None, None)
+        roof = {"bound": "mfma", "achieved": d["tflops"], "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(d["tflops"] / peak, 4), "traffic": traffic,
+                "traffic_source": (f"static: {src} (rocprofv3 PMC passes, 2*FETCH_SIZE + WRITE_SIZE per launch); "
+                                   "not measured in this run") if traffic is not None else None,
+                "kernel": d["kernel"], "avg_kernel_ms": d["avg_ms"], "launches": d["launches"],
+                "event_stride": stride, "algorithmic_flop_per_launch": d["algorithmic_flop_per_launch"],
+                "dtype_peak_note": note}
+    flop_s = vocoder_flops_per_sample(cfg["vocoder_channels"], cfg["mel_channels"])
+    voc_s = ms * 1e-3
+    out = {"value": round(value, 1), "ms_per_step": round(ms, 5), "dtype": dtype, "settle_ms": round(settled, 1),
+           "config": {"stage": stage, "per_gpu_batch": B, "mel_frames": T, "audio_samples_per_utt": 64 * T},
+           "roofline": roof, "vocoder_kernels": per_kernel,
+           "vocoder_flop_per_sample": flop_s,
+           "vocoder_tflops": round(value / cx.world * flop_s / 1e12, 3),
+           # SURVEY.md 8d "MRF HBM fraction": sum of the 4 resblocks' per-kernel algorithmic
+           # bytes / the whole fused vocoder's time per step / 8 TB/s (the resblocks are fused
+           # with the ConvTs, so their own time is not separable: this is a lower bound)
+           "mrf_hbm_fraction": round(mrf_bytes(cfg["vocoder_channels"], B, T) / voc_s / (HBM_PEAK_GBS * 1e9), 4),
+           "mrf_hbm_fraction_def": "sum(resblock bytes 8cL + weights, SURVEY 8d) / whole-vocoder step time / 8 TB/s",
+           "fp32_valu_fraction": round(value / cx.world * flop_s / (FP32_PEAK_TFLOPS * 1e12), 4),
+           "fp32_valu_fraction_def": "algorithmic vocoder FLOP/s / 157.3 TF (MI355X fp32 vector peak)"}
+    return out
+
+
+def pipeline_line(cx: Ctx, B: int, S: int, args, settle_ms: float):
+    m = cx.model("s1")
+    g = torch.Generator().manual_seed(1000 + cx.rank)
+    ids = torch.randint(0, 42, (B, S), generator=g).to(cx.dev)
+    lens = torch.full((B,), S, dtype=torch.long, device=cx.dev)
+    step = lambda: m.inference(ids, lens)  # noqa: E731
+    settled = cx.settle(step, settle_ms)
+    steps = max(10, args.steps // 2)
+    elapsed, _ = cx.timed(step, steps, max(3, args.warmup // 2))
+    T = 5 * S
+    return {"value": round(samples_per(B, T) * steps * cx.world / elapsed, 1),
+            "ms_per_step": round(elapsed / steps * 1e3, 5), "steps": steps, "settle_ms": round(settled, 1),
+            "scaling": "weak", "config": {"workload": "stage1_poc M2TTSModel.inference (configs[2])",
+                                          "per_gpu_batch": B, "global_batch": B * cx.world, "phonemes": S,
+                                          "mel_frames": T}}
+
+
+def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, steps: int):
+    """stage2 inference over a global batch of Bg utterances sharded across the
+    ranks (configs[3] / [4]): one m2_inference_front + RCCL all_reduce(MAX) +
+    m2_inference_back + all_gather of mel / audio per step."""
+    from m2amd.parallel import hip_stages, shard_bounds, sharded_inference
+    import torch.distributed as td
+    m = cx.model("s2")
+    m.set_vocoder_chunking(chunk)
+    try:
+        g = torch.Generator().manual_seed(2024)  # every rank draws the same global batch
+        ids = torch.randint(0, 42, (Bg, S), generator=g).to(cx.dev)
+        lens = torch.full((Bg,), S, dtype=torch.long, device=cx.dev)
+        st = hip_stages(m)
+        step = lambda: sharded_inference(st, ids, lens)  # noqa: E731
+        mel, audio = step()
+        T = mel.shape[1]
+        assert mel.shape[0] == Bg and audio.shape == (Bg, 1, 64 * T)
+        settled = cx.settle(step, settle_ms)
+        elapsed, _ = cx.timed(step, steps, 2)
+        # split of one step: front (incl. the T_max host read) / all_reduce / back, rank-local wall times
+        lo, hi = shard_bounds(Bg, cx.world, cx.rank)
+        hm = m._hip(cx.dev)
+        torch.cuda.synchronize(cx.dev)
+        t0 = time.perf_counter()
+        state, tl = hm.inference_front(ids[lo:hi], lens[lo:hi], 1.0)
+        t1 = time.perf_counter()
+        if cx.dist:
+            t = torch.tensor([tl], dtype=torch.int32, device=cx.dev)
+            td.all_reduce(t, op=td.ReduceOp.MAX)
+            tl = int(t.item())
+        t2 = time.perf_counter()
+        hm.inference_back(state, max(1, tl))
+        t3 = time.perf_counter()
+        torch.cuda.synchronize(cx.dev)
+        t4 = time.perf_counter()
+    finally:
+        m.set_vocoder_chunking(0)
+    return {"value": round(samples_per(Bg, T) * steps / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "steps": steps, "settle_ms": round(settled, 1), "scaling": "strong",
+            "rtf_x_realtime": round(samples_per(Bg, T) * steps / elapsed / SAMPLE_RATE, 1),
+            "config": {"stage": "stage2_quality", "global_batch": Bg, "per_gpu_batch": hi - lo, "phonemes": S,
+                       "mel_frames": T, "vocoder_chunk_frames": chunk, "n_ranks": cx.world,
+                       "collectives": "all_reduce(MAX) 1 x int32 + all_gather mel/audio (RCCL)" if cx.dist
+                       else "none (world 1)"},
+            "rank0_phase_ms": {"front_incl_Tmax_read": round((t1 - t0) * 1e3, 3),
+                               "all_reduce": round((t2 - t1) * 1e3, 3),
+                               "back_enqueue": round((t3 - t2) * 1e3, 3),
+                               "back_drain": round((t4 - t3) * 1e3, 3)}}
+
+
+def run(args):
+    if args.dry_run:
+        return dry_run(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -166,149 +474,85 @@ def main():
         td.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    cx = Ctx(dev, world, rank, dist)
+    B, S = args.batch, args.phonemes
+    wl = args.workload
+    extras = {}
 
-    from m2amd import _lib
-    lib = _lib.load()
-    model = fixture_model(dev)
-    B, S, T = args.batch, args.phonemes, 5 * args.phonemes
-    g = torch.Generator().manual_seed(1000 + rank)
-    mel = torch.randn(B, STAGE1["mel_channels"], T, generator=g).to(dev)
-    ids = torch.randint(0, 42, (B, S), generator=g).to(dev)
-    lens = torch.full((B,), S, dtype=torch.long, device=dev)
-    hm = model._hip(dev)
-    voc_dtype, voc_peak, voc_note = VOC_PATHS[lib.m2_vocoder_path(hm.handle)]
+    if wl == "vocoder":
+        head = vocoder_line(cx, "s1", B, 5 * S, args, args.settle_ms, 1000)
+        desc = "stage1_poc SimpleVocoder B=32 per GPU (configs[1])"
+    elif wl == "s2_vocoder":
+        head = vocoder_line(cx, "s2", 8, 500, args, args.settle_ms, 3000)
+        desc = "stage2_quality SimpleVocoder B=8 T=500 per GPU (configs[3] per-GPU shape)"
+    elif wl == "pipeline":
+        head = pipeline_line(cx, B, S, args, args.settle_ms)
+        desc = head["config"]["workload"]
+    else:
+        Bg, Sg, chunk = (64, 100, 0) if wl == "s2_b64" else (128, 520, 256)
+        head = sharded_line(cx, Bg, Sg, chunk, args, args.settle_ms, args.steps if wl == "s2_b64" else
+                            max(5, args.steps // 10))
+        desc = f"stage2_quality M2TTSModel.inference global B={Bg} S={Sg} sharded x{world} ({wl}, configs[" \
+               f"{3 if wl == 's2_b64' else 4}])"
 
-    def step_vocoder():
-        return model.vocoder(mel)
+    if not args.no_extras:
+        if wl != "pipeline":
+            extras["pipeline"] = pipeline_line(cx, B, S, args, 100.0)
+        if wl == "vocoder":
+            f32 = vocoder_line(cx, "s1", B, 5 * S, args, 100.0, 1000, f32=True)
+            extras["vocoder_exact_f32"] = {k: f32[k] for k in ("value", "ms_per_step", "dtype", "roofline",
+                                                              "vocoder_kernels", "vocoder_tflops")}
+        if wl != "s2_vocoder":
+            s2v = vocoder_line(cx, "s2", 8, 500, args, 100.0, 3000)
+            extras["s2_vocoder_b8_t500"] = s2v
+        s2l = vocoder_line(cx, "s2", 16, 2600, type(args)(**{**vars(args), "steps": max(5, args.steps // 10)}),
+                           100.0, 4000)
+        extras["s2_vocoder_b16_t2600"] = s2l
+        if wl != "s2_b64":
+            extras["s2_b64_sharded"] = sharded_line(cx, 64, 100, 0, args, 100.0, max(10, args.steps // 4))
+        if wl != "s2_longform":
+            extras["s2_longform_sharded"] = sharded_line(cx, 128, 520, 256, args, 100.0, max(3, args.steps // 40))
 
-    def step_pipeline():
-        return model.inference(ids, lens)
+    out = {"metric": METRIC, "value": head["value"], "unit": "audio samples/s", "n_gpus": world,
+           "steps": args.steps if wl != "pipeline" else head["steps"], "warmup": args.warmup,
+           "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+           "scaling": head.get("scaling", "weak"), "vs_baseline": None,
+           "dtype": head.get("dtype", VOC_PATHS[2][0]),
+           "data": "synthetic (seeded N(0,1) mel / U{0..41} phoneme ids; random-init weights, seed 1234, "
+                   "durations pinned to 5 frames/phoneme)",
+           "config": {"workload": desc, **head["config"],
+                      "parallelism": (f"weak-scaled replicas x{world} (dp{world}, no collective in the data path)"
+                                      if head.get("scaling", "weak") == "weak" else
+                                      f"utterance-sharded x{world} (RCCL all_reduce + all_gather)")},
+           "settle_ms": head["settle_ms"],
+           "rtf_x_realtime": round(head["value"] / SAMPLE_RATE, 1),
+           "rtf_x_realtime_per_gpu": round(head["value"] / SAMPLE_RATE / world, 1)}
+    for k in ("roofline", "vocoder_kernels", "vocoder_flop_per_sample", "vocoder_tflops", "mrf_hbm_fraction",
+              "mrf_hbm_fraction_def", "fp32_valu_fraction", "fp32_valu_fraction_def", "rank0_phase_ms"):
+        if k in head:
+            out[k] = head[k]
+    out.update(extras)
 
-    step = step_vocoder if args.workload == "vocoder" else step_pipeline
-
-    nk = lib.m2_profile_kernel_count()
-
-    def timed(fn, steps, warmup, kernel_mask=0, stride=1):
-        """Run `steps` of fn between barriers + syncs; with kernel_mask, HIP
-        events (fence-free, on the launch stream inside m2_vocoder) around
-        the selected fused vocoder kernels of every `stride`-th step."""
-        for _ in range(warmup):
-            fn()
-        if kernel_mask:
-            _lib.check(lib.m2_profile_select(hm.handle, kernel_mask), "m2_profile_select")
-            _lib.check(lib.m2_profile_stride(hm.handle, stride), "m2_profile_stride")
-            _lib.check(lib.m2_profile_enable(hm.handle, (steps + stride - 1) // stride), "m2_profile_enable")
-        torch.cuda.synchronize(dev)
-        if dist:
-            td.barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            fn()
-        torch.cuda.synchronize(dev)
-        if dist:
-            td.barrier()
-        el = time.perf_counter() - t0
-        ms = []
-        if kernel_mask:
-            import ctypes
-            cap = (steps + stride - 1) // stride * nk
-            buf = (ctypes.c_float * cap)()
-            n = ctypes.c_int32(0)
-            _lib.check(lib.m2_profile_read(hm.handle, buf, cap, ctypes.byref(n)), "m2_profile_read")
-            ms = list(buf[: n.value])
-            lib.m2_profile_disable(hm.handle)
-            _lib.check(lib.m2_profile_stride(hm.handle, 1), "m2_profile_stride")
-        if dist:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            td.all_reduce(t, op=td.ReduceOp.MAX)
-            el = float(t.item())
-        return el, ms
-
-    C, M = STAGE1["vocoder_channels"], STAGE1["mel_channels"]
-    fl = vocoder_kernel_flops_per_frame(C, M)
-
-    def kernel_table(kern_ms):
-        rows = []
-        for i in range(nk):
-            vals = [v for v in kern_ms[i::nk] if v >= 0]
-            if not vals:
-                continue
-            avg = sum(vals) / len(vals)
-            flops = fl[i] * B * T
-            rows.append({"index": i, "kernel": lib.m2_profile_kernel_name_for(hm.handle, i).decode(),
-                         "avg_ms": round(avg, 5), "launches": len(vals), "algorithmic_flop_per_launch": flops,
-                         "tflops": round(flops / (avg * 1e-3) / 1e12, 3)})
-        return rows
-
-    # 1) Untimed pass with events on all three kernels: per-kernel table and
-    #    which kernel dominates.  Events drain the pipeline between kernels
-    #    (a few us each), so 2) the timed region carries events around the
-    #    dominant kernel of every PROF_STRIDE-th step only: its average
-    #    duration over those launches of the timed region is the roofline's
-    #    denominator.  3) the same loop with no events at all, for the record.
-    _, all_ms = timed(step, min(args.steps, 20), args.warmup, kernel_mask=(1 << nk) - 1)
-    per_kernel = kernel_table(all_ms)
-    dom_i = max(per_kernel, key=lambda d: d["avg_ms"])["index"] if per_kernel else 0
-    elapsed, kern_ms = timed(step, args.steps, 2, kernel_mask=1 << dom_i, stride=PROF_STRIDE)
-    el_ne, _ = timed(step, args.steps, 2)
-    samples_per_step = B * 64 * T
-    total_samples = samples_per_step * args.steps * world
-    value = total_samples / elapsed
-
-    roofline = None
-    live = kernel_table(kern_ms)
-    if live:
-        dom = live[0]
-        achieved = dom["tflops"]
-        roofline = {"bound": "mfma", "achieved": achieved, "peak": round(voc_peak, 1), "unit": "TFLOP/s",
-                    "frac": round(achieved / voc_peak, 4), "traffic": None, "kernel": dom["kernel"],
-                    "avg_kernel_ms": dom["avg_ms"], "launches": dom["launches"],
-                    "algorithmic_flop_per_launch": dom["algorithmic_flop_per_launch"],
-                    "dtype_peak_note": voc_note}
-        tf = ROOT / "profiles" / "traffic.json"
-        if tf.exists():
-            try:
-                roofline["traffic"] = json.loads(tf.read_text()).get(dom["kernel"].split()[0])
-            except ValueError:
-                pass
-
-    out = {
-        "metric": METRIC, "value": round(value, 1), "unit": "audio samples/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": voc_dtype,
-        "data": "synthetic (seeded N(0,1) mel / U{0..41} phoneme ids; random-init stage1 weights, seed 1234)",
-        "config": {"workload": "stage1_poc SimpleVocoder B=32 (configs[1])" if args.workload == "vocoder"
-                   else "stage1_poc M2TTSModel.inference B=32 S=100 (configs[2])",
-                   "stage": "stage1_poc", "per_gpu_batch": B, "global_batch": B * world, "mel_frames": T,
-                   "audio_samples_per_utt": 64 * T, "parallelism": f"utterance-sharded x{world} (dp{world})"},
-        "ms_per_step_without_kernel_events": round(el_ne / args.steps * 1e3, 4),
-        "rtf_x_realtime": round(value / SAMPLE_RATE, 1),
-        "rtf_x_realtime_per_gpu": round(value / SAMPLE_RATE / world, 1),
-        "roofline": roofline,
-        "vocoder_kernels": per_kernel,  # untimed pass, events on every kernel
-    }
-    if args.workload == "vocoder":
-        out["vocoder_flop_per_sample"] = vocoder_flops_per_sample(STAGE1["vocoder_channels"], STAGE1["mel_channels"])
-        out["vocoder_tflops"] = round(value * out["vocoder_flop_per_sample"] / 1e12, 3)
-
-    if not args.no_pipeline_extra:
-        other = step_pipeline if args.workload == "vocoder" else step_vocoder
-        el2, _ = timed(other, max(5, args.steps // 2), 3)
-        n2 = max(5, args.steps // 2)
-        out["other_workload"] = {"workload": "pipeline" if args.workload == "vocoder" else "vocoder",
-                                 "value": round(samples_per_step * n2 * world / el2, 1),
-                                 "ms_per_step": round(el2 / n2 * 1e3, 4)}
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.workload, B, S, T, args.cpu_budget)
-        out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
-        if not args.no_pipeline_extra:
-            other = "pipeline" if args.workload == "vocoder" else "vocoder"
-            out["cpu_baseline_other"] = cpu_baseline(other, B, S, T, args.cpu_budget / 2)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("vocoder", "pipeline"):
+        out["cpu_baseline"] = cpu_baseline(wl, B, S, 5 * S, args.cpu_budget)
+        out["cpu_baseline"]["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+        if not args.no_extras:
+            other = "pipeline" if wl == "vocoder" else "vocoder"
+            out["cpu_baseline_other"] = cpu_baseline(other, B, S, 5 * S, args.cpu_budget / 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
+        import torch.distributed as td
         td.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(args, argv)
+        return
+    run(args)
 
 
 if __name__ == "__main__":

@@ -134,6 +134,32 @@ int32_t m2_vocoder(const m2_model* model, const float* mel, int32_t mel_layout, 
                    int32_t T, float* out_audio, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* ---- streamed / chunked vocoder (long-form; SURVEY 8b `chunk_frames`) ------
+ * The reference runs SimpleVocoder over the whole mel (tts_model.py:279-297).
+ * A chunk [f0, f1) of mel frames is computed over the window
+ * [f0 - halo, f1 + halo) clipped to [0, T), halo = m2_vocoder_halo_frames()
+ * = the vocoder's receptive field (3 frames per side), so every audio sample
+ * equals the whole-utterance call's bit for bit; the window's mel is copied to
+ * the workspace, vocoded, and the centre of its audio copied out.
+ *   m2_vocoder_set_chunking: m2_vocoder (and m2_inference / _back) then run
+ *     chunk_frames frames at a time (0 = whole utterance, the default); size
+ *     the workspace after changing it (m2_workspace_bytes depends on it).
+ *   m2_vocoder_chunk: audio of frames [f0, f1) only, out_chunk [B,1,64(f1-f0)]
+ *     (for streaming: chunk k can be played while chunk k+1 is computed);
+ *     workspace from m2_vocoder_chunk_workspace_bytes(B, T, f1 - f0). */
+int32_t m2_vocoder_set_chunking(m2_model* model, int32_t chunk_frames);
+int32_t m2_vocoder_halo_frames(void);
+int32_t m2_vocoder_chunk(const m2_model* model, const float* mel, int32_t mel_layout, int32_t B,
+                         int32_t T, int32_t f0, int32_t f1, float* out_chunk, void* workspace,
+                         size_t workspace_bytes, void* stream);
+size_t m2_vocoder_chunk_workspace_bytes(const m2_model* model, int32_t B, int32_t T,
+                                        int32_t chunk_frames);
+
+/* Select the vocoder arithmetic at run time: 1 = exact-f32 MFMA kernels,
+ * 2 = split-f16 MFMA kernels (the default when the model has their packs).
+ * M2_E_ARG when the model has no packs for the requested path. */
+int32_t m2_vocoder_select(m2_model* model, int32_t path);
+
 /* ---- whole-inference entry points (M2TTSModel.inference, tts_model.py:402-438)
  * Two calls split at the one host read the path needs (T_max sizes the
  * outputs), so a step costs two host->library crossings instead of six:

@@ -51,6 +51,12 @@ int32_t hip_status(hipError_t e, const char* where) {
 }
 
 static constexpr int kRates[4] = {4, 4, 2, 2};  // tts_model.py:244
+// Receptive field of one audio sample in mel frames, per side: input_conv 1,
+// ConvT1 ~1 (two taps), then ResBlock/ConvT stages at 4x..64x, 3 frames in
+// total (tools/probe/receptive_field.py propagates the index intervals layer
+// by layer).  A window widened by this many frames computes every sample of
+// its centre exactly as the whole-utterance call does.
+static constexpr int kVocHalo = 3;
 
 
 // ---------------------------------------------------------------------------
@@ -165,6 +171,10 @@ struct m2_model {
     bool tailp = false;
     void* mbuf = nullptr;  // pipelined stage1 mid pack (vx.mp / vx.mpb)
     bool midp = false;
+    bool x3_packed = false;  // split-f16 packs exist (m2_vocoder_select can switch x3 on/off)
+    // streamed vocoder (m2_vocoder_set_chunking): chunks of chunk_frames mel
+    // frames, each computed over a window widened by kVocHalo frames per side
+    int chunk_frames = 0;
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
     mutable int prof_calls = 0;
@@ -228,6 +238,32 @@ void carve_voc(A& a, const m2_config& c, int B, int T, float** bufs) {
         float* p = a.template take<float>(n);
         if (bufs) bufs[i] = p;
     }
+}
+
+// Streamed vocoder scratch: the mel window [B, M, W] (or [B, W, M]), its
+// audio [B, 64 W] and the vocoder intermediates of a W-frame call, W = the
+// widest window (chunk + 2 halo frames, at most T).
+struct ChunkBufs {
+    float *mel, *audio, *voc[3];
+};
+
+template <typename A>
+void carve_chunked(A& a, const m2_config& c, int B, int T, int chunk, ChunkBufs* out) {
+    const int W = std::min(T, chunk + 2 * kVocHalo);
+    float* mel = a.template take<float>((size_t)B * c.mel_channels * W);
+    float* audio = a.template take<float>((size_t)B * 64 * W);
+    float* voc[3];
+    carve_voc(a, c, B, W, voc);
+    if (out) *out = ChunkBufs{mel, audio, {voc[0], voc[1], voc[2]}};
+}
+
+// Vocoder scratch of a T-frame call on this model (streamed when chunking is
+// set and T exceeds one chunk).
+size_t vocoder_ws_bytes(const m2_model* m, int B, int T) {
+    Sizer s;
+    if (m->chunk_frames > 0 && T > m->chunk_frames) carve_chunked(s, m->cfg, B, T, m->chunk_frames, nullptr);
+    else carve_voc(s, m->cfg, B, T, nullptr);
+    return s.off;
 }
 
 // Stage hand-off of m2_inference_front -> m2_inference_back: the encoder
@@ -561,6 +597,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 m->vx.wo = m->vw.wo;
                 m->vx.bo = m->vw.bo;
                 m->x3 = true;
+                m->x3_packed = true;
                 // stage1: the last two upsampling stages as one pipelined
                 // kernel (M2_VOC_TAIL_X3=1 keeps the x3 tail kernel).
                 if (M == 64 && C == 128 && !std::getenv("M2_VOC_TAIL_X3")) {
@@ -664,11 +701,10 @@ int32_t m2_model_config(const m2_model* model, m2_config* out) {
 size_t m2_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T) {
     if (!model || B < 0 || S < 0 || T < 0) return 0;
     const int H = model->cfg.hidden_dim;
-    Sizer a, b, c;
+    Sizer a, b;
     carve_tf(a, B, S, H, nullptr);
     carve_tf(b, B, T, H, nullptr);
-    carve_voc(c, model->cfg, B, T, nullptr);
-    return std::max(a.off, std::max(b.off, c.off)) + 256;
+    return std::max(a.off, std::max(b.off, vocoder_ws_bytes(model, B, T))) + 256;
 }
 
 }  // extern "C"
@@ -846,16 +882,110 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
                          m->cfg.mel_channels, out_mel, st);
 }
 
+}  // extern "C"
+
+namespace {
+int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
+                    float* const* buf, hipStream_t st);
+
+// Audio samples [64 f0, 64 f1) of every utterance of a T-frame mel, computed
+// over the window [f0 - halo, f1 + halo) clipped to [0, T): the window's mel
+// rows are copied to c.mel (same layout, T_w frames), vocoded as a T_w-frame
+// call, and the centre of its audio copied to out (row pitch out_pitch floats,
+// utterance b's chunk at out + b * out_pitch).
+int32_t vocoder_window(const m2_model* m, const float* mel, int32_t layout, int32_t B, int32_t T, int32_t f0,
+                       int32_t f1, float* out, size_t out_pitch, const ChunkBufs& c, hipStream_t st) {
+    const int M = m->cfg.mel_channels;
+    const int w0 = std::max(0, f0 - kVocHalo), w1 = std::min(T, f1 + kVocHalo), W = w1 - w0;
+    if (layout == 1)  // [B,T,M]: utterance b's window is W*M contiguous floats
+        M2_HIP(hipMemcpy2DAsync(c.mel, (size_t)W * M * 4, mel + (size_t)w0 * M, (size_t)T * M * 4, (size_t)W * M * 4, B,
+                                hipMemcpyDeviceToDevice, st));
+    else  // [B,M,T]: one W-float row per (utterance, channel)
+        M2_HIP(hipMemcpy2DAsync(c.mel, (size_t)W * 4, mel + w0, (size_t)T * 4, (size_t)W * 4, (size_t)B * M,
+                                hipMemcpyDeviceToDevice, st));
+    int32_t rc = vocoder_run(m, c.mel, layout, B, W, c.audio, c.voc, st);
+    if (rc) return rc;
+    M2_HIP(hipMemcpy2DAsync(out, out_pitch * 4, c.audio + (size_t)64 * (f0 - w0), (size_t)64 * W * 4,
+                            (size_t)64 * (f1 - f0) * 4, B, hipMemcpyDeviceToDevice, st));
+    return M2_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T,
                    float* out_audio, void* workspace, size_t workspace_bytes, void* stream) {
     M2_CHECK_ARG(m && mel && out_audio && B >= 0 && T >= 0, "m2_vocoder: bad argument");
     M2_CHECK_ARG(mel_layout == 0 || mel_layout == 1, "m2_vocoder: mel_layout must be 0 or 1");
     hipStream_t st = static_cast<hipStream_t>(stream);
     Carve a(workspace, workspace_bytes);
+    if (m->chunk_frames > 0 && T > m->chunk_frames) {  // streamed: chunk by chunk into out_audio
+        ChunkBufs c;
+        carve_chunked(a, m->cfg, B, T, m->chunk_frames, &c);
+        if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
+        if (B == 0) return M2_OK;
+        for (int f0 = 0; f0 < T; f0 += m->chunk_frames) {
+            const int f1 = std::min(T, f0 + m->chunk_frames);
+            const int32_t rc = vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_audio + (size_t)64 * f0,
+                                              (size_t)64 * T, c, st);
+            if (rc) return rc;
+        }
+        return M2_OK;
+    }
     float* buf[3];
     carve_voc(a, m->cfg, B, T, buf);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
+    return vocoder_run(m, mel, mel_layout, B, T, out_audio, buf, st);
+}
+
+int32_t m2_vocoder_chunk(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, int32_t f0,
+                         int32_t f1, float* out_chunk, void* workspace, size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && mel && out_chunk && B >= 0 && T >= 0, "m2_vocoder_chunk: bad argument");
+    M2_CHECK_ARG(mel_layout == 0 || mel_layout == 1, "m2_vocoder_chunk: mel_layout must be 0 or 1");
+    M2_CHECK_ARG(0 <= f0 && f0 < f1 && f1 <= T, "m2_vocoder_chunk: need 0 <= f0 < f1 <= T");
+    Carve a(workspace, workspace_bytes);
+    ChunkBufs c;
+    carve_chunked(a, m->cfg, B, T, f1 - f0, &c);
+    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder_chunk: workspace too small");
+    if (B == 0) return M2_OK;
+    return vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_chunk, (size_t)64 * (f1 - f0), c,
+                          static_cast<hipStream_t>(stream));
+}
+
+size_t m2_vocoder_chunk_workspace_bytes(const m2_model* m, int32_t B, int32_t T, int32_t chunk_frames) {
+    if (!m || B < 0 || T < 0 || chunk_frames <= 0) return 0;
+    Sizer s;
+    carve_chunked(s, m->cfg, B, T, chunk_frames, nullptr);
+    return s.off + 256;
+}
+
+int32_t m2_vocoder_set_chunking(m2_model* m, int32_t chunk_frames) {
+    M2_CHECK_ARG(m && chunk_frames >= 0, "m2_vocoder_set_chunking: bad argument");
+    m->chunk_frames = chunk_frames;
+    return M2_OK;
+}
+
+int32_t m2_vocoder_halo_frames(void) { return kVocHalo; }
+
+int32_t m2_vocoder_select(m2_model* m, int32_t path) {
+    M2_CHECK_ARG(m, "m2_vocoder_select: null model");
+    if (path == 2) {
+        M2_CHECK_ARG(m->x3_packed, "m2_vocoder_select: no split-f16 packs (shape unsupported, weights outside the "
+                                   "f16 range or M2_VOC_F32 set at creation)");
+        m->x3 = true;
+        return M2_OK;
+    }
+    M2_CHECK_ARG(path == 1 && m->fused, "m2_vocoder_select: path must be 1 (exact-f32) or 2 (split-f16)");
+    m->x3 = false;
+    return M2_OK;
+}
+
+}  // extern "C"
+
+namespace {
+int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
+                    float* const* buf, hipStream_t st) {
     int32_t rc;
     if (m->fused) {
         const int call = m->prof_calls;
@@ -885,6 +1015,9 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
     }
     return launch_conv(cur, m->vout_w, m->vout_b, nullptr, nullptr, nullptr, 3, ACT_TANH, false, B, ch, 1, L, out_audio, st);
 }
+}  // namespace
+
+extern "C" {
 
 int32_t m2_vocoder_resblock(const m2_model* m, int32_t k, const float* x, int32_t B, int32_t L,
                             float* y, float* tmp, void* stream) {
@@ -958,8 +1091,8 @@ const char* m2_profile_kernel_name(int32_t index) {
 
 const char* m2_profile_kernel_name_for(const m2_model* m, int32_t index) {
     if (!m || index < 0 || index >= kVocKernels) return "";
-    if (m->tailp && index == 2) return kVocTailpKernelName;
-    if (m->midp && index == 1) return kVocMidpKernelName;
+    if (m->x3 && m->tailp && index == 2) return kVocTailpKernelName;
+    if (m->x3 && m->midp && index == 1) return kVocMidpKernelName;
     return m->x3 ? kVocX3KernelNames[index] : kVocKernelNames[index];
 }
 
@@ -1010,10 +1143,9 @@ int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, co
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_inference_back: front buffer too small");
     // the regulated frames live after the decoder / vocoder scratch
     Carve w(workspace, workspace_bytes);
-    Sizer sz_tf, sz_voc;
+    Sizer sz_tf;
     carve_tf(sz_tf, B, T, H, nullptr);
-    carve_voc(sz_voc, m->cfg, B, T, nullptr);
-    const size_t scratch = std::max(sz_tf.off, sz_voc.off);
+    const size_t scratch = std::max(sz_tf.off, vocoder_ws_bytes(m, B, T));
     (void)w.take<char>(scratch);
     float* reg = w.take<float>((size_t)B * T * H);
     if (!w.ok) return fail(M2_E_WORKSPACE, "m2_inference_back: workspace too small");
@@ -1049,11 +1181,10 @@ int32_t m2_inference(const m2_model* m, const int64_t* ids, const int64_t* lengt
 size_t m2_inference_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T) {
     if (!model || B < 0 || S < 0 || T < 0) return 0;
     const int H = model->cfg.hidden_dim;
-    Sizer a, b, c, d;
+    Sizer a, b, d;
     carve_tf(a, B, S, H, nullptr);
     carve_tf(b, B, T, H, nullptr);
-    carve_voc(c, model->cfg, B, T, nullptr);
-    d.off = std::max(b.off, c.off);
+    d.off = std::max(b.off, vocoder_ws_bytes(model, B, T));
     (void)d.take<float>((size_t)B * T * H);
     return std::max(a.off, d.off) + 256;
 }

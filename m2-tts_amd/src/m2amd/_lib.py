@@ -45,7 +45,12 @@ _SIGNATURES = {
     "m2_length_regulator_expand": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "m2_mel_decoder": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
     "m2_vocoder": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
-    "m2_vocoder_resblock": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "m2_vocoder_set_chunking": (c_i32, [c_vp, c_i32]),
+    "m2_vocoder_halo_frames": (c_i32, []),
+    "m2_vocoder_chunk": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
+    "m2_vocoder_chunk_workspace_bytes": (c_size, [c_vp, c_i32, c_i32, c_i32]),
+    "m2_vocoder_select": (c_i32, [c_vp, c_i32]),
+    "m2_vocoder_resblock":(c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "m2_vocoder_upsample": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "m2_conv1d": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "m2_conv_transpose1d": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),

@@ -11,11 +11,17 @@ CPU tests):
   all_reduce(MAX)  1 x int32                       after the duration predictor
   all_gather       mel [b, T, M] and audio [b, 1, 64T] shards (padded to ceil(B/N))
 Payloads are KB..MB, so the path is latency-bound; weights are replicated.
+
+A step is two phases around the all-reduce: ``front`` (encoder, durations,
+frame counts -> local T_max) and ``back`` (expansion to the global T, decoder,
+vocoder).  On the GPU each phase is ONE library call (m2_inference_front /
+m2_inference_back); the oracle-backed ``Stages`` used by the CPU tests compose
+the same phases from per-stage functions.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Callable, Optional, Tuple
+from typing import Any, Callable, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -32,8 +38,8 @@ def shard_bounds(batch: int, world: int, rank: int) -> Tuple[int, int]:
 
 @dataclass
 class Stages:
-    """The per-shard stage functions.  ``hip_stages(model)`` binds the MI355X
-    kernels; tests bind the CPU oracle to check the sharding logic on gloo."""
+    """Per-shard stage functions composed into the two phases.  Tests bind the
+    CPU oracle here to check the sharding logic on gloo."""
     encode: Callable[[Tensor, Optional[Tensor]], Tensor]          # ids, lengths -> enc [b,S,H]
     durations: Callable[[Tensor], Tensor]                         # enc -> dur [b,S]
     frame_totals: Callable[[Tensor, float], Tensor]               # dur, scale -> T_b [b] (int)
@@ -41,26 +47,33 @@ class Stages:
     decode: Callable[[Tensor], Tensor]                            # [b,T,H] -> mel [b,T,M]
     vocode: Callable[[Tensor], Tensor]                            # mel [b,T,M] -> audio [b,1,64T]
 
+    def front(self, ids: Tensor, lens: Optional[Tensor], scale: float) -> Tuple[Any, int]:
+        enc = self.encode(ids, lens)
+        dur = self.durations(enc)
+        return (enc, dur, scale), int(self.frame_totals(dur, scale).max().item())
 
-def hip_stages(model) -> Stages:
-    from . import ops
+    def back(self, state: Any, T: int) -> Tuple[Tensor, Tensor]:
+        enc, dur, scale = state
+        mel = self.decode(self.regulate(enc, dur, T, scale))
+        return mel, self.vocode(mel)
 
-    def hm(t):
-        return model._hip(t.device)
 
-    def frame_totals(dur, scale):
-        _, tot, _ = ops.frame_counts(dur, scale)
-        return tot
+class HipStages:
+    """The MI355X phases: one m2_inference_front and one m2_inference_back call
+    per step on the model's packed handle (models/tts_model.py)."""
 
-    def regulate(enc, dur, T, scale):
-        cum, _, _ = ops.frame_counts(dur, scale)
-        return ops.expand_frames(enc, cum, T)
+    def __init__(self, model):
+        self.model = model
 
-    return Stages(encode=lambda ids, lens: hm(ids).text_encoder(ids, lens)[0],
-                  durations=lambda enc: hm(enc).duration(enc),
-                  frame_totals=frame_totals, regulate=regulate,
-                  decode=lambda x: hm(x).decoder(x),
-                  vocode=lambda mel: hm(mel).vocoder(mel, layout_btm=True))
+    def front(self, ids: Tensor, lens: Optional[Tensor], scale: float) -> Tuple[Any, int]:
+        return self.model._hip(ids.device).inference_front(ids, lens, scale)
+
+    def back(self, state: Any, T: int) -> Tuple[Tensor, Tensor]:
+        return self.model._hip(state[2].device).inference_back(state, T)
+
+
+def hip_stages(model) -> HipStages:
+    return HipStages(model)
 
 
 def _gather_shards(local: Tensor, batch: int, world: int, group) -> Tensor:
@@ -74,7 +87,14 @@ def _gather_shards(local: Tensor, batch: int, world: int, group) -> Tensor:
     return torch.cat(out, dim=0)
 
 
-def sharded_inference(stages: Stages, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor],
+def _collective_device(ids: Tensor, group) -> torch.device:
+    """nccl (RCCL) reduces device tensors only; gloo host tensors."""
+    if dist.is_initialized() and dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device()) if not ids.is_cuda else ids.device
+    return torch.device("cpu")
+
+
+def sharded_inference(stages, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor],
                       duration_scale: float = 1.0, group=None, gather: bool = True):
     """M2TTSModel.inference (tts_model.py:402-438) over a global batch sharded by
     utterance.  Every rank passes the same global ``phoneme_ids``/lengths
@@ -90,24 +110,13 @@ def sharded_inference(stages: Stages, phoneme_ids: Tensor, phoneme_lengths: Opti
     ids = phoneme_ids[lo:hi]
     lens = phoneme_lengths[lo:hi] if phoneme_lengths is not None else None
     with torch.no_grad():
-        if hi > lo:
-            enc = stages.encode(ids, lens)
-            dur = stages.durations(enc)
-            t_local = int(stages.frame_totals(dur, duration_scale).max().item())
-        else:
-            enc = dur = None
-            t_local = 0
-        t = torch.tensor([t_local], dtype=torch.int32,
-                         device=phoneme_ids.device if phoneme_ids.is_cuda else "cpu")
+        state, t_local = stages.front(ids, lens, duration_scale) if hi > lo else (None, 0)
         if world > 1:
+            t = torch.tensor([t_local], dtype=torch.int32, device=_collective_device(phoneme_ids, group))
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-        T = max(1, int(t.item()))  # all-empty batch -> one zero frame (tts_model.py:158-160)
-        if hi > lo:
-            reg = stages.regulate(enc, dur, T, duration_scale)
-            mel = stages.decode(reg)
-            audio = stages.vocode(mel)
-        else:
-            mel = audio = None
+            t_local = int(t.item())
+        T = max(1, t_local)  # all-empty batch -> one zero frame (tts_model.py:158-160)
+        mel, audio = stages.back(state, T) if hi > lo else (None, None)
     if not gather or world == 1:
         return (mel, audio) if gather else (mel, audio, (lo, hi))
     return _gather_shards(mel, B, world, group), _gather_shards(audio, B, world, group)

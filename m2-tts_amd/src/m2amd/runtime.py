@@ -93,7 +93,9 @@ class HipModel:
                                            ctypes.byref(handle)), "m2_model_create")
         self.handle = handle
         self._ws: Optional[Tensor] = None
+        self._ws_chunk: Optional[Tensor] = None
         self._front: Optional[Tensor] = None
+        self.chunk_frames = 0
         self._sizes: Dict[Tuple, int] = {}
         self._tcap: Dict[Tuple[int, int], int] = {}
         self._finalizer = weakref.finalize(self, lib.m2_model_destroy, handle)
@@ -164,6 +166,67 @@ class HipModel:
         if T > cap or 2 * T < cap:
             self._tcap[(B, S)] = (T + 31) // 32 * 32
         return mel, audio
+
+    def inference_front(self, ids: Tensor, lengths: Optional[Tensor], scale: float) -> Tuple[Tuple, int]:
+        """Front half of inference (m2_inference_front): encoder, durations,
+        frame counts; returns (hand-off state, this batch's T_max) after the
+        one host read.  The hand-off lives in this model's front buffer, so
+        the matching inference_back must come before the next front call."""
+        require_device(ids, lengths, what="M2TTSModel")
+        ids = ids.to(torch.int64).contiguous()
+        B, S = ids.shape
+        lens = lengths.to(torch.int64).contiguous() if lengths is not None else None
+        front = self._scratch("_front", self._size("m2_front_bytes", B, S))
+        ws = self._scratch("_ws", self._size("m2_inference_workspace_bytes", B, S, 0))
+        tmax = ctypes.c_int32(0)
+        _lib.call("m2_inference_front", self.handle, ids.data_ptr(), None if lens is None else lens.data_ptr(), B, S,
+                  float(scale), front.data_ptr(), front.numel(), ws.data_ptr(), ws.numel(), ctypes.byref(tmax),
+                  stream_handle(self.device))
+        return (B, S, front, ids, lens), int(tmax.value)
+
+    def inference_back(self, state: Tuple, T: int) -> Tuple[Tensor, Tensor]:
+        """Back half (m2_inference_back): expansion to exactly T frames (a
+        batch-global T when sharded), mel decoder, vocoder."""
+        B, S, front, _ids, _lens = state
+        mel = torch.empty(B, T, self.M, device=self.device, dtype=torch.float32)
+        audio = torch.empty(B, 1, 64 * T, device=self.device, dtype=torch.float32)
+        ws = self._scratch("_ws", self._size("m2_inference_workspace_bytes", B, S, T))
+        _lib.call("m2_inference_back", self.handle, B, S, T, front.data_ptr(), front.numel(), mel.data_ptr(),
+                  audio.data_ptr(), ws.data_ptr(), ws.numel(), stream_handle(self.device))
+        return mel, audio
+
+    # ------------------------------------------------------------------ vocoder modes
+    def vocoder_select(self, path: int):
+        """1 = exact-f32 MFMA kernels, 2 = split-f16 MFMA kernels (m2_vocoder_select)."""
+        _lib.call("m2_vocoder_select", self.handle, int(path))
+
+    def vocoder_path(self) -> int:
+        return int(_lib.load().m2_vocoder_path(self.handle))
+
+    def set_chunking(self, chunk_frames: int):
+        """Stream the vocoder in chunks of chunk_frames mel frames (0 = off)."""
+        _lib.call("m2_vocoder_set_chunking", self.handle, int(chunk_frames))
+        self._sizes.clear()  # workspace sizes depend on it
+        self.chunk_frames = int(chunk_frames)
+
+    def vocoder_stream(self, mel: Tensor, chunk_frames: int, layout_btm: bool = False):
+        """Yield the audio of mel frames [f0, f0 + chunk_frames) as [B,1,64*n]
+        tensors in order (m2_vocoder_chunk); concatenated they equal
+        vocoder(mel) bit for bit."""
+        mel = f32c(mel)
+        require_device(mel, what="SimpleVocoder")
+        B = mel.shape[0]
+        T = mel.shape[1] if layout_btm else mel.shape[2]
+        if chunk_frames <= 0:
+            raise ValueError("chunk_frames must be positive")
+        ws = self._scratch("_ws_chunk", self._size("m2_vocoder_chunk_workspace_bytes", B, T, chunk_frames))
+        st = stream_handle(self.device)
+        for f0 in range(0, T, chunk_frames):
+            f1 = min(T, f0 + chunk_frames)
+            out = torch.empty(B, 1, 64 * (f1 - f0), device=self.device, dtype=torch.float32)
+            _lib.call("m2_vocoder_chunk", self.handle, mel.data_ptr(), 1 if layout_btm else 0, B, T, f0, f1,
+                      out.data_ptr(), ws.data_ptr(), ws.numel(), st)
+            yield out
 
     # ------------------------------------------------------------------ stages
     def text_encoder(self, ids: Tensor, lengths: Optional[Tensor]):
@@ -238,8 +301,18 @@ class HandleCache:
         if ent is not None and ent[0] == key:
             return ent[1]
         hm = HipModel(module.state_dict(), cfg, device)
+        # per-model vocoder modes survive a rebuild (weights reloaded, .to())
+        chunk = module.__dict__.get("_m2_chunk_frames", 0)
+        if chunk:
+            hm.set_chunking(chunk)
+        path = module.__dict__.get("_m2_voc_path")
+        if path:
+            hm.vocoder_select(path)
         self._entries[device] = (key, hm)
         return hm
+
+    def handles(self):
+        return [hm for _, hm in self._entries.values()]
 
     def clear(self):
         self._entries.clear()

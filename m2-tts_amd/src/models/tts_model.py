@@ -38,6 +38,7 @@ logger = logging.getLogger(__name__)
 Tensor = torch.Tensor
 
 UPSAMPLE_RATES = (4, 4, 2, 2)   # reference tts_model.py:244
+VOCODER_HALO = 3                # receptive field of one audio sample, mel frames per side (m2_vocoder_halo_frames)
 _HANDLES: "weakref.WeakKeyDictionary[nn.Module, HandleCache]" = weakref.WeakKeyDictionary()
 
 
@@ -161,6 +162,25 @@ class SimpleVocoder(nn.Module):
             x = rb(x)
         return ops.conv1d(x, self.output_conv.weight, self.output_conv.bias, act=ops.ACT_TANH)
 
+    def stream(self, mel: Tensor, chunk_frames: int = 256):
+        """Yield the audio of mel [B, M, T] chunk by chunk ([B, 1, 64 n] for
+        n <= chunk_frames frames each), for playback while later chunks are
+        still being computed.  Each chunk is computed over its window widened
+        by the vocoder's receptive field (VOCODER_HALO frames per side): the
+        chunks concatenate to exactly forward(mel) (the reference's one-shot
+        output, tts_model.py:279-297)."""
+        if chunk_frames <= 0:
+            raise ValueError("chunk_frames must be positive")
+        hm = _owner_handle(self, "vocoder", mel.device)
+        if hm is not None:
+            yield from hm.vocoder_stream(mel, chunk_frames)
+            return
+        T = mel.shape[2]
+        for f0 in range(0, T, chunk_frames):
+            f1 = min(T, f0 + chunk_frames)
+            w0, w1 = max(0, f0 - VOCODER_HALO), min(T, f1 + VOCODER_HALO)
+            yield self.forward(mel[:, :, w0:w1])[:, :, 64 * (f0 - w0):64 * (f1 - w0)].contiguous()
+
 
 class M2TTSModel(nn.Module):
     """Text encoder -> duration predictor -> length regulator -> mel decoder ->
@@ -206,6 +226,26 @@ class M2TTSModel(nn.Module):
             cache = HandleCache()
             _HANDLES[self] = cache
         return cache.get(self, self._m2_cfg, device)
+
+    def set_vocoder_chunking(self, chunk_frames: int = 256):
+        """Stream the vocoder in chunks of ``chunk_frames`` mel frames inside
+        forward/inference/vocoder (0 = whole utterance).  Each chunk is
+        computed over a window widened by the vocoder's 3-frame receptive
+        field, so the audio is bit-identical to the unchunked call; the
+        workspace holds one window instead of the whole utterance."""
+        self.__dict__["_m2_chunk_frames"] = int(chunk_frames)
+        cache = _HANDLES.get(self)
+        for hm in (cache.handles() if cache is not None else []):
+            hm.set_chunking(chunk_frames)
+
+    def set_vocoder_precision(self, precision: str = "split"):
+        """"split" = split-f16 MFMA kernels (fp32 operands as f16 hi/lo pairs,
+        the default), "f32" = exact-f32 MFMA kernels."""
+        path = {"split": 2, "f32": 1}[precision]
+        self.__dict__["_m2_voc_path"] = path
+        cache = _HANDLES.get(self)
+        for hm in (cache.handles() if cache is not None else []):
+            hm.vocoder_select(path)
 
     # -------------------------------------------------------------- forward
     def forward(self, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor] = None,

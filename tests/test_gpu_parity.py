@@ -242,9 +242,18 @@ def _check_fingerprint(fp, mel, audio):
     # sum of squares: |d(sumsq)| <= 2*sqrt(sumsq)*||err|| ~ 2*sqrt(n*ms)*sqrt(n)*rms_tol
     np.testing.assert_allclose(a.pow(2).sum(1).numpy(), fp["audio_sumsq"], rtol=2e-3, atol=n * 1e-6)
     np.testing.assert_allclose(a.abs().amax(1).numpy(), fp["audio_maxabs"], atol=1e-3)
+    np.testing.assert_allclose(a.sum(1).numpy(), fp["audio_sum"], rtol=1e-4, atol=n * 1e-6)
     if "mel_head" in fp.files:
         assert maxabs(mel[:, :4], fp["mel_head"]) <= MEL_MAXABS_TOL
         assert maxabs(mel[:, -4:], fp["mel_tail"]) <= MEL_MAXABS_TOL
+        m = mel.double().cpu().flatten(1)
+        nm = m.shape[1]
+        # whole-tensor mel statistics: a per-value error e moves the sum by <= nm*e
+        # and the sum of squares by <= 2*sum|m|*e (observed e ~ 2e-6; bound at 1e-5)
+        np.testing.assert_allclose(m.sum(1).numpy(), fp["mel_sum"], rtol=0, atol=nm * 1e-5)
+        np.testing.assert_allclose(m.pow(2).sum(1).numpy(), fp["mel_sumsq"], rtol=0,
+                                   atol=(2 * m.abs().sum(1) * 1e-5).numpy())
+        np.testing.assert_allclose(m.abs().amax(1).numpy(), fp["mel_maxabs"], rtol=0, atol=MEL_MAXABS_TOL)
     assert B == fp["audio_head"].shape[0]
 
 
@@ -274,12 +283,23 @@ def test_pipeline_bench_shapes(gpu, stage, B, S):
 
 
 def test_pipeline_longform_stage2(gpu):
-    """B=128, S=520 -> T=2600 (30.2 s of mel at hop 256): fingerprints only."""
+    """B=128, S=520 -> T=2600 (30.2 s of mel at hop 256): fingerprints of all
+    128 utterances, and full tensors of the first and last utterance against
+    the oracle run on those two (every utterance has T=2600, so the two-row
+    batch pads to the same global T as the 128-row one)."""
     fp = golden("fp_s2_B128_S520")
     m = build_model("s2", gpu)
-    mel, audio = m.inference(torch.from_numpy(fp["ids"]).to(gpu), torch.from_numpy(fp["lengths"]).to(gpu))
+    ids, lens = torch.from_numpy(fp["ids"]), torch.from_numpy(fp["lengths"])
+    mel, audio = m.inference(ids.to(gpu), lens.to(gpu))
     assert audio.shape == (128, 1, 64 * 2600)
     _check_fingerprint(fp, mel, audio)
+    rows = [0, 127]
+    assert all(int(fp["T"][r]) == 2600 for r in rows)
+    ref_mel, ref_audio = orc.inference(golden_state("s2"), stage_config("s2"), ids[rows], lens[rows], as_written=False)
+    assert ref_mel.shape == (2, 2600, 80)
+    assert maxabs(mel[rows], ref_mel) <= MEL_MAXABS_TOL
+    assert rms(audio[rows], ref_audio) <= AUDIO_RMS_TOL
+    assert maxabs(audio[rows], ref_audio) <= 1e-3
 
 
 def test_repeatable_and_stream_ordered(gpu):

@@ -98,6 +98,31 @@ def test_get_model_size_counts():
     assert info2["total_params"] == 1066610
 
 
+def test_vocoder_halo_is_the_receptive_field():
+    """The streamed vocoder's halo (C constant, Python constant) equals the
+    receptive field propagated through the reference's layer stack."""
+    import sys
+    sys.path.insert(0, str(ROOT / "tools" / "probe"))
+    import receptive_field
+    from m2amd import _lib
+    from models.tts_model import VOCODER_HALO
+    assert receptive_field.halo_frames() == (3, 3)
+    assert _lib.load().m2_vocoder_halo_frames() == VOCODER_HALO == 3
+
+
+def test_oracle_vocoder_chunked_within_reorder_noise():
+    """The oracle (reference ATen ops) on a 3-frame-halo window gives the same
+    centre samples up to fp32 reordering noise (7e-7)."""
+    import m2tts_oracle as orc
+    from conftest import golden_state
+    sd = golden_state("s1")
+    mel = torch.randn(1, 64, 40, generator=torch.Generator().manual_seed(5))
+    full = orc.vocoder(sd, mel)
+    f0, f1 = 12, 25
+    win = orc.vocoder(sd, mel[:, :, f0 - 3:f1 + 3])
+    assert float((win[:, :, 64 * 3:64 * (3 + f1 - f0)] - full[:, :, 64 * f0:64 * f1]).abs().max()) <= 2e-6
+
+
 def test_bench_flop_model():
     import importlib.util
     spec = importlib.util.spec_from_file_location("bench", ROOT / "bench.py")

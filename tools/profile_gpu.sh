@@ -10,9 +10,9 @@ out=gpurun_out/prof_$tag
 mkdir -p $out
 # enough warm-up for the clocks to settle (bench.py's default), so the kernel
 # averages match the bench's own HIP-event timings
-BENCH="python3 bench.py --steps 100 --warmup 300 --no-cpu-baseline --no-pipeline-extra $*"
+BENCH="python3 bench.py --steps 100 --warmup 100 --no-cpu-baseline --no-extras $*"
 # PMC passes: counters per dispatch, so a few timed steps are enough
-PMCBENCH="python3 bench.py --steps 4 --warmup 300 --no-cpu-baseline --no-pipeline-extra $*"
+PMCBENCH="python3 bench.py --steps 4 --warmup 20 --no-cpu-baseline --no-extras $*"
 run() {  # name, rocprof args...
   local name=$1; shift
   local cmd=$PMCBENCH
