@@ -23,7 +23,7 @@ Workloads (BASELINE.json configs):
   s2_b64       configs[3]: stage2 M2TTSModel.inference over a GLOBAL batch of 64
                utterances (100 phonemes -> T=500) sharded by utterance across
                the N ranks (m2amd.parallel.sharded_inference: RCCL all_reduce(MAX)
-               of the frame count + all_gather of mel/audio); strong scaling
+               of the frame count + gather of mel/audio to rank 0); strong scaling
   s2_longform  configs[4]: the same with a global batch of 128 utterances of
                520 phonemes -> T=2600 mel frames (30.2 s at hop 256), vocoder
                streamed in 256-frame chunks (3-frame halo)
@@ -216,9 +216,12 @@ def parse_args(argv=None):
                     default="vocoder")
     ap.add_argument("--batch", type=int, default=32, help="utterances per GPU (vocoder / pipeline)")
     ap.add_argument("--phonemes", type=int, default=100)
+    ap.add_argument("--s2-shape", default="8x500", help="BxT of the s2_vocoder workload")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline line only")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL (default); gloo only to rehearse N ranks sharing one GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group, all-reduce, print one line")
     return ap.parse_args(argv)
@@ -252,6 +255,7 @@ class Ctx:
         self._lib = _lib
         self.nk = self.lib.m2_profile_kernel_count()
         self.models = {}
+        self.backend = "RCCL"
 
     def model(self, stage: str):
         if stage not in self.models:
@@ -267,7 +271,7 @@ class Ctx:
         if not self.dist:
             return v
         import torch.distributed as td
-        t = torch.tensor([v], device=self.dev, dtype=torch.float64)
+        t = torch.tensor([v], device=self.dev if self.backend == "RCCL" else "cpu", dtype=torch.float64)
         td.all_reduce(t, op=td.ReduceOp.MAX)
         return float(t.item())
 
@@ -423,10 +427,12 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
         ids = torch.randint(0, 42, (Bg, S), generator=g).to(cx.dev)
         lens = torch.full((Bg,), S, dtype=torch.long, device=cx.dev)
         st = hip_stages(m)
-        step = lambda: sharded_inference(st, ids, lens)  # noqa: E731
+        # the global batch's mel / audio are gathered to rank 0 (RCCL gather over xGMI)
+        step = lambda: sharded_inference(st, ids, lens, gather_to=0)  # noqa: E731
         mel, audio = step()
-        T = mel.shape[1]
-        assert mel.shape[0] == Bg and audio.shape == (Bg, 1, 64 * T)
+        T = 5 * S  # pinned durations: every utterance has 5 frames per phoneme
+        if cx.rank == 0:
+            assert mel.shape == (Bg, T, 80) and audio.shape == (Bg, 1, 64 * T)
         settled = cx.settle(step, settle_ms)
         elapsed, _ = cx.timed(step, steps, 2)
         # split of one step: front (incl. the T_max host read) / all_reduce / back, rank-local wall times
@@ -437,7 +443,7 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
         state, tl = hm.inference_front(ids[lo:hi], lens[lo:hi], 1.0)
         t1 = time.perf_counter()
         if cx.dist:
-            t = torch.tensor([tl], dtype=torch.int32, device=cx.dev)
+            t = torch.tensor([tl], dtype=torch.int32, device=cx.dev if cx.backend == "RCCL" else "cpu")
             td.all_reduce(t, op=td.ReduceOp.MAX)
             tl = int(t.item())
         t2 = time.perf_counter()
@@ -452,7 +458,7 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
             "rtf_x_realtime": round(samples_per(Bg, T) * steps / elapsed / SAMPLE_RATE, 1),
             "config": {"stage": "stage2_quality", "global_batch": Bg, "per_gpu_batch": hi - lo, "phonemes": S,
                        "mel_frames": T, "vocoder_chunk_frames": chunk, "n_ranks": cx.world,
-                       "collectives": "all_reduce(MAX) 1 x int32 + all_gather mel/audio (RCCL)" if cx.dist
+                       "collectives": f"all_reduce(MAX) 1 x int32 + gather of mel/audio to rank 0 ({cx.backend})" if cx.dist
                        else "none (world 1)"},
             "rank0_phase_ms": {"front_incl_Tmax_read": round((t1 - t0) * 1e3, 3),
                                "all_reduce": round((t2 - t1) * 1e3, 3),
@@ -470,11 +476,16 @@ def run(args):
     if dist:
         import torch.distributed as td
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks may share a GPU
         torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            td.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cx = Ctx(dev, world, rank, dist)
+    cx.backend = "RCCL" if args.dist_backend == "nccl" else "gloo"
     B, S = args.batch, args.phonemes
     wl = args.workload
     extras = {}
@@ -483,8 +494,9 @@ def run(args):
         head = vocoder_line(cx, "s1", B, 5 * S, args, args.settle_ms, 1000)
         desc = "stage1_poc SimpleVocoder B=32 per GPU (configs[1])"
     elif wl == "s2_vocoder":
-        head = vocoder_line(cx, "s2", 8, 500, args, args.settle_ms, 3000)
-        desc = "stage2_quality SimpleVocoder B=8 T=500 per GPU (configs[3] per-GPU shape)"
+        b2, t2 = (int(v) for v in args.s2_shape.split("x"))
+        head = vocoder_line(cx, "s2", b2, t2, args, args.settle_ms, 3000)
+        desc = f"stage2_quality SimpleVocoder B={b2} T={t2} per GPU (configs[3] per-GPU shape: 8x500)"
     elif wl == "pipeline":
         head = pipeline_line(cx, B, S, args, args.settle_ms)
         desc = head["config"]["workload"]

@@ -76,15 +76,29 @@ def hip_stages(model) -> HipStages:
     return HipStages(model)
 
 
-def _gather_shards(local: Tensor, batch: int, world: int, group) -> Tensor:
-    """all_gather of per-rank utterance shards with unequal sizes -> [batch, ...]."""
+def _gather_shards(local: Tensor, batch: int, world: int, group, dst: Optional[int] = None) -> Optional[Tensor]:
+    """Gather per-rank utterance shards of unequal sizes -> [batch, ...]:
+    all_gather (every rank gets the batch) or, with ``dst``, gather to that
+    rank only (the others return None)."""
     per = -(-batch // world)
-    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
-    out = [parts[r][: shard_bounds(batch, world, r)[1] - shard_bounds(batch, world, r)[0]] for r in range(world)]
-    return torch.cat(out, dim=0)
+    if local.shape[0] == per:
+        pad = local.contiguous()
+    else:
+        pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad[: local.shape[0]] = local
+    me = dist.get_rank(group)
+    if dst is None:
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+    else:
+        parts = [torch.empty_like(pad) for _ in range(world)] if me == dst else None
+        dist.gather(pad, parts, dst=dist.get_global_rank(group, dst) if group is not None else dst, group=group)
+        if me != dst:
+            return None
+    n = [shard_bounds(batch, world, r)[1] - shard_bounds(batch, world, r)[0] for r in range(world)]
+    if all(k == per for k in n):
+        return torch.stack(parts).flatten(0, 1) if world > 1 else parts[0]
+    return torch.cat([parts[r][: n[r]] for r in range(world)], dim=0)
 
 
 def _collective_device(ids: Tensor, group) -> torch.device:
@@ -95,12 +109,14 @@ def _collective_device(ids: Tensor, group) -> torch.device:
 
 
 def sharded_inference(stages, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor],
-                      duration_scale: float = 1.0, group=None, gather: bool = True):
+                      duration_scale: float = 1.0, group=None, gather: bool = True,
+                      gather_to: Optional[int] = None):
     """M2TTSModel.inference (tts_model.py:402-438) over a global batch sharded by
     utterance.  Every rank passes the same global ``phoneme_ids``/lengths
     (or the same seed-generated tensors); rank r computes utterances
     shard_bounds(B, N, r).  Returns (mel, audio) for the global batch when
-    ``gather``, else this rank's shard and its bounds."""
+    ``gather`` (on every rank; with ``gather_to=r`` on rank r only, None
+    elsewhere), else this rank's shard and its bounds."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     B = phoneme_ids.shape[0]
@@ -119,4 +135,5 @@ def sharded_inference(stages, phoneme_ids: Tensor, phoneme_lengths: Optional[Ten
         mel, audio = stages.back(state, T) if hi > lo else (None, None)
     if not gather or world == 1:
         return (mel, audio) if gather else (mel, audio, (lo, hi))
-    return _gather_shards(mel, B, world, group), _gather_shards(audio, B, world, group)
+    return (_gather_shards(mel, B, world, group, gather_to),
+            _gather_shards(audio, B, world, group, gather_to))

@@ -45,8 +45,14 @@ def _worker(rank, world, port, outfile):
         for tag, (i, l, scale) in {"b2": (ids, lens, 1.0), "b5": (ids5, lens5, 1.0), "b5s": (ids5, lens5, 1.3)}.items():
             mel, audio = sharded_inference(st, i, l, duration_scale=scale)
             out[tag] = (mel, audio)
+        # gather to one rank only (the serving layout: rank 1 collects, rank 0 gets None)
+        mel_r, audio_r = sharded_inference(st, ids5, lens5, gather_to=1)
+        assert (mel_r is None) == (rank != 1) and (audio_r is None) == (rank != 1)
+        import numpy as np
+        if rank == 1:
+            np.savez(outfile + ".root1.npz", mel=mel_r.numpy(), audio=audio_r.numpy())
+        dist.barrier()
         if rank == 0:
-            import numpy as np
             np.savez(outfile, **{f"{k}_{j}": v[j].numpy() for k, v in out.items() for j in range(2)})
     finally:
         dist.destroy_process_group()
@@ -66,6 +72,8 @@ def test_sharded_inference_matches_unsharded_two_ranks(tmp_path):
     mp.spawn(_worker, args=(2, _free_port(), outfile), nprocs=2, join=True)
     z = np.load(outfile)
     res = {k: (z[f"{k}_0"], z[f"{k}_1"]) for k in ("b2", "b5", "b5s")}
+    r1 = np.load(outfile + ".root1.npz")
+    assert np.array_equal(r1["mel"], res["b5"][0]) and np.array_equal(r1["audio"], res["b5"][1])
     sd = golden_state("s1")
     g = golden("s1_target_free")
     ids, lens = torch.from_numpy(g["ids"]), torch.from_numpy(g["lengths"])
