@@ -38,6 +38,9 @@ extern "C" {
 #define M2_E_WORKSPACE (-3)   /* workspace smaller than m2_workspace_bytes()  */
 #define M2_E_WEIGHTS (-4)     /* weight table incomplete                      */
 #define M2_E_INTERNAL (-5)    /* internal protocol failure (see m2_last_error) */
+#define M2_E_RANGE (-6)       /* an earlier vocoder call on this model produced non-finite audio
+                                 on the split-f16 path (input or activation outside its range);
+                                 see m2_model_check / m2_set_range_policy                        */
 
 /* M2TTSModel.__init__ hyper-parameters (tts_model.py:303-313), plus the
  * positional-encoding table length (TextEncoder max_seq_len, tts_model.py:29). */
@@ -154,6 +157,23 @@ int32_t m2_vocoder_chunk(const m2_model* model, const float* mel, int32_t mel_la
                          size_t workspace_bytes, void* stream);
 size_t m2_vocoder_chunk_workspace_bytes(const m2_model* model, int32_t B, int32_t T,
                                         int32_t chunk_frames);
+
+/* ---- range of the split-f16 arithmetic -------------------------------------
+ * The split path carries fp32 values as f16 hi/lo pairs; a value of magnitude
+ * >= 65520 (input mel or any activation) becomes hi = inf, lo = NaN, and the
+ * NaN reaches the audio, whose last kernel raises a per-model flag (never a
+ * silently wrong finite result).  Transformer activations are bounded by the
+ * LayerNorm weights and checked once at m2_model_create (out of range -> the
+ * exact-f32 transformer kernels).  What a raised flag does:
+ *   policy 0 (report, default): asynchronous, like a HIP kernel error - the
+ *     next m2_vocoder / m2_inference* call on the model returns M2_E_RANGE
+ *     (and clears the flag); m2_model_check synchronises `stream` and
+ *     reports it at once (*flagged = 1, flag cleared).
+ *   policy 1 (fallback): m2_vocoder synchronises after its kernels and, when
+ *     the flag is up, recomputes the call on the exact-f32 kernels (the
+ *     reference's fp32 result, non-finite only if the reference's is). */
+int32_t m2_set_range_policy(m2_model* model, int32_t policy);
+int32_t m2_model_check(m2_model* model, void* stream, int32_t* flagged);
 
 /* Select the vocoder arithmetic at run time: 1 = exact-f32 MFMA kernels,
  * 2 = split-f16 MFMA kernels (the default when the model has their packs).
@@ -279,6 +299,10 @@ const char* m2_profile_kernel_name_for(const m2_model* model, int32_t index);
  * MFMA (v_mfma_f32_16x16x4_f32), 2 fused split-f16 MFMA (fp32 operands as
  * f16 hi/lo pairs, 3 products per fp32 product, fp32 accumulation). */
 int32_t m2_vocoder_path(const m2_model* model);
+/* Transformer arithmetic of this model: 1 = fused split-f16 layers and
+ * attention, 0 = fp32 linears and the exact-f32 attention (weights whose
+ * activation bound leaves the f16 range, or M2_TF_UNFUSED / M2_ATT_F32). */
+int32_t m2_transformer_path(const m2_model* model);
 
 #ifdef __cplusplus
 }

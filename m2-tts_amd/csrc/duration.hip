@@ -162,52 +162,58 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
 // totals, stores Tmax and posts (seq, Tmax) to a host-mapped mailbox with
 // system-scope stores (Tmax first, then seq with release order), which the
 // host polls instead of a device->host copy and a stream synchronisation.
+// Frame counts are clamped to 2^30 per phoneme and summed in 64 bits; the
+// stored prefix sums and totals saturate at INT32_MAX (the host rejects a
+// T_max above m2's frame limit with M2_E_SHAPE instead of wrapping).
+__device__ __forceinline__ int32_t sat32(long long v) { return (int32_t)min(v, (long long)INT32_MAX); }
+
 template <bool SYNC>
 __global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ dur, int is_int,
                                                        float scale, int S, int32_t* __restrict__ cum,
                                                        int32_t* __restrict__ T,
                                                        int32_t* __restrict__ Tmax, unsigned* __restrict__ ticket,
                                                        int32_t* __restrict__ mbox, int32_t seq) {
-    __shared__ int part[256];
+    __shared__ long long part[256];
     const int b = blockIdx.x, tid = threadIdx.x;
     const int chunk = (S + 255) / 256;
     const int lo = min(S, tid * chunk), hi = min(S, lo + chunk);
     const size_t base = (size_t)b * S;
-    int sum = 0;
+    long long sum = 0;
     for (int s = lo; s < hi; ++s) sum += frames_of(dur, is_int, scale, base + s);
     part[tid] = sum;
     __syncthreads();
     // Hillis-Steele inclusive scan over the 256 partials.
     for (int off = 1; off < 256; off <<= 1) {
-        const int v = tid >= off ? part[tid - off] : 0;
+        const long long v = tid >= off ? part[tid - off] : 0;
         __syncthreads();
         part[tid] += v;
         __syncthreads();
     }
-    int run = part[tid] - sum;  // exclusive prefix of this thread's chunk
+    long long run = part[tid] - sum;  // exclusive prefix of this thread's chunk
     int32_t* c = cum + (size_t)b * (S + 1);
     if (tid == 0) c[0] = 0;
     for (int s = lo; s < hi; ++s) {
         run += frames_of(dur, is_int, scale, base + s);
-        c[s + 1] = run;
+        c[s + 1] = sat32(run);
     }
+    const int32_t total = sat32(part[255]);
     if constexpr (!SYNC) {
         if (tid == 255) {
-            T[b] = part[255];
-            atomicMax(Tmax, part[255]);
+            T[b] = total;
+            atomicMax(Tmax, total);
         }
     } else {
         __shared__ bool last;
         if (tid == 255) {
-            __hip_atomic_store(T + b, part[255], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(T + b, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __atomic_thread_fence(__ATOMIC_RELEASE);  // totals before the ticket
             last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
         }
         __syncthreads();
         if (last) {  // every other workgroup's total is visible
-            int m = 0;
+            long long m = 0;
             for (int i = tid; i < (int)gridDim.x; i += 256)
-                m = max(m, __hip_atomic_load(T + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                m = max(m, (long long)__hip_atomic_load(T + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             part[tid] = m;
             __syncthreads();
             for (int off = 128; off > 0; off >>= 1) {
@@ -215,9 +221,10 @@ __global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ 
                 __syncthreads();
             }
             if (tid == 0) {
-                *Tmax = part[0];
+                const int32_t tm = sat32(part[0]);
+                *Tmax = tm;
                 __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(mbox + 1, part[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(mbox + 1, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(mbox, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }

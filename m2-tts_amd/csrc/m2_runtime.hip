@@ -22,7 +22,8 @@ int32_t launch_embed_pe(const int64_t*, const float*, const float*, int, int, in
 int32_t launch_layer_norm(const float*, const float*, const float*, int, int, float*, hipStream_t);
 int32_t launch_linear(const float*, const float*, const float*, const float*, const float*,
                       const float*, int, int, int, int, float*, hipStream_t);
-int32_t launch_attention(const float*, const uint8_t*, int, int, int, int, float*, hipStream_t);
+// force_f32: the exact-f32 MFMA attention (a model whose q/k/v bound is outside the split-f16 range)
+int32_t launch_attention(const float*, const uint8_t*, int, int, int, int, float*, hipStream_t, bool force_f32 = false);
 int32_t launch_duration(const float*, int, int, int, const float* const*, float*, hipStream_t,
                         const float* ln_g = nullptr, const float* ln_b = nullptr, float* enc_out = nullptr);
 int32_t launch_lr_count(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
@@ -57,6 +58,10 @@ static constexpr int kRates[4] = {4, 4, 2, 2};  // tts_model.py:244
 // by layer).  A window widened by this many frames computes every sample of
 // its centre exactly as the whole-utterance call does.
 static constexpr int kVocHalo = 3;
+// Longest regulated utterance the path accepts: 2^24 mel frames (2^30 audio
+// samples, 13.5 h at 22.05 kHz); longer totals (a huge duration_scale or
+// target durations) are M2_E_SHAPE, not a wrapped or truncated int32.
+static constexpr int32_t kMaxFrames = 1 << 24;
 
 
 // ---------------------------------------------------------------------------
@@ -175,6 +180,12 @@ struct m2_model {
     // streamed vocoder (m2_vocoder_set_chunking): chunks of chunk_frames mel
     // frames, each computed over a window widened by kVocHalo frames per side
     int chunk_frames = 0;
+    // split-f16 range: non-finite-audio flag (host-mapped, vx.rflag is its
+    // device address), what a raised flag does (m2_set_range_policy), and the
+    // exact-f32 attention for weights whose q/k/v bound leaves the f16 range
+    int32_t* rflag_host = nullptr;
+    int range_policy = 0;
+    bool att_f32 = false;
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
     mutable int prof_calls = 0;
@@ -293,12 +304,12 @@ int32_t run_layer(const m2_model* m, const m2_layer_w& L, const float* x_in, flo
     int32_t rc;
     if (m->tfused) {
         if ((rc = launch_ln_gemm(x_in, L.n1_w, L.n1_b, L.qkv_p, nullptr, ACT_NONE, R, H, 3 * H, wb.qkv, st))) return rc;
-        if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st))) return rc;
+        if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st, m->att_f32))) return rc;
         return launch_post_attn(wb.att, x_in, L.out_p, L.out_b, L.n2_w, L.n2_b, L.ff1_p, L.ff1_b, L.ff2_p, L.ff2_b, R, H,
                                 x, st);
     }
     if ((rc = launch_linear(x_in, L.n1_w, L.n1_b, L.qkv_w, nullptr, nullptr, ACT_NONE, R, H, 3 * H, wb.qkv, st))) return rc;
-    if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st))) return rc;
+    if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st, m->att_f32))) return rc;
     if ((rc = launch_linear(wb.att, nullptr, nullptr, L.out_w, L.out_b, x_in, ACT_NONE, R, H, H, x, st))) return rc;
     if ((rc = launch_linear(x, L.n2_w, L.n2_b, L.ff1_w, L.ff1_b, nullptr, ACT_RELU, R, H, 2 * H, wb.hid, st))) return rc;
     if ((rc = launch_linear(wb.hid, nullptr, nullptr, L.ff2_w, L.ff2_b, x, ACT_NONE, R, 2 * H, H, x, st))) return rc;
@@ -473,6 +484,55 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             e = hipSuccess;
         }
         if (e != hipSuccess) return bail(e, "pack transformer weights");
+    }
+    // Split-f16 range of the transformer.  Its split operands are LayerNorm
+    // outputs (|x^| <= sqrt(H-1) for a normalised row, so |LN| <= sqrt(H-1)
+    // max|gamma| + max|beta|), q/k/v = W_qkv LN1 (<= max row sum |W| x that),
+    // attention outputs (convex combinations of v) and ReLU(FFN1(LN2)) - all
+    // bounded by the weights, so the check is made once, here: past half the
+    // f16 range the layers use the fp32 linears and the exact-f32 attention.
+    {
+        double worst = 0.0;
+        auto host = [&](const std::string& n) {
+            const int i = idx(n);
+            std::vector<float> h((size_t)table[i].numel);
+            hipError_t er = hipMemcpyAsync(h.data(), weights[i], h.size() * sizeof(float), hipMemcpyDeviceToHost, st);
+            if (er == hipSuccess) er = hipStreamSynchronize(st);
+            if (er != hipSuccess) h.assign(h.size(), INFINITY);
+            return h;
+        };
+        auto amax = [](const std::vector<float>& v) {
+            double a = 0.0;
+            for (float x : v) a = std::max(a, (double)std::fabs(x));
+            return a;
+        };
+        auto ln_bound = [&](const std::string& p) {
+            return std::sqrt((double)std::max(H - 1, 1)) * amax(host(p + ".weight")) + amax(host(p + ".bias"));
+        };
+        auto row_sum = [&](const std::string& n, int N, int K) {
+            const std::vector<float> w = host(n);
+            double best = 0.0;
+            for (int r = 0; r < N; ++r) {
+                double s = 0.0;
+                for (int k = 0; k < K; ++k) s += std::fabs(w[(size_t)r * K + k]);
+                best = std::max(best, s);
+            }
+            return best;
+        };
+        for (int i = 0; i < n_layers; ++i) {
+            const std::string p = i < cfg->text_encoder_layers
+                                      ? "text_encoder.layers." + std::to_string(i)
+                                      : "decoder.layers." + std::to_string(i - cfg->text_encoder_layers);
+            const double b1 = ln_bound(p + ".norm1"), b2 = ln_bound(p + ".norm2");
+            const double qkv = row_sum(p + ".self_attn.qkv.weight", 3 * H, H) * b1;
+            const double hid = row_sum(p + ".ffn.linear1.weight", 2 * H, H) * b2 + amax(host(p + ".ffn.linear1.bias"));
+            worst = std::max(worst, std::max(std::max(b1, b2), std::max(qkv, hid)));
+        }
+        if (cfg->decoder_layers > 0) worst = std::max(worst, ln_bound("decoder.norm"));
+        if (!(worst < 32768.0)) {
+            m->tfused = false;
+            m->att_f32 = true;
+        }
     }
     m->enc_nw = P("text_encoder.norm.weight");
     m->enc_nb = P("text_encoder.norm.bias");
@@ -673,6 +733,22 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             }
         }
     }
+    // the split path's non-finite-audio flag, host-mapped so the host can read
+    // it without a copy (m2_model_check, the M2_E_RANGE check on entry)
+    {
+        void* h = nullptr;
+        void* d = nullptr;
+        e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            if (h) (void)hipHostFree(h);
+            m2_model_destroy(m);
+            return hip_status(e, "hipHostMalloc(range flag)");
+        }
+        std::memset(h, 0, 64);
+        m->rflag_host = static_cast<int32_t*>(h);
+        m->vx.rflag = static_cast<int*>(d);
+    }
     *out = m;
     return M2_OK;
 }
@@ -686,6 +762,7 @@ int32_t m2_model_destroy(m2_model* model) {
     if (model->xbuf) (void)hipFree(model->xbuf);
     if (model->tbuf) (void)hipFree(model->tbuf);
     if (model->mbuf) (void)hipFree(model->mbuf);
+    if (model->rflag_host) (void)hipHostFree(model->rflag_host);
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -850,7 +927,10 @@ int32_t m2_length_regulator_count_sync(const void* dur, int32_t dur_is_int, floa
     if ((rc = launch_lr_count_sync(dur, dur_is_int, scale, B, S, out_cum, out_T, out_Tmax, mb->ticket, mb->dev, seq,
                                    st)))
         return rc;
-    return mailbox_wait(mb, seq, st, host_Tmax, "m2_length_regulator_count_sync");
+    if ((rc = mailbox_wait(mb, seq, st, host_Tmax, "m2_length_regulator_count_sync"))) return rc;
+    M2_CHECK_SHAPE(*host_Tmax <= kMaxFrames, "length regulator: an utterance's frame count exceeds 2^24 (the "
+                                             "durations times duration_scale are out of range)");
+    return M2_OK;
 }
 
 int32_t m2_length_regulator_expand(const float* enc, const int32_t* cum, int32_t B, int32_t S,
@@ -886,7 +966,7 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
 
 namespace {
 int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                    float* const* buf, hipStream_t st);
+                    float* const* buf, hipStream_t st, bool x3);
 
 // Audio samples [64 f0, 64 f1) of every utterance of a T-frame mel, computed
 // over the window [f0 - halo, f1 + halo) clipped to [0, T): the window's mel
@@ -894,7 +974,7 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
 // call, and the centre of its audio copied to out (row pitch out_pitch floats,
 // utterance b's chunk at out + b * out_pitch).
 int32_t vocoder_window(const m2_model* m, const float* mel, int32_t layout, int32_t B, int32_t T, int32_t f0,
-                       int32_t f1, float* out, size_t out_pitch, const ChunkBufs& c, hipStream_t st) {
+                       int32_t f1, float* out, size_t out_pitch, const ChunkBufs& c, hipStream_t st, bool x3) {
     const int M = m->cfg.mel_channels;
     const int w0 = std::max(0, f0 - kVocHalo), w1 = std::min(T, f1 + kVocHalo), W = w1 - w0;
     if (layout == 1)  // [B,T,M]: utterance b's window is W*M contiguous floats
@@ -903,11 +983,58 @@ int32_t vocoder_window(const m2_model* m, const float* mel, int32_t layout, int3
     else  // [B,M,T]: one W-float row per (utterance, channel)
         M2_HIP(hipMemcpy2DAsync(c.mel, (size_t)W * 4, mel + w0, (size_t)T * 4, (size_t)W * 4, (size_t)B * M,
                                 hipMemcpyDeviceToDevice, st));
-    int32_t rc = vocoder_run(m, c.mel, layout, B, W, c.audio, c.voc, st);
+    int32_t rc = vocoder_run(m, c.mel, layout, B, W, c.audio, c.voc, st, x3);
     if (rc) return rc;
     M2_HIP(hipMemcpy2DAsync(out, out_pitch * 4, c.audio + (size_t)64 * (f0 - w0), (size_t)64 * W * 4,
                             (size_t)64 * (f1 - f0) * 4, B, hipMemcpyDeviceToDevice, st));
     return M2_OK;
+}
+
+// One m2_vocoder call on the split (x3) or exact-f32 kernels.
+int32_t vocoder_call(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
+                     void* workspace, size_t workspace_bytes, hipStream_t st, bool x3) {
+    Carve a(workspace, workspace_bytes);
+    if (m->chunk_frames > 0 && T > m->chunk_frames) {  // streamed: chunk by chunk into out_audio
+        ChunkBufs c;
+        carve_chunked(a, m->cfg, B, T, m->chunk_frames, &c);
+        if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
+        if (B == 0) return M2_OK;
+        for (int f0 = 0; f0 < T; f0 += m->chunk_frames) {
+            const int f1 = std::min(T, f0 + m->chunk_frames);
+            const int32_t rc = vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_audio + (size_t)64 * f0,
+                                              (size_t)64 * T, c, st, x3);
+            if (rc) return rc;
+        }
+        return M2_OK;
+    }
+    float* buf[3];
+    carve_voc(a, m->cfg, B, T, buf);
+    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
+    if (B == 0 || T == 0) return M2_OK;
+    return vocoder_run(m, mel, mel_layout, B, T, out_audio, buf, st, x3);
+}
+
+// Sticky range error of an earlier call (policy 0), returned and cleared on entry.
+int32_t range_entry(const m2_model* m, const char* what) {
+    if (m->rflag_host && __atomic_load_n(m->rflag_host, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(m->rflag_host, 0, __ATOMIC_RELEASE);
+        return fail(M2_E_RANGE, (std::string(what) + ": an earlier vocoder call on this model produced non-finite "
+                                 "audio on the split-f16 path (an input or activation of magnitude >= 65520, or "
+                                 "a non-finite input); its output is invalid - re-run it with "
+                                 "m2_vocoder_select(model, 1) or range policy 1").c_str());
+    }
+    return M2_OK;
+}
+
+// Policy 1: wait for the call, and re-run it on the exact-f32 kernels if its
+// audio came out non-finite.
+template <typename F>
+int32_t range_fallback(const m2_model* m, hipStream_t st, bool x3, F redo) {
+    if (m->range_policy != 1 || !x3 || !m->rflag_host) return M2_OK;
+    M2_HIP(hipStreamSynchronize(st));
+    if (!__atomic_load_n(m->rflag_host, __ATOMIC_ACQUIRE)) return M2_OK;
+    __atomic_store_n(m->rflag_host, 0, __ATOMIC_RELEASE);
+    return redo();
 }
 }  // namespace
 
@@ -918,25 +1045,13 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
     M2_CHECK_ARG(m && mel && out_audio && B >= 0 && T >= 0, "m2_vocoder: bad argument");
     M2_CHECK_ARG(mel_layout == 0 || mel_layout == 1, "m2_vocoder: mel_layout must be 0 or 1");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    Carve a(workspace, workspace_bytes);
-    if (m->chunk_frames > 0 && T > m->chunk_frames) {  // streamed: chunk by chunk into out_audio
-        ChunkBufs c;
-        carve_chunked(a, m->cfg, B, T, m->chunk_frames, &c);
-        if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
-        if (B == 0) return M2_OK;
-        for (int f0 = 0; f0 < T; f0 += m->chunk_frames) {
-            const int f1 = std::min(T, f0 + m->chunk_frames);
-            const int32_t rc = vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_audio + (size_t)64 * f0,
-                                              (size_t)64 * T, c, st);
-            if (rc) return rc;
-        }
-        return M2_OK;
-    }
-    float* buf[3];
-    carve_voc(a, m->cfg, B, T, buf);
-    if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
-    if (B == 0 || T == 0) return M2_OK;
-    return vocoder_run(m, mel, mel_layout, B, T, out_audio, buf, st);
+    int32_t rc = range_entry(m, "m2_vocoder");
+    if (rc) return rc;
+    const bool x3 = m->x3;
+    if ((rc = vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, x3))) return rc;
+    return range_fallback(m, st, x3, [&] {
+        return vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, false);
+    });
 }
 
 int32_t m2_vocoder_chunk(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, int32_t f0,
@@ -944,13 +1059,33 @@ int32_t m2_vocoder_chunk(const m2_model* m, const float* mel, int32_t mel_layout
     M2_CHECK_ARG(m && mel && out_chunk && B >= 0 && T >= 0, "m2_vocoder_chunk: bad argument");
     M2_CHECK_ARG(mel_layout == 0 || mel_layout == 1, "m2_vocoder_chunk: mel_layout must be 0 or 1");
     M2_CHECK_ARG(0 <= f0 && f0 < f1 && f1 <= T, "m2_vocoder_chunk: need 0 <= f0 < f1 <= T");
+    int32_t rc = range_entry(m, "m2_vocoder_chunk");
+    if (rc) return rc;
     Carve a(workspace, workspace_bytes);
     ChunkBufs c;
     carve_chunked(a, m->cfg, B, T, f1 - f0, &c);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder_chunk: workspace too small");
     if (B == 0) return M2_OK;
-    return vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_chunk, (size_t)64 * (f1 - f0), c,
-                          static_cast<hipStream_t>(stream));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const bool x3 = m->x3;
+    if ((rc = vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_chunk, (size_t)64 * (f1 - f0), c, st, x3)))
+        return rc;
+    return range_fallback(m, st, x3, [&] {
+        return vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_chunk, (size_t)64 * (f1 - f0), c, st, false);
+    });
+}
+
+int32_t m2_set_range_policy(m2_model* m, int32_t policy) {
+    M2_CHECK_ARG(m && (policy == 0 || policy == 1), "m2_set_range_policy: policy must be 0 (report) or 1 (fallback)");
+    m->range_policy = policy;
+    return M2_OK;
+}
+
+int32_t m2_model_check(m2_model* m, void* stream, int32_t* flagged) {
+    M2_CHECK_ARG(m && flagged, "m2_model_check: bad argument");
+    M2_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    *flagged = m->rflag_host ? __atomic_exchange_n(m->rflag_host, 0, __ATOMIC_ACQ_REL) : 0;
+    return M2_OK;
 }
 
 size_t m2_vocoder_chunk_workspace_bytes(const m2_model* m, int32_t B, int32_t T, int32_t chunk_frames) {
@@ -985,7 +1120,7 @@ int32_t m2_vocoder_select(m2_model* m, int32_t path) {
 
 namespace {
 int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                    float* const* buf, hipStream_t st) {
+                    float* const* buf, hipStream_t st, bool x3) {
     int32_t rc;
     if (m->fused) {
         const int call = m->prof_calls;
@@ -997,7 +1132,7 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
             const size_t slot = (size_t)call * kVocKernels + kidx;
             (void)hipEventRecord(begin ? m->prof_begin[slot] : m->prof_end[slot], st);
         };
-        if (m->x3)
+        if (x3)
             return launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vx,
                                      buf[0], buf[1], out_audio, st, mark);
         return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vw,
@@ -1108,6 +1243,7 @@ int32_t m2_inference_front(const m2_model* m, const int64_t* ids, const int64_t*
                            int32_t* host_Tmax, void* stream) {
     M2_CHECK_ARG(m && host_Tmax && B >= 0 && S >= 0, "m2_inference_front: bad argument");
     M2_CHECK_ARG(ids || B * S == 0, "m2_inference_front: null ids");
+    if (int32_t rc0 = range_entry(m, "m2_inference")) return rc0;
     Carve a(front, front_bytes);
     FrontBufs f;
     carve_front(a, B, S, m->cfg.hidden_dim, &f);
@@ -1192,6 +1328,11 @@ size_t m2_inference_workspace_bytes(const m2_model* model, int32_t B, int32_t S,
 int32_t m2_vocoder_path(const m2_model* m) {
     if (!m) return -1;
     return m->x3 ? 2 : (m->fused ? 1 : 0);
+}
+
+int32_t m2_transformer_path(const m2_model* m) {
+    if (!m) return -1;
+    return (m->tfused && !m->att_f32) ? 1 : 0;
 }
 
 int32_t m2_profile_enable(m2_model* m, int32_t capacity) {

@@ -684,7 +684,7 @@ int32_t launch_linear(const float* x, const float* gamma, const float* beta, con
 }
 
 int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, int H, int heads,
-                         float* out, hipStream_t st) {
+                         float* out, hipStream_t st, bool force_f32) {
     M2_CHECK_SHAPE(heads > 0 && H % heads == 0, "attention: H % heads != 0");
     const int hd = H / heads;
     if (B == 0 || N == 0) return M2_OK;
@@ -695,7 +695,7 @@ int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, in
     // split-f16 MFMA by default; M2_ATT_F32=1: the exact-f32 MFMA kernel
     // (read per launch, so a process can switch: tests/test_gpu_parity.py)
     const char* env = std::getenv("M2_ATT_F32");
-    const bool f32 = env && *env && *env != '0';
+    const bool f32 = force_f32 || (env && *env && *env != '0');
     if (!f32) switch (hd) {
             case 16: return launch_att_split<16>(grid, qkv, mask, N, H, scale, out, st);
             case 32: return launch_att_split<32>(grid, qkv, mask, N, H, scale, out, st);

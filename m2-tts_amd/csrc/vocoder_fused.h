@@ -45,11 +45,19 @@ typedef unsigned int vx_u32x4 __attribute__((ext_vector_type(4)));
 // format of every split-f16 buffer (LDS rows, U1, U2) and of the packed
 // weights.  lo is unscaled and may be an f16 subnormal, an absolute error of
 // at most 2^-25 per value (whole-vocoder waveform RMS 3e-7 vs fp64, against
-// 1.6e-7 for plain fp32: tools/probe/split_sim.py).  One v_cvt_pkrtz_f16_f32
+// 1.6e-7 for plain fp32: tools/probe/split_sim.py).  One v_cvt_pk_f16_f32
 // per pair for hi and one v_fma_mix{lo,hi}_f16 per value for lo (v - hi
-// rounded once); hi rounds toward zero, which leaves lo's bound unchanged.
+// rounded once).
+// Range: hi rounds to nearest even, so |v| >= 65520 (past the f16 range)
+// gives hi = inf and lo = v - inf = NaN, and the NaN propagates through every
+// later MFMA, activation and split to the output: a split path's result is
+// either exact to the bound above or non-finite, never silently wrong (a
+// round-toward-zero hi would saturate at 65504 and lose precision quietly
+// for 65504 < |v| < 131024).  The vocoder's last kernel flags non-finite
+// audio (m2_model_check / M2_E_RANGE; the fallback policy re-runs the call
+// on the exact-f32 kernels).
 __device__ __forceinline__ void split2u(float v0, float v1, unsigned& hi, unsigned& lo) {
-    hi = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v0, v1));
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(v0), "v"(v1));
     asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(v0));
     asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(v1));
 }
@@ -88,7 +96,16 @@ struct VocX {
     // pipelined stage1 mid stage (vocoder_midp.hip); null = the x3 mid kernel
     const vx_u32x4* mp;
     const float* mpb;
+    // set to 1 (vector store) by the last kernel when an audio sample is not
+    // finite; host-mapped (m2_model_check)
+    int* rflag;
 };
+
+// Non-finite output check of the split path's last kernel: any NaN among the
+// four values -> *flag = 1 (rare path; the host reads and clears it).
+__device__ __forceinline__ void flag_nonfinite4(float a, float b, float c, float d, int* flag) {
+    if (flag && ((a != a) | (b != b) | (c != c) | (d != d))) *reinterpret_cast<volatile int*>(flag) = 1;
+}
 
 // Pipelined stage1 tail (vocoder_tailp.hip): ConvT3, ResBlock3, ConvT4,
 // ResBlock4 and output_conv in polyphase form over the columns q of U2.
@@ -167,7 +184,7 @@ struct TailpSrc {
 // happen for the stage1 shapes; the x3 tail is kept then).
 bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                             hipStream_t st);
+                             int* rflag, hipStream_t st);
 extern const char* const kVocTailpKernelName;
 
 bool vocoder_x3_supported(int M, int C);

@@ -138,7 +138,7 @@ using ic = std::integral_constant<int, V>;
 template <int L, int NMB, int NCH>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
-                                           float* __restrict__ arow) {
+                                           float* __restrict__ arow, int* rflag) {
     constexpr int NKB = nkb(L), NF = nfrag(L);
     // ResBlock conv2: + x (the ConvT output, ring R(L-1), two columns ahead),
     // added by two more MFMAs per m-block with an identity A (x hi, x lo) on
@@ -245,6 +245,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                 o.z = tanh_fast(acc[0][2]);
                 o.w = tanh_fast(acc[0][3]);
                 *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
+                flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
             }
         } else {
             // Both m-blocks in one basic block (the compiler interleaves their
@@ -375,7 +376,7 @@ template <int NCH>
 __global__ __launch_bounds__(NWAVES * 64, 6) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
                                                                 const u32x4* __restrict__ W,
                                                                 const float* __restrict__ bias,
-                                                                float* __restrict__ audio) {
+                                                                float* __restrict__ audio, int* rflag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -391,13 +392,13 @@ __global__ __launch_bounds__(NWAVES * 64, 6) void tailp_kernel(const unsigned ch
     else if (w >= 3) __builtin_amdgcn_s_setprio(2);
     else if (w >= 1) __builtin_amdgcn_s_setprio(1);
     switch (w) {
-        case 0: layer_role<0, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 1: layer_role<1, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 2: layer_role<2, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 3: layer_role<3, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 4: layer_role<4, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 5: layer_role<5, 2, NCH>(lds, qa, L2, edge, W, bias, arow); break;
-        case 6: layer_role<6, 1, NCH>(lds, qa, L2, edge, W, bias, arow); break;
+        case 0: layer_role<0, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 1: layer_role<1, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 2: layer_role<2, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 3: layer_role<3, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 4: layer_role<4, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 5: layer_role<5, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 6: layer_role<6, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
         default:
             if (edge) loader_role<NCH, true>(lds, qa, L2, U2 + (size_t)b * L2 * 128);
             else loader_role<NCH, false>(lds, qa, L2, U2 + (size_t)b * L2 * 128);
@@ -407,7 +408,8 @@ __global__ __launch_bounds__(NWAVES * 64, 6) void tailp_kernel(const unsigned ch
 }
 
 template <int NCH>
-int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, hipStream_t st) {
+int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
+               hipStream_t st) {
     static bool attr = false;
     if (!attr) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp_kernel<NCH>),
@@ -415,7 +417,7 @@ int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bi
         attr = true;
     }
     hipLaunchKernelGGL((tailp_kernel<NCH>), dim3(cdiv(L2, 16 * NCH), B), dim3(NWAVES * 64), LDS_BYTES, st,
-                       static_cast<const unsigned char*>(U2), L2, W, bias, audio);
+                       static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
     M2_LAUNCHED("tailp_kernel");
     return M2_OK;
 }
@@ -433,7 +435,7 @@ const char* const kVocTailpKernelName =
     "tailp_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, pipelined)";
 
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                             hipStream_t st) {
+                             int* rflag, hipStream_t st) {
     if (B == 0 || L2 == 0) return M2_OK;
     // Strip length: the shortest instantiated NCH that covers an utterance in
     // at most floor(768 / B) strips, so the grid is about one round of three
@@ -448,9 +450,9 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
         const int chunks = cdiv(L2, 16), strips = std::max(1, 3 * 256 / B), need = cdiv(chunks, strips);
         nch = need <= 21 ? 21 : (need <= 32 ? 32 : 48);
     }
-    if (nch == 21) return tp::launch<21>(U2, L2, B, W, bias, audio, st);
-    if (nch == 48) return tp::launch<48>(U2, L2, B, W, bias, audio, st);
-    return tp::launch<32>(U2, L2, B, W, bias, audio, st);
+    if (nch == 21) return tp::launch<21>(U2, L2, B, W, bias, audio, rflag, st);
+    if (nch == 48) return tp::launch<48>(U2, L2, B, W, bias, audio, rflag, st);
+    return tp::launch<32>(U2, L2, B, W, bias, audio, rflag, st);
 }
 
 // ---------------------------------------------------------------------------

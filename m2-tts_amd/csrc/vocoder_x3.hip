@@ -939,7 +939,9 @@ __global__ __launch_bounds__(Cfg::TW * 64, Cfg::TMIN) void x3_tail_kernel(const 
                 for (int ci = 0; ci < C4; ++ci)
                     acc = fmaf(w.wo[ci * 3 + k], (float)hr[ci] + (float)hr[C4 + ci], acc);
             }
-            arow[t] = tanhf(acc + bo);
+            const float o = tanhf(acc + bo);
+            arow[t] = o;
+            flag_nonfinite4(o, 0.f, 0.f, 0.f, w.rflag);
         }
     }
     XSTAMP(2, 15);
@@ -991,7 +993,7 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     mark(1, false);
     mark(2, true);
     if (w.tp) {  // stage1: the pipelined tail (vocoder_tailp.hip)
-        const int32_t rc = launch_vocoder_tailp(u2, 16 * T, B, w.tp, w.tpb, audio, st);
+        const int32_t rc = launch_vocoder_tailp(u2, 16 * T, B, w.tp, w.tpb, audio, w.rflag, st);
         mark(2, false);
         return rc;
     }

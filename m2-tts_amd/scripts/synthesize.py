@@ -96,6 +96,10 @@ def load_model(checkpoint_path: Path, device: torch.device, config_path: Optiona
     model.load_state_dict(ckpt["model_state_dict"])
     model.to(device)
     model.eval()
+    # one utterance per call and the audio goes to the host anyway: pay the
+    # one synchronisation per vocoder call that guarantees a finite result
+    # (split-f16 out of range -> recomputed on the exact-f32 kernels)
+    model.set_range_policy("fallback")
     logger.info(f"Loaded model from {checkpoint_path}")
     logger.info(f"Training step: {ckpt.get('step', 'unknown')}")
     return model

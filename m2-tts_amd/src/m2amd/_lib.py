@@ -50,7 +50,9 @@ _SIGNATURES = {
     "m2_vocoder_chunk": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
     "m2_vocoder_chunk_workspace_bytes": (c_size, [c_vp, c_i32, c_i32, c_i32]),
     "m2_vocoder_select": (c_i32, [c_vp, c_i32]),
-    "m2_vocoder_resblock":(c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "m2_set_range_policy": (c_i32, [c_vp, c_i32]),
+    "m2_model_check": (c_i32, [c_vp, c_vp, ctypes.POINTER(c_i32)]),
+    "m2_vocoder_resblock": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "m2_vocoder_upsample": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "m2_conv1d": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "m2_conv_transpose1d": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
@@ -68,6 +70,7 @@ _SIGNATURES = {
     "m2_profile_select": (c_i32, [c_vp, ctypes.c_uint32]),
     "m2_profile_stride": (c_i32, [c_vp, c_i32]),
     "m2_vocoder_path": (c_i32, [c_vp]),
+    "m2_transformer_path": (c_i32, [c_vp]),
     "m2_front_bytes": (c_size, [c_vp, c_i32, c_i32]),
     "m2_inference_workspace_bytes": (c_size, [c_vp, c_i32, c_i32, c_i32]),
     "m2_inference_front": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, c_vp, c_size, c_vp, c_vp]),

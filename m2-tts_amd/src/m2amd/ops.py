@@ -13,7 +13,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_SOFTPLUS, ACT_TANH  # noqa: F401
+from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_SOFTPLUS, ACT_TANH, M2Error  # noqa: F401
 
 Tensor = torch.Tensor
 

@@ -9,6 +9,7 @@ storage or version (``load_state_dict``, ``.to()``, in-place edits).
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from typing import Dict, Optional, Tuple
 
@@ -203,6 +204,20 @@ class HipModel:
     def vocoder_path(self) -> int:
         return int(_lib.load().m2_vocoder_path(self.handle))
 
+    def set_range_policy(self, policy: str):
+        """What a non-finite split-path result does (m2_set_range_policy):
+        "report" - the next call raises M2Error (M2_E_RANGE), check() reports
+        it at once; "fallback" - each vocoder call waits for its kernels and
+        re-runs on the exact-f32 kernels when its audio is not finite."""
+        _lib.call("m2_set_range_policy", self.handle, {"report": 0, "fallback": 1}[policy])
+
+    def check(self) -> bool:
+        """Synchronise the current stream; True if a split-path vocoder call
+        since the last check produced non-finite audio (flag cleared)."""
+        flagged = ctypes.c_int32(0)
+        _lib.call("m2_model_check", self.handle, stream_handle(self.device), ctypes.byref(flagged))
+        return bool(flagged.value)
+
     def set_chunking(self, chunk_frames: int):
         """Stream the vocoder in chunks of chunk_frames mel frames (0 = off)."""
         _lib.call("m2_vocoder_set_chunking", self.handle, int(chunk_frames))
@@ -308,6 +323,9 @@ class HandleCache:
         path = module.__dict__.get("_m2_voc_path")
         if path:
             hm.vocoder_select(path)
+        policy = module.__dict__.get("_m2_range_policy") or os.environ.get("M2_RANGE_POLICY")
+        if policy:
+            hm.set_range_policy(policy)
         self._entries[device] = (key, hm)
         return hm
 

@@ -238,6 +238,28 @@ class M2TTSModel(nn.Module):
         for hm in (cache.handles() if cache is not None else []):
             hm.set_chunking(chunk_frames)
 
+    def set_range_policy(self, policy: str = "report"):
+        """The split-f16 vocoder carries fp32 values as f16 hi/lo pairs; an
+        input or activation of magnitude >= 65520 turns its audio non-finite
+        (never silently wrong).  "report" (default): the next call raises, and
+        check_numerics() reports it at once; "fallback": every vocoder call
+        waits for its result and recomputes it on the exact-f32 kernels when
+        it is not finite (costs one host synchronisation per call)."""
+        self.__dict__["_m2_range_policy"] = policy
+        cache = _HANDLES.get(self)
+        for hm in (cache.handles() if cache is not None else []):
+            hm.set_range_policy(policy)
+
+    def check_numerics(self, device: Optional[torch.device] = None):
+        """Synchronise and raise if a split-path vocoder call since the last
+        check produced non-finite audio (M2_E_RANGE semantics)."""
+        cache = _HANDLES.get(self)
+        for hm in (cache.handles() if cache is not None else []):
+            if (device is None or hm.device == torch.device(device)) and hm.check():
+                raise ops.M2Error(
+                    "m2-tts_amd: a split-f16 vocoder call produced non-finite audio (an input or activation "
+                    "of magnitude >= 65520); re-run with set_vocoder_precision('f32') or set_range_policy('fallback')")
+
     def set_vocoder_precision(self, precision: str = "split"):
         """"split" = split-f16 MFMA kernels (fp32 operands as f16 hi/lo pairs,
         the default), "f32" = exact-f32 MFMA kernels."""

@@ -1,0 +1,124 @@
+"""GPU: the split-f16 range guard.  Values of magnitude >= 65520 (mel input or
+any vocoder activation) make the split path's audio non-finite, which its last
+kernel flags; the "fallback" policy recomputes such a call on the exact-f32
+kernels, "report" raises on the next call / check_numerics().  Tiny inputs
+(f16-subnormal lo halves) stay within the waveform bound.  Transformer
+activations are bounded by the weights and checked at model creation."""
+import pytest
+import torch
+
+import m2tts_oracle as orc
+from conftest import AUDIO_RMS_TOL, MEL_MAXABS_TOL, golden, golden_state, maxabs, rms, stage_config
+
+pytestmark = pytest.mark.gpu
+
+
+def build_model(stage, dev, sd=None):
+    from models.tts_model import M2TTSModel
+    m = M2TTSModel(**stage_config(stage).as_dict())
+    m.load_state_dict(sd if sd is not None else golden_state(stage))
+    return m.to(dev).eval()
+
+
+def _mel(stage, T, scale, seed=5):
+    return torch.randn(2, stage_config(stage).mel_channels, T, generator=torch.Generator().manual_seed(seed)) * scale
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_huge_mel_fallback_matches_exact_f32_and_oracle(gpu, stage):
+    mel = _mel(stage, 45, 1e5)
+    assert float(mel.abs().max()) > 65520
+    m = build_model(stage, gpu)
+    m.set_range_policy("fallback")
+    out = m.vocoder(mel.to(gpu))
+    assert torch.isfinite(out).all()
+    m.set_vocoder_precision("f32")
+    exact = m.vocoder(mel.to(gpu))
+    assert torch.equal(out, exact)
+    ref = orc.vocoder(golden_state(stage), mel)
+    assert rms(out, ref) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_huge_mel_report_raises(gpu, stage):
+    from m2amd._lib import M2Error
+    m = build_model(stage, gpu)
+    ok = _mel(stage, 30, 1.0)
+    base = m.vocoder(ok.to(gpu))
+    bad = m.vocoder(_mel(stage, 30, 1e6).to(gpu))
+    with pytest.raises(M2Error, match="non-finite"):
+        m.check_numerics()
+    m.check_numerics()  # cleared
+    assert torch.equal(m.vocoder(ok.to(gpu)), base)
+    m.vocoder(_mel(stage, 30, 1e6).to(gpu))
+    torch.cuda.synchronize()
+    with pytest.raises(M2Error, match="status -6"):  # M2_E_RANGE on the next call
+        m.vocoder(ok.to(gpu))
+    assert torch.equal(m.vocoder(ok.to(gpu)), base)
+    del bad
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_huge_activation_inside_the_vocoder(gpu, stage):
+    """A finite mel, but input_conv's bias puts its activations near 1e5: the
+    split path flags it and the fallback gives the exact-f32 result (== oracle)."""
+    sd = golden_state(stage)
+    sd["vocoder.input_conv.bias"] = sd["vocoder.input_conv.bias"] + 1e5
+    m = build_model(stage, gpu, sd)
+    assert m._hip(gpu).vocoder_path() == 2  # weights themselves stay in the f16 range
+    mel = _mel(stage, 33, 1.0)
+    m.set_range_policy("fallback")
+    out = m.vocoder(mel.to(gpu))
+    assert torch.isfinite(out).all()
+    ref = orc.vocoder(sd, mel)
+    assert rms(out, ref) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+@pytest.mark.parametrize("scale", [1e-3, 1e-6])
+def test_tiny_mel_within_bound(gpu, stage, scale):
+    """Mel values whose lo halves are f16 subnormals (or zero): the absolute
+    error stays far inside the waveform bound and nothing is flagged."""
+    m = build_model(stage, gpu)
+    mel = _mel(stage, 64, scale)
+    out = m.vocoder(mel.to(gpu))
+    ref = orc.vocoder(golden_state(stage), mel)
+    assert rms(out, ref) <= AUDIO_RMS_TOL and maxabs(out, ref) <= 1e-4
+    m.check_numerics()
+
+
+def test_transformer_range_bound_selects_f32(gpu):
+    """Decoder LayerNorm gains of 1e3 push q/k/v past half the f16 range: the
+    model is created on the fp32 transformer path and still matches the oracle."""
+    from m2amd import _lib
+    lib = _lib.load()
+    sd = golden_state("s1")
+    assert lib.m2_transformer_path(build_model("s1", gpu, sd)._hip(gpu).handle) == 1
+    sd["decoder.layers.0.norm1.weight"] = sd["decoder.layers.0.norm1.weight"] * 1e3
+    m = build_model("s1", gpu, sd)
+    assert lib.m2_transformer_path(m._hip(gpu).handle) == 0
+    g = golden("s1_small")
+    ids, lens = torch.from_numpy(g["ids"]), torch.from_numpy(g["lengths"])
+    mel, audio = m.inference(ids.to(gpu), lens.to(gpu))
+    ref_mel, ref_audio = orc.inference(sd, orc.STAGE1, ids, lens, as_written=False)
+    assert maxabs(mel, ref_mel) <= MEL_MAXABS_TOL
+    assert rms(audio, ref_audio) <= AUDIO_RMS_TOL
+
+
+def test_frame_count_overflow_is_an_error(gpu):
+    """Per-phoneme counts clamp at 2^30 and the sums are 64-bit and saturating:
+    a total past the 2^24-frame limit is M2_E_SHAPE, never a wrapped int32."""
+    from m2amd import ops
+    from m2amd._lib import M2Error
+    d = torch.full((2, 100), 1e9, device=gpu)
+    cum, tot, tmax = ops.frame_counts(d)
+    assert int(tot.min()) == 2**31 - 1 and int(tmax.item()) == 2**31 - 1  # saturated, not wrapped
+    assert int(cum[0, 2]) == 2_000_000_000 and int(cum[0, -1]) == 2**31 - 1
+    with pytest.raises(M2Error, match="status -2"):
+        ops.regulate(torch.zeros(2, 100, 8, device=gpu), d)
+    m = build_model("s1", gpu)
+    g = golden("s1_small")
+    with pytest.raises(M2Error, match="status -2"):
+        m.inference(torch.from_numpy(g["ids"]).to(gpu), torch.from_numpy(g["lengths"]).to(gpu), duration_scale=1e7)
+    mel, _ = m.inference(torch.from_numpy(g["ids"]).to(gpu), torch.from_numpy(g["lengths"]).to(gpu))
+    assert mel.shape == tuple(g["mel"].shape)  # the mailbox protocol is intact after the error
