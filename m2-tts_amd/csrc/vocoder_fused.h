@@ -56,8 +56,15 @@ typedef unsigned int vx_u32x4 __attribute__((ext_vector_type(4)));
 // for 65504 < |v| < 131024).  The vocoder's last kernel flags non-finite
 // audio (m2_model_check / M2_E_RANGE; the fallback policy re-runs the call
 // on the exact-f32 kernels).
+// hi comes from a compiler-visible conversion (one v_cvt_pk_f16_f32): it is
+// the first reader of MFMA results in most epilogues, and only an instruction
+// the compiler sees gets the MFMA -> VALU wait states in front of it (an
+// inline-asm reader straight after the MFMA would read its stale destination
+// registers); the fma_mix halves below follow it.
 __device__ __forceinline__ void split2u(float v0, float v1, unsigned& hi, unsigned& lo) {
-    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(v0), "v"(v1));
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    hi = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{v0, v1}, h2_t));
     asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(v0));
     asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(v1));
 }
