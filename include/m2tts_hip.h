@@ -273,6 +273,41 @@ int32_t m2_embed_positional(const int64_t* ids, const float* emb, const float* p
 int32_t m2_add_positional(const float* x, const float* pe, int32_t B, int32_t S, int32_t H,
                           float* y, void* stream);
 
+/* ---- mel features and Griffin-Lim (src/utils/audio.py:45-151) --
+ * The reference's librosa calls: compute_mel_spectrogram = melspectrogram
+ * (periodic Hann, centre zero padding, Slaney mel filters, power 2) ->
+ * power_to_db(ref=max, amin 1e-10, top_db 80) -> [-1, 1] normalisation, per
+ * utterance; mel_to_audio = (x+1)/2 -> db_to_power -> NNLS against the mel
+ * filters (mel_to_stft; here Nesterov projected gradient from the clipped
+ * pseudo-inverse - librosa uses scipy L-BFGS-B from the same start) -> sqrt
+ * -> griffinlim(n_iter, momentum) -> istft -> / max|y|.
+ *   m2_dsp_create: the tables (window, twiddles, mel filters, pseudo-inverse)
+ *     for one (sr, n_fft in {512, 1024, 2048}, hop, win_length, n_mels, fmin,
+ *     fmax); synchronises `stream`.
+ *   audio [B, L] fp32; frames T = m2_dsp_frames(L) = 1 + L / hop;
+ *   m2_stft -> complex64 [B, T, n_fft/2 + 1]; m2_mel_spectrogram -> out_mel
+ *     [B, n_mels, T] normalised dB;
+ *   m2_griffin_lim: from mel [B, n_mels, T] (normalised dB; nnls_iters
+ *     projected-gradient steps) or, when mag != NULL, from magnitudes
+ *     [B, T, n_fft/2+1] (bare griffinlim, no peak normalisation);
+ *     init_angles complex64 [B, T, n_fft/2+1] unit phases (librosa's
+ *     init='random' draw, made explicit); out_audio [B, hop (T - 1)]. */
+typedef struct m2_dsp m2_dsp;
+int32_t m2_dsp_create(int32_t sample_rate, int32_t n_fft, int32_t hop_length, int32_t win_length,
+                      int32_t n_mels, float fmin, float fmax, void* stream, m2_dsp** out);
+int32_t m2_dsp_destroy(m2_dsp* dsp);
+int32_t m2_dsp_frames(const m2_dsp* dsp, int32_t L);
+int32_t m2_stft(const m2_dsp* dsp, const float* audio, int32_t B, int32_t L, void* out_spec, void* stream);
+int32_t m2_mel_spectrogram(const m2_dsp* dsp, const float* audio, int32_t B, int32_t L, float* out_mel,
+                           void* stream);
+/* mel_to_stft alone: mel [B, n_mels, T] -> magnitudes out_mag [B, T, n_fft/2+1]. */
+int32_t m2_mel_to_magnitude(const m2_dsp* dsp, const float* mel, int32_t B, int32_t T, int32_t nnls_iters,
+                            float* out_mag, void* stream);
+size_t m2_griffin_lim_workspace_bytes(const m2_dsp* dsp, int32_t B, int32_t T);
+int32_t m2_griffin_lim(const m2_dsp* dsp, const float* mel, const float* mag, const void* init_angles,
+                       int32_t B, int32_t T, int32_t n_iter, float momentum, int32_t nnls_iters,
+                       float* out_audio, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- measurement ----------------------------------------------------------
  * Kernel timing with HIP events recorded on the launch stream around each of
  * the fused vocoder's kernels (bench.py's roofline).  enable: allocate event

@@ -352,11 +352,23 @@ __device__ __forceinline__ f32x4 mfma_f16(vx_u32x4 a, vx_u32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
 }
 
-template <int HD>
-__global__ __launch_bounds__(512, HD <= 32 ? 4 : 2) void attention_split_kernel(const float* __restrict__ qkv,
-                                                                 const uint8_t* __restrict__ key_mask, int N, int H,
-                                                                 float scale, float* __restrict__ out, int nqb,
-                                                                 int heads, int ngroups) {
+// QT query tiles of 16 per wave (64 * QT queries per workgroup): every K / V
+// fragment read from LDS feeds QT tiles, and every K / V byte a workgroup
+// stages serves QT times as many queries (all K and V of an (utterance,
+// head) pass through each of its query blocks' workgroups).  The launcher
+// picks QT = 2 while the grid keeps a workgroup per CU.
+// MASKED = false (the decoder, mask=None): Q is pre-scaled by
+// scale * log2(e) before it is split, so a score is the raw MFMA dot product
+// (no per-key (scale, fill) table, no fma per score); only the keys past N in
+// the last chunk are set to -inf.  MASKED: the per-key (scale, add) table.
+// The instruction budget matters: per 64-key chunk a wave issues 3 x
+// (4 KS + 2 MT) MFMAs against ~200 VALU (PMC, tools/probe/att_pmc.sh), so
+// address arithmetic is kept to uniform chunk bases plus per-lane 32-bit
+// offsets fixed for the whole kernel.
+template <int HD, int QT, bool MASKED>
+__global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_split_kernel(
+    const float* __restrict__ qkv, const uint8_t* __restrict__ key_mask, int N, int H, float scale,
+    float* __restrict__ out, int nqb, int heads, int ngroups) {
     using P = AttSplit<HD>;
     constexpr int KS = P::KS, DP = P::DP, KRS = P::KRS, VRS = P::VRS;
     constexpr int MT = HD / 16;                  // 16-row d blocks of O^T
@@ -365,8 +377,8 @@ __global__ __launch_bounds__(512, HD <= 32 ? 4 : 2) void attention_split_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* const Ks0 = smem;
     unsigned char* const Vt0 = smem + P::NBUF * P::KBUF;
-    // per key (scale, add): live (scale*log2e, 0), masked (0, -1e9*log2e),
-    // past the end (0, -inf): the base-2 score is one fma of the raw dot product
+    // MASKED: per key (scale, add): live (scale*log2e, 0), masked (0,
+    // -1e9*log2e), past the end (0, -inf): the base-2 score is one fma
     float2* const Mk0 = reinterpret_cast<float2*>(smem + P::NBUF * (P::KBUF + P::VBUF));
     // XCD-aware workgroup order: workgroup L runs on XCD L % 8 (each XCD has
     // its own L2), so the nqb query blocks of one (utterance, head) - which
@@ -375,13 +387,13 @@ __global__ __launch_bounds__(512, HD <= 32 ? 4 : 2) void attention_split_kernel(
     const int grp = xcd + 8 * (r / nqb), qb = r - (r / nqb) * nqb;
     if (grp >= ngroups) return;  // padding of the last round (ngroups % 8 != 0)
     const int b = grp / heads, hh = grp - b * heads;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, g = lane >> 4;
     const int qg = wave & 3, kh = wave >> 2;  // query group, key half
-    const int ct = tid & 255, ch = tid >> 8;  // fetch / stash: thread within a chunk, chunk of the pair
-    const size_t row3 = (size_t)3 * H;
+    const int ct = tid & 255, ch = wave >> 2;  // fetch / stash: thread within a chunk, chunk of the pair
+    const int row3 = 3 * H;
     const float* base = qkv + (size_t)b * N * row3 + hh * HD;
-    const int qi = qb * 64 + qg * 16 + li;
+    const int q0 = qb * 64 * QT + qg * 16 * QT + li;  // query of tile qt: q0 + 16 qt
     const float sl2 = scale * kLog2e;
 
     if constexpr (DP > HD) {  // zero the padded head dims of every K buffer once
@@ -396,36 +408,46 @@ __global__ __launch_bounds__(512, HD <= 32 ? 4 : 2) void attention_split_kernel(
     // Chunk pairs stream through registers PF pairs ahead of their stash.
     // K: thread = (key, head-dim quad), quads fastest (128-B rows); V: thread
     // = (key pair, quad), pairs fastest, so the transposed stores (two keys'
-    // f16 in one dword of a V^T row) hit 32 distinct banks.
+    // f16 in one dword of a V^T row) hit 32 distinct banks.  Per-lane 32-bit
+    // offsets from the chunk's first row, fixed for the whole kernel.
     constexpr int PF = 2;
     constexpr int NQ4 = HD / 4, ITV = (32 * NQ4 + 255) / 256;
+    int koff[IT], kkey[IT], voff[ITV], vkey[ITV];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int i = ct + it * 256, key = i / NQ4, d4 = i - key * NQ4;
+        kkey[it] = key;
+        koff[it] = key * row3 + H + 4 * d4;
+    }
+#pragma unroll
+    for (int it = 0; it < ITV; ++it) {
+        const int i = ct + it * 256, pr = i & 31, d4 = i >> 5;
+        vkey[it] = d4 < NQ4 ? 2 * pr : ATT_KC;  // past the quads: never loaded
+        voff[it] = 2 * pr * row3 + 2 * H + 4 * (d4 < NQ4 ? d4 : 0);
+    }
     float4 kr[PF][IT], vr[PF][ITV][2];
     float2 mkr[PF];
     const int nch = (N + ATT_KC - 1) / ATT_KC, npair = (nch + 1) / 2;
     auto fetch = [&](int pr_, auto sc) {  // chunk 2 pr_ + ch
         constexpr int sl = decltype(sc)::value;
-        const int j0 = (2 * pr_ + ch) * ATT_KC;
+        const int j0 = (2 * pr_ + ch) * ATT_KC, lim = N - j0;  // keys of this chunk with key < lim exist
+        const float* cb = base + (size_t)j0 * row3;
 #pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = ct + it * 256, key = i / NQ4, d4 = i - key * NQ4, j = j0 + key;
-            kr[sl][it] = j < N ? *reinterpret_cast<const float4*>(base + j * row3 + H + 4 * d4)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int it = 0; it < IT; ++it)
+            kr[sl][it] = kkey[it] < lim ? *reinterpret_cast<const float4*>(cb + koff[it]) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int it = 0; it < ITV; ++it) {
-            const int i = ct + it * 256, pr = i & 31, d4 = i >> 5;
+        for (int it = 0; it < ITV; ++it)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int j = j0 + 2 * pr + h;
-                vr[sl][it][h] = (j < N && d4 < NQ4) ? *reinterpret_cast<const float4*>(base + j * row3 + 2 * H + 4 * d4)
-                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int h = 0; h < 2; ++h)
+                vr[sl][it][h] = vkey[it] + h < lim ? *reinterpret_cast<const float4*>(cb + voff[it] + h * row3)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (MASKED) {
+            if (ct < ATT_KC) {
+                const int j = j0 + ct;
+                mkr[sl] = j >= N ? make_float2(0.f, -INFINITY)
+                                 : ((key_mask && key_mask[(size_t)b * N + j] == 0)
+                                        ? make_float2(0.f, kMaskFill * kLog2e) : make_float2(sl2, 0.f));
             }
-        }
-        if (ct < ATT_KC) {
-            const int j = j0 + ct;
-            mkr[sl] = j >= N ? make_float2(0.f, -INFINITY)
-                             : ((key_mask && key_mask[(size_t)b * N + j] == 0) ? make_float2(0.f, kMaskFill * kLog2e)
-                                                                                : make_float2(sl2, 0.f));
         }
     };
     auto stash = [&](int buf, auto sc) {  // this thread's chunk of the pair into buffer buf
@@ -461,101 +483,156 @@ __global__ __launch_bounds__(512, HD <= 32 ? 4 : 2) void attention_split_kernel(
                 }
             }
         }
-        if (ct < ATT_KC) Mk0[buf * ATT_KC + ct] = mkr[sl];
+        if constexpr (MASKED) {
+            if (ct < ATT_KC) Mk0[buf * ATT_KC + ct] = mkr[sl];
+        }
     };
 
     fetch(0, ic_<0>{});
     if (npair > 1) fetch(1, ic_<1>{});
-    vx_u32x4 qh[KS], ql[KS];  // B = Q^T: lane (query li, group g) holds head dims 32 ks + 8 g .. + 7
+    // B = Q^T: lane (query li, group g) holds head dims 32 ks + 8 g .. + 7;
+    // unmasked: pre-scaled by scale * log2(e) (the score is then the dot)
+    const float qsc = MASKED ? 1.f : sl2;
+    vx_u32x4 qh[QT][KS], ql[QT][KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-        float v[8];
+    for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int d = 32 * ks + 8 * g + e;
-            v[e] = (qi < N && d < HD) ? base[(size_t)qi * row3 + d] : 0.f;
+        for (int ks = 0; ks < KS; ++ks) {
+            const int qi = q0 + 16 * qt;
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int d = 32 * ks + 8 * g + e;
+                v[e] = (qi < N && d < HD) ? base[(size_t)qi * row3 + d] * qsc : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                unsigned hi, lo;
+                split2u(v[2 * e], v[2 * e + 1], hi, lo);
+                qh[qt][ks][e] = hi;
+                ql[qt][ks][e] = lo;
+            }
         }
+    f32x4 acc[QT][MT];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            unsigned hi, lo;
-            split2u(v[2 * e], v[2 * e + 1], hi, lo);
-            qh[ks][e] = hi;
-            ql[ks][e] = lo;
-        }
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[QT], lsum[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        m[qt] = -INFINITY;
+        lsum[qt] = 0.f;
     }
-    f32x4 acc[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = -INFINITY, lsum = 0.f;
     stash(ch, ic_<0>{});
     __syncthreads();
 
-    // chunk 2p + kh of this wave from buffer 2 (p & 1) + kh
-    auto process = [&](int buf) {
+    // chunk c of this wave (2p + kh) from buffer buf
+    auto process = [&](int buf, int c) {
         const unsigned char* K = Ks0 + buf * P::KBUF;
         const unsigned char* V = Vt0 + buf * P::VBUF;
         const float2* MK = Mk0 + buf * ATT_KC;
-        float s[4][4];  // [16-key block][r]: key 16*kb + 4*g + r of query li (base-2 scores)
-        float cmax = -INFINITY;
+        const int lim = N - c * ATT_KC;  // keys 16 kb + 4 g + r >= lim are past the end
+        float s[QT][4][4];  // [tile][16-key block][r]: key 16*kb + 4*g + r of query li (base-2 scores)
+        float cmax[QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) cmax[qt] = -INFINITY;
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
-            f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 st[QT];
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) st[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const unsigned char* kp = K + (16 * kb + li) * KRS + 2 * (32 * ks + 8 * g);
                 const vx_u32x4 ah = *reinterpret_cast<const vx_u32x4*>(kp);
                 const vx_u32x4 al = *reinterpret_cast<const vx_u32x4*>(kp + 2 * DP);
-                st = mfma_f16(ah, qh[ks], st);
-                st = mfma_f16(ah, ql[ks], st);
-                st = mfma_f16(al, qh[ks], st);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) st[qt] = mfma_f16(ah, qh[qt][ks], st[qt]);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) st[qt] = mfma_f16(ah, ql[qt][ks], st[qt]);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) st[qt] = mfma_f16(al, qh[qt][ks], st[qt]);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float2 mk = MK[16 * kb + 4 * g + r];
-                s[kb][r] = __builtin_fmaf(st[r], mk.x, mk.y);  // masked: 0 * dot + fill, exactly the fill
-                cmax = vmax(cmax, s[kb][r]);
+                float2 mk = make_float2(1.f, 0.f);
+                if constexpr (MASKED) mk = MK[16 * kb + 4 * g + r];
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+                    // masked: 0 * dot + fill, exactly the fill
+                    s[qt][kb][r] = MASKED ? __builtin_fmaf(st[qt][r], mk.x, mk.y) : st[qt][r];
             }
         }
-        cmax = vmax(cmax, __shfl_xor(cmax, 16));
-        cmax = vmax(cmax, __shfl_xor(cmax, 32));
-        const float mn = vmax(m, cmax);
-        // raw v_exp_f32 (results below 2^-126 flush to 0: weights that small
-        // vanish next to the row's maximum weight 1 anyway)
-        const float corr = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first chunk -> 0
-        lsum *= corr;
+        if constexpr (!MASKED) {
+            if (lim < ATT_KC) {  // the last chunk: keys past N score -inf (wave-uniform branch)
 #pragma unroll
-        for (int t = 0; t < MT; ++t) acc[t] *= corr;
+                for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
+                    for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] - mn);
-                lsum += s[kb][r];
+                        for (int qt = 0; qt < QT; ++qt)
+                            s[qt][kb][r] = 16 * kb + 4 * g + r < lim ? s[qt][kb][r] : -INFINITY;
             }
+        }
+        // row maximum: v_max3 over compiler-visible fmaxf (the first readers of
+        // the MFMA results must be instructions the compiler sees, so it puts
+        // the MFMA -> VALU wait states in front of them)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            unsigned ph[4], pl[4];  // B = P^T: keys 32j + 4g + e (e < 4), 32j + 16 + 4g + e - 4
-            split2u(s[2 * j][0], s[2 * j][1], ph[0], pl[0]);
-            split2u(s[2 * j][2], s[2 * j][3], ph[1], pl[1]);
-            split2u(s[2 * j + 1][0], s[2 * j + 1][1], ph[2], pl[2]);
-            split2u(s[2 * j + 1][2], s[2 * j + 1][3], ph[3], pl[3]);
-            const vx_u32x4 bh{ph[0], ph[1], ph[2], ph[3]}, bl{pl[0], pl[1], pl[2], pl[3]};
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+                cmax[qt] = fmaxf(fmaxf(fmaxf(cmax[qt], s[qt][kb][0]), s[qt][kb][1]), fmaxf(s[qt][kb][2], s[qt][kb][3]));
+        vx_u32x4 bh[QT][2], bl[QT][2];  // B = P^T of tile qt, 32-key half j
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            float cm = vmax(cmax[qt], __shfl_xor(cmax[qt], 16));
+            cm = vmax(cm, __shfl_xor(cm, 32));
+            const float mn = vmax(m[qt], cm);
+            // raw v_exp_f32 (results below 2^-126 flush to 0: weights that small
+            // vanish next to the row's maximum weight 1 anyway)
+            const float corr = __builtin_amdgcn_exp2f(m[qt] - mn);  // m = -inf on the first chunk -> 0
+            lsum[qt] *= corr;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[qt][t] *= corr;
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    s[qt][kb][r] = __builtin_amdgcn_exp2f(s[qt][kb][r] - mn);
+                    lsum[qt] += s[qt][kb][r];
+                }
+            m[qt] = mn;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                unsigned ph[4], pl[4];  // keys 32j + 4g + e (e < 4), 32j + 16 + 4g + e - 4
+                split2u(s[qt][2 * j][0], s[qt][2 * j][1], ph[0], pl[0]);
+                split2u(s[qt][2 * j][2], s[qt][2 * j][3], ph[1], pl[1]);
+                split2u(s[qt][2 * j + 1][0], s[qt][2 * j + 1][1], ph[2], pl[2]);
+                split2u(s[qt][2 * j + 1][2], s[qt][2 * j + 1][3], ph[3], pl[3]);
+                bh[qt][j] = vx_u32x4{ph[0], ph[1], ph[2], ph[3]};
+                bl[qt][j] = vx_u32x4{pl[0], pl[1], pl[2], pl[3]};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
                 const unsigned char* vp = V + (16 * t + li) * VRS + 2 * (32 * j + 8 * g);
                 const vx_u32x4 vh = *reinterpret_cast<const vx_u32x4*>(vp);
                 const vx_u32x4 vl = *reinterpret_cast<const vx_u32x4*>(vp + 2 * ATT_KC);
-                acc[t] = mfma_f16(vh, bh, acc[t]);
-                acc[t] = mfma_f16(vh, bl, acc[t]);
-                acc[t] = mfma_f16(vl, bh, acc[t]);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    acc[qt][t] = mfma_f16(vh, bh[qt][j], acc[qt][t]);
+                    acc[qt][t] = mfma_f16(vh, bl[qt][j], acc[qt][t]);
+                    acc[qt][t] = mfma_f16(vl, bh[qt][j], acc[qt][t]);
+                }
             }
-        }
-        m = mn;
     };
     // pair p: buffers 2 (p & 1) + {0, 1}; registers of slot p % PF (unrolled by PF)
     auto pair = [&](int p, auto sc) {
         constexpr int sl = decltype(sc)::value;
-        if (2 * p + kh < nch) process(2 * (p & 1) + kh);  // wave-uniform
+        if (2 * p + kh < nch) process(2 * (p & 1) + kh, 2 * p + kh);  // wave-uniform
         if (p + 1 < npair) {
             // the other buffer pair was last read in pair p-1, before the previous barrier
             stash(2 * ((p + 1) & 1) + ch, ic_<(sl + 1) % PF>{});
@@ -569,50 +646,79 @@ __global__ __launch_bounds__(512, HD <= 32 ? 4 : 2) void attention_split_kernel(
         if (p + 1 < npair) pair(p + 1, ic_<1>{});
     }
     // merge the two key halves: kh 1 hands (m, lsum partial, acc) to kh 0 via LDS
-    float* xs = reinterpret_cast<float*>(smem) + (qg * 64 + lane) * (2 + 4 * MT);
+    constexpr int XW = 2 + 4 * MT;
+    float* xs = reinterpret_cast<float*>(smem) + (qg * 64 + lane) * (QT * XW);
     if (kh == 1) {
-        xs[0] = m;
-        xs[1] = lsum;
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+        for (int qt = 0; qt < QT; ++qt) {
+            xs[qt * XW] = m[qt];
+            xs[qt * XW + 1] = lsum[qt];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) xs[2 + 4 * t + r] = acc[t][r];
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xs[qt * XW + 2 + 4 * t + r] = acc[qt][t][r];
+        }
     }
     __syncthreads();
     if (kh == 1) return;
-    const float mb = xs[0], mt = vmax(m, mb);
-    const float fa = __builtin_amdgcn_exp2f(m - mt), fb = __builtin_amdgcn_exp2f(mb - mt);
-    lsum = lsum * fa + xs[1] * fb;
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int qt = 0; qt < QT; ++qt) {
+        const float mb = xs[qt * XW], mt = vmax(m[qt], mb);
+        const float fa = __builtin_amdgcn_exp2f(m[qt] - mt), fb = __builtin_amdgcn_exp2f(mb - mt);
+        float ls = lsum[qt] * fa + xs[qt * XW + 1] * fb;
+        ls += __shfl_xor(ls, 16);
+        ls += __shfl_xor(ls, 32);
+        const int qi = q0 + 16 * qt;
+        if (qi < N) {
+            const float inv = 1.0f / ls;
+            float* orow = out + ((size_t)b * N + qi) * H + hh * HD;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[t][r] = acc[t][r] * fa + xs[2 + 4 * t + r] * fb;
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
-    if (qi >= N) return;
-    const float inv = 1.0f / lsum;
-    float* orow = out + ((size_t)b * N + qi) * H + hh * HD;
+            for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) orow[16 * t + 4 * g + r] = acc[t][r] * inv;
+                for (int r = 0; r < 4; ++r)
+                    orow[16 * t + 4 * g + r] = (acc[qt][t][r] * fa + xs[qt * XW + 2 + 4 * t + r] * fb) * inv;
+        }
+    }
 }
 
-template <int HD>
-static int32_t launch_att_split(dim3 grid, const float* qkv, const uint8_t* mask, int N, int H, float scale,
-                                float* out, hipStream_t st) {
-    const int nqb = (int)grid.x, heads = (int)grid.y, ngroups = (int)(grid.y * grid.z);
+template <int HD, int QT, bool MASKED>
+static int32_t launch_att_split_qt(int N, int heads, int B, const float* qkv, const uint8_t* mask, int H, float scale,
+                                   float* out, hipStream_t st) {
+    static_assert(4 * 64 * QT * (2 + 4 * (HD / 16)) * 4 <= AttSplit<HD>::LDS, "merge area inside the buffers");
+    const int nqb = cdiv(N, 64 * QT), ngroups = heads * B;
     const dim3 g1(8 * nqb * ((ngroups + 7) / 8));
     static bool attr = false;
     if (!attr) {
-        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attention_split_kernel<HD>),
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attention_split_kernel<HD, QT, MASKED>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, AttSplit<HD>::LDS));
         attr = true;
     }
-    hipLaunchKernelGGL(attention_split_kernel<HD>, g1, dim3(512), AttSplit<HD>::LDS, st, qkv, mask, N, H, scale, out,
-                       nqb, heads, ngroups);
+    hipLaunchKernelGGL((attention_split_kernel<HD, QT, MASKED>), g1, dim3(512), AttSplit<HD>::LDS, st, qkv, mask, N,
+                       H, scale, out, nqb, heads, ngroups);
     M2_LAUNCHED("attention_split_kernel");
     return M2_OK;
+}
+
+// QT = 2 halves the K/V bytes each query costs; taken for head_dim <= 32
+// while the grid keeps at least one workgroup per CU (M2_ATT_QT=1/2 forces
+// one).  tools/probe/att_bench.py, us per launch, QT=1 -> 2: 32x500x64
+// 19.0 -> 17.6; hd 48 at QT 2 spills (64x500x96 58.9 -> 301).
+template <int HD>
+static int32_t launch_att_split(dim3 grid, const float* qkv, const uint8_t* mask, int N, int H, float scale,
+                                float* out, hipStream_t st) {
+    const int heads = (int)grid.y, B = (int)grid.z;
+    static const int forced = [] {
+        const char* e = std::getenv("M2_ATT_QT");
+        return e ? std::atoi(e) : 0;
+    }();
+    // (head_dim > 32: two tiles' registers spill past the 256-VGPR cap, 6-8x slower)
+    const bool qt2 = forced ? forced == 2 : (HD <= 32 && (long)cdiv(N, 128) * heads * B >= 256);
+    if (mask) {
+        if (qt2) return launch_att_split_qt<HD, 2, true>(N, heads, B, qkv, mask, H, scale, out, st);
+        return launch_att_split_qt<HD, 1, true>(N, heads, B, qkv, mask, H, scale, out, st);
+    }
+    if (qt2) return launch_att_split_qt<HD, 2, false>(N, heads, B, qkv, mask, H, scale, out, st);
+    return launch_att_split_qt<HD, 1, false>(N, heads, B, qkv, mask, H, scale, out, st);
 }
 
 // ---------------------------------------------------------------------------

@@ -70,6 +70,14 @@ _SIGNATURES = {
     "m2_profile_select": (c_i32, [c_vp, ctypes.c_uint32]),
     "m2_profile_stride": (c_i32, [c_vp, c_i32]),
     "m2_vocoder_path": (c_i32, [c_vp]),
+    "m2_dsp_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, ctypes.POINTER(c_vp)]),
+    "m2_dsp_destroy": (c_i32, [c_vp]),
+    "m2_dsp_frames": (c_i32, [c_vp, c_i32]),
+    "m2_stft": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "m2_mel_spectrogram": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "m2_griffin_lim_workspace_bytes": (c_size, [c_vp, c_i32, c_i32]),
+    "m2_mel_to_magnitude": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "m2_griffin_lim": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_i32, c_vp, c_vp, c_size, c_vp]),
     "m2_transformer_path": (c_i32, [c_vp]),
     "m2_front_bytes": (c_size, [c_vp, c_i32, c_i32]),
     "m2_inference_workspace_bytes": (c_size, [c_vp, c_i32, c_i32, c_i32]),
