@@ -438,19 +438,31 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
         # split of one step: front (incl. the T_max host read) / all_reduce / back, rank-local wall times
         lo, hi = shard_bounds(Bg, cx.world, cx.rank)
         hm = m._hip(cx.dev)
-        torch.cuda.synchronize(cx.dev)
-        t0 = time.perf_counter()
-        state, tl = hm.inference_front(ids[lo:hi], lens[lo:hi], 1.0)
-        t1 = time.perf_counter()
-        if cx.dist:
-            t = torch.tensor([tl], dtype=torch.int32, device=cx.dev if cx.backend == "RCCL" else "cpu")
-            td.all_reduce(t, op=td.ReduceOp.MAX)
-            tl = int(t.item())
-        t2 = time.perf_counter()
-        hm.inference_back(state, max(1, tl))
-        t3 = time.perf_counter()
-        torch.cuda.synchronize(cx.dev)
-        t4 = time.perf_counter()
+        # host wall phases and GPU-elapsed (events on the launch stream) of the
+        # two halves, median of 21 steps: host-bound iff wall >> GPU-elapsed
+        ph = []
+        for _ in range(21):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            torch.cuda.synchronize(cx.dev)
+            t0 = time.perf_counter()
+            ev[0].record()
+            state, tl = hm.inference_front(ids[lo:hi], lens[lo:hi], 1.0)
+            ev[1].record()
+            t1 = time.perf_counter()
+            if cx.dist:
+                t = torch.tensor([tl], dtype=torch.int32, device=cx.dev if cx.backend == "RCCL" else "cpu")
+                td.all_reduce(t, op=td.ReduceOp.MAX)
+                tl = int(t.item())
+            t2 = time.perf_counter()
+            ev[2].record()
+            hm.inference_back(state, max(1, tl))
+            ev[3].record()
+            t3 = time.perf_counter()
+            torch.cuda.synchronize(cx.dev)
+            t4 = time.perf_counter()
+            ph.append(((t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t4 - t3) * 1e3,
+                       ev[0].elapsed_time(ev[1]), ev[2].elapsed_time(ev[3])))
+        med = [sorted(c)[len(c) // 2] for c in zip(*ph)]
     finally:
         m.set_vocoder_chunking(0)
     return {"value": round(samples_per(Bg, T) * steps / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
@@ -460,10 +472,11 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
                        "mel_frames": T, "vocoder_chunk_frames": chunk, "n_ranks": cx.world,
                        "collectives": f"all_reduce(MAX) 1 x int32 + gather of mel/audio to rank 0 ({cx.backend})" if cx.dist
                        else "none (world 1)"},
-            "rank0_phase_ms": {"front_incl_Tmax_read": round((t1 - t0) * 1e3, 3),
-                               "all_reduce": round((t2 - t1) * 1e3, 3),
-                               "back_enqueue": round((t3 - t2) * 1e3, 3),
-                               "back_drain": round((t4 - t3) * 1e3, 3)}}
+            "rank0_phase_ms": {"front_incl_Tmax_read": round(med[0], 3), "all_reduce": round(med[1], 3),
+                               "back_enqueue": round(med[2], 3), "back_drain": round(med[3], 3),
+                               "front_gpu_elapsed": round(med[4], 3), "back_gpu_elapsed": round(med[5], 3),
+                               "def": "median of 21 steps; *_gpu_elapsed = HIP events on the launch stream "
+                                      "around each half (GPU time incl. any launch gaps)"}}
 
 
 def run(args):
@@ -522,6 +535,10 @@ def run(args):
         extras["s2_vocoder_b16_t2600"] = s2l
         if wl != "s2_b64":
             extras["s2_b64_sharded"] = sharded_line(cx, 64, 100, 0, args, 100.0, max(10, args.steps // 4))
+        if world == 1:
+            # the per-GPU share of configs[3] at N=8 (8 utterances), run alone:
+            # what bounds a small per-GPU batch (host phases vs GPU-elapsed)
+            extras["s2_b8_per_gpu_share"] = sharded_line(cx, 8, 100, 0, args, 100.0, max(20, args.steps // 2))
         if wl != "s2_longform":
             extras["s2_longform_sharded"] = sharded_line(cx, 128, 520, 256, args, 100.0, max(3, args.steps // 40))
 

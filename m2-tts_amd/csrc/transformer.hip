@@ -330,6 +330,42 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
 // Row strides 160 / 288 B (RS/16 = 2 mod 4): conflict-free ds_read_b128.
 template <int V>
 using ic_ = std::integral_constant<int, V>;
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(const F& f) {
+    if constexpr (I < N) {
+        f(ic_<I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+// Diagnostic build only (-DATT_STAMPS): per-wave s_memtime stamps at phase
+// boundaries of attention_split_kernel, [workgroup][wave][16]; slots 14 / 15
+// = s_memrealtime (100 MHz) at start / end (tools/probe/att_stamps.py).
+#ifdef ATT_STAMPS
+__device__ unsigned long long g_att_stamps[2048][8][16];
+#define ASTAMP(i)                                                                                        \
+    do {                                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        unsigned long long _t;                                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                      \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048) g_att_stamps[blockIdx.x][threadIdx.x >> 6][i] = _t; \
+    } while (0)
+#define ASTAMP_RT(i)                                                                                     \
+    do {                                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        unsigned long long _t;                                                                           \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                  \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048) g_att_stamps[blockIdx.x][threadIdx.x >> 6][i] = _t; \
+    } while (0)
+#else
+#define ASTAMP(i) \
+    do {          \
+    } while (0)
+#define ASTAMP_RT(i) \
+    do {             \
+    } while (0)
+#endif
 
 // Key split: a workgroup is 8 waves = 4 query groups x 2 key halves; the
 // key-half-0 waves take the even 64-key chunks, the key-half-1 waves the odd
@@ -337,6 +373,17 @@ using ic_ = std::integral_constant<int, V>;
 // (flash-decoding inside the workgroup).  Twice the waves per query of the
 // 4-wave form at the same LDS per wave: the per-chunk latency chain (LDS ->
 // MFMA -> softmax -> MFMA) is what bounds this kernel.
+// max over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (the 16-lane groups of
+// one query).  (A permlane16/32_swap form gave wrong maxima in the masked
+// head_dim-48 instance - tools/probe/att_check.py - and the lazy path below
+// needs this only on the chunks that move the base.)
+__device__ __forceinline__ float grp4_max(float x) {
+    x = vmax(x, __shfl_xor(x, 16));
+    return vmax(x, __shfl_xor(x, 32));
+}
+// lazy-rescale threshold (base-2 units): weights stay <= 2^kLazyT
+constexpr float kLazyT = 8.f;
+
 template <int HD>
 struct AttSplit {
     static constexpr int KS = (HD + 31) / 32, DP = 32 * KS;  // QK^T k-steps, padded head dim
@@ -386,13 +433,14 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
     const int L = blockIdx.x, xcd = L & 7, r = L >> 3;
     const int grp = xcd + 8 * (r / nqb), qb = r - (r / nqb) * nqb;
     if (grp >= ngroups) return;  // padding of the last round (ngroups % 8 != 0)
+    ASTAMP_RT(14);
+    ASTAMP(0);
     const int b = grp / heads, hh = grp - b * heads;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, g = lane >> 4;
     const int qg = wave & 3, kh = wave >> 2;  // query group, key half
     const int ct = tid & 255, ch = wave >> 2;  // fetch / stash: thread within a chunk, chunk of the pair
     const int row3 = 3 * H;
-    const float* base = qkv + (size_t)b * N * row3 + hh * HD;
     const int q0 = qb * 64 * QT + qg * 16 * QT + li;  // query of tile qt: q0 + 16 qt
     const float sl2 = scale * kLog2e;
 
@@ -408,49 +456,51 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
     // Chunk pairs stream through registers PF pairs ahead of their stash.
     // K: thread = (key, head-dim quad), quads fastest (128-B rows); V: thread
     // = (key pair, quad), pairs fastest, so the transposed stores (two keys'
-    // f16 in one dword of a V^T row) hit 32 distinct banks.  Per-lane 32-bit
-    // offsets from the chunk's first row, fixed for the whole kernel.
+    // f16 in one dword of a V^T row) hit 32 distinct banks.  Loads are
+    // buffer loads through a per-chunk descriptor (base = the chunk's first
+    // row, records = the rows left before N): per-lane byte offsets fixed for
+    // the whole kernel, no address arithmetic per load (the VALU issue is what
+    // bounds this loop), and rows past N read as zeros (they score -inf).
+    // Every load is unconditional: a load inside a branch makes the compiler
+    // wait for it at once (s_waitcnt vmcnt(0) at the join), which serialised
+    // the prologue's loads (tools/probe/att_stamps.py).
+    // PF = 2 pairs ahead; requesting every pair of N <= 512 in the prologue
+    // (4 register slots) measured 5 % slower: the loop is VALU-issue bound.
     constexpr int PF = 2;
     constexpr int NQ4 = HD / 4, ITV = (32 * NQ4 + 255) / 256;
-    int koff[IT], kkey[IT], voff[ITV], vkey[ITV];
+    const float* ubase = qkv + (size_t)b * N * row3;  // this utterance's rows
+    const int hoff = hh * HD;
+    int kvo[IT], vvo[ITV][2];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int i = ct + it * 256, key = i / NQ4, d4 = i - key * NQ4;
-        kkey[it] = key;
-        koff[it] = key * row3 + H + 4 * d4;
+        kvo[it] = 4 * (key * row3 + H + hoff + 4 * d4);
     }
 #pragma unroll
     for (int it = 0; it < ITV; ++it) {
-        const int i = ct + it * 256, pr = i & 31, d4 = i >> 5;
-        vkey[it] = d4 < NQ4 ? 2 * pr : ATT_KC;  // past the quads: never loaded
-        voff[it] = 2 * pr * row3 + 2 * H + 4 * (d4 < NQ4 ? d4 : 0);
+        const int i = ct + it * 256, pr = i & 31, d4 = i >> 5;  // lanes past the quads load, are not stashed
+#pragma unroll
+        for (int h = 0; h < 2; ++h) vvo[it][h] = 4 * ((2 * pr + h) * row3 + 2 * H + hoff + 4 * (d4 < NQ4 ? d4 : 0));
     }
     float4 kr[PF][IT], vr[PF][ITV][2];
-    float2 mkr[PF];
+    int mraw[PF];
     const int nch = (N + ATT_KC - 1) / ATT_KC, npair = (nch + 1) / 2;
     auto fetch = [&](int pr_, auto sc) {  // chunk 2 pr_ + ch
         constexpr int sl = decltype(sc)::value;
-        const int j0 = (2 * pr_ + ch) * ATT_KC, lim = N - j0;  // keys of this chunk with key < lim exist
-        const float* cb = base + (size_t)j0 * row3;
+        const int j0 = (2 * pr_ + ch) * ATT_KC;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ubase) + (size_t)j0 * row3, 0,
+                                                          4 * max(N - j0, 0) * row3, 0x00020000);
 #pragma unroll
         for (int it = 0; it < IT; ++it)
-            kr[sl][it] = kkey[it] < lim ? *reinterpret_cast<const float4*>(cb + koff[it]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            kr[sl][it] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, kvo[it], 0, 0));
 #pragma unroll
         for (int it = 0; it < ITV; ++it)
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                vr[sl][it][h] = vkey[it] + h < lim ? *reinterpret_cast<const float4*>(cb + voff[it] + h * row3)
-                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (MASKED) {
-            if (ct < ATT_KC) {
-                const int j = j0 + ct;
-                mkr[sl] = j >= N ? make_float2(0.f, -INFINITY)
-                                 : ((key_mask && key_mask[(size_t)b * N + j] == 0)
-                                        ? make_float2(0.f, kMaskFill * kLog2e) : make_float2(sl2, 0.f));
-            }
-        }
+                vr[sl][it][h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vvo[it][h], 0, 0));
+        if constexpr (MASKED) mraw[sl] = key_mask[(size_t)b * N + min(j0 + (ct & (ATT_KC - 1)), N - 1)];
     };
-    auto stash = [&](int buf, auto sc) {  // this thread's chunk of the pair into buffer buf
+    auto stash = [&](int buf, int pr_, auto sc) {  // this thread's chunk of pair pr_ into buffer buf
         constexpr int sl = decltype(sc)::value;
         unsigned char* Kb = Ks0 + buf * P::KBUF;
         unsigned char* Vb = Vt0 + buf * P::VBUF;
@@ -484,27 +534,43 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
             }
         }
         if constexpr (MASKED) {
-            if (ct < ATT_KC) Mk0[buf * ATT_KC + ct] = mkr[sl];
+            if (ct < ATT_KC) {
+                const int j = (2 * pr_ + ch) * ATT_KC + ct;
+                Mk0[buf * ATT_KC + ct] = j >= N ? make_float2(0.f, -INFINITY)
+                                                : (mraw[sl] == 0 ? make_float2(0.f, kMaskFill * kLog2e)
+                                                                 : make_float2(sl2, 0.f));
+            }
         }
     };
 
-    fetch(0, ic_<0>{});
-    if (npair > 1) fetch(1, ic_<1>{});
     // B = Q^T: lane (query li, group g) holds head dims 32 ks + 8 g .. + 7;
-    // unmasked: pre-scaled by scale * log2(e) (the score is then the dot)
+    // unmasked: pre-scaled by scale * log2(e) (the score is then the dot).
+    // Q rows (past N: zeros, never stored) are requested before the first
+    // K / V pairs and converted after them.
+    float4 qr[QT][KS][2];
+    {
+        const auto rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ubase), 0, 4 * N * row3, 0x00020000);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int qo = 4 * ((q0 + 16 * qt) * row3 + hoff + 32 * ks + 8 * g);
+                qr[qt][ks][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rq, qo, 0, 0));
+                qr[qt][ks][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rq, qo + 16, 0, 0));
+            }
+    }
+    static_for<PF>([&](auto kc) { fetch(decltype(kc)::value, kc); });  // unconditional (zero rows past N)
     const float qsc = MASKED ? 1.f : sl2;
     vx_u32x4 qh[QT][KS], ql[QT][KS];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            const int qi = q0 + 16 * qt;
+            const float q8[8] = {qr[qt][ks][0].x, qr[qt][ks][0].y, qr[qt][ks][0].z, qr[qt][ks][0].w,
+                                 qr[qt][ks][1].x, qr[qt][ks][1].y, qr[qt][ks][1].z, qr[qt][ks][1].w};
             float v[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int d = 32 * ks + 8 * g + e;
-                v[e] = (qi < N && d < HD) ? base[(size_t)qi * row3 + d] * qsc : 0.f;
-            }
+            for (int e = 0; e < 8; ++e) v[e] = 32 * ks + 8 * g + e < HD ? q8[e] * qsc : 0.f;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 unsigned hi, lo;
@@ -521,13 +587,23 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
     float m[QT], lsum[QT];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
-        m[qt] = -INFINITY;
+        m[qt] = MASKED ? -INFINITY : 0.f;
         lsum[qt] = 0.f;
     }
-    stash(ch, ic_<0>{});
+    bool fresh = true;  // unmasked: no chunk processed yet by this wave (wave-uniform)
+    ASTAMP(1);
+    stash(ch, 0, ic_<0>{});
     __syncthreads();
+    ASTAMP(2);
 
     // chunk c of this wave (2p + kh) from buffer buf
+    // MASKED (the encoder): per-key (scale, fill) table, eager online softmax.
+    // Unmasked (the decoder): lazy rescaling - the scores are accumulated
+    // relative to the running base m (the QK MFMAs start from C = -m) and m
+    // moves only on the wave's first chunk or when a score exceeds it by more
+    // than kLazyT, so most chunks take no subtraction per score and no
+    // rescale of acc / lsum.  Exact up to rounding: numerator and lsum share
+    // the base, every weight 2^(s - m) stays <= 2^kLazyT.
     auto process = [&](int buf, int c) {
         const unsigned char* K = Ks0 + buf * P::KBUF;
         const unsigned char* V = Vt0 + buf * P::VBUF;
@@ -535,13 +611,18 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
         const int lim = N - c * ATT_KC;  // keys 16 kb + 4 g + r >= lim are past the end
         float s[QT][4][4];  // [tile][16-key block][r]: key 16*kb + 4*g + r of query li (base-2 scores)
         float cmax[QT];
+        f32x4 c0[QT];
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) cmax[qt] = -INFINITY;
+        for (int qt = 0; qt < QT; ++qt) {
+            cmax[qt] = -INFINITY;
+            const float nm = (MASKED || fresh) ? 0.f : -m[qt];
+            c0[qt] = f32x4{nm, nm, nm, nm};
+        }
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
             f32x4 st[QT];
 #pragma unroll
-            for (int qt = 0; qt < QT; ++qt) st[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int qt = 0; qt < QT; ++qt) st[qt] = c0[qt];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const unsigned char* kp = K + (16 * kb + li) * KRS + 2 * (32 * ks + 8 * g);
@@ -583,26 +664,56 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb)
                 cmax[qt] = fmaxf(fmaxf(fmaxf(cmax[qt], s[qt][kb][0]), s[qt][kb][1]), fmaxf(s[qt][kb][2], s[qt][kb][3]));
+        if constexpr (MASKED) {
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const float mn = vmax(m[qt], grp4_max(cmax[qt]));
+                // raw v_exp_f32 (results below 2^-126 flush to 0: weights that small
+                // vanish next to the row's maximum weight 1 anyway)
+                const float corr = __builtin_amdgcn_exp2f(m[qt] - mn);  // m = -inf on the first chunk -> 0
+                lsum[qt] *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[qt][t] *= corr;
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qt][kb][r] -= mn;
+                m[qt] = mn;
+            }
+        } else {
+            bool up = fresh;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) up = up || cmax[qt] > kLazyT;
+            if (__builtin_amdgcn_ballot_w64(up) != 0) {  // wave-uniform: move the base
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    const float cm = grp4_max(cmax[qt]);  // finite: a processed chunk has a live key
+                    const float d = fresh ? cm : vmax(cm, 0.f);
+                    m[qt] += d;
+                    if (!fresh) {
+                        const float corr = __builtin_amdgcn_exp2f(-d);
+                        lsum[qt] *= corr;
+#pragma unroll
+                        for (int t = 0; t < MT; ++t) acc[qt][t] *= corr;
+                    }
+#pragma unroll
+                    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[qt][kb][r] -= d;
+                }
+            }
+            fresh = false;
+        }
         vx_u32x4 bh[QT][2], bl[QT][2];  // B = P^T of tile qt, 32-key half j
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
-            float cm = vmax(cmax[qt], __shfl_xor(cmax[qt], 16));
-            cm = vmax(cm, __shfl_xor(cm, 32));
-            const float mn = vmax(m[qt], cm);
-            // raw v_exp_f32 (results below 2^-126 flush to 0: weights that small
-            // vanish next to the row's maximum weight 1 anyway)
-            const float corr = __builtin_amdgcn_exp2f(m[qt] - mn);  // m = -inf on the first chunk -> 0
-            lsum[qt] *= corr;
-#pragma unroll
-            for (int t = 0; t < MT; ++t) acc[qt][t] *= corr;
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    s[qt][kb][r] = __builtin_amdgcn_exp2f(s[qt][kb][r] - mn);
+                    s[qt][kb][r] = __builtin_amdgcn_exp2f(s[qt][kb][r]);
                     lsum[qt] += s[qt][kb][r];
                 }
-            m[qt] = mn;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 unsigned ph[4], pl[4];  // keys 32j + 4g + e (e < 4), 32j + 16 + 4g + e - 4
@@ -635,19 +746,26 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
         if (2 * p + kh < nch) process(2 * (p & 1) + kh, 2 * p + kh);  // wave-uniform
         if (p + 1 < npair) {
             // the other buffer pair was last read in pair p-1, before the previous barrier
-            stash(2 * ((p + 1) & 1) + ch, ic_<(sl + 1) % PF>{});
+            stash(2 * ((p + 1) & 1) + ch, p + 1, ic_<(sl + 1) % PF>{});
             if (p + PF < npair) fetch(p + PF, ic_<sl>{});  // slot sl is free again
         }
         __syncthreads();
+#ifdef ATT_STAMPS
+        if (p < 9) ASTAMP(3 + p);
+#endif
     };
 #pragma unroll 1
-    for (int p = 0; p < npair; p += PF) {
-        pair(p, ic_<0>{});
-        if (p + 1 < npair) pair(p + 1, ic_<1>{});
-    }
+    for (int p = 0; p < npair; p += PF)
+        static_for<PF>([&](auto kc) {
+            if (p + decltype(kc)::value < npair) pair(p + decltype(kc)::value, kc);
+        });
     // merge the two key halves: kh 1 hands (m, lsum partial, acc) to kh 0 via LDS
     constexpr int XW = 2 + 4 * MT;
     float* xs = reinterpret_cast<float*>(smem) + (qg * 64 + lane) * (QT * XW);
+    if (!MASKED && fresh) {  // this wave processed no chunk (kh 1 of a one-chunk utterance)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) m[qt] = -INFINITY;
+    }
     if (kh == 1) {
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
@@ -660,6 +778,7 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
         }
     }
     __syncthreads();
+    ASTAMP(12);
     if (kh == 1) return;
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
@@ -679,7 +798,16 @@ __global__ __launch_bounds__(512, (HD <= 32 && QT == 1) ? 4 : 2) void attention_
                     orow[16 * t + 4 * g + r] = (acc[qt][t][r] * fa + xs[qt * XW + 2 + 4 * t + r] * fb) * inv;
         }
     }
+    ASTAMP(13);
+    ASTAMP_RT(15);
 }
+
+#ifdef ATT_STAMPS
+extern "C" int32_t m2_debug_stamps_att(void* host, size_t bytes) {
+    return (int32_t)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_stamps),
+                                        bytes < sizeof(g_att_stamps) ? bytes : sizeof(g_att_stamps));
+}
+#endif
 
 template <int HD, int QT, bool MASKED>
 static int32_t launch_att_split_qt(int N, int heads, int B, const float* qkv, const uint8_t* mask, int H, float scale,
