@@ -692,14 +692,40 @@ struct CfgS1 {
     // head ConvT1 / ResBlock1: m-blocks per item sharing B (2: half the B reads)
     static constexpr int G_T1 = X3_G_T1, G_R1 = X3_G_R1;
 };
+#ifndef X3S2_TF  // stage2 tiling experiments (tools/probe/s2_tiles.sh)
+#define X3S2_TF 16
+#define X3S2_NT_R1 5
+#endif
+#ifndef X3S2_W2
+#define X3S2_W2 28
+#define X3S2_NT_R2 4
+#endif
+#ifndef X3S2_W3
+#define X3S2_W3 120
+#define X3S2_NT_T3 4
+#define X3S2_NT_R3 4
+#endif
 struct CfgS2 {
     static constexpr int M = 80, MP = 96, C = 256;
-    static constexpr int TF = 12, HW = 8, HMIN = 2;
-    static constexpr int W2 = 28, MW = 8, MMIN = 2;
-    static constexpr int W3 = 120, TW = 8, TMIN = 2;
-    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
+    static constexpr int TF = X3S2_TF, HW = 8, HMIN = 2;
+    static constexpr int W2 = X3S2_W2, MW = 8, MMIN = 2;
+    static constexpr int W3 = X3S2_W3, TW = 8, TMIN = 2;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = X3S2_NT_R1, NT_T2 = 4, NT_R2 = X3S2_NT_R2, NT_T3 = X3S2_NT_T3,
+                         NT_R3 = X3S2_NT_R3, NT_T4 = 4, NT_R4 = 4;
     static constexpr int G_T1 = 1, G_R1 = 1;
 };
+// Stage2 mid / tail tilings for small grids (run<CfgS2> picks per call): at
+// B=8, T=500 the default windows make 576 mid workgroups (1.1 rounds of 512
+// slots at two per CU) and 536 tail workgroups (2.1 rounds of 256 at one
+// per CU); 32 / 125 make 504 and 512 (one and two full rounds), at 1.20x /
+// 1.075x the time per workgroup (5-tile chunks where 4 were enough).
+// Measured B=8 T=500: mid 26.4 -> 22.9 us, tail 35.5 -> 26.1 us; large grids
+// keep the defaults (tools/probe/s2_tiles.sh).
+struct CfgS2Alt : CfgS2 {
+    static constexpr int W2 = 32, NT_R2 = 5;
+    static constexpr int W3 = 125, NT_T3 = 5, NT_R3 = 5;
+};
+constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
 
 // Diagnostic build only (-DM2_STAMPS): per-wave s_memtime stamps at phase
 // boundaries, [kernel][workgroup][wave][16] (tools/probe/stamps.py --x3).
@@ -955,12 +981,32 @@ int32_t set_lds(K kernel, size_t bytes) {
     return M2_OK;
 }
 
+// Full rounds of a grid of n workgroups at the kernel's occupancy.
+template <typename K>
+long grid_rounds(K kernel, int threads, size_t lds, long n) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    }
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kernel), threads, lds) !=
+            hipSuccess || per <= 0)
+        per = 1;
+    const long slots = (long)per * ncu;
+    return (n + slots - 1) / slots;
+}
+
 template <class Cfg>
 int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1, void* U2, float* audio,
             hipStream_t st, const std::function<void(int, bool)>& mark) {
     using HP = HeadPlan<Cfg::MP, Cfg::C, Cfg::TF, head_planar<Cfg>()>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
+    constexpr bool S2 = std::is_same<Cfg, CfgS2>::value;
+    using MPA = MidPlan<CfgS2Alt::C / 2, CfgS2Alt::W2>;
+    using TPA = TailPlan<CfgS2Alt::C / 4, CfgS2Alt::W3>;
     static bool attr = false;
     if (!attr) {
         int32_t rc;
@@ -968,7 +1014,26 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         if ((rc = set_lds(x3_head_kernel<Cfg, true>, HP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_mid_kernel<Cfg>, MP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_tail_kernel<Cfg>, TP::LDS_BYTES))) return rc;
+        if constexpr (S2) {
+            if ((rc = set_lds(x3_mid_kernel<CfgS2Alt>, MPA::LDS_BYTES))) return rc;
+            if ((rc = set_lds(x3_tail_kernel<CfgS2Alt>, TPA::LDS_BYTES))) return rc;
+        }
         attr = true;
+    }
+    bool alt_mid = false, alt_tail = false;
+    if constexpr (S2) {
+        if (!w.mp) {
+            const long r0 = grid_rounds(x3_mid_kernel<Cfg>, Cfg::MW * 64, MP::LDS_BYTES, (long)cdiv(4 * T, Cfg::W2) * B);
+            const long r1 = grid_rounds(x3_mid_kernel<CfgS2Alt>, Cfg::MW * 64, MPA::LDS_BYTES,
+                                        (long)cdiv(4 * T, CfgS2Alt::W2) * B);
+            alt_mid = r1 * kAltMidCost < (double)r0;
+        }
+        if (!w.tp) {
+            const long r0 = grid_rounds(x3_tail_kernel<Cfg>, Cfg::TW * 64, TP::LDS_BYTES, (long)cdiv(16 * T, Cfg::W3) * B);
+            const long r1 = grid_rounds(x3_tail_kernel<CfgS2Alt>, Cfg::TW * 64, TPA::LDS_BYTES,
+                                        (long)cdiv(16 * T, CfgS2Alt::W3) * B);
+            alt_tail = r1 * kAltTailCost < (double)r0;
+        }
     }
     auto* u1 = static_cast<unsigned char*>(U1);
     auto* u2 = static_cast<unsigned char*>(U2);
@@ -985,6 +1050,10 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     if (w.mp) {  // stage1: the pipelined mid stage (vocoder_midp.hip)
         const int32_t rc = launch_vocoder_midp(u1, 4 * T, B, w.mp, w.mpb, u2, st);
         if (rc) return rc;
+    } else if (S2 && alt_mid) {
+        hipLaunchKernelGGL((x3_mid_kernel<CfgS2Alt>), dim3(cdiv(4 * T, CfgS2Alt::W2), B), dim3(Cfg::MW * 64),
+                           MPA::LDS_BYTES, st, u1, 4 * T, w, u2);
+        M2_LAUNCHED("x3_mid_kernel");
     } else {
         hipLaunchKernelGGL((x3_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(Cfg::MW * 64), MP::LDS_BYTES, st,
                            u1, 4 * T, w, u2);
@@ -997,8 +1066,12 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         mark(2, false);
         return rc;
     }
-    hipLaunchKernelGGL((x3_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(Cfg::TW * 64), TP::LDS_BYTES, st, u2,
-                       16 * T, w, audio);
+    if (S2 && alt_tail)
+        hipLaunchKernelGGL((x3_tail_kernel<CfgS2Alt>), dim3(cdiv(16 * T, CfgS2Alt::W3), B), dim3(Cfg::TW * 64),
+                           TPA::LDS_BYTES, st, u2, 16 * T, w, audio);
+    else
+        hipLaunchKernelGGL((x3_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(Cfg::TW * 64), TP::LDS_BYTES, st,
+                           u2, 16 * T, w, audio);
     mark(2, false);
     M2_LAUNCHED("x3_tail_kernel");
     return M2_OK;
