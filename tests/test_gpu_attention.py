@@ -86,3 +86,20 @@ def test_attention_long_form(gpu):
     qkv = make_qkv(2, 2600, 96, 2, "random", gen)
     got = ops.attention_core(qkv.to(gpu), 2, None).cpu().double()
     assert float((got - ref_attention(qkv, 2, None)).abs().max()) <= TOL
+
+
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("N", [257, 500])
+def test_attention_wide_grid_head_dim_32(gpu, masked, N):
+    """B=64, hd 32: grids of >= 256 workgroups take the two-query-tile
+    variant (128 queries per workgroup), masked and unmasked."""
+    from m2amd import ops
+    heads, H, B = 2, 64, 64
+    gen = torch.Generator().manual_seed(N + masked)
+    qkv = make_qkv(B, N, H, heads, "random", gen)
+    mask = None
+    if masked:
+        lens = torch.randint(1, N + 1, (B,), generator=gen)
+        mask = torch.arange(N)[None, :] < lens[:, None]
+    got = ops.attention_core(qkv.to(gpu), heads, None if mask is None else mask.to(gpu)).cpu().double()
+    assert float((got - ref_attention(qkv, heads, mask)).abs().max()) <= TOL
