@@ -316,6 +316,57 @@ int32_t run_layer(const m2_model* m, const m2_layer_w& L, const float* x_in, flo
     return M2_OK;
 }
 
+// A stack of layers; x_in -> x (x_in may be x).  On the fused path each
+// layer's post-attention kernel also runs the next layer's LN1 -> QKV on its
+// row tile (and, with fin_W, the final LN -> projection into fin_out: then
+// *fin_done), one launch per layer fewer; results are identical to the
+// separate launches (same fp32 y into the same LayerNorm / GEMM code).
+int32_t run_stack(const m2_model* m, const std::vector<m2_layer_w>& layers, const float* x_in, float* x, TfBufs& wb,
+                  const uint8_t* mask, int B, int N, hipStream_t st, const float* fin_g = nullptr,
+                  const float* fin_b = nullptr, const float* fin_W = nullptr, const float* fin_bias = nullptr,
+                  int fin_N = 0, float* fin_out = nullptr, bool* fin_done = nullptr) {
+    const int H = m->cfg.hidden_dim, R = B * N, n = (int)layers.size();
+    if (fin_done) *fin_done = false;
+    int32_t rc;
+    static const bool chain_ok = [] {  // M2_TF_CHAIN=0: separate ln_gemm launches (A/B)
+        const char* e = std::getenv("M2_TF_CHAIN");
+        return !e || std::atoi(e) != 0;
+    }();
+    const bool chain = chain_ok && m->tfused && tf_post_next_supported(H, 3 * H);
+    if (!chain) {
+        const float* cur = x_in;
+        for (const auto& L : layers) {
+            if ((rc = run_layer(m, L, cur, x, wb, mask, B, N, st))) return rc;
+            cur = x;
+        }
+        return M2_OK;
+    }
+    if (n == 0) return M2_OK;
+    const float* cur = x_in;
+    if ((rc = launch_ln_gemm(cur, layers[0].n1_w, layers[0].n1_b, layers[0].qkv_p, nullptr, ACT_NONE, R, H, 3 * H,
+                             wb.qkv, st)))
+        return rc;
+    for (int l = 0; l < n; ++l) {
+        const m2_layer_w& L = layers[l];
+        if ((rc = launch_attention(wb.qkv, mask, B, N, H, m->cfg.num_heads, wb.att, st, m->att_f32))) return rc;
+        if (l + 1 < n) {
+            const m2_layer_w& Nx = layers[l + 1];
+            rc = launch_post_attn_next(wb.att, cur, L.out_p, L.out_b, L.n2_w, L.n2_b, L.ff1_p, L.ff1_b, L.ff2_p,
+                                       L.ff2_b, R, H, x, Nx.n1_w, Nx.n1_b, Nx.qkv_p, nullptr, 3 * H, wb.qkv, st);
+        } else if (fin_W && tf_post_next_supported(H, fin_N)) {
+            rc = launch_post_attn_next(wb.att, cur, L.out_p, L.out_b, L.n2_w, L.n2_b, L.ff1_p, L.ff1_b, L.ff2_p,
+                                       L.ff2_b, R, H, x, fin_g, fin_b, fin_W, fin_bias, fin_N, fin_out, st);
+            if (!rc && fin_done) *fin_done = true;
+        } else {
+            rc = launch_post_attn(wb.att, cur, L.out_p, L.out_b, L.n2_w, L.n2_b, L.ff1_p, L.ff1_b, L.ff2_p, L.ff2_b, R,
+                                  H, x, st);
+        }
+        if (rc) return rc;
+        cur = x;
+    }
+    return M2_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -805,9 +856,7 @@ int32_t text_encoder_layers(const m2_model* m, const int64_t* ids, const int64_t
     if ((rc = launch_embed_pe(ids, m->emb, m->pe, B, S, H, m->cfg.vocab_size, wb.x, lengths,
                               const_cast<uint8_t*>(mask), st)))
         return rc;
-    for (const auto& L : m->enc)
-        if ((rc = run_layer(m, L, wb.x, wb.x, wb, mask, B, S, st))) return rc;
-    return M2_OK;
+    return run_stack(m, m->enc, wb.x, wb.x, wb, mask, B, S, st);
 }
 }  // namespace
 
@@ -950,11 +999,12 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_mel_decoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
     int32_t rc;
-    const float* cur = x;
-    for (const auto& L : m->dec) {
-        if ((rc = run_layer(m, L, cur, wb.x, wb, nullptr, B, T, st))) return rc;
-        cur = wb.x;
-    }
+    bool projected = false;
+    if ((rc = run_stack(m, m->dec, x, wb.x, wb, nullptr, B, T, st, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b,
+                        m->cfg.mel_channels, out_mel, &projected)))
+        return rc;
+    if (projected) return M2_OK;
+    const float* cur = m->dec.empty() ? x : wb.x;
     if (m->tfused)
         return launch_ln_gemm(cur, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b, ACT_NONE, B * T, H, m->cfg.mel_channels,
                               out_mel, st);

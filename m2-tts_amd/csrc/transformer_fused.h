@@ -20,5 +20,12 @@ int32_t launch_ln_gemm(const float* x, const float* g, const float* b, const flo
 int32_t launch_post_attn(const float* att, const float* x, const float* Wo, const float* bo, const float* g2,
                          const float* b2n, const float* W1, const float* b1, const float* W2, const float* b2, int R,
                          int H, float* y, hipStream_t st);
+// post_attn followed, on the same row tile, by z = LN(y; gn, bn) . Wn^T (+ bn2)
+// with NN output columns (the next layer's LN1 -> QKV, or the final LN -> mel).
+bool tf_post_next_supported(int H, int NN);
+int32_t launch_post_attn_next(const float* att, const float* x, const float* Wo, const float* bo, const float* g2,
+                              const float* b2n, const float* W1, const float* b1, const float* W2, const float* b2,
+                              int R, int H, float* y, const float* gn, const float* bn, const float* Wn,
+                              const float* bn2, int NN, float* z, hipStream_t st);
 
 }  // namespace m2

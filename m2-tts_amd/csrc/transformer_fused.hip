@@ -224,13 +224,21 @@ __global__ __launch_bounds__(256) void ln_gemm_kernel(const float* __restrict__ 
 
 // y = o + (relu(LN2(o) . W1^T + b1) . W2^T + b2),  o = x + att . Wo^T + bo.
 // y may alias x (each tile reads its rows before writing them).
-template <int H>
+// NN > 0: the next launch's row-local LN + GEMM runs on the tile too,
+// z = LN(y; gn, bn) . Wn^T (+ bn2) with NN output columns - the next layer's
+// LN1 -> QKV, or the decoder's final LN -> mel projection - so y is read back
+// from LDS instead of HBM and one launch per layer goes away.
+template <int H, int NN = 0>
 __global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict__ att, const float* x,
                                                         const u32x4* __restrict__ Wo, const float* __restrict__ bo,
                                                         const float* __restrict__ g2, const float* __restrict__ b2n,
                                                         const u32x4* __restrict__ W1, const float* __restrict__ b1,
                                                         const u32x4* __restrict__ W2, const float* __restrict__ b2,
-                                                        int R, float* y) {
+                                                        int R, float* y, const float* __restrict__ gn = nullptr,
+                                                        const float* __restrict__ bn = nullptr,
+                                                        const u32x4* __restrict__ Wn = nullptr,
+                                                        const float* __restrict__ bn2 = nullptr,
+                                                        float* __restrict__ z = nullptr) {
     constexpr int F = 2 * H;
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att tile, then LN2(o) (split)
     __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];           // o (fp32)
@@ -271,11 +279,25 @@ __global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict_
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
             const int rr = rb * 16 + i, row = r0 + rr, col = nb * 16 + 4 * gq;
-            if (row < R)
-                *reinterpret_cast<f32x4*>(y + (size_t)row * H + col) =
-                    *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
+            const f32x4 v = *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
+            if (row < R) *reinterpret_cast<f32x4*>(y + (size_t)row * H + col) = v;
+            if constexpr (NN > 0) *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = v;  // y kept for the next LN
         }
     });
+    if constexpr (NN > 0) {
+        Strip<H> sn;
+        if (wave < NN / 16) sn.load(Wn, wave);
+        __syncthreads();
+        ln_rows<H>(O, A, gn, bn);  // same rounding as ln_gemm_kernel's
+        __syncthreads();
+        gemm_cols<H, NN / 16>(A, Wn, sn, bn2, [&](int nb, const f32x4 (&acc)[2]) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                const int row = r0 + rb * 16 + i;
+                if (row < R) *reinterpret_cast<f32x4*>(z + (size_t)row * NN + nb * 16 + 4 * gq) = acc[rb];
+            }
+        });
+    }
 }
 
 }  // namespace tfx
@@ -363,6 +385,38 @@ int32_t launch_post_attn(const float* att, const float* x, const float* Wo, cons
     }
     M2_LAUNCHED("post_attn_kernel");
     return M2_OK;
+}
+
+bool tf_post_next_supported(int H, int NN) {
+    return (H == 32 && (NN == 96 || NN == 32 || NN == 64)) || (H == 64 && (NN == 192 || NN == 64 || NN == 80)) ||
+           (H == 96 && (NN == 288 || NN == 80 || NN == 96));
+}
+
+int32_t launch_post_attn_next(const float* att, const float* x, const float* Wo, const float* bo, const float* g2,
+                              const float* b2n, const float* W1, const float* b1, const float* W2, const float* b2,
+                              int R, int H, float* y, const float* gn, const float* bn, const float* Wn,
+                              const float* bn2, int NN, float* z, hipStream_t st) {
+    if (R == 0) return M2_OK;
+    const dim3 grid(cdiv(R, tfx::TR)), blk(256);
+    auto f4 = [](const float* p) { return reinterpret_cast<const vx_u32x4*>(p); };
+#define M2_PAN(HH, NNN)                                                                                           \
+    if (H == HH && NN == NNN) {                                                                                   \
+        hipLaunchKernelGGL((tfx::post_attn_kernel<HH, NNN>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n, f4(W1), b1, \
+                           f4(W2), b2, R, y, gn, bn, f4(Wn), bn2, z);                                             \
+        M2_LAUNCHED("post_attn_kernel");                                                                          \
+        return M2_OK;                                                                                             \
+    }
+    M2_PAN(32, 96)
+    M2_PAN(32, 32)
+    M2_PAN(32, 64)
+    M2_PAN(64, 192)
+    M2_PAN(64, 64)
+    M2_PAN(64, 80)
+    M2_PAN(96, 288)
+    M2_PAN(96, 80)
+    M2_PAN(96, 96)
+#undef M2_PAN
+    return fail(M2_E_SHAPE, "post_attn: unsupported (hidden_dim, next width)");
 }
 
 }  // namespace m2

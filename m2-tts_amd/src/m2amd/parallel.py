@@ -66,10 +66,15 @@ class HipStages:
         self.model = model
 
     def front(self, ids: Tensor, lens: Optional[Tensor], scale: float) -> Tuple[Any, int]:
-        return self.model._hip(ids.device).inference_front(ids, lens, scale)
+        # one handle lookup per step (its weight-identity check walks every
+        # parameter, ~25 us of host time): the back half reuses this handle
+        hm = self.model._hip(ids.device)
+        state, t = hm.inference_front(ids, lens, scale)
+        return (hm, state), t
 
     def back(self, state: Any, T: int) -> Tuple[Tensor, Tensor]:
-        return self.model._hip(state[2].device).inference_back(state, T)
+        hm, st = state
+        return hm.inference_back(st, T)
 
 
 def hip_stages(model) -> HipStages:
