@@ -28,14 +28,24 @@ X3 = {
         "bar", "outconv"],
 }
 x3 = "--x3" in sys.argv
-argv = [a for a in sys.argv[1:] if a != "--x3"]
+s2 = "--s2" in sys.argv  # stage2 (C=256, M=80; random-init weights), T from --T=
+argv = [a for a in sys.argv[1:] if a not in ("--x3", "--s2") and not a.startswith("--T=")]
+T = int(next((a[4:] for a in sys.argv if a.startswith("--T=")), "500"))
 if x3:
     PHASES = X3
 B = int(argv[0]) if argv else 4
 dev = torch.device("cuda", 0)
 lib = _lib.load()
-model = bench.fixture_model(dev)
-mel = torch.randn(B, 64, 500, device=dev)
+if s2:
+    from models.tts_model import M2TTSModel
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import m2tts_oracle as orc
+    torch.manual_seed(0)
+    model = M2TTSModel(**orc.STAGE2.as_dict()).to(dev).eval()
+    mel = torch.randn(B, 80, T, device=dev)
+else:
+    model = bench.fixture_model(dev)
+    mel = torch.randn(B, 64, T, device=dev)
 for _ in range(3):
     model.vocoder(mel)
 torch.cuda.synchronize()
