@@ -17,7 +17,7 @@ import bench  # noqa: E402
 from m2amd import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
-model = bench.fixture_model(dev)
+model = bench.fixture_model(bench.STAGE1, dev)
 g = torch.Generator().manual_seed(0)
 ids = torch.randint(0, 42, (32, 100), generator=g).to(dev)
 lens = torch.full((32,), 100, dtype=torch.int64).to(dev)

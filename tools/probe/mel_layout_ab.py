@@ -16,7 +16,7 @@ sys.path.insert(0, str(ROOT / "m2-tts_amd" / "src"))
 import bench  # noqa: E402
 
 dev = torch.device("cuda", 0)
-model = bench.fixture_model(dev)
+model = bench.fixture_model(bench.STAGE1, dev)
 hm = model._hip(dev)
 g = torch.Generator().manual_seed(0)
 mel_btm = torch.randn(32, 500, 64, generator=g).to(dev)

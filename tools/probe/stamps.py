@@ -44,7 +44,7 @@ if s2:
     model = M2TTSModel(**orc.STAGE2.as_dict()).to(dev).eval()
     mel = torch.randn(B, 80, T, device=dev)
 else:
-    model = bench.fixture_model(dev)
+    model = bench.fixture_model(bench.STAGE1, dev)
     mel = torch.randn(B, 64, T, device=dev)
 for _ in range(3):
     model.vocoder(mel)

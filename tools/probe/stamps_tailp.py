@@ -25,7 +25,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = 500
 dev = torch.device("cuda", 0)
 lib = _lib.load()
-model = bench.fixture_model(dev)
+model = bench.fixture_model(bench.STAGE1, dev)
 mel = torch.randn(B, 64, T, device=dev)
 for _ in range(3):
     model.vocoder(mel)

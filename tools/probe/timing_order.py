@@ -16,7 +16,7 @@ from m2amd import _lib  # noqa: E402
 
 dev = torch.device("cuda", 0)
 lib = _lib.load()
-model = bench.fixture_model(dev)
+model = bench.fixture_model(bench.STAGE1, dev)
 mel = torch.randn(32, 64, 500, device=dev)
 h = model._hip(dev).handle
 

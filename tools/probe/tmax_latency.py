@@ -16,7 +16,7 @@ import bench  # noqa: E402
 from m2amd import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
-model = bench.fixture_model(dev)
+model = bench.fixture_model(bench.STAGE1, dev)
 d = (torch.rand(32, 100) * 10).to(dev)
 mel = torch.randn(32, 64, 500, device=dev)
 
