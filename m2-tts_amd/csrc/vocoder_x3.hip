@@ -981,22 +981,19 @@ int32_t set_lds(K kernel, size_t bytes) {
     return M2_OK;
 }
 
-// Full rounds of a grid of n workgroups at the kernel's occupancy.
+// Workgroup slots of the device for a kernel (CUs x its occupancy), queried
+// once per kernel: the vocoder calls this on every launch decision.
 template <typename K>
-long grid_rounds(K kernel, int threads, size_t lds, long n) {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    }
-    int per = 0;
+long grid_slots(K kernel, int threads, size_t lds) {
+    int ncu = 0, dev = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kernel), threads, lds) !=
             hipSuccess || per <= 0)
         per = 1;
-    const long slots = (long)per * ncu;
-    return (n + slots - 1) / slots;
+    return (long)per * ncu;
 }
+inline long rounds_of(long n, long slots) { return (n + slots - 1) / slots; }
 
 template <class Cfg>
 int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1, void* U2, float* audio,
@@ -1022,18 +1019,16 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     }
     bool alt_mid = false, alt_tail = false;
     if constexpr (S2) {
-        if (!w.mp) {
-            const long r0 = grid_rounds(x3_mid_kernel<Cfg>, Cfg::MW * 64, MP::LDS_BYTES, (long)cdiv(4 * T, Cfg::W2) * B);
-            const long r1 = grid_rounds(x3_mid_kernel<CfgS2Alt>, Cfg::MW * 64, MPA::LDS_BYTES,
-                                        (long)cdiv(4 * T, CfgS2Alt::W2) * B);
-            alt_mid = r1 * kAltMidCost < (double)r0;
-        }
-        if (!w.tp) {
-            const long r0 = grid_rounds(x3_tail_kernel<Cfg>, Cfg::TW * 64, TP::LDS_BYTES, (long)cdiv(16 * T, Cfg::W3) * B);
-            const long r1 = grid_rounds(x3_tail_kernel<CfgS2Alt>, Cfg::TW * 64, TPA::LDS_BYTES,
-                                        (long)cdiv(16 * T, CfgS2Alt::W3) * B);
-            alt_tail = r1 * kAltTailCost < (double)r0;
-        }
+        static const long sm0 = grid_slots(x3_mid_kernel<Cfg>, Cfg::MW * 64, MP::LDS_BYTES),
+                          sm1 = grid_slots(x3_mid_kernel<CfgS2Alt>, Cfg::MW * 64, MPA::LDS_BYTES),
+                          st0 = grid_slots(x3_tail_kernel<Cfg>, Cfg::TW * 64, TP::LDS_BYTES),
+                          st1 = grid_slots(x3_tail_kernel<CfgS2Alt>, Cfg::TW * 64, TPA::LDS_BYTES);
+        if (!w.mp)
+            alt_mid = rounds_of((long)cdiv(4 * T, CfgS2Alt::W2) * B, sm1) * kAltMidCost <
+                      (double)rounds_of((long)cdiv(4 * T, Cfg::W2) * B, sm0);
+        if (!w.tp)
+            alt_tail = rounds_of((long)cdiv(16 * T, CfgS2Alt::W3) * B, st1) * kAltTailCost <
+                       (double)rounds_of((long)cdiv(16 * T, Cfg::W3) * B, st0);
     }
     auto* u1 = static_cast<unsigned char*>(U1);
     auto* u2 = static_cast<unsigned char*>(U2);
