@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""stage2 inference at a small per-GPU batch (configs[3]'s share at N=8:
+B=8, S=100), front + back per step, for a rocprofv3 --kernel-trace run
+(the trace then shows each kernel's duration and the launch gaps):
+    rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/probe/s2_small_trace.py
+    python3 tools/probe/s2_small_trace.py --summarize DIR/run_kernel_trace.csv
+"""
+import csv
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent.parent
+
+
+def summarize(path, steps=20):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    names = [r["Kernel_Name"].split("(")[0].replace("void ", "")[:70] for r in rows]
+    st = [int(r["Start_Timestamp"]) for r in rows]
+    en = [int(r["End_Timestamp"]) for r in rows]
+    # a step starts at the embedding kernel (first kernel of m2_inference_front)
+    starts = [i for i, n in enumerate(names) if "embed" in n]
+    starts = starts[-steps - 1:]
+    per = {}
+    spans, busy = [], []
+    for a, b in zip(starts, starts[1:]):
+        spans.append((st[b] - st[a]) / 1e3)
+        busy.append(sum(en[i] - st[i] for i in range(a, b)) / 1e3)
+        for i in range(a, b):
+            per.setdefault((i - a, names[i]), []).append((en[i] - st[i]) / 1e3)
+    n = len(spans)
+    print(f"steps {n}: span median {sorted(spans)[n // 2]:.1f} us, kernel-busy median {sorted(busy)[n // 2]:.1f} us")
+    for (i, nm), v in sorted(per.items()):
+        v.sort()
+        print(f"{i:3d} {v[len(v) // 2]:7.2f} us  {nm}")
+
+
+def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--summarize":
+        summarize(sys.argv[2])
+        return
+    import torch
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "m2-tts_amd" / "src"))
+    import bench
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    m = bench.fixture_model(bench.STAGE2, dev)
+    g = torch.Generator().manual_seed(2024)
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    ids = torch.randint(0, 42, (B, 100), generator=g).to(dev)
+    lens = torch.full((B,), 100, dtype=torch.long, device=dev)
+    hm = m._hip(dev)
+    with torch.no_grad():
+        for _ in range(200):
+            state, tl = hm.inference_front(ids, lens, 1.0)
+            hm.inference_back(state, max(1, tl))
+    torch.cuda.synchronize()
+    print("done")
+
+
+if __name__ == "__main__":
+    main()
