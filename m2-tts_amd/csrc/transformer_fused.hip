@@ -14,8 +14,8 @@
 // residuals and biases stay fp32.  Weights are packed once at model creation
 // (pack_bfrag_split), activations are split when they are written to LDS.
 //
-// GEMM tiles: a workgroup (4 waves) owns 32 rows; wave w computes the
-// 16-column blocks nb = w, w+4, ... for both 16-row halves, as the transposed
+// GEMM tiles: a workgroup (NW = 4 or 8 waves, tf_waves) owns 32 rows; wave w
+// computes the 16-column blocks nb = w, w+NW, ... for both 16-row halves, as the transposed
 // product D^T = W . X^T: A = the weights (lane: 8 k of one output column,
 // packed [n-block][k-step][hi|lo][lane][8 f16], one global_load_dwordx4 per
 // lane and k-step, L2-resident), B = the activations from LDS hi / lo planes
@@ -23,6 +23,7 @@
 // mod 4: conflict-free).  A lane of D^T then holds 4 consecutive output
 // columns of one row, so the epilogues write 16-B fp32 or 8-B f16 pieces.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "m2_common.h"
@@ -84,19 +85,19 @@ __device__ __forceinline__ void gemm_strip(const unsigned char* X, const Strip<K
     }
 }
 
-// Columns [nb*16, nb*16+16) of X . W^T for nb = wave, wave+4, ...: the next
+// Columns [nb*16, nb*16+16) of X . W^T for nb = wave, wave+NW, ...: the next
 // strip is requested before the current one is consumed (and the first one
 // by the caller, before its LDS staging), so weight latency overlaps work.
 // epi(nb, acc) consumes each finished block (lane: row rb*16 + (lane&15),
 // columns nb*16 + 4*(lane>>4) + r).
-template <int K, int NB, typename Epi>
+template <int K, int NB, int NW, typename Epi>
 __device__ __forceinline__ void gemm_cols(const unsigned char* X, const u32x4* __restrict__ Wp, Strip<K>& cur,
                                           const float* __restrict__ bias, Epi epi) {
     const int wave = threadIdx.x >> 6, g = (threadIdx.x & 63) >> 4;
 #pragma unroll 1
-    for (int nb = wave; nb < NB; nb += 4) {
+    for (int nb = wave; nb < NB; nb += NW) {
         Strip<K> nxt;
-        if (nb + 4 < NB) nxt.load(Wp, nb + 4);
+        if (nb + NW < NB) nxt.load(Wp, nb + NW);
         f32x4 acc[2];
         f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
         if (bias) {
@@ -106,7 +107,7 @@ __device__ __forceinline__ void gemm_cols(const unsigned char* X, const u32x4* _
         acc[0] = acc[1] = bv;
         gemm_strip<K>(X, cur, acc);
         epi(nb, acc);
-        if (nb + 4 < NB) cur = nxt;
+        if (nb + NW < NB) cur = nxt;
     }
 }
 
@@ -122,12 +123,14 @@ __device__ __forceinline__ void put_split4(unsigned char* p, float a, float b, f
 
 // LayerNorm of TR rows of H floats in LDS (src, stride frs(H)) -> split rows
 // (dst, stride srs(H)): 8 lanes per row, each H/8 consecutive channels;
-// two-pass mean / biased variance as nn.LayerNorm.
+// two-pass mean / biased variance as nn.LayerNorm.  Threads 0-255 only (an
+// 8-wave workgroup's upper half skips it).
 template <int H>
 __device__ __forceinline__ void ln_rows(const float* src, unsigned char* dst, const float* __restrict__ g,
                                         const float* __restrict__ b) {
     constexpr int PER = H / 8;
     static_assert(PER % 4 == 0, "H multiple of 32");
+    if (threadIdx.x >= 8 * TR) return;
     const int row = threadIdx.x >> 3, part = threadIdx.x & 7;
     const float* xr = src + row * frs(H) + part * PER;
     float v[PER];
@@ -173,7 +176,7 @@ __device__ __forceinline__ void ln_rows(const float* src, unsigned char* dst, co
 template <int H>
 __device__ __forceinline__ void load_rows(const float* __restrict__ x, int r0, int R, float* dst) {
     constexpr int H4 = H / 4;
-    for (int i = threadIdx.x; i < TR * H4; i += 256) {
+    for (int i = threadIdx.x; i < TR * H4; i += blockDim.x) {
         const int r = i / H4, c = (i - r * H4) * 4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (r0 + r < R) v = *reinterpret_cast<const float4*>(x + (size_t)(r0 + r) * H + c);
@@ -184,7 +187,7 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ x, int r0, i
 template <int H>
 __device__ __forceinline__ void load_rows_split(const float* __restrict__ x, int r0, int R, unsigned char* dst) {
     constexpr int H4 = H / 4;
-    for (int i = threadIdx.x; i < TR * H4; i += 256) {
+    for (int i = threadIdx.x; i < TR * H4; i += blockDim.x) {
         const int r = i / H4, c = (i - r * H4) * 4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (r0 + r < R) v = *reinterpret_cast<const float4*>(x + (size_t)(r0 + r) * H + c);
@@ -193,8 +196,8 @@ __device__ __forceinline__ void load_rows_split(const float* __restrict__ x, int
 }
 
 // y[R][N] = act(LN?(x)[R][K] . W^T + b) for N % 16 == 0.
-template <int K, int N, bool LN, int ACT>
-__global__ __launch_bounds__(256) void ln_gemm_kernel(const float* __restrict__ x, const float* __restrict__ g,
+template <int K, int N, bool LN, int ACT, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void ln_gemm_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                       const float* __restrict__ bln, const u32x4* __restrict__ Wp,
                                                       const float* __restrict__ bias, int R, float* __restrict__ y) {
     static_assert(LN, "ln_gemm: LN form only");
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(256) void ln_gemm_kernel(const float* __restrict__ 
     __syncthreads();
     ln_rows<K>(X, Xn, g, bln);
     __syncthreads();
-    gemm_cols<K, N / 16>(Xn, Wp, st, bias, [&](int nb, const f32x4 (&acc)[2]) {
+    gemm_cols<K, N / 16, NW>(Xn, Wp, st, bias, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
             const int row = r0 + rb * 16 + i;
@@ -228,8 +231,8 @@ __global__ __launch_bounds__(256) void ln_gemm_kernel(const float* __restrict__ 
 // z = LN(y; gn, bn) . Wn^T (+ bn2) with NN output columns - the next layer's
 // LN1 -> QKV, or the decoder's final LN -> mel projection - so y is read back
 // from LDS instead of HBM and one launch per layer goes away.
-template <int H, int NN = 0>
-__global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict__ att, const float* x,
+template <int H, int NN = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void post_attn_kernel(const float* __restrict__ att, const float* x,
                                                         const u32x4* __restrict__ Wo, const float* __restrict__ bo,
                                                         const float* __restrict__ g2, const float* __restrict__ b2n,
                                                         const u32x4* __restrict__ W1, const float* __restrict__ b1,
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict_
     load_rows_split<H>(att, r0, R, A);
     __syncthreads();
     // o = x + att . Wo^T + bo   (components.py:86, 137: x + dropout(attn(...)))
-    gemm_cols<H, H / 16>(A, Wo, so, bo, [&](int nb, const f32x4 (&acc)[2]) {
+    gemm_cols<H, H / 16, NW>(A, Wo, so, bo, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
             const int rr = rb * 16 + i, row = r0 + rr, col = nb * 16 + 4 * gq;
@@ -260,11 +263,11 @@ __global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict_
         }
     });
     Strip<H> s1;
-    s1.load(W1, wave);  // F/16 >= 4 blocks: every wave has one
+    if (wave < F / 16) s1.load(W1, wave);
     __syncthreads();
     ln_rows<H>(O, A, g2, b2n);
     __syncthreads();
-    gemm_cols<H, F / 16>(A, W1, s1, b1, [&](int nb, const f32x4 (&acc)[2]) {
+    gemm_cols<H, F / 16, NW>(A, W1, s1, b1, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
             const f32x4 v = acc[rb];
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict_
     Strip<F> s2;
     if (wave < H / 16) s2.load(W2, wave);
     __syncthreads();
-    gemm_cols<F, H / 16>(Hd, W2, s2, b2, [&](int nb, const f32x4 (&acc)[2]) {
+    gemm_cols<F, H / 16, NW>(Hd, W2, s2, b2, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
             const int rr = rb * 16 + i, row = r0 + rr, col = nb * 16 + 4 * gq;
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(256) void post_attn_kernel(const float* __restrict_
         __syncthreads();
         ln_rows<H>(O, A, gn, bn);  // same rounding as ln_gemm_kernel's
         __syncthreads();
-        gemm_cols<H, NN / 16>(A, Wn, sn, bn2, [&](int nb, const f32x4 (&acc)[2]) {
+        gemm_cols<H, NN / 16, NW>(A, Wn, sn, bn2, [&](int nb, const f32x4 (&acc)[2]) {
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
                 const int row = r0 + rb * 16 + i;
@@ -343,20 +346,39 @@ bool pack_bfrag_split(const float* W, int N, int K, std::vector<float>* out) {
     return true;
 }
 
+// Waves per workgroup: 8 when the grid is short of two workgroups per CU
+// (small batches: every 32-row tile is then a serial chain of GEMM rounds, and
+// 8 waves halve the rounds: post_attn at stage2 B=8 S=100 13.8 -> 10.5 us,
+// tools/probe/tf_waves_ab.sh), else 4.  M2_TF_WAVES=4|8 forces one.  (An L2
+// warm-up of the layer's weights at kernel start measured 1 us slower: across
+// steps they stay L2-resident.)
+static int tf_waves(int R) {
+    static const int forced = [] {
+        const char* e = std::getenv("M2_TF_WAVES");
+        const int v = e ? std::atoi(e) : 0;
+        return (v == 4 || v == 8) ? v : 0;
+    }();
+    if (forced) return forced;
+    return cdiv(R, tfx::TR) < 2 * 256 ? 8 : 4;
+}
+
 int32_t launch_ln_gemm(const float* x, const float* g, const float* b, const float* Wp, const float* bias, int act,
                        int R, int K, int N, float* y, hipStream_t st) {
     if (R == 0) return M2_OK;
-    const dim3 grid(cdiv(R, tfx::TR)), blk(256);
+    const int nw = tf_waves(R);
+    const dim3 grid(cdiv(R, tfx::TR)), blk(64 * nw);
     const vx_u32x4* W = reinterpret_cast<const vx_u32x4*>(Wp);
-#define M2_LNG(KK, NN)                                                                                           \
-    if (K == KK && N == NN) {                                                                                    \
-        if (g && act == ACT_NONE)                                                                                \
-            hipLaunchKernelGGL((tfx::ln_gemm_kernel<KK, NN, true, ACT_NONE>), grid, blk, 0, st, x, g, b, W, bias, R, \
-                               y);                                                                               \
-        else                                                                                                     \
-            return fail(M2_E_SHAPE, "ln_gemm: unsupported mode");                                               \
-        M2_LAUNCHED("ln_gemm_kernel");                                                                           \
-        return M2_OK;                                                                                            \
+#define M2_LNG(KK, NN)                                                                                             \
+    if (K == KK && N == NN) {                                                                                      \
+        if (!g || act != ACT_NONE) return fail(M2_E_SHAPE, "ln_gemm: unsupported mode");                          \
+        if (nw == 8)                                                                                               \
+            hipLaunchKernelGGL((tfx::ln_gemm_kernel<KK, NN, true, ACT_NONE, 8>), grid, blk, 0, st, x, g, b, W, bias, \
+                               R, y);                                                                              \
+        else                                                                                                       \
+            hipLaunchKernelGGL((tfx::ln_gemm_kernel<KK, NN, true, ACT_NONE, 4>), grid, blk, 0, st, x, g, b, W, bias, \
+                               R, y);                                                                              \
+        M2_LAUNCHED("ln_gemm_kernel");                                                                             \
+        return M2_OK;                                                                                              \
     }
     M2_LNG(32, 96)
     M2_LNG(32, 32)
@@ -375,14 +397,25 @@ int32_t launch_post_attn(const float* att, const float* x, const float* Wo, cons
                          const float* b2n, const float* W1, const float* b1, const float* W2, const float* b2, int R,
                          int H, float* y, hipStream_t st) {
     if (R == 0) return M2_OK;
-    const dim3 grid(cdiv(R, tfx::TR)), blk(256);
+    const int nw = tf_waves(R);
+    const dim3 grid(cdiv(R, tfx::TR)), blk(64 * nw);
     auto f4 = [](const float* p) { return reinterpret_cast<const vx_u32x4*>(p); };
+#define M2_PA(HH)                                                                                                   \
+    case HH:                                                                                                        \
+        if (nw == 8)                                                                                                \
+            hipLaunchKernelGGL((tfx::post_attn_kernel<HH, 0, 8>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n,    \
+                               f4(W1), b1, f4(W2), b2, R, y);                                                       \
+        else                                                                                                        \
+            hipLaunchKernelGGL((tfx::post_attn_kernel<HH, 0, 4>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n,    \
+                               f4(W1), b1, f4(W2), b2, R, y);                                                       \
+        break;
     switch (H) {
-        case 32: hipLaunchKernelGGL((tfx::post_attn_kernel<32>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n, f4(W1), b1, f4(W2), b2, R, y); break;
-        case 64: hipLaunchKernelGGL((tfx::post_attn_kernel<64>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n, f4(W1), b1, f4(W2), b2, R, y); break;
-        case 96: hipLaunchKernelGGL((tfx::post_attn_kernel<96>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n, f4(W1), b1, f4(W2), b2, R, y); break;
+        M2_PA(32)
+        M2_PA(64)
+        M2_PA(96)
         default: return fail(M2_E_SHAPE, "post_attn: unsupported hidden_dim");
     }
+#undef M2_PA
     M2_LAUNCHED("post_attn_kernel");
     return M2_OK;
 }
@@ -397,14 +430,19 @@ int32_t launch_post_attn_next(const float* att, const float* x, const float* Wo,
                               int R, int H, float* y, const float* gn, const float* bn, const float* Wn,
                               const float* bn2, int NN, float* z, hipStream_t st) {
     if (R == 0) return M2_OK;
-    const dim3 grid(cdiv(R, tfx::TR)), blk(256);
+    const int nw = tf_waves(R);
+    const dim3 grid(cdiv(R, tfx::TR)), blk(64 * nw);
     auto f4 = [](const float* p) { return reinterpret_cast<const vx_u32x4*>(p); };
-#define M2_PAN(HH, NNN)                                                                                           \
-    if (H == HH && NN == NNN) {                                                                                   \
-        hipLaunchKernelGGL((tfx::post_attn_kernel<HH, NNN>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n, f4(W1), b1, \
-                           f4(W2), b2, R, y, gn, bn, f4(Wn), bn2, z);                                             \
-        M2_LAUNCHED("post_attn_kernel");                                                                          \
-        return M2_OK;                                                                                             \
+#define M2_PAN(HH, NNN)                                                                                              \
+    if (H == HH && NN == NNN) {                                                                                      \
+        if (nw == 8)                                                                                                 \
+            hipLaunchKernelGGL((tfx::post_attn_kernel<HH, NNN, 8>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n,   \
+                               f4(W1), b1, f4(W2), b2, R, y, gn, bn, f4(Wn), bn2, z);                                \
+        else                                                                                                         \
+            hipLaunchKernelGGL((tfx::post_attn_kernel<HH, NNN, 4>), grid, blk, 0, st, att, x, f4(Wo), bo, g2, b2n,   \
+                               f4(W1), b1, f4(W2), b2, R, y, gn, bn, f4(Wn), bn2, z);                                \
+        M2_LAUNCHED("post_attn_kernel");                                                                             \
+        return M2_OK;                                                                                                \
     }
     M2_PAN(32, 96)
     M2_PAN(32, 32)
