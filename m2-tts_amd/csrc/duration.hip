@@ -104,18 +104,34 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const int lane = tid & 63, wave = tid >> 6;
     const float* e = enc + (size_t)b * S * H;
     if constexpr (LN) {
-        for (int p = wave; p < 18; p += DUR_WAVES) {
-            const int s = s0 - 2 + p;
+        // every row of this wave is loaded before the first is normalised (one
+        // memory round trip per wave instead of one per row)
+        constexpr int NR = (18 + DUR_WAVES - 1) / DUR_WAVES, KP = (H + 63) / 64;
+        float xv[NR][KP];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int p = wave + j * DUR_WAVES, s = s0 - 2 + p;
+            const float* xr = e + (size_t)min(max(s, 0), S - 1) * H;
+#pragma unroll
+            for (int q = 0; q < KP; ++q) xv[j][q] = (lane + 64 * q < H) ? xr[lane + 64 * q] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int p = wave + j * DUR_WAVES, s = s0 - 2 + p;
+            if (p >= 18) break;
             float* d = X + p * XS;
             if (s >= 0 && s < S) {
-                const float* xr = e + (size_t)s * H;
                 float mean, rstd;
-                ln_row_stats(xr, H, lane, mean, rstd);
+                ln_row_stats_regs<KP>(xv[j], H, lane, mean, rstd);
                 float* yo = (p >= 2 && p < 2 + DUR_TS) ? enc_out + ((size_t)b * S + s) * H : nullptr;
-                for (int k = lane; k < H; k += 64) {
-                    const float y = ln_apply(xr[k], mean, rstd, lng[k], lnb[k]);
-                    d[k] = y;
-                    if (yo) yo[k] = y;
+#pragma unroll
+                for (int q = 0; q < KP; ++q) {
+                    const int k = lane + 64 * q;
+                    if (k < H) {
+                        const float y = ln_apply(xv[j][q], mean, rstd, lng[k], lnb[k]);
+                        d[k] = y;
+                        if (yo) yo[k] = y;
+                    }
                 }
             } else {
                 for (int k = lane; k < H; k += 64) d[k] = 0.f;

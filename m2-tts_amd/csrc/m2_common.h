@@ -105,6 +105,27 @@ __device__ __forceinline__ void ln_row_stats(const float* xr, int K, int lane, f
     rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(v, (float)K), kLnEps)));
 }
 
+// ln_row_stats on a row already in registers: x[q] = row[lane + 64 q] for
+// lane + 64 q < K (the same additions in the same order).
+template <int KP>
+__device__ __forceinline__ void ln_row_stats_regs(const float (&x)[KP], int K, int lane, float& mean, float& rstd) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < KP; ++q)
+        if (lane + 64 * q < K) s = __fadd_rn(s, x[q]);
+    for (int o = 32; o > 0; o >>= 1) s = __fadd_rn(s, __shfl_xor(s, o));
+    mean = __fdiv_rn(s, (float)K);
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < KP; ++q)
+        if (lane + 64 * q < K) {
+            const float d = __fsub_rn(x[q], mean);
+            v = __fmaf_rn(d, d, v);
+        }
+    for (int o = 32; o > 0; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o));
+    rstd = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(v, (float)K), kLnEps)));
+}
+
 __device__ __forceinline__ float ln_apply(float x, float mean, float rstd, float g, float b) {
     return __fmaf_rn(__fmul_rn(__fsub_rn(x, mean), rstd), g, b);
 }

@@ -321,18 +321,29 @@ int32_t run_layer(const m2_model* m, const m2_layer_w& L, const float* x_in, flo
 // row tile (and, with fin_W, the final LN -> projection into fin_out: then
 // *fin_done), one launch per layer fewer; results are identical to the
 // separate launches (same fp32 y into the same LayerNorm / GEMM code).
-int32_t run_stack(const m2_model* m, const std::vector<m2_layer_w>& layers, const float* x_in, float* x, TfBufs& wb,
-                  const uint8_t* mask, int B, int N, hipStream_t st, const float* fin_g = nullptr,
-                  const float* fin_b = nullptr, const float* fin_W = nullptr, const float* fin_bias = nullptr,
-                  int fin_N = 0, float* fin_out = nullptr, bool* fin_done = nullptr) {
-    const int H = m->cfg.hidden_dim, R = B * N, n = (int)layers.size();
-    if (fin_done) *fin_done = false;
-    int32_t rc;
+bool tf_chain(const m2_model* m) {
     static const bool chain_ok = [] {  // M2_TF_CHAIN=0: separate ln_gemm launches (A/B)
         const char* e = std::getenv("M2_TF_CHAIN");
         return !e || std::atoi(e) != 0;
     }();
-    const bool chain = chain_ok && m->tfused && tf_post_next_supported(H, 3 * H);
+    const int H = m->cfg.hidden_dim;
+    return chain_ok && m->tfused && tf_post_next_supported(H, 3 * H);
+}
+
+// The first layer's input rows built by its LN1 -> QKV launch (embedding /
+// frame expansion fused in; tf_chain stacks only).
+bool tf_first_fused(const m2_model* m, const std::vector<m2_layer_w>& layers) {
+    return tf_chain(m) && !layers.empty() && tf_src_fused_supported(m->cfg.hidden_dim, 3 * m->cfg.hidden_dim);
+}
+
+int32_t run_stack(const m2_model* m, const std::vector<m2_layer_w>& layers, const float* x_in, float* x, TfBufs& wb,
+                  const uint8_t* mask, int B, int N, hipStream_t st, const float* fin_g = nullptr,
+                  const float* fin_b = nullptr, const float* fin_W = nullptr, const float* fin_bias = nullptr,
+                  int fin_N = 0, float* fin_out = nullptr, bool* fin_done = nullptr, bool qkv_ready = false) {
+    const int H = m->cfg.hidden_dim, R = B * N, n = (int)layers.size();
+    if (fin_done) *fin_done = false;
+    int32_t rc;
+    const bool chain = tf_chain(m);
     if (!chain) {
         const float* cur = x_in;
         for (const auto& L : layers) {
@@ -343,8 +354,8 @@ int32_t run_stack(const m2_model* m, const std::vector<m2_layer_w>& layers, cons
     }
     if (n == 0) return M2_OK;
     const float* cur = x_in;
-    if ((rc = launch_ln_gemm(cur, layers[0].n1_w, layers[0].n1_b, layers[0].qkv_p, nullptr, ACT_NONE, R, H, 3 * H,
-                             wb.qkv, st)))
+    if (!qkv_ready && (rc = launch_ln_gemm(cur, layers[0].n1_w, layers[0].n1_b, layers[0].qkv_p, nullptr, ACT_NONE, R,
+                                           H, 3 * H, wb.qkv, st)))
         return rc;
     for (int l = 0; l < n; ++l) {
         const m2_layer_w& L = layers[l];
@@ -853,6 +864,15 @@ int32_t text_encoder_layers(const m2_model* m, const int64_t* ids, const int64_t
     int32_t rc;
     const uint8_t* mask = nullptr;
     if (lengths) mask = out_mask ? out_mask : wb.mask;  // written by the embedding launch
+    if (tf_first_fused(m, m->enc)) {
+        const m2_layer_w& L0 = m->enc[0];
+        if ((rc = launch_embed_ln_gemm(ids, m->emb, m->pe, B, S, H, m->cfg.vocab_size, lengths,
+                                       const_cast<uint8_t*>(mask), wb.x, L0.n1_w, L0.n1_b, L0.qkv_p, 3 * H, wb.qkv,
+                                       st)))
+            return rc;
+        return run_stack(m, m->enc, wb.x, wb.x, wb, mask, B, S, st, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                         nullptr, true);
+    }
     if ((rc = launch_embed_pe(ids, m->emb, m->pe, B, S, H, m->cfg.vocab_size, wb.x, lengths,
                               const_cast<uint8_t*>(mask), st)))
         return rc;
@@ -988,10 +1008,15 @@ int32_t m2_length_regulator_expand(const float* enc, const int32_t* cum, int32_t
     return launch_lr_expand(enc, cum, B, S, H, T_out, out, static_cast<hipStream_t>(stream));
 }
 
-int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, float* out_mel,
-                       void* workspace, size_t workspace_bytes, void* stream) {
-    M2_CHECK_ARG(m && x && out_mel && B >= 0 && T >= 0, "m2_mel_decoder: bad argument");
-    hipStream_t st = static_cast<hipStream_t>(stream);
+}  // extern "C"
+
+namespace {
+// The mel decoder on x [B, T, H]; with enc / cum given, x is first filled by
+// the length regulator's frame expansion of enc, fused into the first layer's
+// LN1 -> QKV launch when tf_first_fused (else a separate lr_expand launch).
+int32_t mel_decoder(const m2_model* m, float* x, int32_t B, int32_t T, float* out_mel, void* workspace,
+                    size_t workspace_bytes, hipStream_t st, const float* enc = nullptr, const int32_t* cum = nullptr,
+                    int32_t S = 0) {
     const int H = m->cfg.hidden_dim;
     Carve a(workspace, workspace_bytes);
     TfBufs wb;
@@ -999,9 +1024,20 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_mel_decoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
     int32_t rc;
+    bool qkv_ready = false;
+    if (enc) {
+        if (tf_first_fused(m, m->dec)) {
+            const m2_layer_w& L0 = m->dec[0];
+            if ((rc = launch_expand_ln_gemm(enc, cum, B, S, T, H, x, L0.n1_w, L0.n1_b, L0.qkv_p, 3 * H, wb.qkv, st)))
+                return rc;
+            qkv_ready = true;
+        } else if ((rc = launch_lr_expand(enc, cum, B, S, H, T, x, st))) {
+            return rc;
+        }
+    }
     bool projected = false;
     if ((rc = run_stack(m, m->dec, x, wb.x, wb, nullptr, B, T, st, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b,
-                        m->cfg.mel_channels, out_mel, &projected)))
+                        m->cfg.mel_channels, out_mel, &projected, qkv_ready)))
         return rc;
     if (projected) return M2_OK;
     const float* cur = m->dec.empty() ? x : wb.x;
@@ -1010,6 +1046,16 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
                               out_mel, st);
     return launch_linear(cur, m->dec_nw, m->dec_nb, m->mel_w, m->mel_b, nullptr, ACT_NONE, B * T, H,
                          m->cfg.mel_channels, out_mel, st);
+}
+}  // namespace
+
+extern "C" {
+
+int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, float* out_mel,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && x && out_mel && B >= 0 && T >= 0, "m2_mel_decoder: bad argument");
+    return mel_decoder(m, const_cast<float*>(x), B, T, out_mel, workspace, workspace_bytes,
+                       static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"
@@ -1336,8 +1382,10 @@ int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, co
     float* reg = w.take<float>((size_t)B * T * H);
     if (!w.ok) return fail(M2_E_WORKSPACE, "m2_inference_back: workspace too small");
     int32_t rc;
-    if ((rc = m2_length_regulator_expand(f.enc, f.cum, B, S, H, T, reg, stream))) return rc;
-    if ((rc = m2_mel_decoder(m, reg, B, T, out_mel, workspace, scratch, stream))) return rc;
+    // frame expansion + decoder (the expansion fused into the first layer's launch)
+    if ((rc = mel_decoder(m, reg, B, T, out_mel, workspace, scratch, static_cast<hipStream_t>(stream), f.enc, f.cum,
+                          S)))
+        return rc;
     return m2_vocoder(m, out_mel, 1, B, T, out_audio, workspace, scratch, stream);
 }
 

@@ -28,4 +28,16 @@ int32_t launch_post_attn_next(const float* att, const float* x, const float* Wo,
                               int R, int H, float* y, const float* gn, const float* bn, const float* Wn,
                               const float* bn2, int NN, float* z, hipStream_t st);
 
+// The first layer's LN1 -> QKV with its input rows built in the same launch
+// (and stored to x, the residual input): the embedding + positional encoding +
+// padding mask of the encoder (embed_pe_kernel), or the length regulator's
+// frame expansion of the decoder (lr_expand_kernel).  (H, N) = (32, 96),
+// (64, 192), (96, 288).
+bool tf_src_fused_supported(int H, int N);
+int32_t launch_embed_ln_gemm(const int64_t* ids, const float* emb, const float* pe, int B, int S, int H, int vocab,
+                             const int64_t* lengths, uint8_t* mask, float* x, const float* g, const float* b,
+                             const float* Wp, int N, float* y, hipStream_t st);
+int32_t launch_expand_ln_gemm(const float* enc, const int32_t* cum, int B, int S, int T, int H, float* x,
+                              const float* g, const float* b, const float* Wp, int N, float* y, hipStream_t st);
+
 }  // namespace m2

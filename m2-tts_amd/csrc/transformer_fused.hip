@@ -195,19 +195,96 @@ __device__ __forceinline__ void load_rows_split(const float* __restrict__ x, int
     }
 }
 
-// y[R][N] = act(LN?(x)[R][K] . W^T + b) for N % 16 == 0.
-template <int K, int N, bool LN, int ACT, int NW = 4>
+// Where ln_gemm_kernel's rows come from.  SRC_X: x.  The first layer of a
+// stack can build its input rows itself, one launch fewer per stack (the rows
+// are also stored to xo, the layer's residual input, so the values are the
+// ones the separate launch would have written):
+//   SRC_EMBED   x = E[ids] * sqrt(H) + pe[s] and the padding mask (embed_pe_kernel)
+//   SRC_EXPAND  x = enc row of the phoneme frame t falls in, zero past the
+//               utterance's total (lr_expand_kernel's search)
+enum { SRC_X = 0, SRC_EMBED = 1, SRC_EXPAND = 2 };
+struct RowSrc {
+    const int64_t* ids = nullptr;  // embed: [R] token ids, S positions per utterance
+    const float* emb = nullptr;
+    const float* pe = nullptr;
+    int vocab = 0;
+    float scale = 1.f;
+    const int64_t* lengths = nullptr;  // optional: mask[r] = s < lengths[b]
+    uint8_t* mask = nullptr;
+    const float* enc = nullptr;  // expand: [B][S][H] encoder output, cum [B][S + 1]
+    const int32_t* cum = nullptr;
+    int S = 1, T = 1;
+    float* xo = nullptr;
+};
+
+template <int H, int SRC>
+__device__ __forceinline__ void load_src_rows(const float* __restrict__ x, const RowSrc& src, int r0, int R,
+                                              float* dst, int* sp) {
+    constexpr int H4 = H / 4;
+    if constexpr (SRC == SRC_X) {
+        load_rows<H>(x, r0, R, dst);
+    } else {
+        if constexpr (SRC == SRC_EXPAND) {
+            // source phoneme of each of the tile's frames: smallest s with cum[s+1] > t
+            if (threadIdx.x < TR) {
+                const int row = r0 + threadIdx.x;
+                int v = -1;
+                if (row < R) {
+                    const int b = row / src.T, t = row - b * src.T;
+                    const int32_t* c = src.cum + (size_t)b * (src.S + 1);
+                    if (t < c[src.S]) {
+                        int lo = 0, hi = src.S - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi) >> 1;
+                            if (c[mid + 1] > t) hi = mid;
+                            else lo = mid + 1;
+                        }
+                        v = b * src.S + lo;
+                    }
+                }
+                sp[threadIdx.x] = v;
+            }
+            __syncthreads();
+        }
+        for (int i = threadIdx.x; i < TR * H4; i += blockDim.x) {
+            const int r = i / H4, c = (i - r * H4) * 4, row = r0 + r;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < R) {
+                if constexpr (SRC == SRC_EMBED) {
+                    const int64_t id = src.ids[row];
+                    const int s = row % src.S;
+                    float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (id >= 0 && id < src.vocab) e = *reinterpret_cast<const float4*>(src.emb + id * H + c);
+                    const float4 p = *reinterpret_cast<const float4*>(src.pe + (size_t)s * H + c);
+                    v = make_float4(__builtin_fmaf(e.x, src.scale, p.x), __builtin_fmaf(e.y, src.scale, p.y),
+                                    __builtin_fmaf(e.z, src.scale, p.z), __builtin_fmaf(e.w, src.scale, p.w));
+                    if (src.lengths && c == 0) src.mask[row] = (int64_t)s < src.lengths[row / src.S] ? 1 : 0;
+                } else {
+                    const int q = sp[r];
+                    if (q >= 0) v = *reinterpret_cast<const float4*>(src.enc + (size_t)q * H + c);
+                }
+                *reinterpret_cast<float4*>(src.xo + (size_t)row * H + c) = v;
+            }
+            *reinterpret_cast<float4*>(dst + r * frs(H) + c) = v;
+        }
+    }
+}
+
+// y[R][N] = act(LN?(x)[R][K] . W^T + b) for N % 16 == 0; x from SRC (above).
+template <int K, int N, bool LN, int ACT, int NW = 4, int SRC = SRC_X>
 __global__ __launch_bounds__(64 * NW) void ln_gemm_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                       const float* __restrict__ bln, const u32x4* __restrict__ Wp,
-                                                      const float* __restrict__ bias, int R, float* __restrict__ y) {
+                                                      const float* __restrict__ bias, int R, float* __restrict__ y,
+                                                      RowSrc src = RowSrc{}) {
     static_assert(LN, "ln_gemm: LN form only");
     __shared__ __attribute__((aligned(16))) float X[TR * frs(K)];
     __shared__ __attribute__((aligned(16))) unsigned char Xn[TR * srs(K)];
+    __shared__ int sp[SRC == SRC_EXPAND ? TR : 1];
     const int r0 = blockIdx.x * TR;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     Strip<K> st;
     if (wave < N / 16) st.load(Wp, wave);
-    load_rows<K>(x, r0, R, X);
+    load_src_rows<K, SRC>(x, src, r0, R, X, sp);
     __syncthreads();
     ln_rows<K>(X, Xn, g, bln);
     __syncthreads();
@@ -391,6 +468,63 @@ int32_t launch_ln_gemm(const float* x, const float* g, const float* b, const flo
     M2_LNG(64, 80)
 #undef M2_LNG
     return fail(M2_E_SHAPE, "ln_gemm: unsupported (K, N)");
+}
+
+// The first layer's LN1 -> QKV on rows it builds itself (SRC_EMBED / SRC_EXPAND).
+static int32_t launch_src_ln_gemm(int srcmode, const tfx::RowSrc& src, const float* g, const float* b,
+                                  const float* Wp, int R, int K, int N, float* y, hipStream_t st) {
+    if (R == 0) return M2_OK;
+    const int nw = tf_waves(R);
+    const dim3 grid(cdiv(R, tfx::TR)), blk(64 * nw);
+    const vx_u32x4* W = reinterpret_cast<const vx_u32x4*>(Wp);
+#define M2_SLG(KK, NN, SS)                                                                                        \
+    if (K == KK && N == NN && srcmode == SS) {                                                                    \
+        if (nw == 8)                                                                                              \
+            hipLaunchKernelGGL((tfx::ln_gemm_kernel<KK, NN, true, ACT_NONE, 8, SS>), grid, blk, 0, st, nullptr, g, \
+                               b, W, nullptr, R, y, src);                                                         \
+        else                                                                                                      \
+            hipLaunchKernelGGL((tfx::ln_gemm_kernel<KK, NN, true, ACT_NONE, 4, SS>), grid, blk, 0, st, nullptr, g, \
+                               b, W, nullptr, R, y, src);                                                         \
+        M2_LAUNCHED("ln_gemm_kernel");                                                                            \
+        return M2_OK;                                                                                             \
+    }
+    M2_SLG(32, 96, tfx::SRC_EMBED)
+    M2_SLG(64, 192, tfx::SRC_EMBED)
+    M2_SLG(96, 288, tfx::SRC_EMBED)
+    M2_SLG(32, 96, tfx::SRC_EXPAND)
+    M2_SLG(64, 192, tfx::SRC_EXPAND)
+    M2_SLG(96, 288, tfx::SRC_EXPAND)
+#undef M2_SLG
+    return fail(M2_E_SHAPE, "ln_gemm: unsupported (K, N) for a fused row source");
+}
+
+bool tf_src_fused_supported(int H, int N) { return (H == 32 && N == 96) || (H == 64 && N == 192) || (H == 96 && N == 288); }
+
+int32_t launch_embed_ln_gemm(const int64_t* ids, const float* emb, const float* pe, int B, int S, int H, int vocab,
+                             const int64_t* lengths, uint8_t* mask, float* x, const float* g, const float* b,
+                             const float* Wp, int N, float* y, hipStream_t st) {
+    tfx::RowSrc src;
+    src.ids = ids;
+    src.emb = emb;
+    src.pe = pe;
+    src.vocab = vocab;
+    src.scale = (float)std::sqrt((double)H);  // as launch_embed_pe
+    src.lengths = lengths;
+    src.mask = mask;
+    src.S = S;
+    src.xo = x;
+    return launch_src_ln_gemm(tfx::SRC_EMBED, src, g, b, Wp, B * S, H, N, y, st);
+}
+
+int32_t launch_expand_ln_gemm(const float* enc, const int32_t* cum, int B, int S, int T, int H, float* x,
+                              const float* g, const float* b, const float* Wp, int N, float* y, hipStream_t st) {
+    tfx::RowSrc src;
+    src.enc = enc;
+    src.cum = cum;
+    src.S = S;
+    src.T = T;
+    src.xo = x;
+    return launch_src_ln_gemm(tfx::SRC_EXPAND, src, g, b, Wp, B * T, H, N, y, st);
 }
 
 int32_t launch_post_attn(const float* att, const float* x, const float* Wo, const float* bo, const float* g2,

@@ -9,7 +9,8 @@ all-reduce(MAX) of a single int32 before the decoder; everything else is
 independent.  Collectives (RCCL over xGMI with the "nccl" backend; gloo in the
 CPU tests):
   all_reduce(MAX)  1 x int32                       after the duration predictor
-  all_gather       mel [b, T, M] and audio [b, 1, 64T] shards (padded to ceil(B/N))
+  all_gather       mel [b, T, M] and audio [b, 1, 64T] shards (padded to ceil(B/N)),
+                   one collective over rows [mel | audio] per utterance
 Payloads are KB..MB, so the path is latency-bound; weights are replicated.
 
 A step is two phases around the all-reduce: ``front`` (encoder, durations,
@@ -140,5 +141,11 @@ def sharded_inference(stages, phoneme_ids: Tensor, phoneme_lengths: Optional[Ten
         mel, audio = stages.back(state, T) if hi > lo else (None, None)
     if not gather or world == 1:
         return (mel, audio) if gather else (mel, audio, (lo, hi))
-    return (_gather_shards(mel, B, world, group, gather_to),
-            _gather_shards(audio, B, world, group, gather_to))
+    # one collective for both outputs: each utterance's mel and audio as one row
+    b, Mw = mel.shape[0], mel[0].numel()
+    both = torch.cat([mel.reshape(b, -1), audio.reshape(b, -1).to(mel.dtype)], dim=1)
+    g = _gather_shards(both, B, world, group, gather_to)
+    if g is None:
+        return None, None
+    return (g[:, :Mw].reshape((B,) + tuple(mel.shape[1:])).contiguous(),
+            g[:, Mw:].reshape((B,) + tuple(audio.shape[1:])).to(audio.dtype).contiguous())

@@ -17,8 +17,10 @@ def summarize(path, steps=20):
     names = [r["Kernel_Name"].split("(")[0].replace("void ", "")[:70] for r in rows]
     st = [int(r["Start_Timestamp"]) for r in rows]
     en = [int(r["End_Timestamp"]) for r in rows]
-    # a step starts at the embedding kernel (first kernel of m2_inference_front)
-    starts = [i for i, n in enumerate(names) if "embed" in n]
+    # a step starts at the embedding kernel (first kernel of m2_inference_front;
+    # with the fused first layer, ln_gemm_kernel<..., SRC_EMBED = 1>)
+    starts = [i for i, n in enumerate(names) if "embed" in n or (n.startswith("m2::tfx::ln_gemm_kernel") and
+                                                                   n.endswith(", 1>"))]
     starts = starts[-steps - 1:]
     per = {}
     spans, busy = [], []
