@@ -49,6 +49,14 @@ constexpr int R0_OFF = 0, R1_OFF = RROWS * RS0, R2_OFF = R1_OFF + RROWS * RS1;
 constexpr int LDS_BYTES = R2_OFF + RROWS * RS1;
 constexpr int NWAVES = 13;              // 4 phases x 3 layers + 1 loader (wave 12)
 
+// Byte offset of 16-B unit u in row `row` of ring R1 / R2 (stride RS1): units
+// swap pairwise (u ^ 1) in rows 4-7 of every 8.  With RS1 / 16 = 2 (mod 4) the
+// B-fragment and residual reads (ds_read_b128, 16-lane groups) were already
+// conflict-free but the epilogue stores (ds_write_b128: 8 consecutive rows,
+// 32 banks) hit two-way conflicts; the swap makes all three conflict-free
+// (tools/probe/midp_banks.py models every access of the kernel).
+__device__ __forceinline__ unsigned r12_at(int row, int u) { return row * RS1 + 16 * (u ^ ((row >> 2) & 1)); }
+
 __device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
 }
@@ -71,7 +79,6 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
                                            unsigned char* __restrict__ u2row) {
     constexpr int NKB = mkb(L);
-    constexpr int RSI = L == 0 ? RS0 : RS1;             // input ring row stride
     constexpr int IN_OFF = L == 0 ? R0_OFF : (L == 1 ? R1_OFF : R2_OFF);
     constexpr int LO_IN = L == 0 ? 128 : 256;           // lo half offset in an input row
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
@@ -94,11 +101,12 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) {
             const MSlot sl = mslot(L, S, kb, g);  // the input ring runs one column ahead of this layer
-            radr[kb][j] = IN_OFF + sl.oct * 16 + ((16 * j + li + sl.dq - 1) & (RROWS - 1)) * RSI;
+            const int row = (16 * j + li + sl.dq - 1) & (RROWS - 1);
+            radr[kb][j] = IN_OFF + (L == 0 ? row * RS0 + sl.oct * 16 : r12_at(row, sl.oct));
         }
-        xadr[j] = R1_OFF + ((16 * j + li - 2) & (RROWS - 1)) * RS1 + 64 * S + 16 * g;
-        oadr[j] = (L == 0 ? R1_OFF : R2_OFF) + ((16 * j + li) & (RROWS - 1)) * RS1 + 64 * S + 256 * (g & 1) +
-                  16 * (g >> 1);
+        xadr[j] = R1_OFF + r12_at((16 * j + li - 2) & (RROWS - 1), 4 * S + g);
+        // unit 4S + 16 (g & 1) + (g >> 1) (+ 2h below: bit 1, so the swap of bit 0 commutes)
+        oadr[j] = (L == 0 ? R1_OFF : R2_OFF) + r12_at((16 * j + li) & (RROWS - 1), 4 * S + 16 * (g & 1) + (g >> 1));
     }
     u32x4 aid[2];  // identity A of m-block h: row li takes fragment row 16h + li = 8g + e
 #pragma unroll
