@@ -172,7 +172,7 @@ struct m2_model {
     void* xbuf = nullptr;
     m2::VocX vx{};
     bool x3 = false;
-    void* tbuf = nullptr;  // pipelined stage1 tail pack (vx.tp / vx.tpb)
+    void* tbuf = nullptr;  // pipelined tail pack (stage1: vx.tp / vx.tpb, stage2: vx.tp2 / vx.tp2b)
     bool tailp = false;
     void* mbuf = nullptr;  // pipelined stage1 mid pack (vx.mp / vx.mpb)
     bool midp = false;
@@ -720,9 +720,10 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 m->vx.bo = m->vw.bo;
                 m->x3 = true;
                 m->x3_packed = true;
-                // stage1: the last two upsampling stages as one pipelined
-                // kernel (M2_VOC_TAIL_X3=1 keeps the x3 tail kernel).
-                if (M == 64 && C == 128 && !std::getenv("M2_VOC_TAIL_X3")) {
+                // stage1 / stage2: the last two upsampling stages as one
+                // pipelined kernel (M2_VOC_TAIL_X3=1 keeps the x3 tail kernel).
+                const bool s2tail = M == 80 && C == 256;
+                if (((M == 64 && C == 128) || s2tail) && !std::getenv("M2_VOC_TAIL_X3")) {
                     const char* names[14] = {
                         "vocoder.upsamples.2.weight",         "vocoder.upsamples.2.bias",
                         "vocoder.resblocks.2.conv1.weight", "vocoder.resblocks.2.conv1.bias",
@@ -740,7 +741,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                     std::vector<uint16_t> pw;
                     std::vector<float> pb;
                     bool rok = true;
-                    if (got && pack_tailp(src, &pw, &pb, &rok) && rok) {
+                    if (got && (s2tail ? pack_tailp2(src, &pw, &pb, &rok) : pack_tailp(src, &pw, &pb, &rok)) && rok) {
                         const size_t wb = pw.size() * sizeof(uint16_t);
                         e = hipMalloc(&m->tbuf, wb + pb.size() * sizeof(float));
                         if (e == hipSuccess) e = hipMemcpyAsync(m->tbuf, pw.data(), wb, hipMemcpyHostToDevice, st);
@@ -754,8 +755,15 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                             if (m->tbuf) (void)hipFree(m->tbuf);
                             return bail(e, "upload tailp pack");
                         }
-                        m->vx.tp = static_cast<const vx_u32x4*>(m->tbuf);
-                        m->vx.tpb = reinterpret_cast<const float*>(static_cast<char*>(m->tbuf) + wb);
+                        const auto* tw = static_cast<const vx_u32x4*>(m->tbuf);
+                        const auto* tb = reinterpret_cast<const float*>(static_cast<char*>(m->tbuf) + wb);
+                        if (s2tail) {
+                            m->vx.tp2 = tw;
+                            m->vx.tp2b = tb;
+                        } else {
+                            m->vx.tp = tw;
+                            m->vx.tpb = tb;
+                        }
                         m->tailp = true;
                     }
                 }
@@ -1322,7 +1330,7 @@ const char* m2_profile_kernel_name(int32_t index) {
 
 const char* m2_profile_kernel_name_for(const m2_model* m, int32_t index) {
     if (!m || index < 0 || index >= kVocKernels) return "";
-    if (m->x3 && m->tailp && index == 2) return kVocTailpKernelName;
+    if (m->x3 && m->tailp && index == 2) return m->vx.tp2 ? kVocTailp2KernelName : kVocTailpKernelName;
     if (m->x3 && m->midp && index == 1) return kVocMidpKernelName;
     return m->x3 ? kVocX3KernelNames[index] : kVocKernelNames[index];
 }

@@ -103,6 +103,9 @@ struct VocX {
     // pipelined stage1 mid stage (vocoder_midp.hip); null = the x3 mid kernel
     const vx_u32x4* mp;
     const float* mpb;
+    // pipelined stage2 tail (vocoder_tailp2.hip); null = the x3 tail kernel
+    const vx_u32x4* tp2;
+    const float* tp2b;
     // set to 1 (vector store) by the last kernel when an audio sample is not
     // finite; host-mapped (m2_model_check)
     int* rflag;
@@ -193,6 +196,12 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>*
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                              int* rflag, hipStream_t st);
 extern const char* const kVocTailpKernelName;
+// The same five modules at stage2 widths (C = 256: U2 64 channels) for the
+// pipelined stage2 tail (vocoder_tailp2.hip, two waves per layer).
+bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
+int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
+                              int* rflag, hipStream_t st);
+extern const char* const kVocTailp2KernelName;
 
 bool vocoder_x3_supported(int M, int C);
 int vocoder_x3_mel_pad(int M);  // input-conv channel count after padding to the k-block layout

@@ -1,0 +1,527 @@
+// Pipelined SimpleVocoder tail for stage2 (C = 256; tts_model.py:279-297, the
+// last two upsampling stages): ConvT3 (64 -> 32 channels, x2) + leaky,
+// ResBlock3, ConvT4 (32 -> 16, x2) + leaky, ResBlock4, output_conv (16 -> 1)
+// + tanh, split-f16 arithmetic (vocoder_x3.hip).  The stage1 design of
+// vocoder_tailp.hip at twice the channels: every signal is a 64-row column
+// over the columns q of U2 (64 channels at 16T):
+//   u3 (ConvT3 out, ResBlock3)  2 phases x 32 channels, row 32 p3 + c
+//   u4 (ConvT4 out, ResBlock4)  4 phases x 16 channels, row 16 p4 + c
+//   audio                       4 phases x 1 channel
+// and every layer is a k3-over-q convolution of 64 output rows (4 m-blocks)
+// whose K is a list of (dq, input octet) slots (tp2::kslot).  A layer's
+// weights (8-16 fragment pairs per m-block pair) no longer fit one wave, so
+// each layer runs on two waves of two m-blocks each, paired so that a wave's
+// m-blocks read the same B fragments where the slots allow:
+//   ConvT3    wave w = output phase w (both read columns q and q -1 / q + 1)
+//   ResBlock3 wave w = phase w (taps (dq, phase) of t3 - 1, t3, t3 + 1)
+//   ConvT4    wave 0 = phases 1, 2 (both read column q only), wave 1 = 0, 3
+//   ResBlock4 wave w = phases 2w, 2w + 1 (16-channel units p-1 .. p+2 of the
+//             unit sequence (q-1, 3), (q, 0..3), (q+1, 0), two per fragment)
+//   output_conv one wave, one m-block (rows 0-3 = the 4 audio phases)
+// 13 layer waves + 1 loader wave, one workgroup per CU (104 KB of rings).
+// Pipeline protocol, warm-up chunk, zero columns outside [0, L2), lean
+// epilogues and the identity-A residual MFMAs are those of vocoder_tailp.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+#include <vector>
+
+#include "m2_common.h"
+#include "vocoder_fused.h"
+
+namespace m2 {
+namespace tp2 {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef vx_u32x4 u32x4;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// LDS rings: R0 = U2, R(l+1) = output of layer l; a ring row is one column as
+// a 128-B hi row (64 f16) in the hi plane and a 128-B lo row kLoOff(n) bytes
+// later.  Octet o of row r sits at 16 * (o ^ (r & 7)): every fragment read
+// (ds_read_b128), residual read and epilogue store (ds_write_b128) of the
+// kernel is then bank-conflict free (tools/probe/tailp2_banks.py models them
+// all).  R0 and R6 hold 3 chunks of 16 columns (their only reader is one step
+// behind the writer), the others 4.
+constexpr int kRingRows[7] = {48, 64, 64, 64, 64, 64, 48};
+constexpr int kRingOff(int n) { return n == 0 ? 0 : kRingOff(n - 1) + kRingRows[n - 1] * 256; }
+constexpr int kLoOff(int n) { return kRingRows[n] * 128; }
+constexpr int kPeriod(int n) { return kRingRows[n] / 16; }
+constexpr int LDS_BYTES = kRingOff(7);
+static_assert(LDS_BYTES <= 160 * 1024, "one workgroup per CU");
+constexpr int NWAVES = 14;  // layers 0-5: two waves each, output conv: one, loader: one
+
+__device__ __forceinline__ unsigned ring_at(int n, int row, int oct) {
+    return kRingOff(n) + row * 128 + 16 * (oct ^ (row & 7));
+}
+__device__ __forceinline__ int ring_row(int n, int j, int c) {
+    const int r = 16 * j + c, R = kRingRows[n];
+    return r < 0 ? r + R : (r >= R ? r - R : r);
+}
+
+__device__ __forceinline__ f32x4 mfma_h(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
+
+constexpr int off_l(int l) { return l + 1; }
+constexpr int last_step(int nch) { return nch - 1 + off_l(6); }
+
+template <int V>
+using ic = std::integral_constant<int, V>;
+
+// ---------------------------------------------------------------------------
+// Slot tables (shared by the packer and the kernel).
+struct Slot {
+    int dq, oct;
+};
+constexpr int kLayers = 7;
+constexpr int nwv(int l) { return l == 6 ? 1 : 2; }   // waves of layer l
+constexpr int nmbw(int l) { return l == 6 ? 1 : 2; }  // m-blocks per wave
+constexpr int nkb(int l) { return l == 0 ? 4 : ((l == 1 || l == 2 || l == 6) ? 3 : 2); }
+constexpr int unit0(int l) { return l == 0 ? 0 : unit0(l - 1) + nwv(l - 1) * nmbw(l - 1) * nkb(l - 1); }
+constexpr int kUnits = unit0(kLayers);
+constexpr int unit_of(int l, int w, int m, int kb) { return unit0(l) + (w * nmbw(l) + m) * nkb(l) + kb; }
+// dense m-block (output rows 16 d .. 16 d + 15) of wave w's m-block m
+constexpr int dmb(int l, int w, int m) { return l == 3 ? (w == 0 ? 1 + m : (m == 0 ? 0 : 3)) : nmbw(l) * w + m; }
+constexpr int fdiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+// 16-channel units of a 4-phase signal around column q: (q-1, 3), (q, 0..3), (q+1, 0)
+constexpr Slot s4unit(int j) { return j == 0 ? Slot{-1, 3} : (j == 5 ? Slot{1, 0} : Slot{0, j - 1}); }
+constexpr Slot kslot(int l, int w, int m, int kb, int g) {
+    if (l == 0)  // phase w: columns (q, q-1) for phase 0, (q+1, q) for phase 1; 64 channels = 2 k-blocks each
+        return Slot{kb < 2 ? (w == 0 ? 0 : 1) : (w == 0 ? -1 : 0), 4 * (kb & 1) + g};
+    if (l == 1 || l == 2) {  // phase w, tap t3 + kb - 1: phase pp mod 2 of column q + floor(pp / 2)
+        const int pp = w + kb - 1, dq = fdiv(pp, 2);
+        return Slot{dq, 4 * (pp - 2 * dq) + g};
+    }
+    if (l == 3) {  // ConvT4 output phase s reads two (column, phase) slots of u3
+        const int s = dmb(l, w, m);
+        const int dq = s == 0 ? (kb == 0 ? 0 : -1) : (s == 3 ? (kb == 0 ? 1 : 0) : 0);
+        const int ph = (s == 0 || s == 3) ? kb : 1 - kb;  // s0: (q,0) (q-1,1); s1, s2: (q,1) (q,0); s3: (q+1,0) (q,1)
+        return Slot{dq, 4 * ph + g};
+    }
+    // ResBlock4 convs (phase p = 2w + m reads units p .. p+2) and the output conv
+    // (all units): k-block kb of a wave = unit pair gi = (l == 6 ? kb : w + kb)
+    const int gi = l == 6 ? kb : w + kb;
+    const Slot u = s4unit(2 * gi + g / 2);
+    return Slot{u.dq, 2 * u.oct + (g & 1)};
+}
+// The wave's distinct B fragments: ConvT4 wave 1 (phases 0, 3) reads four, one
+// pair per m-block; every other wave's m-blocks share theirs (one per k-block).
+constexpr int nfrag(int l, int w) { return (l == 3 && w == 1) ? 4 : nkb(l); }
+constexpr int frag_of(int l, int w, int m, int kb) { return (l == 3 && w == 1) ? 2 * m + kb : kb; }
+constexpr Slot fslot(int l, int w, int f, int g) {
+    return (l == 3 && w == 1) ? kslot(l, w, f / 2, f % 2, g) : kslot(l, w, 0, f, g);
+}
+
+// One wave: layer L, half W (m-blocks dmb(L, W, 0..NMB-1)).  As in
+// vocoder_tailp.hip's layer_role: weights and biases in VGPRs for the whole
+// strip, LDS addresses precomputed per ring phase (the step loop is unrolled by
+// the lcm of the ring periods), one fp32 accumulator per m-block for the three
+// split products, identity-A MFMAs for the ResBlock residual.
+template <int L, int W, int NCH>
+__device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
+                                           const u32x4* __restrict__ W_, const float* __restrict__ bias,
+                                           float* __restrict__ arow, int* rflag) {
+    constexpr int NMB = nmbw(L), NKB = nkb(L), NF = nfrag(L, W);
+    constexpr bool RES = L == 2 || L == 5;
+    constexpr int PI = kPeriod(L), PO = L < 6 ? kPeriod(L + 1) : 1, PX = RES ? kPeriod(L - 1) : 1;
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    u32x4 a[NMB][NKB][2];
+    float bv[NMB][4];
+#pragma unroll
+    for (int m = 0; m < NMB; ++m) {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            const int u = unit_of(L, W, m, kb);
+            a[m][kb][0] = W_[u * 128 + lane];
+            a[m][kb][1] = W_[u * 128 + 64 + lane];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[m][r] = bias[L * 64 + (NMB * W + m) * 16 + 4 * g + r];  // MFMA row order
+    }
+    unsigned radr[NF][PI], xadr[PX], oadr[PO];
+#pragma unroll
+    for (int j = 0; j < PI; ++j)
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            const Slot sl = fslot(L, W, f, g);
+            radr[f][j] = ring_at(L, ring_row(L, j, li + sl.dq - 1), sl.oct);
+        }
+    // residual x: the block input (ring R(L-1), two columns ahead), octets 4W .. 4W+3
+#pragma unroll
+    for (int j = 0; j < PX; ++j) xadr[j] = RES ? ring_at(L - 1, ring_row(L - 1, j, li - 2), 4 * W + g) : 0u;
+    // epilogue: lane group g stores the hi (g even) / lo (g odd) octet 2 d + (g >> 1)
+    // of m-block d = dmb(L, W, m); the m-blocks' addresses differ by an XOR of
+    // 32 (d ^ d0) in the octet field (the swizzle is an XOR on bits 4-6)
+#pragma unroll
+    for (int j = 0; j < PO; ++j)
+        oadr[j] = L < 6 ? (g & 1) * kLoOff(L + 1) + ring_at(L + 1, ring_row(L + 1, j, li), 2 * dmb(L, W, 0) + (g >> 1))
+                        : 0u;
+    u32x4 aid[NMB];  // identity A of m-block m: row li takes fragment row 16 m + li = 8 g + e
+#pragma unroll
+    for (int m = 0; m < NMB; ++m) {
+        h8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (_Float16)(16 * m + li == 8 * g + e ? 1.f : 0.f);
+        aid[m] = __builtin_bit_cast(u32x4, v);
+    }
+    const int sL = qa + 6 - L;  // first column of chunk 0
+    auto work = [&](int k, auto jc) {
+        constexpr int kk = decltype(jc)::value;
+        constexpr int ji = kk % PI, jx = kk % PX, jo = kk % PO;
+        u32x4 bh[NF], bl[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            bh[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][ji]);
+            bl[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][ji] + kLoOff(L));
+        }
+        u32x4 xh, xl;
+        if constexpr (RES) {
+            xh = *reinterpret_cast<const u32x4*>(lds + xadr[jx]);
+            xl = *reinterpret_cast<const u32x4*>(lds + xadr[jx] + kLoOff(L - 1));
+        }
+        f32x4 acc[NMB];
+#pragma unroll
+        for (int m = 0; m < NMB; ++m) acc[m] = f32x4{bv[m][0], bv[m][1], bv[m][2], bv[m][3]};
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int pr = 0; pr < 3; ++pr)
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+                    const int f = frag_of(L, W, m, kb);
+                    acc[m] = mfma_h(a[m][kb][pr == 2], pr == 1 ? bl[f] : bh[f], acc[m]);
+                }
+        if constexpr (RES) {
+#pragma unroll
+            for (int m = 0; m < NMB; ++m) acc[m] = mfma_h(aid[m], xh, acc[m]);
+#pragma unroll
+            for (int m = 0; m < NMB; ++m) acc[m] = mfma_h(aid[m], xl, acc[m]);
+        }
+        const int x0 = sL + 16 * k;
+        if constexpr (L == 6) {
+            // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
+            const int x = x0 + li;
+            if (g == 0 && k >= 0 && x >= 0 && x < L2) {
+                float4 o;
+                o.x = tanh_fast(acc[0][0]);
+                o.y = tanh_fast(acc[0][1]);
+                o.z = tanh_fast(acc[0][2]);
+                o.w = tanh_fast(acc[0][3]);
+                *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
+                flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
+            }
+        } else {
+            auto epilogue = [&](auto zc) {
+                constexpr bool ZERO = decltype(zc)::value;
+                float v[NMB][4];
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[m][r] = acc[m][r];
+                    if constexpr (!RES) leaky4(v[m]);
+                }
+                if constexpr (ZERO) {
+                    const int x = x0 + li;
+                    const bool out = x < 0 || x >= L2;
+#pragma unroll
+                    for (int m = 0; m < NMB; ++m)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[m][r] = out ? 0.f : v[m][r];
+                }
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+                    unsigned h0, h1, l0, l1;
+                    split2u(v[m][0], v[m][1], h0, l0);
+                    split2u(v[m][2], v[m][3], h1, l1);
+                    const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
+                    const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
+                    const unsigned mx = 32u * (unsigned)(dmb(L, W, m) ^ dmb(L, W, 0));
+                    *reinterpret_cast<u32x4*>(lds + (oadr[jo] ^ mx)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+                }
+            };
+            if (edge && (x0 < 0 || x0 + 16 > L2)) epilogue(std::true_type{});  // wave-uniform
+            else epilogue(std::false_type{});
+        }
+    };
+    constexpr int LAST = last_step(NCH);
+    auto step = [&](int s, auto jc) {
+        if (s <= LAST) {
+            const int k = s - off_l(L);
+            if (k >= -1 && k < NCH) work(k, jc);
+            step_barrier();
+        }
+    };
+    constexpr int U = (PI == 3 || PO == 3 || PX == 3) ? 12 : 4;
+    constexpr int J0 = ((-1 - off_l(L)) % U + U) % U;
+    auto iter = [&](int s, auto... i) { (step(s + decltype(i)::value, ic<(J0 + decltype(i)::value) % U>{}), ...); };
+#pragma unroll 1
+    for (int s = -1; s <= LAST; s += U) {
+        if constexpr (U == 4)
+            iter(s, ic<0>{}, ic<1>{}, ic<2>{}, ic<3>{});
+        else
+            iter(s, ic<0>{}, ic<1>{}, ic<2>{}, ic<3>{}, ic<4>{}, ic<5>{}, ic<6>{}, ic<7>{}, ic<8>{}, ic<9>{},
+                 ic<10>{}, ic<11>{});
+    }
+}
+
+// U2 rows (256 B: hi[64] lo[64]) into ring R0, two chunks ahead: chunk c =
+// columns [qa + 7 + 16c, +16), zero outside [0, L2).  Lane (r = lane >> 4, pc =
+// lane & 15) moves 16 B of columns r, r + 4, r + 8, r + 12 (pc < 8: hi octet pc,
+// else lo octet pc - 8); loads unconditional (clamped) so their waits are counted.
+template <int NCH, bool EDGE>
+__device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, const unsigned char* __restrict__ u2) {
+    const int lane = threadIdx.x & 63, r = lane >> 4, pc = lane & 15;
+    auto fetch = [&](int c, u32x4 (&v)[4]) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            int col = qa + 7 + 16 * c + r + 4 * h;
+            if (EDGE) col = min(max(col, 0), L2 - 1);
+            v[h] = *reinterpret_cast<const u32x4*>(u2 + (size_t)col * 256 + pc * 16);
+        }
+    };
+    u32x4 buf[3][4];
+    unsigned wadr[3][4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) wadr[j][h] = (pc >> 3) * kLoOff(0) + ring_at(0, ring_row(0, j, r + 4 * h), pc & 7);
+    auto step = [&](int s, auto jc, u32x4 (&cur)[4], u32x4 (&ahead)[4]) {
+        constexpr int j = decltype(jc)::value;
+        fetch(min(s + 2, NCH - 1), ahead);
+        if (s < NCH) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int col = qa + 7 + 16 * s + r + 4 * h;
+                const bool in = !EDGE || (col >= 0 && col < L2);
+                const u32x4 z{0u, 0u, 0u, 0u};
+                *reinterpret_cast<u32x4*>(lds + wadr[j][h]) = in ? cur[h] : z;
+            }
+        }
+        step_barrier();
+    };
+    fetch(-1, buf[0]);
+    fetch(0, buf[1]);
+    int s = -1;
+#pragma unroll 1
+    for (; s + 2 <= last_step(NCH); s += 3) {
+        step(s, ic<2>{}, buf[0], buf[2]);
+        step(s + 1, ic<0>{}, buf[1], buf[0]);
+        step(s + 2, ic<1>{}, buf[2], buf[1]);
+    }
+#pragma unroll 1
+    for (; s <= last_step(NCH); ++s) step_barrier();
+}
+
+template <int NCH>
+__global__ __launch_bounds__(NWAVES * 64, 1) void tailp2_kernel(const unsigned char* __restrict__ U2, int L2,
+                                                                 const u32x4* __restrict__ W,
+                                                                 const float* __restrict__ bias,
+                                                                 float* __restrict__ audio, int* rflag) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
+    float* arow = audio + (size_t)b * 4 * L2;
+    // later layers: younger waves, the step waits for the slowest role
+    if (w >= 10) __builtin_amdgcn_s_setprio(3);
+    else if (w >= 6) __builtin_amdgcn_s_setprio(2);
+    else if (w >= 2) __builtin_amdgcn_s_setprio(1);
+    switch (w) {
+        case 0: layer_role<0, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 1: layer_role<0, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 2: layer_role<1, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 3: layer_role<1, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 4: layer_role<2, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 5: layer_role<2, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 6: layer_role<3, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 7: layer_role<3, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 8: layer_role<4, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 9: layer_role<4, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 10: layer_role<5, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 11: layer_role<5, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 12: layer_role<6, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        default:
+            if (edge) loader_role<NCH, true>(lds, qa, L2, U2 + (size_t)b * L2 * 256);
+            else loader_role<NCH, false>(lds, qa, L2, U2 + (size_t)b * L2 * 256);
+            break;
+    }
+}
+
+template <int NCH>
+int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
+               hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp2_kernel<NCH>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        attr = true;
+    }
+    hipLaunchKernelGGL((tailp2_kernel<NCH>), dim3(cdiv(L2, 16 * NCH), B), dim3(NWAVES * 64), LDS_BYTES, st,
+                       static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
+    M2_LAUNCHED("tailp2_kernel");
+    return M2_OK;
+}
+
+}  // namespace tp2
+
+const char* const kVocTailp2KernelName =
+    "tailp2_kernel (stage2 ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, pipelined)";
+
+int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
+                              int* rflag, hipStream_t st) {
+    if (B == 0 || L2 == 0) return M2_OK;
+    // Strip length: the instantiated NCH minimising rounds x (NCH + 7 pipeline
+    // steps) at one workgroup per CU.  M2_TAILP2_NCH forces one.
+    static constexpr int kN[] = {8, 16, 32, 64, 128, 192};
+    static const int forced = [] {
+        const char* e = std::getenv("M2_TAILP2_NCH");
+        const int v = e ? std::atoi(e) : 0;
+        for (int n : kN)
+            if (v == n) return v;
+        return 0;
+    }();
+    int nch = forced;
+    if (!nch) {
+        const long chunks = cdiv(L2, 16);
+        long best = -1;
+        for (int n : kN) {
+            const long wgs = (long)cdiv((int)chunks, n) * B, rounds = (wgs + 255) / 256, cost = rounds * (n + 7);
+            if (best < 0 || cost < best) best = cost, nch = n;
+        }
+    }
+    switch (nch) {
+        case 8: return tp2::launch<8>(U2, L2, B, W, bias, audio, rflag, st);
+        case 16: return tp2::launch<16>(U2, L2, B, W, bias, audio, rflag, st);
+        case 32: return tp2::launch<32>(U2, L2, B, W, bias, audio, rflag, st);
+        case 64: return tp2::launch<64>(U2, L2, B, W, bias, audio, rflag, st);
+        case 128: return tp2::launch<128>(U2, L2, B, W, bias, audio, rflag, st);
+        default: return tp2::launch<192>(U2, L2, B, W, bias, audio, rflag, st);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host packing: each layer as a dense polyphase matrix Wd[row][dq + 1][input
+// row] (64 x 3 x 64), cut into (wave, m-block, k-block) fragment pairs along
+// tp2::kslot: A[row = lane & 15][slot g = lane >> 4, element e] =
+// Wd[16 dmb + (lane & 15)][dq + 1][8 oct + e], zero on a slot the m-block
+// already read.  Every non-zero of Wd must sit on a slot.
+namespace {
+
+int floordiv2(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+struct Dense64 {
+    std::vector<float> w = std::vector<float>(64 * 3 * 64, 0.f);
+    float& at(int row, int dq, int in) { return w[(row * 3 + dq + 1) * 64 + in]; }
+};
+
+// ConvTranspose1d(k=4, stride 2, pad 1), W [Cin][Cout][4], on a Pin-phase input
+// -> 2 Pin phases of Cout channels: out[2i] = x[i] W1 + x[i-1] W3,
+// out[2i+1] = x[i+1] W0 + x[i] W2 (tts_model.py:255-263).
+void dense_convT2(Dense64& d, const float* W, int Pin, int Cin, int Cout) {
+    const int taps[2][2][2] = {{{0, 1}, {-1, 3}}, {{1, 0}, {0, 2}}};
+    for (int pin = 0; pin < Pin; ++pin)
+        for (int s = 0; s < 2; ++s)
+            for (int j = 0; j < 2; ++j) {
+                const int pp = pin + taps[s][j][0], dq = floordiv2(pp, Pin), p2 = pp - dq * Pin, kk = taps[s][j][1];
+                for (int co = 0; co < Cout; ++co)
+                    for (int ci = 0; ci < Cin; ++ci)
+                        d.at((2 * pin + s) * Cout + co, dq, p2 * Cin + ci) += W[((size_t)ci * Cout + co) * 4 + kk];
+            }
+}
+
+// Conv1d(k=3, pad 1), W [Cout][Cin][3], on a P-phase signal.
+void dense_conv3(Dense64& d, const float* W, int P, int Cin, int Cout) {
+    for (int p = 0; p < P; ++p)
+        for (int k = 0; k < 3; ++k) {
+            const int pp = p + k - 1, dq = floordiv2(pp, P), p2 = pp - dq * P;
+            for (int co = 0; co < Cout; ++co)
+                for (int ci = 0; ci < Cin; ++ci) d.at(p * Cout + co, dq, p2 * Cin + ci) += W[((size_t)co * Cin + ci) * 3 + k];
+        }
+}
+
+void put_split(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) {
+    if (!(std::fabs(v) < 65504.f)) *range_ok = false;
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)(v - (float)h);
+    uint16_t hb, lb;
+    std::memcpy(&hb, &h, 2);
+    std::memcpy(&lb, &l, 2);
+    out[idx] = hb;
+    out[idx + 64 * 8] = lb;
+}
+
+}  // namespace
+
+bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
+    using namespace tp2;
+    Dense64 d[kLayers];
+    dense_convT2(d[0], s.wt3, 1, 64, 32);
+    dense_conv3(d[1], s.w31, 2, 32, 32);
+    dense_conv3(d[2], s.w32, 2, 32, 32);
+    dense_convT2(d[3], s.wt4, 2, 32, 16);
+    dense_conv3(d[4], s.w41, 4, 16, 16);
+    dense_conv3(d[5], s.w42, 4, 16, 16);
+    dense_conv3(d[6], s.wo, 4, 16, 1);
+    const int nrows[kLayers] = {64, 64, 64, 64, 64, 64, 4};
+    // every non-zero dense weight must be read by some slot of its m-block
+    for (int l = 0; l < kLayers; ++l)
+        for (int w = 0; w < nwv(l); ++w)
+            for (int m = 0; m < nmbw(l); ++m)
+                for (int rr = 0; rr < 16; ++rr) {
+                    const int row = 16 * dmb(l, w, m) + rr;
+                    if (row >= nrows[l]) continue;
+                    for (int dq = -1; dq <= 1; ++dq)
+                        for (int in = 0; in < 64; ++in) {
+                            if (d[l].at(row, dq, in) == 0.f) continue;
+                            bool found = false;
+                            for (int kb = 0; kb < nkb(l) && !found; ++kb)
+                                for (int g = 0; g < 4; ++g) {
+                                    const Slot sl = kslot(l, w, m, kb, g);
+                                    if (sl.dq == dq && sl.oct == in / 8) found = true;
+                                }
+                            if (!found) return false;
+                        }
+                }
+    wout->assign((size_t)kUnits * 2 * 64 * 8, 0);
+    for (int l = 0; l < kLayers; ++l)
+        for (int w = 0; w < nwv(l); ++w)
+            for (int m = 0; m < nmbw(l); ++m)
+                for (int kb = 0; kb < nkb(l); ++kb) {
+                    const int u = unit_of(l, w, m, kb);
+                    for (int lane = 0; lane < 64; ++lane) {
+                        const int row = 16 * dmb(l, w, m) + (lane & 15), g = lane >> 4;
+                        const Slot sl = kslot(l, w, m, kb, g);
+                        bool dup = false;  // a (dq, octet) this m-block already reads in an earlier slot
+                        for (int j = 0; j < kb * 4 + g; ++j) {
+                            const Slot o = kslot(l, w, m, j / 4, j % 4);
+                            dup = dup || (o.dq == sl.dq && o.oct == sl.oct);
+                        }
+                        for (int e = 0; e < 8; ++e) {
+                            float v = 0.f;
+                            if (row < nrows[l] && !dup) v = d[l].at(row, sl.dq, 8 * sl.oct + e);
+                            put_split(*wout, (((size_t)u * 2) * 64 + lane) * 8 + e, v, range_ok);
+                        }
+                    }
+                }
+    // biases in MFMA row order: [layer][wave][m-block][16 rows]
+    bout->assign(kLayers * 64, 0.f);
+    const float* bsrc[kLayers] = {s.bt3, s.b31, s.b32, s.bt4, s.b41, s.b42, s.bo};
+    const int cper[kLayers] = {32, 32, 32, 16, 16, 16, 1};
+    for (int l = 0; l < kLayers; ++l)
+        for (int w = 0; w < nwv(l); ++w)
+            for (int m = 0; m < nmbw(l); ++m)
+                for (int rr = 0; rr < 16; ++rr) {
+                    const int row = 16 * dmb(l, w, m) + rr;
+                    if (row < nrows[l]) (*bout)[l * 64 + (nmbw(l) * w + m) * 16 + rr] = bsrc[l][row % cper[l]];
+                }
+    return true;
+}
+
+}  // namespace m2

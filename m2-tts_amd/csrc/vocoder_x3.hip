@@ -1026,7 +1026,7 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         if (!w.mp)
             alt_mid = rounds_of((long)cdiv(4 * T, CfgS2Alt::W2) * B, sm1) * kAltMidCost <
                       (double)rounds_of((long)cdiv(4 * T, Cfg::W2) * B, sm0);
-        if (!w.tp)
+        if (!w.tp && !w.tp2)
             alt_tail = rounds_of((long)cdiv(16 * T, CfgS2Alt::W3) * B, st1) * kAltTailCost <
                        (double)rounds_of((long)cdiv(16 * T, Cfg::W3) * B, st0);
     }
@@ -1056,6 +1056,11 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     }
     mark(1, false);
     mark(2, true);
+    if (w.tp2) {  // stage2: the pipelined tail (vocoder_tailp2.hip)
+        const int32_t rc = launch_vocoder_tailp2(u2, 16 * T, B, w.tp2, w.tp2b, audio, w.rflag, st);
+        mark(2, false);
+        return rc;
+    }
     if (w.tp) {  // stage1: the pipelined tail (vocoder_tailp.hip)
         const int32_t rc = launch_vocoder_tailp(u2, 16 * T, B, w.tp, w.tpb, audio, w.rflag, st);
         mark(2, false);
