@@ -16,6 +16,11 @@
 // ConvT4 pairs phases 1, 2 (which read column q only: one k-block) and 0, 3
 // (tp::prow), 9 MFMAs per step instead of 12.
 //
+// Round 2 (default): ResBlock4's conv2 and output_conv are one composed layer
+// (outc_role below), so 6 layers, 7 waves and 7 pipeline steps of fill; the
+// description below is of the 7-layer form (M2_TAILP_SEVEN=1), which the
+// 6-layer one follows for its first five layers.
+//
 // Systolic pipeline.  One workgroup owns a strip of 16*NCH columns of one
 // utterance and runs 8 waves with fixed roles: a loader wave streams U2 into
 // an LDS ring, and each of the 7 layers is done by one wave for all its
@@ -69,9 +74,30 @@ constexpr int kRingRows[7] = {48, 64, 64, 64, 64, 64, 48};
 constexpr int kRingOff(int n) { return n == 0 ? 0 : kRingOff(n - 1) + kRingRows[n - 1] * 128; }
 constexpr int kLoOff(int n) { return kRingRows[n] * 64; }
 constexpr int kPeriod(int n) { return kRingRows[n] / 16; }  // chunks per ring (3 or 4)
-constexpr int LDS_BYTES = kRingOff(7);
-static_assert(LDS_BYTES * 3 <= 160 * 1024, "three workgroups per CU");
-constexpr int NWAVES = 8;  // 7 layer waves (all m-blocks of a layer) + 1 loader
+// NL computing layers use rings R0 .. R(NL-1) and NL + 1 waves (one per layer
+// + the loader): NL = 7 53,248 B, NL = 6 (outc_role) 47,120 B.
+// NL = 6 also keeps the outc edge-term slot (4 floats) after the rings.
+constexpr int kCorrSlot = kRingOff(6);
+constexpr int lds_bytes(int nl) { return nl == 6 ? kCorrSlot + 16 : kRingOff(nl); }
+constexpr int nwaves(int nl) { return nl + 1; }
+static_assert(lds_bytes(7) * 3 <= 160 * 1024, "three workgroups per CU");
+#ifdef M2_STAMPS
+constexpr int NWAVES = 8;  // stamp buffer size (the larger variant)
+#endif
+
+// The composed ResBlock4-conv2 + output_conv layer (outc_role): weight units
+// after the 22 of the seven-layer form, its bias (rows 0..3) and the edge
+// terms (vL[8], vR[8], kL, kR) after the seven layers' biases.
+constexpr int kOutcUnit0 = kUnits, kOutcUnits = 4, kOutcBias = kLayers * 32, kOutcCorr = kOutcBias + 32;
+constexpr int kBiasFloats = kOutcCorr + 32;
+// Fragment f, lane group g: 0, 1 on ring R5 (ResBlock4's intermediate h),
+// 2, 3 on ring R4 (ConvT4's output x); slots of f = 3 repeated in f = 2 carry
+// zero weights.
+__host__ __device__ constexpr Slot outc_slot(int f, int g) {
+    return f == 0 || f == 2 ? Slot{0, g}
+                            : (f == 1 ? (g < 2 ? Slot{-1, 2 + g} : Slot{1, g - 2})
+                                      : (g == 0 ? Slot{-1, 3} : (g == 1 ? Slot{1, 0} : Slot{0, g})));
+}
 
 // Byte offset of (row, octet) in ring n's hi plane; row in [0, kRingRows[n]).
 __device__ __forceinline__ unsigned ring_at(int n, int row, int oct) {
@@ -121,8 +147,10 @@ __device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __built
 // Layer l computes chunk k in step k + l + 1; the last step is layer 6's
 // chunk NCH - 1.  (Staggered epilogues, where some layers store chunk k one
 // step after computing it, measured slower and were dropped.)
+// NL = number of computing layers: 7 (ResBlock4 conv2 and output_conv as two
+// layers) or 6 (the two composed into one, outc_role below).
 constexpr int off_l(int l) { return l + 1; }
-constexpr int last_step(int nch) { return nch - 1 + off_l(6); }
+constexpr int last_step(int nch, int nl) { return nch - 1 + off_l(nl - 1); }
 
 template <int V>
 using ic = std::integral_constant<int, V>;
@@ -135,7 +163,7 @@ using ic = std::integral_constant<int, V>;
 // packed multiply and two max), the split (3 VALU per pair), two permlane16
 // swaps and one ds_write_b128; the zeroing of columns outside [0, L2) is a
 // scalar branch taken only by chunks that straddle an utterance end.
-template <int L, int NMB, int NCH>
+template <int L, int NMB, int NCH, int NL>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
                                            float* __restrict__ arow, int* rflag) {
@@ -198,7 +226,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
         for (int e = 0; e < 8; ++e) v[e] = (_Float16)(16 * m + li == 8 * g + e ? 1.f : 0.f);
         aid[m] = __builtin_bit_cast(u32x4, v);
     }
-    const int sL = qa + 6 - L;  // first column of chunk 0
+    const int sL = qa + NL - 1 - L;  // first column of chunk 0
     auto work = [&](int k, auto jc) {
         constexpr int kk = decltype(jc)::value;  // k mod lcm of the ring periods
         constexpr int ji = kk % PI, jx = kk % PX, jo = kk % PO;
@@ -235,7 +263,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
             for (int m = 0; m < NMB; ++m) acc[m] = mfma_h(aid[m], xl, acc[m]);
         }
         const int x0 = sL + 16 * k;  // this chunk's first column
-        if constexpr (L == 6) {
+        if constexpr (L == NL - 1) {
             // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
             const int x = x0 + li;
             if (g == 0 && k >= 0 && x >= 0 && x < L2) {
@@ -267,6 +295,25 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                     for (int m = 0; m < NMB; ++m)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) v[m][r] = out ? 0.f : v[m][r];
+                    if constexpr (L == 4 && NL == 6) {
+                        // outc_role's edge terms: lane group g holds channels
+                        // 4(g & 1) .. +3 of phase 2m + (g >> 1) in m-block m, so
+                        // groups 0, 1 have h[:, 0] at column 0 and groups 2, 3
+                        // h[:, L4 - 1] at column L2 - 1 (m-block 1); each adds
+                        // its four products (group 0 / 2 also kL / kR) into
+                        // slot g.  (Opaque pointer: the 18 constants are loaded
+                        // in this rare branch, not hoisted into VGPRs.)
+                        const float* cp = bias + kOutcCorr;
+                        asm volatile("" : "+s"(cp));
+                        const bool right = g >= 2;
+                        if (right ? x == L2 - 1 : x == 0) {
+                            const float* cv = cp + (right ? 8 + 4 * (g - 2) : 4 * g);
+                            float d = g == 0 ? cp[16] : (g == 2 ? cp[17] : 0.f);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) d = fmaf(cv[r], right ? v[1][r] : v[0][r], d);
+                            *reinterpret_cast<float*>(lds + kCorrSlot + 4 * g) = d;
+                        }
+                    }
                 }
 #pragma unroll
                 for (int m = 0; m < NMB; ++m) {
@@ -283,11 +330,14 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                     *reinterpret_cast<u32x4*>(lds + (oadr[jo] ^ (MX * m))) = u32x4{s0[0], s1[0], s0[1], s1[1]};
                 }
             };
-            if (edge && (x0 < 0 || x0 + 16 > L2)) epilogue(std::true_type{});  // wave-uniform
+            // (layer 4 of the six-layer form also takes it for a chunk that
+            // starts at column 0 or ends at L2: outc_role's edge terms)
+            constexpr int EW = L == 4 && NL == 6 ? 1 : 0;
+            if (edge && (x0 < EW || x0 + 16 > L2 - EW)) epilogue(std::true_type{});  // wave-uniform
             else epilogue(std::false_type{});
         }
     };
-    constexpr int LAST = last_step(NCH);
+    constexpr int LAST = last_step(NCH, NL);
     auto step = [&](int s, auto jc) {
         if (s <= LAST) {
             TPSTAMP(s + 1, 0);
@@ -314,11 +364,106 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
     }
 }
 
+// ResBlock4 conv2 and output_conv composed into one layer (NL = 6): the
+// resblock's output y = conv2(h) + b2 + x feeds only the output conv, which
+// is linear, so audio = tanh(Wc * h + Wo * x + bo') with Wc = Wo o W2 (a k5
+// conv on h, ResBlock4's intermediate, ring R5) and Wo (k3 on x, ConvT4's
+// output, ring R4, two columns ahead like a residual read).  On the 4-phase
+// column form both still span columns q-1 .. q+1: fragments 0, 1 read R5
+// (tp::fslot of the 2-phase layers: (q, 0..3), (q-1, 2|3), (q+1, 0|1)),
+// fragments 2, 3 read R4 (those of output_conv), 4 k-blocks = 12 MFMAs per
+// chunk against 10 + 6 for the two layers, one pipeline step and one wave
+// fewer.  The reference zero-pads y, not h: the composed form sees a y at
+// t = -1 and t = L4 (b2 + conv2 of the edge sample), so the two edge samples
+// of an utterance subtract that term (kL + vL . h[:, 0], kR + vR . h[:, L4-1])
+// before tanh.  Layer 4 computes those two sums from its fp32 outputs in the
+// epilogue of the chunk that holds the column and leaves them in an LDS slot
+// (kCorrSlot; one writer per strip, read at least one step later), so this
+// role, at the 80-VGPR budget with its four fragment pairs, adds one read.
+template <int NCH>
+__device__ __forceinline__ void outc_role(unsigned char* lds, int qa, int L2, bool edge,
+                                          const u32x4* __restrict__ W, const float* __restrict__ bias,
+                                          float* __restrict__ arow, int* rflag) {
+    constexpr int L = 5, NL = 6, NF = 4, P = 4;  // rings R4 and R5 both hold 4 chunks
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    u32x4 a[NF][2];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        a[f][0] = W[(kOutcUnit0 + f) * 128 + lane];
+        a[f][1] = W[(kOutcUnit0 + f) * 128 + 64 + lane];
+    }
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = bias[kOutcBias + 4 * g + r];
+    // Fragment addresses as one VGPR each: on a 64-row ring the row of ring
+    // phase j is (c + 16 j) mod 64 and the swizzle depends on row bits 1-2
+    // only, so ring_at(n, ring_row(n, j, c), o) - kRingOff(n) =
+    // (rbase + 1024 j) & 4095 with rbase its j = 0 value (four VGPRs instead
+    // of sixteen: this role holds four weight fragment pairs).
+    static_assert(kRingRows[4] == 64 && kRingRows[5] == 64, "64-row rings");
+    unsigned rbase[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        const Slot sl = outc_slot(f, g);
+        // R5 holds layer 4's columns one ahead of this layer's, R4 layer 3's two
+        rbase[f] = f < 2 ? ring_at(5, ring_row(5, 0, li + sl.dq - 1), sl.oct) - kRingOff(5)
+                         : ring_at(4, ring_row(4, 0, li + sl.dq - 2), sl.oct) - kRingOff(4);
+    }
+    auto radr = [&](int f, int j) { return (f < 2 ? kRingOff(5) : kRingOff(4)) + ((rbase[f] + 1024u * j) & 4095u); };
+    auto work = [&](int k, auto jc) {
+        constexpr int j = decltype(jc)::value;
+        u32x4 bh[NF], bl[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            bh[f] = *reinterpret_cast<const u32x4*>(lds + radr(f, j));
+            bl[f] = *reinterpret_cast<const u32x4*>(lds + radr(f, j) + (f < 2 ? kLoOff(5) : kLoOff(4)));
+        }
+        const int x0 = qa + 16 * k, x = x0 + li;
+        f32x4 acc = f32x4{bv[0], bv[1], bv[2], bv[3]};
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int pr = 0; pr < 3; ++pr) acc = mfma_h(a[f][pr == 2], pr == 1 ? bl[f] : bh[f], acc);
+        float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+        if (edge && (x0 <= 0 || x0 + 16 >= L2)) {  // wave-uniform
+            // the edge terms layer 4 left in the slot (written in an earlier step)
+            const f32x4 e = *reinterpret_cast<const f32x4*>(lds + kCorrSlot);
+            if (x == 0) v[0] -= e[0] + e[1];
+            if (x == L2 - 1) v[3] -= e[2] + e[3];
+        }
+        if (g == 0 && k >= 0 && x >= 0 && x < L2) {
+            float4 o;
+            o.x = tanh_fast(v[0]);
+            o.y = tanh_fast(v[1]);
+            o.z = tanh_fast(v[2]);
+            o.w = tanh_fast(v[3]);
+            *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
+            flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
+        }
+    };
+    constexpr int LAST = last_step(NCH, NL);
+    auto step = [&](int s, auto jc) {
+        if (s <= LAST) {
+            const int k = s - off_l(L);
+            if (k >= 0 && k < NCH) work(k, jc);  // chunk -1 feeds no later layer
+            step_barrier();
+        }
+    };
+    constexpr int J0 = ((-1 - off_l(L)) % P + P) % P;
+#pragma unroll 1
+    for (int s = -1; s <= LAST; s += P) {
+        step(s, ic<J0 % P>{});
+        step(s + 1, ic<(J0 + 1) % P>{});
+        step(s + 2, ic<(J0 + 2) % P>{});
+        step(s + 3, ic<(J0 + 3) % P>{});
+    }
+}
+
 // U2 rows (128 B: hi[32] lo[32], the mid kernel's output format) into ring R0,
 // two chunks ahead: chunk c = columns [qa + 7 + 16c, +16), zero outside [0, L2).
 // EDGE: the strip's columns (with the prologue / epilogue chunks) may leave
 // [0, L2); interior strips skip the clamps and the zero selects.
-template <int NCH, bool EDGE>
+template <int NCH, int NL, bool EDGE>
 __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, const unsigned char* __restrict__ u2) {
     const int lane = threadIdx.x & 63, r = lane >> 3, pc = lane & 7;
     // Every step issues its two loads unconditionally (column clamped into the
@@ -328,7 +473,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     auto fetch = [&](int c, u32x4 (&v)[2]) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            int col = qa + 7 + 16 * c + r + 8 * h;
+            int col = qa + NL + 16 * c + r + 8 * h;
             if (EDGE) col = min(max(col, 0), L2 - 1);
             v[h] = *reinterpret_cast<const u32x4*>(u2 + (size_t)col * 128 + pc * 16);
         }
@@ -351,7 +496,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
         if (s < NCH) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int col = qa + 7 + 16 * s + r + 8 * h;
+                const int col = qa + NL + 16 * s + r + 8 * h;
                 const bool in = !EDGE || (col >= 0 && col < L2);
                 const u32x4 z{0u, 0u, 0u, 0u};
                 *reinterpret_cast<u32x4*>(lds + wadr[j][h]) = in ? cur[h] : z;
@@ -363,20 +508,20 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     fetch(0, buf[1]);
     int s = -1;
 #pragma unroll 1
-    for (; s + 2 <= last_step(NCH); s += 3) {  // covers every step with work (s <= NCH - 1)
+    for (; s + 2 <= last_step(NCH, NL); s += 3) {  // covers every step with work (s <= NCH - 1)
         step(s, ic<2>{}, buf[0], buf[2]);
         step(s + 1, ic<0>{}, buf[1], buf[0]);
         step(s + 2, ic<1>{}, buf[2], buf[1]);
     }
 #pragma unroll 1
-    for (; s <= last_step(NCH); ++s) step_barrier();
+    for (; s <= last_step(NCH, NL); ++s) step_barrier();
 }
 
-template <int NCH>
-__global__ __launch_bounds__(NWAVES * 64, 6) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
-                                                                const u32x4* __restrict__ W,
-                                                                const float* __restrict__ bias,
-                                                                float* __restrict__ audio, int* rflag) {
+template <int NCH, int NL>
+__global__ __launch_bounds__(nwaves(NL) * 64, 6) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
+                                                                    const u32x4* __restrict__ W,
+                                                                    const float* __restrict__ bias,
+                                                                    float* __restrict__ audio, int* rflag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -391,35 +536,52 @@ __global__ __launch_bounds__(NWAVES * 64, 6) void tailp_kernel(const unsigned ch
     if (w >= 5) __builtin_amdgcn_s_setprio(3);
     else if (w >= 3) __builtin_amdgcn_s_setprio(2);
     else if (w >= 1) __builtin_amdgcn_s_setprio(1);
+    const unsigned char* u2 = U2 + (size_t)b * L2 * 128;
     switch (w) {
-        case 0: layer_role<0, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 1: layer_role<1, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 2: layer_role<2, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 3: layer_role<3, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 4: layer_role<4, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 5: layer_role<5, 2, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 6: layer_role<6, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 0: layer_role<0, 2, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 1: layer_role<1, 2, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 2: layer_role<2, 2, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 3: layer_role<3, 2, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 4: layer_role<4, 2, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 5:
+            if constexpr (NL == 7) layer_role<5, 2, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
+            else outc_role<NCH>(lds, qa, L2, edge, W, bias, arow, rflag);
+            break;
+        case 6:
+            if constexpr (NL == 7) {
+                layer_role<6, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
+                break;
+            }
+            [[fallthrough]];
         default:
-            if (edge) loader_role<NCH, true>(lds, qa, L2, U2 + (size_t)b * L2 * 128);
-            else loader_role<NCH, false>(lds, qa, L2, U2 + (size_t)b * L2 * 128);
+            if (edge) loader_role<NCH, NL, true>(lds, qa, L2, u2);
+            else loader_role<NCH, NL, false>(lds, qa, L2, u2);
             break;
     }
     TPSTAMP(63, 0);
 }
 
-template <int NCH>
+template <int NCH, int NL>
 int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
                hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp_kernel<NCH>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp_kernel<NCH, NL>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes(NL)));
         attr = true;
     }
-    hipLaunchKernelGGL((tailp_kernel<NCH>), dim3(cdiv(L2, 16 * NCH), B), dim3(NWAVES * 64), LDS_BYTES, st,
-                       static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
+    hipLaunchKernelGGL((tailp_kernel<NCH, NL>), dim3(cdiv(L2, 16 * NCH), B), dim3(nwaves(NL) * 64), lds_bytes(NL),
+                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
     M2_LAUNCHED("tailp_kernel");
     return M2_OK;
+}
+
+template <int NL>
+int32_t launch_nl(int nch, const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
+                  int* rflag, hipStream_t st) {
+    if (nch == 21) return launch<21, NL>(U2, L2, B, W, bias, audio, rflag, st);
+    if (nch == 48) return launch<48, NL>(U2, L2, B, W, bias, audio, rflag, st);
+    return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st);
 }
 
 }  // namespace tp
@@ -450,9 +612,16 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
         const int chunks = cdiv(L2, 16), strips = std::max(1, 3 * 256 / B), need = cdiv(chunks, strips);
         nch = need <= 21 ? 21 : (need <= 32 ? 32 : 48);
     }
-    if (nch == 21) return tp::launch<21>(U2, L2, B, W, bias, audio, rflag, st);
-    if (nch == 48) return tp::launch<48>(U2, L2, B, W, bias, audio, rflag, st);
-    return tp::launch<32>(U2, L2, B, W, bias, audio, rflag, st);
+    // M2_TAILP_SEVEN=1: ResBlock4 conv2 and the output conv as two layers
+    // (the round-2 form; A/B and test switch, read per call).
+    // (A wave -> role map that balances the MFMA load of the SIMDs — the
+    // hardware puts wave w on SIMD c[(w + r) mod 4], c = (0, 2, 1, 3), with a
+    // rotation r per co-resident workgroup, tools/probe/simd_map.hip — gave
+    // classes of 18/21/16/12 MFMAs instead of 18/24/16/9 and measured the same:
+    // the step is latency-bound, not bound by one SIMD's MFMA pipe.)
+    const bool seven = std::getenv("M2_TAILP_SEVEN") != nullptr;
+    return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st)
+                 : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -508,6 +677,8 @@ void put_split(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) 
 
 }  // namespace
 
+bool pack_outc(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok);
+
 bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
     Dense d[tp::kLayers];
     dense_convT2(d[0], s.wt3, 1, 32, 16);
@@ -532,7 +703,7 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
                         }
                     if (missing) return false;  // a non-zero weight that no slot reads
                 }
-    wout->assign((size_t)tp::kUnits * 2 * 64 * 8, 0);
+    wout->assign((size_t)(tp::kUnits + tp::kOutcUnits) * 2 * 64 * 8, 0);
     for (int l = 0; l < tp::kLayers; ++l)
         for (int mb = 0; mb < tp::nmb(l); ++mb)
             for (int kb = 0; kb < tp::nkbm(l, mb); ++kb) {
@@ -553,11 +724,78 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
                     }
                 }
             }
-    bout->assign(tp::kLayers * 32, 0.f);
+    bout->assign(tp::kBiasFloats, 0.f);
     const float* bsrc[tp::kLayers] = {s.bt3, s.b31, s.b32, s.bt4, s.b41, s.b42, s.bo};
     const int cper[tp::kLayers] = {16, 16, 16, 8, 8, 8, 1};
     for (int l = 0; l < tp::kLayers; ++l)
         for (int R = 0; R < nrows[l]; ++R) (*bout)[l * 32 + R] = bsrc[l][tp::prow(l, R) % cper[l]];
+    return pack_outc(s, wout, bout, range_ok);
+}
+
+// The composed ResBlock4-conv2 + output_conv layer (outc_role), in double:
+// audio[t] = tanh(bo' + sum_d Wo[c][d] x[c][t+d] + sum_j Wc[c'][j] h[c'][t+j]),
+// Wc[c'][j] = sum_{d+e=j} sum_c Wo[c][d] W2[c][c'][e], bo' = bo + sum_d sum_c
+// Wo[c][d] b2[c]; on the 4-phase columns (row p = output phase, input row
+// p2*8 + c at column q + dq).  Edge terms: the y the composed form sees at
+// t = -1 is b2 + W2[.][.][2] h[., 0], at t = L4 it is b2 + W2[.][.][0] h[., L4-1].
+bool pack_outc(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
+    double dh[4][3][32] = {}, dx[4][3][32] = {};
+    auto wo = [&](int c, int k) { return (double)s.wo[c * 3 + k]; };
+    auto w2 = [&](int c, int ci, int k) { return (double)s.w42[(c * 8 + ci) * 3 + k]; };
+    for (int p = 0; p < 4; ++p)
+        for (int d = -1; d <= 1; ++d)
+            for (int c = 0; c < 8; ++c) {
+                const int tx = p + d, qx = floordiv(tx, 4);
+                dx[p][qx + 1][(tx - 4 * qx) * 8 + c] += wo(c, d + 1);
+                for (int e = -1; e <= 1; ++e)
+                    for (int ci = 0; ci < 8; ++ci) {
+                        const int th = p + d + e, qh = floordiv(th, 4);
+                        dh[p][qh + 1][(th - 4 * qh) * 8 + ci] += wo(c, d + 1) * w2(c, ci, e + 1);
+                    }
+            }
+    // every non-zero on a slot (fragments 0, 1: h; 2, 3: x)
+    for (int p = 0; p < 4; ++p)
+        for (int dq = -1; dq <= 1; ++dq)
+            for (int in = 0; in < 32; ++in)
+                for (int src = 0; src < 2; ++src) {
+                    if ((src ? dx : dh)[p][dq + 1][in] == 0.0) continue;
+                    bool found = false;
+                    for (int f = 2 * src; f < 2 * src + 2; ++f)
+                        for (int g = 0; g < 4; ++g) {
+                            const tp::Slot sl = tp::outc_slot(f, g);
+                            found = found || (sl.dq == dq && sl.oct == in / 8);
+                        }
+                    if (!found) return false;
+                }
+    for (int f = 0; f < tp::kOutcUnits; ++f)
+        for (int lane = 0; lane < 64; ++lane) {
+            const int row = lane & 15, g = lane >> 4;
+            const tp::Slot sl = tp::outc_slot(f, g);
+            const bool dup = f == 3 && g >= 2;  // (q, 2), (q, 3) of x are read by fragment 2
+            for (int e = 0; e < 8; ++e) {
+                double v = 0.0;
+                if (row < 4 && !dup) v = (f < 2 ? dh : dx)[row][sl.dq + 1][8 * sl.oct + e];
+                put_split(*wout, (((size_t)(tp::kOutcUnit0 + f) * 2) * 64 + lane) * 8 + e, (float)v, range_ok);
+            }
+        }
+    double bo = s.bo[0], kl = 0.0, kr = 0.0;
+    for (int c = 0; c < 8; ++c) {
+        for (int k = 0; k < 3; ++k) bo += wo(c, k) * s.b42[c];
+        kl += wo(c, 0) * s.b42[c];
+        kr += wo(c, 2) * s.b42[c];
+    }
+    for (int r = 0; r < 4; ++r) (*bout)[tp::kOutcBias + r] = (float)bo;
+    for (int ci = 0; ci < 8; ++ci) {
+        double vl = 0.0, vr = 0.0;
+        for (int c = 0; c < 8; ++c) {
+            vl += wo(c, 0) * w2(c, ci, 2);
+            vr += wo(c, 2) * w2(c, ci, 0);
+        }
+        (*bout)[tp::kOutcCorr + ci] = (float)vl;
+        (*bout)[tp::kOutcCorr + 8 + ci] = (float)vr;
+    }
+    (*bout)[tp::kOutcCorr + 16] = (float)kl;
+    (*bout)[tp::kOutcCorr + 17] = (float)kr;
     return true;
 }
 
