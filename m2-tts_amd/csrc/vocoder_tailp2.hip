@@ -21,6 +21,10 @@
 // 13 layer waves + 1 loader wave, one workgroup per CU (104 KB of rings).
 // Pipeline protocol, warm-up chunk, zero columns outside [0, L2), lean
 // epilogues and the identity-A residual MFMAs are those of vocoder_tailp.hip.
+// Default (NL = 6): ResBlock4's conv2 and output_conv composed into one layer
+// on one wave (outc2_role; the stage1 tail's outc_role at 16 channels): 11
+// layer waves + the loader, 92 KB of rings, one pipeline step fewer.
+// M2_TAILP2_SEVEN=1 keeps the seven-layer form.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -49,9 +53,13 @@ constexpr int kRingRows[7] = {48, 64, 64, 64, 64, 64, 48};
 constexpr int kRingOff(int n) { return n == 0 ? 0 : kRingOff(n - 1) + kRingRows[n - 1] * 256; }
 constexpr int kLoOff(int n) { return kRingRows[n] * 128; }
 constexpr int kPeriod(int n) { return kRingRows[n] / 16; }
-constexpr int LDS_BYTES = kRingOff(7);
-static_assert(LDS_BYTES <= 160 * 1024, "one workgroup per CU");
-constexpr int NWAVES = 14;  // layers 0-5: two waves each, output conv: one, loader: one
+static_assert(kRingOff(7) <= 160 * 1024, "one workgroup per CU");
+// NL = 7: layers 0-5 two waves each, output conv one, loader one (14 waves);
+// NL = 6: layers 0-4 two waves each, the composed layer one, loader one (12),
+// plus the composed layer's edge-term slot (8 floats) after the rings.
+constexpr int kCorrSlot = kRingOff(6);
+constexpr int lds_bytes(int nl) { return nl == 6 ? kCorrSlot + 32 : kRingOff(7); }
+constexpr int nwaves(int nl) { return nl == 6 ? 12 : 14; }
 
 __device__ __forceinline__ unsigned ring_at(int n, int row, int oct) {
     return kRingOff(n) + row * 128 + 16 * (oct ^ (row & 7));
@@ -70,7 +78,7 @@ __device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt
 __device__ __forceinline__ float tanh_fast(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
 
 constexpr int off_l(int l) { return l + 1; }
-constexpr int last_step(int nch) { return nch - 1 + off_l(6); }
+constexpr int last_step(int nch, int nl) { return nch - 1 + off_l(nl - 1); }
 
 template <int V>
 using ic = std::integral_constant<int, V>;
@@ -118,13 +126,27 @@ constexpr int frag_of(int l, int w, int m, int kb) { return (l == 3 && w == 1) ?
 constexpr Slot fslot(int l, int w, int f, int g) {
     return (l == 3 && w == 1) ? kslot(l, w, f / 2, f % 2, g) : kslot(l, w, 0, f, g);
 }
+// The composed ResBlock4-conv2 + output_conv layer (outc2_role): fragments
+// 0-3 on ring R5 (ResBlock4's intermediate h; the k5 taps of the 4 output
+// phases read the 16-channel units (q-1, 2), (q-1, 3), (q, 0..3), (q+1, 0),
+// (q+1, 1), two per fragment), 4-6 on ring R4 (ConvT4's output x; the output
+// conv's units).  Weight units after kUnits, its bias (rows 0-3) after the
+// seven layers' biases, then the edge terms vL[16], vR[16], kL, kR.
+constexpr int kOutcF = 7, kOutcUnit0 = kUnits, kOutcBias = kLayers * 64, kOutcCorr = kOutcBias + 64;
+constexpr int kBiasFloats = kOutcCorr + 64;
+constexpr Slot outc_hunit(int j) { return j < 2 ? Slot{-1, 2 + j} : (j < 6 ? Slot{0, j - 2} : Slot{1, j - 6}); }
+constexpr Slot outc_slot(int f, int g) {
+    if (f >= 4) return kslot(6, 0, 0, f - 4, g);
+    const Slot u = outc_hunit(2 * f + g / 2);
+    return Slot{u.dq, 2 * u.oct + (g & 1)};
+}
 
 // One wave: layer L, half W (m-blocks dmb(L, W, 0..NMB-1)).  As in
 // vocoder_tailp.hip's layer_role: weights and biases in VGPRs for the whole
 // strip, LDS addresses precomputed per ring phase (the step loop is unrolled by
 // the lcm of the ring periods), one fp32 accumulator per m-block for the three
 // split products, identity-A MFMAs for the ResBlock residual.
-template <int L, int W, int NCH>
+template <int L, int W, int NCH, int NL>
 __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
                                            const u32x4* __restrict__ W_, const float* __restrict__ bias,
                                            float* __restrict__ arow, int* rflag) {
@@ -171,7 +193,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
         for (int e = 0; e < 8; ++e) v[e] = (_Float16)(16 * m + li == 8 * g + e ? 1.f : 0.f);
         aid[m] = __builtin_bit_cast(u32x4, v);
     }
-    const int sL = qa + 6 - L;  // first column of chunk 0
+    const int sL = qa + NL - 1 - L;  // first column of chunk 0
     auto work = [&](int k, auto jc) {
         constexpr int kk = decltype(jc)::value;
         constexpr int ji = kk % PI, jx = kk % PX, jo = kk % PO;
@@ -205,7 +227,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
             for (int m = 0; m < NMB; ++m) acc[m] = mfma_h(aid[m], xl, acc[m]);
         }
         const int x0 = sL + 16 * k;
-        if constexpr (L == 6) {
+        if constexpr (L == NL - 1) {
             // rows 0..3 (lane group 0) = audio samples 4x .. 4x+3
             const int x = x0 + li;
             if (g == 0 && k >= 0 && x >= 0 && x < L2) {
@@ -234,6 +256,23 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                     for (int m = 0; m < NMB; ++m)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) v[m][r] = out ? 0.f : v[m][r];
+                    if constexpr (L == 4 && NL == 6) {
+                        // outc2_role's edge terms: wave 0's m-block 0 is phase 0
+                        // (h[:, 0] at column 0), wave 1's m-block 1 phase 3
+                        // (h[:, L4 - 1] at column L2 - 1); lane group g holds
+                        // channels 4g .. 4g + 3 and adds its products (group 0
+                        // also kL / kR) into slot 4W + g.  (Opaque pointer: the
+                        // constants load in this rare branch, not hoisted.)
+                        const float* cp = bias + kOutcCorr;
+                        asm volatile("" : "+s"(cp));
+                        if (W == 0 ? x == 0 : x == L2 - 1) {
+                            const float* cv = cp + 16 * W + 4 * g;
+                            float d = g == 0 ? cp[32 + W] : 0.f;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) d = fmaf(cv[r], v[W][r], d);
+                            *reinterpret_cast<float*>(lds + kCorrSlot + 4 * (4 * W + g)) = d;
+                        }
+                    }
                 }
 #pragma unroll
                 for (int m = 0; m < NMB; ++m) {
@@ -246,11 +285,14 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                     *reinterpret_cast<u32x4*>(lds + (oadr[jo] ^ mx)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
                 }
             };
-            if (edge && (x0 < 0 || x0 + 16 > L2)) epilogue(std::true_type{});  // wave-uniform
+            // (layer 4 of the six-layer form also takes it for a chunk that
+            // starts at column 0 or ends at L2: outc2_role's edge terms)
+            constexpr int EW = L == 4 && NL == 6 ? 1 : 0;
+            if (edge && (x0 < EW || x0 + 16 > L2 - EW)) epilogue(std::true_type{});  // wave-uniform
             else epilogue(std::false_type{});
         }
     };
-    constexpr int LAST = last_step(NCH);
+    constexpr int LAST = last_step(NCH, NL);
     auto step = [&](int s, auto jc) {
         if (s <= LAST) {
             const int k = s - off_l(L);
@@ -271,17 +313,100 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
     }
 }
 
+// ResBlock4 conv2 + output_conv composed (NL = 6; vocoder_tailp.hip's
+// outc_role at 16 channels): audio = tanh(Wc * h + Wo * x + bo') with
+// Wc = Wo o W2 a k5 conv on ResBlock4's intermediate h (ring R5) and Wo on
+// ConvT4's output x (ring R4, two columns ahead); 7 k-blocks = 21 MFMAs on one
+// wave, in place of ResBlock4 conv2 (two waves of 2 x 2 x 3 + 4) and the
+// output conv (9).  The utterance's two edge samples subtract the y the
+// reference pads with zeros (terms from layer 4, LDS slot kCorrSlot).
+template <int NCH>
+__device__ __forceinline__ void outc2_role(unsigned char* lds, int qa, int L2, bool edge,
+                                           const u32x4* __restrict__ W_, const float* __restrict__ bias,
+                                           float* __restrict__ arow, int* rflag) {
+    constexpr int L = 5, NL = 6, NF = kOutcF, P = 4;
+    static_assert(kRingRows[4] == 64 && kRingRows[5] == 64, "64-row rings");
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+    u32x4 a[NF][2];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        a[f][0] = W_[(kOutcUnit0 + f) * 128 + lane];
+        a[f][1] = W_[(kOutcUnit0 + f) * 128 + 64 + lane];
+    }
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = bias[kOutcBias + 4 * g + r];
+    // one VGPR per fragment: on a 64-row ring (8 KB planes) the address of
+    // ring phase j is (rbase + 2048 j) & 8191 past the ring (the swizzle reads
+    // row bits 0-2 only)
+    unsigned rbase[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        const Slot sl = outc_slot(f, g);
+        rbase[f] = f < 4 ? ring_at(5, ring_row(5, 0, li + sl.dq - 1), sl.oct) - kRingOff(5)
+                         : ring_at(4, ring_row(4, 0, li + sl.dq - 2), sl.oct) - kRingOff(4);
+    }
+    auto radr = [&](int f, int j) { return (f < 4 ? kRingOff(5) : kRingOff(4)) + ((rbase[f] + 2048u * j) & 8191u); };
+    auto work = [&](int k, auto jc) {
+        constexpr int j = decltype(jc)::value;
+        u32x4 bh[NF], bl[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            bh[f] = *reinterpret_cast<const u32x4*>(lds + radr(f, j));
+            bl[f] = *reinterpret_cast<const u32x4*>(lds + radr(f, j) + (f < 4 ? kLoOff(5) : kLoOff(4)));
+        }
+        f32x4 acc = f32x4{bv[0], bv[1], bv[2], bv[3]};
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int pr = 0; pr < 3; ++pr) acc = mfma_h(a[f][pr == 2], pr == 1 ? bl[f] : bh[f], acc);
+        const int x0 = qa + 16 * k, x = x0 + li;
+        float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+        if (edge && (x0 <= 0 || x0 + 16 >= L2)) {  // wave-uniform
+            const f32x4 e0 = *reinterpret_cast<const f32x4*>(lds + kCorrSlot);
+            const f32x4 e1 = *reinterpret_cast<const f32x4*>(lds + kCorrSlot + 16);
+            if (x == 0) v[0] -= (e0[0] + e0[1]) + (e0[2] + e0[3]);
+            if (x == L2 - 1) v[3] -= (e1[0] + e1[1]) + (e1[2] + e1[3]);
+        }
+        if (g == 0 && k >= 0 && x >= 0 && x < L2) {
+            float4 o;
+            o.x = tanh_fast(v[0]);
+            o.y = tanh_fast(v[1]);
+            o.z = tanh_fast(v[2]);
+            o.w = tanh_fast(v[3]);
+            *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
+            flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
+        }
+    };
+    constexpr int LAST = last_step(NCH, NL);
+    auto step = [&](int s, auto jc) {
+        if (s <= LAST) {
+            const int k = s - off_l(L);
+            if (k >= 0 && k < NCH) work(k, jc);  // chunk -1 feeds no later layer
+            step_barrier();
+        }
+    };
+    constexpr int J0 = ((-1 - off_l(L)) % P + P) % P;
+#pragma unroll 1
+    for (int s = -1; s <= LAST; s += P) {
+        step(s, ic<J0 % P>{});
+        step(s + 1, ic<(J0 + 1) % P>{});
+        step(s + 2, ic<(J0 + 2) % P>{});
+        step(s + 3, ic<(J0 + 3) % P>{});
+    }
+}
+
 // U2 rows (256 B: hi[64] lo[64]) into ring R0, two chunks ahead: chunk c =
 // columns [qa + 7 + 16c, +16), zero outside [0, L2).  Lane (r = lane >> 4, pc =
 // lane & 15) moves 16 B of columns r, r + 4, r + 8, r + 12 (pc < 8: hi octet pc,
 // else lo octet pc - 8); loads unconditional (clamped) so their waits are counted.
-template <int NCH, bool EDGE>
+template <int NCH, int NL, bool EDGE>
 __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, const unsigned char* __restrict__ u2) {
     const int lane = threadIdx.x & 63, r = lane >> 4, pc = lane & 15;
     auto fetch = [&](int c, u32x4 (&v)[4]) {
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-            int col = qa + 7 + 16 * c + r + 4 * h;
+            int col = qa + NL + 16 * c + r + 4 * h;
             if (EDGE) col = min(max(col, 0), L2 - 1);
             v[h] = *reinterpret_cast<const u32x4*>(u2 + (size_t)col * 256 + pc * 16);
         }
@@ -298,7 +423,7 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
         if (s < NCH) {
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-                const int col = qa + 7 + 16 * s + r + 4 * h;
+                const int col = qa + NL + 16 * s + r + 4 * h;
                 const bool in = !EDGE || (col >= 0 && col < L2);
                 const u32x4 z{0u, 0u, 0u, 0u};
                 *reinterpret_cast<u32x4*>(lds + wadr[j][h]) = in ? cur[h] : z;
@@ -310,20 +435,20 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     fetch(0, buf[1]);
     int s = -1;
 #pragma unroll 1
-    for (; s + 2 <= last_step(NCH); s += 3) {
+    for (; s + 2 <= last_step(NCH, NL); s += 3) {
         step(s, ic<2>{}, buf[0], buf[2]);
         step(s + 1, ic<0>{}, buf[1], buf[0]);
         step(s + 2, ic<1>{}, buf[2], buf[1]);
     }
 #pragma unroll 1
-    for (; s <= last_step(NCH); ++s) step_barrier();
+    for (; s <= last_step(NCH, NL); ++s) step_barrier();
 }
 
-template <int NCH>
-__global__ __launch_bounds__(NWAVES * 64, 1) void tailp2_kernel(const unsigned char* __restrict__ U2, int L2,
-                                                                 const u32x4* __restrict__ W,
-                                                                 const float* __restrict__ bias,
-                                                                 float* __restrict__ audio, int* rflag) {
+template <int NCH, int NL>
+__global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsigned char* __restrict__ U2, int L2,
+                                                                     const u32x4* __restrict__ W,
+                                                                     const float* __restrict__ bias,
+                                                                     float* __restrict__ audio, int* rflag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -333,40 +458,69 @@ __global__ __launch_bounds__(NWAVES * 64, 1) void tailp2_kernel(const unsigned c
     if (w >= 10) __builtin_amdgcn_s_setprio(3);
     else if (w >= 6) __builtin_amdgcn_s_setprio(2);
     else if (w >= 2) __builtin_amdgcn_s_setprio(1);
+    const unsigned char* u2 = U2 + (size_t)b * L2 * 256;
     switch (w) {
-        case 0: layer_role<0, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 1: layer_role<0, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 2: layer_role<1, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 3: layer_role<1, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 4: layer_role<2, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 5: layer_role<2, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 6: layer_role<3, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 7: layer_role<3, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 8: layer_role<4, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 9: layer_role<4, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 10: layer_role<5, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 11: layer_role<5, 1, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 12: layer_role<6, 0, NCH>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 0: layer_role<0, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 1: layer_role<0, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 2: layer_role<1, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 3: layer_role<1, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 4: layer_role<2, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 5: layer_role<2, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 6: layer_role<3, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 7: layer_role<3, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 8: layer_role<4, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 9: layer_role<4, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 10:
+            if constexpr (NL == 7) layer_role<5, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
+            else outc2_role<NCH>(lds, qa, L2, edge, W, bias, arow, rflag);
+            break;
+        case 11:
+            if constexpr (NL == 7) {
+                layer_role<5, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
+                break;
+            }
+            [[fallthrough]];
+        case 12:
+            if constexpr (NL == 7) {
+                if (w == 12) {
+                    layer_role<6, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
+                    break;
+                }
+            }
+            [[fallthrough]];
         default:
-            if (edge) loader_role<NCH, true>(lds, qa, L2, U2 + (size_t)b * L2 * 256);
-            else loader_role<NCH, false>(lds, qa, L2, U2 + (size_t)b * L2 * 256);
+            if (edge) loader_role<NCH, NL, true>(lds, qa, L2, u2);
+            else loader_role<NCH, NL, false>(lds, qa, L2, u2);
             break;
     }
 }
 
-template <int NCH>
+template <int NCH, int NL>
 int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
                hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp2_kernel<NCH>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp2_kernel<NCH, NL>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes(NL)));
         attr = true;
     }
-    hipLaunchKernelGGL((tailp2_kernel<NCH>), dim3(cdiv(L2, 16 * NCH), B), dim3(NWAVES * 64), LDS_BYTES, st,
-                       static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
+    hipLaunchKernelGGL((tailp2_kernel<NCH, NL>), dim3(cdiv(L2, 16 * NCH), B), dim3(nwaves(NL) * 64), lds_bytes(NL),
+                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
     M2_LAUNCHED("tailp2_kernel");
     return M2_OK;
+}
+
+template <int NL>
+int32_t launch_nl(int nch, const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
+                  int* rflag, hipStream_t st) {
+    switch (nch) {
+        case 8: return launch<8, NL>(U2, L2, B, W, bias, audio, rflag, st);
+        case 16: return launch<16, NL>(U2, L2, B, W, bias, audio, rflag, st);
+        case 32: return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st);
+        case 64: return launch<64, NL>(U2, L2, B, W, bias, audio, rflag, st);
+        case 128: return launch<128, NL>(U2, L2, B, W, bias, audio, rflag, st);
+        default: return launch<192, NL>(U2, L2, B, W, bias, audio, rflag, st);
+    }
 }
 
 }  // namespace tp2
@@ -377,8 +531,11 @@ const char* const kVocTailp2KernelName =
 int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                               int* rflag, hipStream_t st) {
     if (B == 0 || L2 == 0) return M2_OK;
-    // Strip length: the instantiated NCH minimising rounds x (NCH + 7 pipeline
-    // steps) at one workgroup per CU.  M2_TAILP2_NCH forces one.
+    // Strip length: the instantiated NCH minimising rounds x (NCH + NL pipeline
+    // steps) at one workgroup per CU.  M2_TAILP2_NCH forces one;
+    // M2_TAILP2_SEVEN=1 the seven-layer form (read per call: A/B and tests).
+    const bool seven = std::getenv("M2_TAILP2_SEVEN") != nullptr;
+    const int nl = seven ? 7 : 6;
     static constexpr int kN[] = {8, 16, 32, 64, 128, 192};
     static const int forced = [] {
         const char* e = std::getenv("M2_TAILP2_NCH");
@@ -392,18 +549,12 @@ int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, 
         const long chunks = cdiv(L2, 16);
         long best = -1;
         for (int n : kN) {
-            const long wgs = (long)cdiv((int)chunks, n) * B, rounds = (wgs + 255) / 256, cost = rounds * (n + 7);
+            const long wgs = (long)cdiv((int)chunks, n) * B, rounds = (wgs + 255) / 256, cost = rounds * (n + nl);
             if (best < 0 || cost < best) best = cost, nch = n;
         }
     }
-    switch (nch) {
-        case 8: return tp2::launch<8>(U2, L2, B, W, bias, audio, rflag, st);
-        case 16: return tp2::launch<16>(U2, L2, B, W, bias, audio, rflag, st);
-        case 32: return tp2::launch<32>(U2, L2, B, W, bias, audio, rflag, st);
-        case 64: return tp2::launch<64>(U2, L2, B, W, bias, audio, rflag, st);
-        case 128: return tp2::launch<128>(U2, L2, B, W, bias, audio, rflag, st);
-        default: return tp2::launch<192>(U2, L2, B, W, bias, audio, rflag, st);
-    }
+    return seven ? tp2::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st)
+                 : tp2::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -459,6 +610,8 @@ void put_split(std::vector<uint16_t>& out, size_t idx, float v, bool* range_ok) 
 
 }  // namespace
 
+bool pack_outc2(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok);
+
 bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
     using namespace tp2;
     Dense64 d[kLayers];
@@ -489,7 +642,7 @@ bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<flo
                             if (!found) return false;
                         }
                 }
-    wout->assign((size_t)kUnits * 2 * 64 * 8, 0);
+    wout->assign((size_t)(kUnits + kOutcF) * 2 * 64 * 8, 0);
     for (int l = 0; l < kLayers; ++l)
         for (int w = 0; w < nwv(l); ++w)
             for (int m = 0; m < nmbw(l); ++m)
@@ -511,7 +664,7 @@ bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<flo
                     }
                 }
     // biases in MFMA row order: [layer][wave][m-block][16 rows]
-    bout->assign(kLayers * 64, 0.f);
+    bout->assign(kBiasFloats, 0.f);
     const float* bsrc[kLayers] = {s.bt3, s.b31, s.b32, s.bt4, s.b41, s.b42, s.bo};
     const int cper[kLayers] = {32, 32, 32, 16, 16, 16, 1};
     for (int l = 0; l < kLayers; ++l)
@@ -521,6 +674,73 @@ bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<flo
                     const int row = 16 * dmb(l, w, m) + rr;
                     if (row < nrows[l]) (*bout)[l * 64 + (nmbw(l) * w + m) * 16 + rr] = bsrc[l][row % cper[l]];
                 }
+    return pack_outc2(s, wout, bout, range_ok);
+}
+
+// The composed layer (outc2_role), in double: audio[t] = tanh(bo' + sum_d
+// Wo[c][d] x[c][t+d] + sum_j Wc[c'][j] h[c'][t+j]), Wc[c'][j] = sum_{d+e=j}
+// sum_c Wo[c][d] W2[c][c'][e], bo' = bo + sum_d sum_c Wo[c][d] b2[c]; rows =
+// the 4 output phases, input row p2 * 16 + c at column q + dq.  Edge terms as
+// in vocoder_tailp.hip's pack_outc.
+bool pack_outc2(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
+    using namespace tp2;
+    constexpr int C = 16;
+    std::vector<double> dh(4 * 3 * 64, 0.0), dx(4 * 3 * 64, 0.0);
+    auto at = [](std::vector<double>& d, int p, int dq, int in) -> double& { return d[(p * 3 + dq + 1) * 64 + in]; };
+    auto wo = [&](int c, int k) { return (double)s.wo[c * 3 + k]; };
+    auto w2 = [&](int c, int ci, int k) { return (double)s.w42[(c * C + ci) * 3 + k]; };
+    for (int p = 0; p < 4; ++p)
+        for (int d = -1; d <= 1; ++d)
+            for (int c = 0; c < C; ++c) {
+                const int tx = p + d, qx = floordiv2(tx, 4);
+                at(dx, p, qx, (tx - 4 * qx) * C + c) += wo(c, d + 1);
+                for (int e = -1; e <= 1; ++e)
+                    for (int ci = 0; ci < C; ++ci) {
+                        const int th = p + d + e, qh = floordiv2(th, 4);
+                        at(dh, p, qh, (th - 4 * qh) * C + ci) += wo(c, d + 1) * w2(c, ci, e + 1);
+                    }
+            }
+    for (int p = 0; p < 4; ++p)
+        for (int dq = -1; dq <= 1; ++dq)
+            for (int in = 0; in < 64; ++in)
+                for (int src = 0; src < 2; ++src) {
+                    if (at(src ? dx : dh, p, dq, in) == 0.0) continue;
+                    bool found = false;
+                    for (int f = src ? 4 : 0; f < (src ? kOutcF : 4); ++f)
+                        for (int g = 0; g < 4; ++g) {
+                            const Slot sl = outc_slot(f, g);
+                            found = found || (sl.dq == dq && sl.oct == in / 8);
+                        }
+                    if (!found) return false;
+                }
+    for (int f = 0; f < kOutcF; ++f)
+        for (int lane = 0; lane < 64; ++lane) {
+            const int row = lane & 15, g = lane >> 4;
+            const Slot sl = outc_slot(f, g);
+            for (int e = 0; e < 8; ++e) {
+                double v = 0.0;
+                if (row < 4) v = at(f < 4 ? dh : dx, row, sl.dq, 8 * sl.oct + e);
+                put_split(*wout, (((size_t)(kOutcUnit0 + f) * 2) * 64 + lane) * 8 + e, (float)v, range_ok);
+            }
+        }
+    double bo = s.bo[0], kl = 0.0, kr = 0.0;
+    for (int c = 0; c < C; ++c) {
+        for (int k = 0; k < 3; ++k) bo += wo(c, k) * s.b42[c];
+        kl += wo(c, 0) * s.b42[c];
+        kr += wo(c, 2) * s.b42[c];
+    }
+    for (int r = 0; r < 4; ++r) (*bout)[kOutcBias + r] = (float)bo;
+    for (int ci = 0; ci < C; ++ci) {
+        double vl = 0.0, vr = 0.0;
+        for (int c = 0; c < C; ++c) {
+            vl += wo(c, 0) * w2(c, ci, 2);
+            vr += wo(c, 2) * w2(c, ci, 0);
+        }
+        (*bout)[kOutcCorr + ci] = (float)vl;
+        (*bout)[kOutcCorr + 16 + ci] = (float)vr;
+    }
+    (*bout)[kOutcCorr + 32] = (float)kl;
+    (*bout)[kOutcCorr + 33] = (float)kr;
     return true;
 }
 

@@ -53,3 +53,27 @@ def test_tailp2_vs_x3_tail(gpu, monkeypatch, B, T):
     ref = mx.vocoder(mel.to(gpu))
     assert torch.isfinite(out).all()
     assert float((out - ref).abs().max()) <= 2e-6
+
+
+@pytest.mark.parametrize("B,T", [(3, 1), (2, 2), (3, 61)])
+def test_tailp2_outc_edges_vs_oracle(gpu, B, T):
+    """The composed ResBlock4-conv2 + output_conv layer (the default six-layer
+    form) corrects the two utterance-edge samples for the reference's zero
+    padding of the resblock output."""
+    m = build_model(gpu)
+    mel = torch.randn(B, stage_config("s2").mel_channels, T, generator=torch.Generator().manual_seed(300 + T))
+    out = m.vocoder(mel.to(gpu)).cpu()
+    ref = orc.vocoder(golden_state("s2"), mel)
+    assert maxabs(out[..., :4], ref[..., :4]) <= 1e-5 and maxabs(out[..., -4:], ref[..., -4:]) <= 1e-5
+    assert rms(out, ref) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("B,T", [(8, 500), (16, 2600), (5, 333)])
+def test_tailp2_outc_vs_seven_layers(gpu, monkeypatch, B, T):
+    mel = torch.randn(B, stage_config("s2").mel_channels, T, generator=torch.Generator().manual_seed(B + T))
+    m = build_model(gpu)
+    out = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_TAILP2_SEVEN", "1")
+    ref = m.vocoder(mel.to(gpu))
+    assert torch.isfinite(out).all()
+    assert float((out - ref).abs().max()) <= 2e-6
