@@ -697,6 +697,31 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 xp.push_back(pack_x3_conv3(w2.data(), c2, c2, c2, &ok, true));
                 xs.push_back(&m->vx.w2[k]);
             }
+            // stage1 head: input_conv composed into ConvT1 (fp32 bias / edge
+            // tables ride in the same buffer as u16 pairs)
+            const vx_u32x4* hcb_at = nullptr;
+            const vx_u32x4* hce_at = nullptr;
+            if (M == 64 && C == 128) {
+                std::vector<uint16_t> hw;
+                std::vector<float> hb, he;
+                const auto bi = fetch("vocoder.input_conv.bias"), wt0 = fetch("vocoder.upsamples.0.weight"),
+                           bt0 = fetch("vocoder.upsamples.0.bias");
+                bool hok = true;
+                if (pack_x3_head_comp(wi.data(), bi.data(), wt0.data(), bt0.data(), M, vocoder_x3_mel_pad(M), C, &hw,
+                                      &hb, &he, &hok) && hok) {
+                    auto as_u16 = [](const std::vector<float>& f) {
+                        std::vector<uint16_t> u(f.size() * 2);
+                        std::memcpy(u.data(), f.data(), f.size() * sizeof(float));
+                        return u;
+                    };
+                    xp.push_back(std::move(hw));
+                    xs.push_back(&m->vx.hc);
+                    xp.push_back(as_u16(hb));
+                    xs.push_back(&hcb_at);
+                    xp.push_back(as_u16(he));
+                    xs.push_back(&hce_at);
+                }
+            }
             if (ok) {
                 size_t xt = 0;
                 std::vector<size_t> xo;
@@ -710,6 +735,8 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 if (e != hipSuccess) { (void)hipFree(m->vbuf); (void)hipFree(m->xbuf); return bail(e, "upload x3 pack"); }
                 for (size_t i = 0; i < xp.size(); ++i)
                     *xs[i] = reinterpret_cast<const vx_u32x4*>(static_cast<uint16_t*>(m->xbuf) + xo[i]);
+                m->vx.hcb = reinterpret_cast<const float*>(hcb_at);
+                m->vx.hce = reinterpret_cast<const float*>(hce_at);
                 m->vx.bi = m->vw.bi;
                 for (int k = 0; k < 4; ++k) {
                     m->vx.bt[k] = m->vw.bt[k];

@@ -106,6 +106,12 @@ struct VocX {
     // pipelined stage2 tail (vocoder_tailp2.hip); null = the x3 tail kernel
     const vx_u32x4* tp2;
     const float* tp2b;
+    // stage1 head with input_conv composed into ConvT1 (vocoder_x3.hip,
+    // head_convT1c_planar): weights, per-phase bias, edge tables; null = the
+    // two layers
+    const vx_u32x4* hc;
+    const float* hcb;
+    const float* hce;
     // set to 1 (vector store) by the last kernel when an audio sample is not
     // finite; host-mapped (m2_model_check)
     int* rflag;
@@ -214,5 +220,8 @@ int32_t launch_vocoder_x3(const float* mel, bool trans, int M, int C, int B, int
 constexpr bool res_fold_channels(int C) { return C == 8 || C == 16; }
 std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPad, bool* range_ok, bool res);
 std::vector<uint16_t> pack_x3_convT(const float* W, int Cin, int Cout, int R, bool* range_ok);
+// input_conv o ConvT1 (R = 4) for the stage1 head; false when the shapes do not fit
+bool pack_x3_head_comp(const float* Win, const float* bin, const float* WT, const float* bT, int M, int MP, int C,
+                       std::vector<uint16_t>* w, std::vector<float>* bias, std::vector<float>* edge, bool* range_ok);
 
 }  // namespace m2

@@ -480,6 +480,72 @@ __device__ __forceinline__ void head_convT1_planar(const u32x4* __restrict__ Wp,
     }
 }
 
+// input_conv composed into ConvT1 (stage1 head, round 2): the input conv
+// (k3, no activation) feeds only ConvT1, which is linear before its leaky, so
+// u = leaky(Wc * mel + bc[ph]) with Wc[ph] = W_T[ph] o W_in a 4-tap transposed
+// conv straight from the mel window (output phase ph at input column q reads
+// mel frames q + d0 + 1 - k, k = 0..3, d0 = 0 for ph < 2 else 1): K = 4 x 64
+// mel channels, the same 8 k-blocks as ConvT1's 2 x 128, and no input-conv
+// layer (its MFMAs, barrier and LDS round trip) at all.  The reference's
+// ConvT1 sees zeros at input frames -1 and T, where the composed form sees
+// the input conv of the zero-padded mel (b_in + W_in[.,.,2] mel[0] /
+// b_in + W_in[.,.,0] mel[T-1]); outputs t = 0, 1 and 4T - 2, 4T - 1 subtract
+// that term: E[ph][co][m] . mel[edge] + e[ph][co] (hce: [4][C1][MP] then
+// [4][C1], fp32; phases 0, 1 left edge, 2, 3 right edge), computed by the
+// lanes that hold those outputs, in a wave-uniform branch only the two edge
+// windows of an utterance take.  Bias bc: [4][C1] (it depends on the phase).
+template <int MP, int COUT, int RSM, int RSO>
+__device__ __forceinline__ void head_convT1c_planar(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
+                                                    const float* __restrict__ hce, XW mel, unsigned char* u, int f0,
+                                                    int T, APipe* ap, const u32x4* wp_next) {
+    constexpr int MB = COUT / 16, NKB = nkb_of<MP, 4>(), NT = 4;
+    static_assert(NKB == 8 && pd_of<MP, 4, 1>() == 4, "the ConvT1 weight pipeline shape");
+    const int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ph = item / MB, mb = item - ph * MB;
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4, co0 = mb * 16 + 4 * g;
+    const int qs = qs_u(ph, f0), d0 = ph < 2 ? 0 : 1;  // taps: mel frames q + d0 + 1 - k
+    const u32x4* wp = Wp + (size_t)(ph * MB + mb) * NKB * 128 + lane;
+    const unsigned char* bp = mel.p + (qs + li + d0 + 1 - mel.start) * RSM;
+    f32x4 acc[1][NT];
+    f32x4 bv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = bias[ph * COUT + co0 + r];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[0][n] = bv;
+    mma_x3<MP, 4, -1, RSM, NT, false, 1, NKB * 128, true>(wp, bp, nullptr, acc, *ap, wp_next);
+    const int L = 4 * T, qe = ph < 2 ? 0 : T - 1;  // the input column of this phase's edge outputs
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int q = qs + 16 * n + li, t = 4 * q + ph;
+        if (qe >= qs + 16 * n && qe < qs + 16 * n + 16) {  // wave-uniform: this tile holds an edge output
+            if (q == qe) {
+                // opaque pointer: the table loads stay in this rare branch
+                const float* ep = hce;
+                asm volatile("" : "+s"(ep));
+                const unsigned char* mrow = mel.p + (qe - mel.start) * RSM;  // mel[0] / mel[T - 1]
+                float c[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) c[r] = ep[4 * COUT * MP + ph * COUT + co0 + r];
+#pragma unroll 1
+                for (int o = 0; o < MP / 8; ++o) {
+                    const h8 hi = *reinterpret_cast<const h8*>(mrow + 16 * o);
+                    const h8 lo = *reinterpret_cast<const h8*>(mrow + 2 * MP + 16 * o);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float x = (float)hi[e] + (float)lo[e];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) c[r] = fmaf(ep[(ph * COUT + co0 + r) * MP + 8 * o + e], x, c[r]);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[0][n][r] -= c[r];
+            }
+        }
+        store_row<COUT, ACT_LEAKY, false, false>(acc[0][n], u + (ph * kPlane + 16 * n + li) * RSO, nullptr, co0,
+                                                 t < 0 || t >= L, true, nullptr, t);
+    }
+}
+
 // ResBlock1 conv (k3, pad 1) between planes: input planes start at qsi(p),
 // output plane p covers q in [qso(p), +64).  CONV2: + x from the u planes,
 // stored straight to U1 (t < L and q < f0 + tf only); else leaky into the
@@ -754,7 +820,9 @@ constexpr bool head_planar() {
     return X3_PLANAR && Cfg::TF + 1 <= 64 && 4 * (Cfg::C / 2 / 16) == Cfg::HW && Cfg::G_T1 == 1 && Cfg::G_R1 == 1;
 }
 
-template <class Cfg, bool TRANS>
+// COMP (stage1 planar head): input_conv composed into ConvT1
+// (head_convT1c_planar; w.hc / w.hcb / w.hce).
+template <class Cfg, bool TRANS, bool COMP = false>
 __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const float* __restrict__ mel, int T,
                                                                             VocX w, unsigned char* __restrict__ U1) {
     constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
@@ -779,7 +847,47 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     // input columns, one item per wave = (phase, m-block)
     constexpr bool PLANAR = ONE && head_planar<Cfg>();
     XSTAMP(0, 0);
-    if constexpr (ONE) {
+    if constexpr (COMP) {
+        static_assert(PLANAR, "the composed head runs on the phase-planar path");
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        constexpr int MB1 = C1 / 16;
+        APipe ap;
+        const u32x4* wp0 = w.hc + (size_t)wv * nkb_of<MP, 4>() * 128 + (threadIdx.x & 63);
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            ap[kb][0][0] = wp0[kb * 128];
+            ap[kb][0][1] = wp0[kb * 128 + 64];
+        }
+        // the mel window goes to region A (the u planes it feeds are written
+        // into region B in the same phase; the h planes overwrite it later)
+        static_assert(Pl::CAP_MEL * Pl::RS_M <= Pl::RA, "mel window in region A");
+        const XW melA{lds, f0 - 3};
+        gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melA);
+        XSTAMP(0, 1);
+        __syncthreads();
+        XSTAMP(0, 2);
+        XSTAMP(0, 3);  // (no input-conv layer)
+        XSTAMP(0, 4);
+        unsigned char* up = lds + Pl::RA;
+        unsigned char* hp = lds;
+        head_convT1c_planar<MP, C1, Pl::RS_M, Pl::RS_1>(
+            w.hc, w.hcb, w.hce, melA, up, f0, T, &ap,
+            w.w1[0] + (size_t)(wv % MB1) * nkb_of<C1, 3>() * 128 + (threadIdx.x & 63));
+        XSTAMP(0, 5);
+        __syncthreads();
+        XSTAMP(0, 6);
+        head_rb1_planar<C1, Pl::RS_1, false>(w.w1[0], w.b1[0], up, hp, nullptr, f0, TF, 4 * T, &ap,
+                                             w.w2[0] + (size_t)(wv % MB1) * nkb_of<C1, 3>() * 128 +
+                                                 (threadIdx.x & 63),
+                                             nullptr);
+        XSTAMP(0, 7);
+        __syncthreads();
+        XSTAMP(0, 8);
+        head_rb1_planar<C1, Pl::RS_1, true>(w.w2[0], w.b2[0], hp, nullptr, up, f0, TF, 4 * T, &ap, nullptr,
+                                            U1 + (size_t)b * 4 * T * 4 * C1);
+        XSTAMP(0, 9);
+        return;
+    } else if constexpr (ONE) {
         const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         APipe ap;
         const u32x4* wp0 = I0::wp(w.wi, wv);
@@ -1009,6 +1117,10 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         int32_t rc;
         if ((rc = set_lds(x3_head_kernel<Cfg, false>, HP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_head_kernel<Cfg, true>, HP::LDS_BYTES))) return rc;
+        if constexpr (head_planar<Cfg>()) {
+            if ((rc = set_lds(x3_head_kernel<Cfg, false, true>, HP::LDS_BYTES))) return rc;
+            if ((rc = set_lds(x3_head_kernel<Cfg, true, true>, HP::LDS_BYTES))) return rc;
+        }
         if ((rc = set_lds(x3_mid_kernel<Cfg>, MP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_tail_kernel<Cfg>, TP::LDS_BYTES))) return rc;
         if constexpr (S2) {
@@ -1033,12 +1145,22 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     auto* u1 = static_cast<unsigned char*>(U1);
     auto* u2 = static_cast<unsigned char*>(U2);
     mark(0, true);
-    if (trans)
-        hipLaunchKernelGGL((x3_head_kernel<Cfg, true>), dim3(cdiv(T, Cfg::TF), B), dim3(Cfg::HW * 64), HP::LDS_BYTES, st,
-                           mel, T, w, u1);
-    else
-        hipLaunchKernelGGL((x3_head_kernel<Cfg, false>), dim3(cdiv(T, Cfg::TF), B), dim3(Cfg::HW * 64), HP::LDS_BYTES, st,
-                           mel, T, w, u1);
+    // M2_HEAD_COMP=1: the composed input_conv o ConvT1 head (stage1; opt-in:
+    // 14.5 % fewer cycles per workgroup by phase stamps but no shorter kernel
+    // on the box, profiles/ab/r02l_head_comp.txt; read per call)
+    bool comp = false;
+    if constexpr (head_planar<Cfg>()) comp = w.hc && std::getenv("M2_HEAD_COMP");
+    const dim3 hg(cdiv(T, Cfg::TF), B), hb(Cfg::HW * 64);
+    if constexpr (head_planar<Cfg>()) {
+        if (comp && trans)
+            hipLaunchKernelGGL((x3_head_kernel<Cfg, true, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
+        else if (comp)
+            hipLaunchKernelGGL((x3_head_kernel<Cfg, false, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
+    }
+    if (!comp && trans)
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
+    else if (!comp)
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, false>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
     mark(0, false);
     M2_LAUNCHED("x3_head_kernel");
     mark(1, true);
@@ -1156,6 +1278,59 @@ std::vector<uint16_t> pack_x3_conv3(const float* W, int Cout, int Cin, int CinPa
         }
     }
     return out;
+}
+
+// input_conv o ConvT1 for the composed stage1 head (head_convT1c_planar), in
+// double: Wc(ph, co, m, k) = sum_{j = 0, 1; tin = j + 2 - k in [0, 2]} sum_ci
+// W_T[ci][co][kj(ph)] W_in[ci][m][tin] (ConvT tap j: input frame q + d0 - j,
+// kernel index kj; input-conv tap tin: mel frame i - 1 + tin); bc[ph][co] =
+// b_T[co] + sum_j sum_ci W_T[ci][co][kj] b_in[ci]; edge tables E[ph][co][m] =
+// sum_ci W_T[ci][co][k_edge] W_in[ci][m][2 (ph < 2) | 0], e[ph][co] = sum_ci
+// W_T[ci][co][k_edge] b_in[ci], k_edge = k1 (frame -1) for ph < 2, k0 (frame T).
+bool pack_x3_head_comp(const float* Win, const float* bin, const float* WT, const float* bT, int M, int MP, int C,
+                       std::vector<uint16_t>* w, std::vector<float>* bias, std::vector<float>* edge, bool* range_ok) {
+    const int C1 = C / 2, R = 4, P = R / 2;
+    if (MP % 8 || MP < M) return false;
+    auto kj = [&](int ph, int j) {
+        const int k0 = (ph + P < R) ? ph + P : ph + P - R, k1 = (ph + P < R) ? ph + P + R : ph + P;
+        return j ? k1 : k0;
+    };
+    auto wt = [&](int ci, int co, int k) { return (double)WT[((size_t)ci * C1 + co) * 2 * R + k]; };
+    auto wi = [&](int ci, int m, int k) { return m < M ? (double)Win[((size_t)ci * M + m) * 3 + k] : 0.0; };
+    std::vector<double> wc((size_t)R * C1 * MP * 4, 0.0);  // [ph][co][m][k]
+    for (int ph = 0; ph < R; ++ph)
+        for (int co = 0; co < C1; ++co)
+            for (int j = 0; j < 2; ++j) {
+                const int k = kj(ph, j);
+                for (int ci = 0; ci < C; ++ci) {
+                    const double a = wt(ci, co, k);
+                    for (int tin = 0; tin < 3; ++tin) {
+                        const int kk = j + 2 - tin;  // composed tap: mel frame q + d0 + 1 - kk
+                        for (int m = 0; m < M; ++m) wc[(((size_t)ph * C1 + co) * MP + m) * 4 + kk] += a * wi(ci, m, tin);
+                    }
+                }
+            }
+    *w = pack_x3(R, C1, MP, 4, [&](int ph, int co, int m, int k) { return (float)wc[(((size_t)ph * C1 + co) * MP + m) * 4 + k]; },
+                 range_ok);
+    bias->assign((size_t)R * C1, 0.f);
+    edge->assign((size_t)R * C1 * MP + (size_t)R * C1, 0.f);
+    for (int ph = 0; ph < R; ++ph)
+        for (int co = 0; co < C1; ++co) {
+            double b = bT[co];
+            for (int j = 0; j < 2; ++j)
+                for (int ci = 0; ci < C; ++ci) b += wt(ci, co, kj(ph, j)) * bin[ci];
+            (*bias)[(size_t)ph * C1 + co] = (float)b;
+            const int ke = kj(ph, ph < 2 ? 1 : 0), tin = ph < 2 ? 2 : 0;
+            double e = 0.0;
+            for (int ci = 0; ci < C; ++ci) e += wt(ci, co, ke) * bin[ci];
+            (*edge)[(size_t)R * C1 * MP + (size_t)ph * C1 + co] = (float)e;
+            for (int m = 0; m < M; ++m) {
+                double v = 0.0;
+                for (int ci = 0; ci < C; ++ci) v += wt(ci, co, ke) * wi(ci, m, tin);
+                (*edge)[((size_t)ph * C1 + co) * MP + m] = (float)v;
+            }
+        }
+    return true;
 }
 
 std::vector<uint16_t> pack_x3_convT(const float* W, int Cin, int Cout, int R, bool* range_ok) {

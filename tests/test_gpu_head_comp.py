@@ -1,0 +1,60 @@
+"""GPU: the stage1 vocoder head with input_conv composed into ConvT1
+(vocoder_x3.hip, head_convT1c_planar: a 4-tap transposed conv straight from
+the mel, with the outputs at t = 0, 1, 4T-2, 4T-1 corrected for the zeros the
+reference's ConvT1 sees at input frames -1 and T) against the CPU oracle (the
+reference's SimpleVocoder.forward, tts_model.py:279-297) and against the
+two-layer head (the default), over lengths that put the utterance edges in
+every window position, both mel layouts.  The composed head is opt-in
+(M2_HEAD_COMP=1): it measured no faster (vocoder head).
+"""
+import pytest
+import torch
+
+import m2tts_oracle as orc
+from conftest import AUDIO_RMS_TOL, golden_state, maxabs, rms, stage_config
+
+pytestmark = pytest.mark.gpu
+
+
+def build_model(dev):
+    from models.tts_model import M2TTSModel
+    m = M2TTSModel(**stage_config("s1").as_dict())
+    m.load_state_dict(golden_state("s1"))
+    return m.to(dev).eval()
+
+
+@pytest.mark.parametrize("B,T", [(3, 1), (2, 2), (2, 5), (3, 63), (2, 64), (1, 127), (2, 137)])
+def test_head_comp_vs_oracle(gpu, monkeypatch, B, T):
+    monkeypatch.setenv("M2_HEAD_COMP", "1")
+    m = build_model(gpu)
+    mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(400 + T))
+    out = m.vocoder(mel.to(gpu)).cpu()
+    ref = orc.vocoder(golden_state("s1"), mel)
+    assert out.shape == ref.shape
+    assert rms(out, ref) <= AUDIO_RMS_TOL and maxabs(out, ref) <= 1e-4
+    # the samples the corrected head outputs feed (t = 0, 1 and 4T - 2, 4T - 1 at 16x)
+    assert maxabs(out[..., :48], ref[..., :48]) <= 1e-5 and maxabs(out[..., -48:], ref[..., -48:]) <= 1e-5
+
+
+@pytest.mark.parametrize("B,T", [(32, 500), (5, 333), (2, 2600), (4, 1)])
+def test_head_comp_vs_two_layers(gpu, monkeypatch, B, T):
+    """The composed layer reorders fp32 sums of the same products (and the
+    composed weights are rounded once): agreement well inside the bound."""
+    mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(B * T + 1))
+    m = build_model(gpu)
+    ref = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_HEAD_COMP", "1")
+    out = m.vocoder(mel.to(gpu))
+    assert torch.isfinite(out).all()
+    assert float((out - ref).abs().max()) <= 2e-5 and rms(out.cpu(), ref.cpu()) <= 2e-6
+
+
+def test_head_comp_btm_layout(gpu, monkeypatch):
+    """The decoder hands the vocoder [B, T, M] mel (read transposed in place)."""
+    monkeypatch.setenv("M2_HEAD_COMP", "1")
+    m = build_model(gpu)
+    mel = torch.randn(3, stage_config("s1").mel_channels, 70, generator=torch.Generator().manual_seed(9))
+    a = m.vocoder(mel.to(gpu))
+    hm = m._hip(gpu)
+    b = hm.vocoder(mel.transpose(1, 2).contiguous().to(gpu), layout_btm=True)
+    assert torch.equal(a, b)
