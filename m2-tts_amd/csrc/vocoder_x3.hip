@@ -806,9 +806,23 @@ __device__ unsigned long long g_x3_stamps[3][4096][16][16];
         const int _wg = blockIdx.y * gridDim.x + blockIdx.x;                                             \
         if ((threadIdx.x & 63) == 0 && _wg < 4096) g_x3_stamps[K][_wg][threadIdx.x >> 6][i] = _t;        \
     } while (0)
+// s_memrealtime (100 MHz) into slot i: with an s_memtime pair of the same
+// wave it gives the shader clock over that interval (tools/probe/stamps.py)
+#define XSTAMP_RT(K, i)                                                                                  \
+    do {                                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        unsigned long long _t;                                                                           \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                  \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        const int _wg = blockIdx.y * gridDim.x + blockIdx.x;                                             \
+        if ((threadIdx.x & 63) == 0 && _wg < 4096) g_x3_stamps[K][_wg][threadIdx.x >> 6][i] = _t;        \
+    } while (0)
 #else
 #define XSTAMP(K, i) \
     do {             \
+    } while (0)
+#define XSTAMP_RT(K, i) \
+    do {                \
     } while (0)
 #endif
 
@@ -846,6 +860,7 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     // phase-planar ConvT1 / ResBlock1: planes of 64 rows hold TF + 2 <= 65
     // input columns, one item per wave = (phase, m-block)
     constexpr bool PLANAR = ONE && head_planar<Cfg>();
+    XSTAMP_RT(0, 14);
     XSTAMP(0, 0);
     if constexpr (COMP) {
         static_assert(PLANAR, "the composed head runs on the phase-planar path");
@@ -886,6 +901,7 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         head_rb1_planar<C1, Pl::RS_1, true>(w.w2[0], w.b2[0], hp, nullptr, up, f0, TF, 4 * T, &ap, nullptr,
                                             U1 + (size_t)b * 4 * T * 4 * C1);
         XSTAMP(0, 9);
+        XSTAMP_RT(0, 15);
         return;
     } else if constexpr (ONE) {
         const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -926,6 +942,8 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
             head_rb1_planar<C1, Pl::RS_1, true>(w.w2[0], w.b2[0], hp, nullptr, up, f0, TF, 4 * T, &ap, nullptr,
                                                 U1 + (size_t)b * 4 * T * 4 * C1);
             XSTAMP(0, 9);
+            XSTAMP_RT(0, 15);
+        XSTAMP_RT(0, 15);
             return;
         }
         xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N, 1, NW>(
@@ -948,6 +966,7 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, NW, true>(
             w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T, &ap, nullptr, U1 + (size_t)b * 4 * T * 4 * C1);
         XSTAMP(0, 9);
+        XSTAMP_RT(0, 15);
         return;
     } else {
         gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melw);

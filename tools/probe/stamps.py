@@ -46,7 +46,8 @@ if s2:
 else:
     model = bench.fixture_model(bench.STAGE1, dev)
     mel = torch.randn(B, 64, T, device=dev)
-for _ in range(3):
+import os  # noqa: E402
+for _ in range(int(os.environ.get("STAMPS_WARM", "3"))):  # STAMPS_WARM=2000: a settled clock
     model.vocoder(mel)
 torch.cuda.synchronize()
 buf = np.zeros(3 * 4096 * 16 * 16, dtype=np.uint64)
@@ -58,6 +59,8 @@ for k, names in PHASES.items():
     st = all_st[k]
     used = st[:, 0, 0] != 0
     st = st[used]
+    if st.shape[0] == 0:  # a pipelined kernel (no x3 stamps)
+        continue
     nph = len(names)
     nw = int((st[0, :, 0] != 0).sum())
     st = st[:, :nw, : nph + 1]
@@ -67,3 +70,12 @@ for k, names in PHASES.items():
     for i, nm in enumerate(names):
         print(f"   {nm:10s} {np.median(d[:, :, i].max(axis=1)):8.0f} | {np.median(d[:, :, i].mean(axis=1)):8.0f}")
     print(f"   total      {np.median(tot):8.0f}")
+if x3:  # head: shader clock per wave from s_memtime (slots 0, 9) over s_memrealtime (14, 15, 100 MHz)
+    st = all_st[0]
+    st = st[st[:, 0, 0] != 0]
+    ok = (st[:, :, 15] > st[:, :, 14]) & (st[:, :, 9] > st[:, :, 0])
+    ghz = (st[:, :, 9] - st[:, :, 0])[ok] / ((st[:, :, 15] - st[:, :, 14])[ok] / 100e6) / 1e9
+    if ghz.size:
+        print(f"head shader clock (GHz, per wave): median {np.median(ghz):.3f}  p10 {np.percentile(ghz, 10):.3f}  "
+              f"p90 {np.percentile(ghz, 90):.3f}  over {ghz.size} waves")
+
