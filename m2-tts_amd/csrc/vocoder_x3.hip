@@ -491,12 +491,50 @@ __device__ __forceinline__ void head_convT1_planar(const u32x4* __restrict__ Wp,
 // the input conv of the zero-padded mel (b_in + W_in[.,.,2] mel[0] /
 // b_in + W_in[.,.,0] mel[T-1]); outputs t = 0, 1 and 4T - 2, 4T - 1 subtract
 // that term: E[ph][co][m] . mel[edge] + e[ph][co] (hce: [4][C1][MP] then
-// [4][C1], fp32; phases 0, 1 left edge, 2, 3 right edge), computed by the
-// lanes that hold those outputs, in a wave-uniform branch only the two edge
-// windows of an utterance take.  Bias bc: [4][C1] (it depends on the phase).
+// [4][C1], fp32; phases 0, 1 left edge, 2, 3 right edge).  The edge windows
+// of an utterance compute those 256 sums cooperatively before the layer
+// (head_edge_terms: their table loads issued at kernel start) into an LDS
+// table `corr` that the lanes holding the edge outputs read (null elsewhere).
+// (A per-lane loop over the table in the epilogue made the edge windows the
+// kernel's critical path.)  Bias bc: [4][C1] (it depends on the phase).
+// The composed head's edge terms, all 1024 threads of an edge window: thread
+// t sums 16 of the 64 products of value v = t / 4 (= ph * COUT + co); four
+// adjacent lanes reduce by shuffles.  ev: this thread's 16 table entries,
+// loaded at kernel start (head_edge_load).
+template <int MP, int COUT>
+__device__ __forceinline__ void head_edge_load(const float* __restrict__ hce, float4 (&ev)[4], float& eb) {
+    static_assert(4 * COUT * 4 == 1024 && MP == 64, "1024 threads: 4 phases x COUT values x 4 parts of 16");
+    const int t = threadIdx.x, v = t >> 2, part = t & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ev[i] = *reinterpret_cast<const float4*>(hce + (size_t)v * MP + 16 * part + 4 * i);
+    eb = hce[4 * COUT * MP + v];
+}
+template <int MP, int COUT, int RSM>
+__device__ __forceinline__ void head_edge_terms(const float4 (&ev)[4], float eb, XW mel, int T, bool left, bool right,
+                                                unsigned char* corr) {
+    const int t = threadIdx.x, v = t >> 2, part = t & 3, ph = v / COUT;
+    const bool need = ph < 2 ? left : right;  // wave-uniform (16 waves, 4 per phase)
+    float d = 0.f;
+    if (need) {
+        const unsigned char* row = mel.p + ((ph < 2 ? 0 : T - 1) - mel.start) * RSM + 2 * 16 * part;
+        const float e[16] = {ev[0].x, ev[0].y, ev[0].z, ev[0].w, ev[1].x, ev[1].y, ev[1].z, ev[1].w,
+                             ev[2].x, ev[2].y, ev[2].z, ev[2].w, ev[3].x, ev[3].y, ev[3].z, ev[3].w};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const h8 hi = *reinterpret_cast<const h8*>(row + 16 * h);
+            const h8 lo = *reinterpret_cast<const h8*>(row + 2 * MP + 16 * h);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d = fmaf(e[8 * h + i], (float)hi[i] + (float)lo[i], d);
+        }
+    }
+    d += __shfl_xor(d, 1);
+    d += __shfl_xor(d, 2);
+    if (part == 0) *reinterpret_cast<float*>(corr + 4 * v) = need ? d + eb : 0.f;
+}
+
 template <int MP, int COUT, int RSM, int RSO>
 __device__ __forceinline__ void head_convT1c_planar(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
-                                                    const float* __restrict__ hce, XW mel, unsigned char* u, int f0,
+                                                    const unsigned char* corr, XW mel, unsigned char* u, int f0,
                                                     int T, APipe* ap, const u32x4* wp_next) {
     constexpr int MB = COUT / 16, NKB = nkb_of<MP, 4>(), NT = 4;
     static_assert(NKB == 8 && pd_of<MP, 4, 1>() == 4, "the ConvT1 weight pipeline shape");
@@ -517,26 +555,9 @@ __device__ __forceinline__ void head_convT1c_planar(const u32x4* __restrict__ Wp
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
         const int q = qs + 16 * n + li, t = 4 * q + ph;
-        if (qe >= qs + 16 * n && qe < qs + 16 * n + 16) {  // wave-uniform: this tile holds an edge output
+        if (corr && qe >= qs + 16 * n && qe < qs + 16 * n + 16) {  // wave-uniform: a tile with an edge output
             if (q == qe) {
-                // opaque pointer: the table loads stay in this rare branch
-                const float* ep = hce;
-                asm volatile("" : "+s"(ep));
-                const unsigned char* mrow = mel.p + (qe - mel.start) * RSM;  // mel[0] / mel[T - 1]
-                float c[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) c[r] = ep[4 * COUT * MP + ph * COUT + co0 + r];
-#pragma unroll 1
-                for (int o = 0; o < MP / 8; ++o) {
-                    const h8 hi = *reinterpret_cast<const h8*>(mrow + 16 * o);
-                    const h8 lo = *reinterpret_cast<const h8*>(mrow + 2 * MP + 16 * o);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float x = (float)hi[e] + (float)lo[e];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) c[r] = fmaf(ep[(ph * COUT + co0 + r) * MP + 8 * o + e], x, c[r]);
-                    }
-                }
+                const f32x4 c = *reinterpret_cast<const f32x4*>(corr + 4 * (ph * COUT + co0));
 #pragma unroll
                 for (int r = 0; r < 4; ++r) acc[0][n][r] -= c[r];
             }
@@ -875,18 +896,28 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         }
         // the mel window goes to region A (the u planes it feeds are written
         // into region B in the same phase; the h planes overwrite it later)
-        static_assert(Pl::CAP_MEL * Pl::RS_M <= Pl::RA, "mel window in region A");
+        static_assert(Pl::CAP_MEL * Pl::RS_M + 4 * 4 * C1 <= Pl::RA, "mel window + edge terms in region A");
         const XW melA{lds, f0 - 3};
+        unsigned char* corr = lds + Pl::CAP_MEL * Pl::RS_M;
+        // the windows holding an utterance edge (workgroup-uniform)
+        const bool left = f0 == 0, right = T - 1 >= f0 - 1 && T - 1 < f0 + TF;
+        float4 ev[4];
+        float eb = 0.f;
+        if (left || right) head_edge_load<MP, C1>(w.hce, ev, eb);
         gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melA);
         XSTAMP(0, 1);
         __syncthreads();
+        if (left || right) {
+            head_edge_terms<MP, C1, Pl::RS_M>(ev, eb, melA, T, left, right, corr);
+            __syncthreads();
+        }
         XSTAMP(0, 2);
         XSTAMP(0, 3);  // (no input-conv layer)
         XSTAMP(0, 4);
         unsigned char* up = lds + Pl::RA;
         unsigned char* hp = lds;
         head_convT1c_planar<MP, C1, Pl::RS_M, Pl::RS_1>(
-            w.hc, w.hcb, w.hce, melA, up, f0, T, &ap,
+            w.hc, w.hcb, (left || right) ? corr : nullptr, melA, up, f0, T, &ap,
             w.w1[0] + (size_t)(wv % MB1) * nkb_of<C1, 3>() * 128 + (threadIdx.x & 63));
         XSTAMP(0, 5);
         __syncthreads();
@@ -1164,11 +1195,11 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     auto* u1 = static_cast<unsigned char*>(U1);
     auto* u2 = static_cast<unsigned char*>(U2);
     mark(0, true);
-    // M2_HEAD_COMP=1: the composed input_conv o ConvT1 head (stage1; opt-in:
-    // 14.5 % fewer cycles per workgroup by phase stamps but no shorter kernel
-    // on the box, profiles/ab/r02l_head_comp.txt; read per call)
+    // the composed input_conv o ConvT1 head when packed (stage1; 22.1 -> 19.7
+    // us, profiles/ab/r02l_head_comp.txt); M2_HEAD_INCONV=1 runs the two
+    // layers (A/B and test switch, read per call)
     bool comp = false;
-    if constexpr (head_planar<Cfg>()) comp = w.hc && std::getenv("M2_HEAD_COMP");
+    if constexpr (head_planar<Cfg>()) comp = w.hc && !std::getenv("M2_HEAD_INCONV");
     const dim3 hg(cdiv(T, Cfg::TF), B), hb(Cfg::HW * 64);
     if constexpr (head_planar<Cfg>()) {
         if (comp && trans)

@@ -3,9 +3,8 @@
 the mel, with the outputs at t = 0, 1, 4T-2, 4T-1 corrected for the zeros the
 reference's ConvT1 sees at input frames -1 and T) against the CPU oracle (the
 reference's SimpleVocoder.forward, tts_model.py:279-297) and against the
-two-layer head (the default), over lengths that put the utterance edges in
-every window position, both mel layouts.  The composed head is opt-in
-(M2_HEAD_COMP=1): it measured no faster (vocoder head).
+two-layer head (M2_HEAD_INCONV=1), over lengths that put the utterance edges
+in every window position, both mel layouts.
 """
 import pytest
 import torch
@@ -24,8 +23,7 @@ def build_model(dev):
 
 
 @pytest.mark.parametrize("B,T", [(3, 1), (2, 2), (2, 5), (3, 63), (2, 64), (1, 127), (2, 137)])
-def test_head_comp_vs_oracle(gpu, monkeypatch, B, T):
-    monkeypatch.setenv("M2_HEAD_COMP", "1")
+def test_head_comp_vs_oracle(gpu, B, T):
     m = build_model(gpu)
     mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(400 + T))
     out = m.vocoder(mel.to(gpu)).cpu()
@@ -42,16 +40,15 @@ def test_head_comp_vs_two_layers(gpu, monkeypatch, B, T):
     composed weights are rounded once): agreement well inside the bound."""
     mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(B * T + 1))
     m = build_model(gpu)
-    ref = m.vocoder(mel.to(gpu))
-    monkeypatch.setenv("M2_HEAD_COMP", "1")
     out = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_HEAD_INCONV", "1")
+    ref = m.vocoder(mel.to(gpu))
     assert torch.isfinite(out).all()
     assert float((out - ref).abs().max()) <= 2e-5 and rms(out.cpu(), ref.cpu()) <= 2e-6
 
 
-def test_head_comp_btm_layout(gpu, monkeypatch):
+def test_head_comp_btm_layout(gpu):
     """The decoder hands the vocoder [B, T, M] mel (read transposed in place)."""
-    monkeypatch.setenv("M2_HEAD_COMP", "1")
     m = build_model(gpu)
     mel = torch.randn(3, stage_config("s1").mel_channels, 70, generator=torch.Generator().manual_seed(9))
     a = m.vocoder(mel.to(gpu))
