@@ -701,7 +701,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             // tables ride in the same buffer as u16 pairs)
             const vx_u32x4* hcb_at = nullptr;
             const vx_u32x4* hce_at = nullptr;
-            if (M == 64 && C == 128) {
+            if ((M == 64 && C == 128) || (M == 80 && C == 256)) {
                 std::vector<uint16_t> hw;
                 std::vector<float> hb, he;
                 const auto bi = fetch("vocoder.input_conv.bias"), wt0 = fetch("vocoder.upsamples.0.weight"),

@@ -240,12 +240,15 @@ constexpr bool kFold = res_fold_channels(C);
 // of one phase, co0 .. co0 + 16 NMB, sharing the B fragments) starting at
 // tile0.  Output position of column j (relative to the layer's first input
 // q0 / a0): t = (p0 + j) * RR + ph (RR = 1, ph = 0 for conv3).
+// corr (the composed stage2 head): per-(phase, channel) terms subtracted from
+// the outputs of input column qe (an utterance edge), before the activation.
 template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int ACT, bool RES, bool XR, int RR,
           int JMAX, int NMB, bool PRE, bool GO = false>
 __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
                                          const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
                                          int ph, int tile0, int L, u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2],
-                                         const u32x4* wp_next, unsigned char* gout = nullptr) {
+                                         const u32x4* wp_next, unsigned char* gout = nullptr,
+                                         const unsigned char* corr = nullptr, int qe = 0) {
     constexpr int WS = nkb_of<CIN, NTAP>() * 128;  // u32x4 between consecutive m-blocks' weights
     f32x4 acc[NMB][NTT];
 #pragma unroll
@@ -259,6 +262,18 @@ __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const flo
     mma_x3<CIN, NTAP, STEP, RSI, NTT, XR, NMB, WS, PRE>(wp, bp, xr, acc, a, wp_next);
     const bool edge = (p0 + tile0 * 16) * RR < 0 || (p0 + (tile0 + NTT) * 16) * RR > L;
     const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
+    if (corr) {  // wave-uniform
+#pragma unroll
+        for (int n = 0; n < NTT; ++n)
+            if (qe >= p0 + (tile0 + n) * 16 && qe < p0 + (tile0 + n) * 16 + 16 && p0 + (tile0 + n) * 16 + li == qe) {
+#pragma unroll
+                for (int m = 0; m < NMB; ++m) {
+                    const f32x4 c = *reinterpret_cast<const f32x4*>(corr + 4 * (ph * COUT + co0 + 16 * m));
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[m][n][r] -= c[r];
+                }
+            }
+    }
 #pragma unroll
     for (int m = 0; m < NMB; ++m) {
         const int cm = co0 + 16 * m;
@@ -402,6 +417,59 @@ __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float
         for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < IT::N; item += blockDim.x >> 6)
             body(item, std::false_type{});
     }
+}
+
+// The composed input_conv o ConvT1 on the generic item path (the stage2
+// head): head_convT1c_planar's layer over (phase, m-block, chunk) items, 4
+// mel taps (frames q + d0 + 1 - k), per-phase bias, edge terms from `corr`.
+template <int MP, int COUT, int NT, int RSI, int RSO, int NQ>
+__device__ __forceinline__ void xconvT1c(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
+                                         const unsigned char* corr, XW mel, XW out, int q0, int T) {
+    constexpr int R = 4, MB = (COUT + 15) / 16, NKB = nkb_of<MP, 4>();
+    using CH = Chunks<(NQ + 15) / 16, NT>;
+    constexpr int N = R * MB * CH::NCH;
+    const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+#pragma unroll 1
+    for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < N; item += blockDim.x >> 6) {
+        const int rg = item % (R * MB), k = item / (R * MB), ph = rg / MB, mb = rg - ph * MB;
+        const int tile0 = CH::lo(k), nt = CH::lo(k + 1) - tile0, d0 = ph < 2 ? 0 : 1, co0 = mb * 16 + 4 * g;
+        const u32x4* wp = Wp + (size_t)(ph * MB + mb) * NKB * 128 + lane;
+        const unsigned char* bp = mel.p + (q0 + tile0 * 16 + li + d0 + 1 - mel.start) * RSI;
+        const int qe = ph < 2 ? 0 : T - 1;
+        u32x4 al[pd_of<MP, 4, 1>()][1][2];
+        if (nt == CH::QHI)
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, 1, false>(
+                wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
+        else
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, 1, false>(
+                wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
+    }
+}
+
+// Edge terms of the composed stage2 head: thread v (4 x COUT threads) sums
+// E[v][0..M) . mel[edge] + e[v] into corr (the windows holding an edge only).
+template <int M, int MP, int COUT, int RSM>
+__device__ __forceinline__ void head_edge_terms_s2(const float* __restrict__ hce, XW mel, int T, bool left,
+                                                   bool right, unsigned char* corr) {
+    const int v = threadIdx.x, ph = v / COUT;
+    if (v >= 4 * COUT) return;
+    const bool need = ph < 2 ? left : right;
+    float d = 0.f;
+    if (need) {
+        const unsigned char* row = mel.p + ((ph < 2 ? 0 : T - 1) - mel.start) * RSM;
+        d = hce[4 * COUT * MP + v];
+#pragma unroll
+        for (int o = 0; o < M / 8; ++o) {
+            const h8 hi = *reinterpret_cast<const h8*>(row + 16 * o);
+            const h8 lo = *reinterpret_cast<const h8*>(row + 2 * MP + 16 * o);
+            const float4 e0 = *reinterpret_cast<const float4*>(hce + (size_t)v * MP + 8 * o);
+            const float4 e1 = *reinterpret_cast<const float4*>(hce + (size_t)v * MP + 8 * o + 4);
+            const float e[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d = fmaf(e[i], (float)hi[i] + (float)lo[i], d);
+        }
+    }
+    *reinterpret_cast<float*>(corr + 4 * v) = d;
 }
 
 // ---------------------------------------------------------------------------
@@ -883,7 +951,41 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     constexpr bool PLANAR = ONE && head_planar<Cfg>();
     XSTAMP_RT(0, 14);
     XSTAMP(0, 0);
-    if constexpr (COMP) {
+    if constexpr (COMP && !PLANAR) {
+        // stage2: the composed layer on the generic item path; the mel window
+        // in region A (the u rows it feeds are region B), edge terms after it
+        static_assert(!ONE, "generic path");
+        static_assert(Pl::CAP_MEL * Pl::RS_M + 4 * 4 * C1 <= Pl::RA, "mel window + edge terms in region A");
+        static_assert(4 * C1 <= Cfg::HW * 64, "one thread per edge term");
+        const XW melA{lds, f0 - 3};
+        unsigned char* corr = lds + Pl::CAP_MEL * Pl::RS_M;
+        // ConvT1's input columns here are [f0 - 1, f0 + TF]
+        const bool left = f0 == 0, right = T - 1 >= f0 - 1 && T - 1 <= f0 + TF;
+        gload_mel<TRANS, M, MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * M * T, T, melA);
+        XSTAMP(0, 1);
+        __syncthreads();
+        if (left || right) {
+            head_edge_terms_s2<M, MP, C1, Pl::RS_M>(w.hce, melA, T, left, right, corr);
+            __syncthreads();
+        }
+        XSTAMP(0, 2);
+        XSTAMP(0, 3);
+        XSTAMP(0, 4);
+        xconvT1c<MP, C1, Cfg::NT_T1, Pl::RS_M, Pl::RS_1, Pl::NQ>(w.hc, w.hcb, (left || right) ? corr : nullptr, melA,
+                                                              uw, f0 - 1, T);
+        XSTAMP(0, 5);
+        __syncthreads();
+        XSTAMP(0, 6);
+        xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1,
+                                                                                 4 * T);
+        XSTAMP(0, 7);
+        __syncthreads();
+        XSTAMP(0, 8);
+        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, 0, true>(
+            w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T, nullptr, nullptr, U1 + (size_t)b * 4 * T * 4 * C1);
+        XSTAMP(0, 9);
+        return;
+    } else if constexpr (COMP) {
         static_assert(PLANAR, "the composed head runs on the phase-planar path");
         const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         constexpr int MB1 = C1 / 16;
@@ -974,7 +1076,6 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
                                                 U1 + (size_t)b * 4 * T * 4 * C1);
             XSTAMP(0, 9);
             XSTAMP_RT(0, 15);
-        XSTAMP_RT(0, 15);
             return;
         }
         xconv3<MP, C, Cfg::NT_IN, ACT_NONE, false, Pl::RS_M, Pl::RS_C, Pl::A0_N, 1, NW>(
@@ -1167,10 +1268,8 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         int32_t rc;
         if ((rc = set_lds(x3_head_kernel<Cfg, false>, HP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_head_kernel<Cfg, true>, HP::LDS_BYTES))) return rc;
-        if constexpr (head_planar<Cfg>()) {
-            if ((rc = set_lds(x3_head_kernel<Cfg, false, true>, HP::LDS_BYTES))) return rc;
-            if ((rc = set_lds(x3_head_kernel<Cfg, true, true>, HP::LDS_BYTES))) return rc;
-        }
+        if ((rc = set_lds(x3_head_kernel<Cfg, false, true>, HP::LDS_BYTES))) return rc;
+        if ((rc = set_lds(x3_head_kernel<Cfg, true, true>, HP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_mid_kernel<Cfg>, MP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_tail_kernel<Cfg>, TP::LDS_BYTES))) return rc;
         if constexpr (S2) {
@@ -1198,15 +1297,12 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     // the composed input_conv o ConvT1 head when packed (stage1; 22.1 -> 19.7
     // us, profiles/ab/r02l_head_comp.txt); M2_HEAD_INCONV=1 runs the two
     // layers (A/B and test switch, read per call)
-    bool comp = false;
-    if constexpr (head_planar<Cfg>()) comp = w.hc && !std::getenv("M2_HEAD_INCONV");
+    const bool comp = w.hc && !std::getenv("M2_HEAD_INCONV");
     const dim3 hg(cdiv(T, Cfg::TF), B), hb(Cfg::HW * 64);
-    if constexpr (head_planar<Cfg>()) {
-        if (comp && trans)
-            hipLaunchKernelGGL((x3_head_kernel<Cfg, true, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
-        else if (comp)
-            hipLaunchKernelGGL((x3_head_kernel<Cfg, false, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
-    }
+    if (comp && trans)
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, true, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
+    else if (comp)
+        hipLaunchKernelGGL((x3_head_kernel<Cfg, false, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
     if (!comp && trans)
         hipLaunchKernelGGL((x3_head_kernel<Cfg, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
     else if (!comp)

@@ -55,3 +55,33 @@ def test_head_comp_btm_layout(gpu):
     hm = m._hip(gpu)
     b = hm.vocoder(mel.transpose(1, 2).contiguous().to(gpu), layout_btm=True)
     assert torch.equal(a, b)
+
+
+def build_s2(dev):
+    from models.tts_model import M2TTSModel
+    m = M2TTSModel(**stage_config("s2").as_dict())
+    m.load_state_dict(golden_state("s2"))
+    return m.to(dev).eval()
+
+
+@pytest.mark.parametrize("B,T", [(3, 1), (2, 2), (2, 15), (2, 16), (1, 17), (2, 47)])
+def test_head_comp_s2_vs_oracle(gpu, B, T):
+    """Stage2 (M = 80, C = 256): the composed layer on the generic item path,
+    16-frame windows; the edge columns also appear as halo columns."""
+    m = build_s2(gpu)
+    mel = torch.randn(B, stage_config("s2").mel_channels, T, generator=torch.Generator().manual_seed(500 + T))
+    out = m.vocoder(mel.to(gpu)).cpu()
+    ref = orc.vocoder(golden_state("s2"), mel)
+    assert rms(out, ref) <= AUDIO_RMS_TOL and maxabs(out, ref) <= 1e-4
+    assert maxabs(out[..., :48], ref[..., :48]) <= 1e-5 and maxabs(out[..., -48:], ref[..., -48:]) <= 1e-5
+
+
+@pytest.mark.parametrize("B,T", [(8, 500), (16, 2600), (3, 33)])
+def test_head_comp_s2_vs_two_layers(gpu, monkeypatch, B, T):
+    mel = torch.randn(B, stage_config("s2").mel_channels, T, generator=torch.Generator().manual_seed(B * T + 2))
+    m = build_s2(gpu)
+    out = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_HEAD_INCONV", "1")
+    ref = m.vocoder(mel.to(gpu))
+    assert torch.isfinite(out).all()
+    assert float((out - ref).abs().max()) <= 2e-5 and rms(out.cpu(), ref.cpu()) <= 2e-6
