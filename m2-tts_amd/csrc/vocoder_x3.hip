@@ -881,6 +881,14 @@ struct CfgS2Alt : CfgS2 {
     static constexpr int W3 = 125, NT_T3 = 5, NT_R3 = 5;
 };
 constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
+// Stage2 head windows of 24 frames for large grids (composed head: less
+// weight streaming per frame; 16x2600 0.569 -> 0.548 ms, 64x500 0.430 ->
+// 0.421 ms per vocoder step, but 8x500 0.072 -> 0.075 ms: 168 workgroups
+// leave CUs idle), taken when the 16-frame grid has >= 1024 workgroups.
+struct CfgS2H24 : CfgS2 {
+    static constexpr int TF = 24;
+};
+constexpr long kS2WideHeadWGs = 1024;
 
 // Diagnostic build only (-DM2_STAMPS): per-wave s_memtime stamps at phase
 // boundaries, [kernel][workgroup][wave][16] (tools/probe/stamps.py --x3).
@@ -1258,6 +1266,7 @@ template <class Cfg>
 int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1, void* U2, float* audio,
             hipStream_t st, const std::function<void(int, bool)>& mark) {
     using HP = HeadPlan<Cfg::MP, Cfg::C, Cfg::TF, head_planar<Cfg>()>;
+    using HP24 = HeadPlan<CfgS2H24::MP, CfgS2H24::C, CfgS2H24::TF, false>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
     constexpr bool S2 = std::is_same<Cfg, CfgS2>::value;
@@ -1273,6 +1282,8 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         if ((rc = set_lds(x3_mid_kernel<Cfg>, MP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_tail_kernel<Cfg>, TP::LDS_BYTES))) return rc;
         if constexpr (S2) {
+            if ((rc = set_lds(x3_head_kernel<CfgS2H24, false, true>, HP24::LDS_BYTES))) return rc;
+            if ((rc = set_lds(x3_head_kernel<CfgS2H24, true, true>, HP24::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_mid_kernel<CfgS2Alt>, MPA::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_tail_kernel<CfgS2Alt>, TPA::LDS_BYTES))) return rc;
         }
@@ -1299,7 +1310,18 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     // layers (A/B and test switch, read per call)
     const bool comp = w.hc && !std::getenv("M2_HEAD_INCONV");
     const dim3 hg(cdiv(T, Cfg::TF), B), hb(Cfg::HW * 64);
-    if (comp && trans)
+    bool wide = false;  // stage2, composed head, large grid: 24-frame windows
+    if constexpr (S2) wide = comp && (long)cdiv(T, Cfg::TF) * B >= kS2WideHeadWGs && !std::getenv("M2_S2_HEAD_TF16");
+    if (wide) {
+        if constexpr (S2) {
+            const dim3 hg24(cdiv(T, CfgS2H24::TF), B);
+            if (trans)
+                hipLaunchKernelGGL((x3_head_kernel<CfgS2H24, true, true>), hg24, hb, HP24::LDS_BYTES, st, mel, T, w, u1);
+            else
+                hipLaunchKernelGGL((x3_head_kernel<CfgS2H24, false, true>), hg24, hb, HP24::LDS_BYTES, st, mel, T, w,
+                                   u1);
+        }
+    } else if (comp && trans)
         hipLaunchKernelGGL((x3_head_kernel<Cfg, true, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
     else if (comp)
         hipLaunchKernelGGL((x3_head_kernel<Cfg, false, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);
