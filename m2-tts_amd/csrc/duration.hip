@@ -51,21 +51,40 @@ __device__ __forceinline__ int frames_of(const void* dur, int is_int, float scal
     return frames_from(static_cast<const float*>(dur)[i], scale);
 }
 
+// This wave's weight fragments of one conv (n-block = wave), requested at
+// kernel start so their L2 round trips overlap the encoder-row loads and the
+// LayerNorm instead of sitting between the barriers (H <= 128: one n-block
+// per wave).
 template <int H>
-__device__ __forceinline__ void dur_conv_mfma(const float* in, const float4* __restrict__ Wp,
-                                              const float* __restrict__ b, const float* __restrict__ a,
-                                              const float* __restrict__ c, float* out, int pos0, int S) {
+struct DurW {
+    float4 w[3 * H / 16];
+};
+template <int H>
+__device__ __forceinline__ void dur_wload(const float4* __restrict__ Wp, DurW<H>& r) {
+    static_assert(H / 16 <= DUR_WAVES, "one n-block per wave");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave < H / 16) {
+        const float4* wp = Wp + (size_t)wave * (3 * H / 16) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < 3 * H / 16; ++k) r.w[k] = wp[k * 64];
+    }
+}
+
+template <int H>
+__device__ __forceinline__ void dur_conv_mfma(const float* in, const DurW<H>& W, const float* __restrict__ b,
+                                              const float* __restrict__ a, const float* __restrict__ c, float* out,
+                                              int pos0, int S) {
     constexpr int XS = H + 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-    for (int nb = wave; nb < H / 16; nb += DUR_WAVES) {
-        const float4* wp = Wp + (size_t)nb * (3 * H / 16) * 64 + lane;
+    if (wave < H / 16) {
+        const int nb = wave;
         dur_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int tap = 0; tap < 3; ++tap) {
             const float* x0 = in + (i + tap) * XS + g;
 #pragma unroll
             for (int s4 = 0; s4 < H / 16; ++s4) {
-                const float4 w = wp[(tap * (H / 16) + s4) * 64];
+                const float4 w = W.w[tap * (H / 16) + s4];
                 const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
@@ -103,6 +122,9 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const int b = blockIdx.y, s0 = blockIdx.x * DUR_TS, tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const float* e = enc + (size_t)b * S * H;
+    DurW<H> W1, W2;
+    dur_wload<H>(w1, W1);
+    dur_wload<H>(w2, W2);
     if constexpr (LN) {
         // every row of this wave is loaded before the first is normalised (one
         // memory round trip per wave instead of one per row)
@@ -148,9 +170,9 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     }
     for (int idx = tid; idx < 2 * XS; idx += NT) Y1[16 * XS + idx] = 0.f;
     __syncthreads();
-    dur_conv_mfma<H>(X, w1, b1, a1, c1, Y1, s0 - 1, S);
+    dur_conv_mfma<H>(X, W1, b1, a1, c1, Y1, s0 - 1, S);
     __syncthreads();
-    dur_conv_mfma<H>(Y1, w2, b2, a2, c2, Y2, s0, S);
+    dur_conv_mfma<H>(Y1, W2, b2, a2, c2, Y2, s0, S);
     __syncthreads();
     // k=1 projection H -> 1: one wave per phoneme, shuffle reduction.
     for (int p = wave; p < DUR_TS; p += DUR_WAVES) {
