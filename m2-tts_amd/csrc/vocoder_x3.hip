@@ -860,9 +860,12 @@ struct CfgS1 {
 #define X3S2_NT_T3 4
 #define X3S2_NT_R3 4
 #endif
+#ifndef X3S2_HW  // stage2 head waves per workgroup (tiling experiments)
+#define X3S2_HW 8
+#endif
 struct CfgS2 {
     static constexpr int M = 80, MP = 96, C = 256;
-    static constexpr int TF = X3S2_TF, HW = 8, HMIN = 2;
+    static constexpr int TF = X3S2_TF, HW = X3S2_HW, HMIN = 2;
     static constexpr int W2 = X3S2_W2, MW = 8, MMIN = 2;
     static constexpr int W3 = X3S2_W3, TW = 8, TMIN = 2;
     static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = X3S2_NT_R1, NT_T2 = 4, NT_R2 = X3S2_NT_R2, NT_T3 = X3S2_NT_T3,
@@ -885,8 +888,11 @@ constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
 // weight streaming per frame; 16x2600 0.569 -> 0.548 ms, 64x500 0.430 ->
 // 0.421 ms per vocoder step, but 8x500 0.072 -> 0.075 ms: 168 workgroups
 // leave CUs idle), taken when the 16-frame grid has >= 1024 workgroups.
+// 16 waves per workgroup there (more latency hiding at one workgroup per CU:
+// head 140.8 -> 135.2 us at 64x500, 170.6 -> 165.4 at 16x2600; at 8x500 the
+// 16-frame, 8-wave head stays, tools/probe/s2_tiles.sh with X3S2_HW=16).
 struct CfgS2H24 : CfgS2 {
-    static constexpr int TF = 24;
+    static constexpr int TF = 24, HW = 16;
 };
 constexpr long kS2WideHeadWGs = 1024;
 
