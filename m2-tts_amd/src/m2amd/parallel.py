@@ -5,12 +5,15 @@ global batch by utterance is exact with ONE coupling: the mel decoder is
 unmasked over frames and the length regulator pads every utterance to the
 batch maximum (tts_model.py:165-176, 211-228), so each utterance's mel depends
 on the GLOBAL frame count T.  The ranks therefore agree on T with one
-all-reduce(MAX) of a single int32 before the decoder; everything else is
+all-reduce(MAX) of one int32 pair before the decoder; everything else is
 independent.  Collectives (RCCL over xGMI with the "nccl" backend; gloo in the
 CPU tests):
-  all_reduce(MAX)  1 x int32                       after the duration predictor
-  all_gather       mel [b, T, M] and audio [b, 1, 64T] shards (padded to ceil(B/N)),
-                   one collective over rows [mel | audio] per utterance
+  broadcast        (optional, src=r) the global phoneme ids / lengths from rank r
+  all_reduce(MAX)  2 x int32 (T_local, M)          after the duration predictor
+  gather / all_gather  mel [b, T, M] and audio [b, 1, 64T] shards (padded to
+                   ceil(B/N)), one collective over rows [mel | audio] per
+                   utterance; optionally left in flight (async_gather) so it
+                   overlaps the next step
 Payloads are KB..MB, so the path is latency-bound; weights are replicated.
 
 A step is two phases around the all-reduce: ``front`` (encoder, durations,
@@ -47,6 +50,10 @@ class Stages:
     regulate: Callable[[Tensor, Tensor, int, float], Tensor]      # enc, dur, T, scale -> [b,T,H]
     decode: Callable[[Tensor], Tensor]                            # [b,T,H] -> mel [b,T,M]
     vocode: Callable[[Tensor], Tensor]                            # mel [b,T,M] -> audio [b,1,64T]
+    mel_width: int = 0                                            # M (for ranks with an empty shard)
+
+    def mel_channels(self) -> int:
+        return self.mel_width
 
     def front(self, ids: Tensor, lens: Optional[Tensor], scale: float) -> Tuple[Any, int]:
         enc = self.encode(ids, lens)
@@ -66,6 +73,9 @@ class HipStages:
     def __init__(self, model):
         self.model = model
 
+    def mel_channels(self) -> int:
+        return int(self.model._m2_cfg.mel_channels)
+
     def front(self, ids: Tensor, lens: Optional[Tensor], scale: float) -> Tuple[Any, int]:
         # one handle lookup per step (its weight-identity check walks every
         # parameter, ~25 us of host time): the back half reuses this handle
@@ -82,10 +92,52 @@ def hip_stages(model) -> HipStages:
     return HipStages(model)
 
 
-def _gather_shards(local: Tensor, batch: int, world: int, group, dst: Optional[int] = None) -> Optional[Tensor]:
+def _collective_device(ref: Optional[Tensor], group) -> torch.device:
+    """nccl (RCCL) moves device tensors only; gloo host tensors."""
+    if dist.is_initialized() and dist.get_backend(group) == "nccl":
+        return ref.device if (ref is not None and ref.is_cuda) else torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def broadcast_inputs(phoneme_ids: Optional[Tensor], phoneme_lengths: Optional[Tensor], src: int = 0,
+                     group=None, device: Optional[torch.device] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """Rank ``src`` holds the global batch (e.g. the CLI's text); every rank
+    returns it.  One broadcast of the header (B, S, lengths present) and one of
+    the payload [B, S + 1] int64 (ids and lengths as one row per utterance;
+    RCCL over xGMI with the "nccl" backend, 51 KB for configs[3])."""
+    me = dist.get_rank(group)
+    ref = phoneme_ids if me == src else None
+    cdev = _collective_device(ref, group)
+    g_src = dist.get_global_rank(group, src) if group is not None else src
+    hdr = torch.zeros(3, dtype=torch.int64, device=cdev)
+    if me == src:
+        if phoneme_ids is None or phoneme_ids.dim() != 2:
+            raise ValueError("broadcast_inputs: the source rank needs phoneme_ids [B, S]")
+        hdr[0], hdr[1] = phoneme_ids.shape
+        hdr[2] = int(phoneme_lengths is not None)
+    dist.broadcast(hdr, src=g_src, group=group)
+    B, S, has_len = (int(v) for v in hdr.tolist())
+    if me == src:
+        rows = torch.empty(B, S + 1, dtype=torch.int64, device=cdev)
+        rows[:, :S] = phoneme_ids.to(cdev, torch.int64)
+        rows[:, S] = phoneme_lengths.to(cdev, torch.int64) if has_len else 0
+    else:
+        rows = torch.empty(B, S + 1, dtype=torch.int64, device=cdev)
+    if B * (S + 1):
+        dist.broadcast(rows, src=g_src, group=group)
+    out_dev = device if device is not None else (phoneme_ids.device if phoneme_ids is not None else cdev)
+    rows = rows.to(out_dev)
+    return rows[:, :S].contiguous(), (rows[:, S].contiguous() if has_len else None)
+
+
+def _gather_shards(local: Tensor, batch: int, world: int, group, dst: Optional[int] = None,
+                   async_op: bool = False):
     """Gather per-rank utterance shards of unequal sizes -> [batch, ...]:
     all_gather (every rank gets the batch) or, with ``dst``, gather to that
-    rank only (the others return None)."""
+    rank only (the others get None).  A rank with an empty shard joins with
+    padding rows.  With ``async_op`` the collective is left in flight (RCCL
+    runs it on its own stream, after the work already queued on the current
+    one) and a callable that waits and assembles the result is returned."""
     per = -(-batch // world)
     if local.shape[0] == per:
         pad = local.contiguous()
@@ -93,59 +145,103 @@ def _gather_shards(local: Tensor, batch: int, world: int, group, dst: Optional[i
         pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         pad[: local.shape[0]] = local
     me = dist.get_rank(group)
+    parts = None
     if dst is None:
         parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad, group=group)
+        work = dist.all_gather(parts, pad, group=group, async_op=async_op)
     else:
         parts = [torch.empty_like(pad) for _ in range(world)] if me == dst else None
-        dist.gather(pad, parts, dst=dist.get_global_rank(group, dst) if group is not None else dst, group=group)
-        if me != dst:
-            return None
+        work = dist.gather(pad, parts, dst=dist.get_global_rank(group, dst) if group is not None else dst,
+                           group=group, async_op=async_op)
     n = [shard_bounds(batch, world, r)[1] - shard_bounds(batch, world, r)[0] for r in range(world)]
-    if all(k == per for k in n):
-        return torch.stack(parts).flatten(0, 1) if world > 1 else parts[0]
-    return torch.cat([parts[r][: n[r]] for r in range(world)], dim=0)
+
+    def finish():
+        if async_op and work is not None:
+            work.wait()
+        if parts is None:
+            return None
+        if all(k == per for k in n):
+            return torch.stack(parts).flatten(0, 1) if world > 1 else parts[0]
+        return torch.cat([parts[r][: n[r]] for r in range(world)], dim=0)
+
+    return finish if async_op else finish()
 
 
-def _collective_device(ids: Tensor, group) -> torch.device:
-    """nccl (RCCL) reduces device tensors only; gloo host tensors."""
-    if dist.is_initialized() and dist.get_backend(group) == "nccl":
-        return torch.device("cuda", torch.cuda.current_device()) if not ids.is_cuda else ids.device
-    return torch.device("cpu")
+class PendingGather:
+    """The (mel, audio) of a sharded step whose gather is still in flight
+    (``sharded_inference(..., async_gather=True)``): ``wait()`` returns them
+    (None on ranks that are not the destination)."""
+
+    def __init__(self, finish: Callable, mel_shape, audio_shape, audio_dtype):
+        self._finish, self._ms, self._as, self._ad = finish, mel_shape, audio_shape, audio_dtype
+        self._out = None
+
+    def wait(self):
+        if self._finish is not None:
+            g = self._finish()
+            self._finish = None
+            if g is None:
+                self._out = (None, None)
+            else:
+                Mw = 1
+                for v in self._ms[1:]:
+                    Mw *= v
+                self._out = (g[:, :Mw].reshape(self._ms).contiguous(),
+                             g[:, Mw:].reshape(self._as).to(self._ad).contiguous())
+        return self._out
 
 
-def sharded_inference(stages, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor],
+def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Optional[Tensor],
                       duration_scale: float = 1.0, group=None, gather: bool = True,
-                      gather_to: Optional[int] = None):
+                      gather_to: Optional[int] = None, src: Optional[int] = None,
+                      async_gather: bool = False):
     """M2TTSModel.inference (tts_model.py:402-438) over a global batch sharded by
-    utterance.  Every rank passes the same global ``phoneme_ids``/lengths
-    (or the same seed-generated tensors); rank r computes utterances
-    shard_bounds(B, N, r).  Returns (mel, audio) for the global batch when
-    ``gather`` (on every rank; with ``gather_to=r`` on rank r only, None
-    elsewhere), else this rank's shard and its bounds."""
+    utterance.
+
+    Inputs: with ``src=r`` only rank r needs ``phoneme_ids`` / lengths (the
+    others may pass None): it broadcasts them (``broadcast_inputs``).
+    Without ``src`` every rank passes the same global tensors (e.g. generated
+    from one seed).  Rank r computes utterances shard_bounds(B, N, r); a rank
+    whose shard is empty (B < N) still joins every collective.
+
+    Returns (mel, audio) for the global batch when ``gather`` (on every rank;
+    with ``gather_to=r`` on rank r only, None elsewhere), else this rank's
+    shard and its bounds.  ``async_gather`` (with ``gather``) leaves the
+    gather in flight and returns a PendingGather, so the next step's work
+    overlaps it; call ``.wait()`` for the tensors."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if src is not None and world > 1:
+        phoneme_ids, phoneme_lengths = broadcast_inputs(phoneme_ids, phoneme_lengths, src, group)
     B = phoneme_ids.shape[0]
-    if gather and world > 1 and B < world:  # same decision on every rank, before any collective
-        raise ValueError("sharded_inference with gather needs at least one utterance per rank (B >= world)")
     lo, hi = shard_bounds(B, world, rank)
     ids = phoneme_ids[lo:hi]
     lens = phoneme_lengths[lo:hi] if phoneme_lengths is not None else None
     with torch.no_grad():
         state, t_local = stages.front(ids, lens, duration_scale) if hi > lo else (None, 0)
+        M = stages.mel_channels()
         if world > 1:
-            t = torch.tensor([t_local], dtype=torch.int32, device=_collective_device(phoneme_ids, group))
+            # one all_reduce(MAX) of (T_local, M): the batch-global frame count,
+            # and the mel width for ranks whose shard is empty
+            t = torch.tensor([t_local, M], dtype=torch.int32, device=_collective_device(phoneme_ids, group))
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-            t_local = int(t.item())
+            t_local, M = (int(v) for v in t.tolist())
         T = max(1, t_local)  # all-empty batch -> one zero frame (tts_model.py:158-160)
-        mel, audio = stages.back(state, T) if hi > lo else (None, None)
+        if hi > lo:
+            mel, audio = stages.back(state, T)
+        else:
+            dev = phoneme_ids.device
+            mel = torch.zeros(0, T, M, dtype=torch.float32, device=dev)
+            audio = torch.zeros(0, 1, 64 * T, dtype=torch.float32, device=dev)
     if not gather or world == 1:
+        if async_gather and gather:
+            out = PendingGather(None, None, None, None)
+            out._out = (mel, audio)
+            return out
         return (mel, audio) if gather else (mel, audio, (lo, hi))
     # one collective for both outputs: each utterance's mel and audio as one row
-    b, Mw = mel.shape[0], mel[0].numel()
-    both = torch.cat([mel.reshape(b, -1), audio.reshape(b, -1).to(mel.dtype)], dim=1)
-    g = _gather_shards(both, B, world, group, gather_to)
-    if g is None:
-        return None, None
-    return (g[:, :Mw].reshape((B,) + tuple(mel.shape[1:])).contiguous(),
-            g[:, Mw:].reshape((B,) + tuple(audio.shape[1:])).to(audio.dtype).contiguous())
+    b, Mw = mel.shape[0], T * M
+    both = torch.cat([mel.reshape(b, Mw), audio.reshape(b, 64 * T).to(mel.dtype)], dim=1)
+    fin = _gather_shards(both, B, world, group, gather_to, async_op=async_gather)
+    pend = PendingGather(fin if async_gather else (lambda: fin), (B, T, M), (B, 1, 64 * T), audio.dtype)
+    return pend if async_gather else pend.wait()

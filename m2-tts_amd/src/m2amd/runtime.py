@@ -209,7 +209,9 @@ class HipModel:
         "report" - the next call raises M2Error (M2_E_RANGE), check() reports
         it at once; "fallback" - each vocoder call waits for its kernels and
         re-runs on the exact-f32 kernels when its audio is not finite."""
-        _lib.call("m2_set_range_policy", self.handle, {"report": 0, "fallback": 1}[policy])
+        if policy not in RANGE_POLICIES:
+            raise ValueError(f"range policy {policy!r}: expected one of {sorted(RANGE_POLICIES)}")
+        _lib.call("m2_set_range_policy", self.handle, RANGE_POLICIES[policy])
 
     def check(self) -> bool:
         """Synchronise the current stream; True if a split-path vocoder call
@@ -304,6 +306,21 @@ class HipModel:
         return y
 
 
+RANGE_POLICIES = {"report": 0, "fallback": 1}
+
+
+def default_range_policy() -> str:
+    """The split-f16 range policy a new handle gets: "fallback" (never a
+    non-finite result for finite inputs the exact-f32 path handles), unless
+    M2_RANGE_POLICY names another one."""
+    env = os.environ.get("M2_RANGE_POLICY")
+    if env is None or env == "":
+        return "fallback"
+    if env not in RANGE_POLICIES:
+        raise ValueError(f"M2_RANGE_POLICY={env!r}: expected one of {sorted(RANGE_POLICIES)}")
+    return env
+
+
 class HandleCache:
     """Per-device HipModel for one nn.Module, rebuilt when its weights change."""
 
@@ -323,9 +340,7 @@ class HandleCache:
         path = module.__dict__.get("_m2_voc_path")
         if path:
             hm.vocoder_select(path)
-        policy = module.__dict__.get("_m2_range_policy") or os.environ.get("M2_RANGE_POLICY")
-        if policy:
-            hm.set_range_policy(policy)
+        hm.set_range_policy(module.__dict__.get("_m2_range_policy") or default_range_policy())
         self._entries[device] = (key, hm)
         return hm
 

@@ -238,13 +238,19 @@ class M2TTSModel(nn.Module):
         for hm in (cache.handles() if cache is not None else []):
             hm.set_chunking(chunk_frames)
 
-    def set_range_policy(self, policy: str = "report"):
+    def set_range_policy(self, policy: str = "fallback"):
         """The split-f16 vocoder carries fp32 values as f16 hi/lo pairs; an
         input or activation of magnitude >= 65520 turns its audio non-finite
-        (never silently wrong).  "report" (default): the next call raises, and
-        check_numerics() reports it at once; "fallback": every vocoder call
-        waits for its result and recomputes it on the exact-f32 kernels when
-        it is not finite (costs one host synchronisation per call)."""
+        (never silently wrong).  "fallback" (the default, also without this
+        call; M2_RANGE_POLICY overrides it for new handles): every vocoder
+        call waits for its result and recomputes it on the exact-f32 kernels
+        when it is not finite, so a call never returns non-finite audio for an
+        input the reference's fp32 path handles (costs one host
+        synchronisation per call: bench.py's ``vocoder_default_policy``).
+        "report" (opt-in, what the throughput benchmarks use): asynchronous -
+        the next call raises, check_numerics() reports it at once."""
+        if policy not in runtime.RANGE_POLICIES:
+            raise ValueError(f"range policy {policy!r}: expected one of {sorted(runtime.RANGE_POLICIES)}")
         self.__dict__["_m2_range_policy"] = policy
         cache = _HANDLES.get(self)
         for hm in (cache.handles() if cache is not None else []):
@@ -254,8 +260,13 @@ class M2TTSModel(nn.Module):
         """Synchronise and raise if a split-path vocoder call since the last
         check produced non-finite audio (M2_E_RANGE semantics)."""
         cache = _HANDLES.get(self)
+        want = None
+        if device is not None:
+            want = torch.device(device)
+            if want.type == "cuda" and want.index is None:
+                want = torch.device("cuda", torch.cuda.current_device())
         for hm in (cache.handles() if cache is not None else []):
-            if (device is None or hm.device == torch.device(device)) and hm.check():
+            if (want is None or hm.device == want) and hm.check():
                 raise ops.M2Error(
                     "m2-tts_amd: a split-f16 vocoder call produced non-finite audio (an input or activation "
                     "of magnitude >= 65520); re-run with set_vocoder_precision('f32') or set_range_policy('fallback')")

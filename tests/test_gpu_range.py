@@ -43,11 +43,12 @@ def test_huge_mel_fallback_matches_exact_f32_and_oracle(gpu, stage):
 def test_huge_mel_report_raises(gpu, stage):
     from m2amd._lib import M2Error
     m = build_model(stage, gpu)
+    m.set_range_policy("report")  # opt-in (the default is "fallback")
     ok = _mel(stage, 30, 1.0)
     base = m.vocoder(ok.to(gpu))
     bad = m.vocoder(_mel(stage, 30, 1e6).to(gpu))
     with pytest.raises(M2Error, match="non-finite"):
-        m.check_numerics()
+        m.check_numerics("cuda")  # an unindexed device names the current one
     m.check_numerics()  # cleared
     assert torch.equal(m.vocoder(ok.to(gpu)), base)
     m.vocoder(_mel(stage, 30, 1e6).to(gpu))
@@ -72,6 +73,27 @@ def test_huge_activation_inside_the_vocoder(gpu, stage):
     assert torch.isfinite(out).all()
     ref = orc.vocoder(sd, mel)
     assert rms(out, ref) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_default_policy_inference_never_nan(gpu, stage):
+    """Without any policy call, inference() on weights whose vocoder
+    activations overflow the split-f16 range returns the exact-f32 result
+    (the reference's), in the same call - never non-finite audio."""
+    sd = golden_state(stage)
+    sd["vocoder.input_conv.bias"] = sd["vocoder.input_conv.bias"] + 1e5
+    m = build_model(stage, gpu, sd)
+    g = golden(f"{stage}_small")
+    ids, lens = torch.from_numpy(g["ids"]), torch.from_numpy(g["lengths"])
+    mel, audio = m.inference(ids.to(gpu), lens.to(gpu))
+    assert torch.isfinite(audio).all()
+    ref_mel, ref_audio = orc.inference(sd, stage_config(stage), ids, lens, as_written=False)
+    assert maxabs(mel, ref_mel) <= MEL_MAXABS_TOL
+    assert rms(audio, ref_audio) <= AUDIO_RMS_TOL
+    m.set_vocoder_precision("f32")
+    _, exact = m.inference(ids.to(gpu), lens.to(gpu))
+    assert torch.equal(audio, exact)
+    m.check_numerics()  # nothing left pending
 
 
 @pytest.mark.parametrize("stage", ["s1", "s2"])

@@ -131,3 +131,20 @@ def test_bench_flop_model():
     assert bench.vocoder_flops_per_sample(128, 64) == 14896.0
     assert bench.vocoder_flops_per_sample(256, 80) == 58336.0
     assert sum(bench.vocoder_kernel_flops_per_frame(128, 64)) == 14896 * 64
+
+
+def test_range_policy_default_and_env_validation(monkeypatch):
+    """New handles get the "fallback" policy (no non-finite audio returned for
+    finite inputs) unless M2_RANGE_POLICY names another; a bad value is an
+    error naming the variable, at configuration time."""
+    from m2amd.runtime import default_range_policy
+    from models.tts_model import M2TTSModel
+    monkeypatch.delenv("M2_RANGE_POLICY", raising=False)
+    assert default_range_policy() == "fallback"
+    monkeypatch.setenv("M2_RANGE_POLICY", "report")
+    assert default_range_policy() == "report"
+    monkeypatch.setenv("M2_RANGE_POLICY", "fallbak")
+    with pytest.raises(ValueError, match="M2_RANGE_POLICY"):
+        default_range_policy()
+    with pytest.raises(ValueError, match="range policy"):
+        M2TTSModel().set_range_policy("nope")

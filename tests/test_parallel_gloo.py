@@ -25,7 +25,8 @@ def oracle_stages(sd, cfg):
                   frame_totals=frame_totals,
                   regulate=lambda enc, dur, T, scale: orc.length_regulator(enc, dur * scale if scale != 1.0 else dur, T),
                   decode=lambda x: orc.mel_decoder(sd, cfg, x),
-                  vocode=lambda mel: orc.vocoder(sd, mel.transpose(1, 2)))
+                  vocode=lambda mel: orc.vocoder(sd, mel.transpose(1, 2)),
+                  mel_width=cfg.mel_channels)
 
 
 def _worker(rank, world, port, outfile):
@@ -48,9 +49,27 @@ def _worker(rank, world, port, outfile):
         # gather to one rank only (the serving layout: rank 1 collects, rank 0 gets None)
         mel_r, audio_r = sharded_inference(st, ids5, lens5, gather_to=1)
         assert (mel_r is None) == (rank != 1) and (audio_r is None) == (rank != 1)
+        # inputs on rank 0 only (broadcast), gather left in flight while another step runs
+        pend = sharded_inference(st, ids5 if rank == 0 else None, lens5 if rank == 0 else None, src=0,
+                                 gather_to=0, async_gather=True)
+        mel_n, _ = sharded_inference(st, ids5 if rank == 0 else None, lens5 if rank == 0 else None, src=0)
+        mel_b, audio_b = pend.wait()
+        assert (mel_b is None) == (rank != 0)
+        assert torch.equal(mel_n, out["b5"][0])
+        # B = 1 < world: rank 1's shard is empty and it still joins every collective
+        one = {}
+        one["all"] = sharded_inference(st, ids[:1], lens[:1])
+        one["to1"] = sharded_inference(st, ids[:1], lens[:1], gather_to=1)
+        one["src"] = sharded_inference(st, ids[:1] if rank == 0 else None, lens[:1] if rank == 0 else None, src=0)
+        assert (one["to1"][0] is None) == (rank != 1)
         import numpy as np
         if rank == 1:
-            np.savez(outfile + ".root1.npz", mel=mel_r.numpy(), audio=audio_r.numpy())
+            np.savez(outfile + ".root1.npz", mel=mel_r.numpy(), audio=audio_r.numpy(),
+                     one_mel=one["to1"][0].numpy(), one_audio=one["to1"][1].numpy(),
+                     src_mel=one["src"][0].numpy())
+        if rank == 0:
+            np.savez(outfile + ".bcast.npz", mel=mel_b.numpy(), audio=audio_b.numpy(),
+                     one_mel=one["all"][0].numpy(), one_audio=one["all"][1].numpy())
         dist.barrier()
         if rank == 0:
             np.savez(outfile, **{f"{k}_{j}": v[j].numpy() for k, v in out.items() for j in range(2)})
@@ -74,6 +93,10 @@ def test_sharded_inference_matches_unsharded_two_ranks(tmp_path):
     res = {k: (z[f"{k}_0"], z[f"{k}_1"]) for k in ("b2", "b5", "b5s")}
     r1 = np.load(outfile + ".root1.npz")
     assert np.array_equal(r1["mel"], res["b5"][0]) and np.array_equal(r1["audio"], res["b5"][1])
+    bc = np.load(outfile + ".bcast.npz")
+    assert np.array_equal(bc["mel"], res["b5"][0]) and np.array_equal(bc["audio"], res["b5"][1])
+    assert np.array_equal(bc["one_mel"], r1["one_mel"]) and np.array_equal(bc["one_audio"], r1["one_audio"])
+    assert np.array_equal(bc["one_mel"], r1["src_mel"])
     sd = golden_state("s1")
     g = golden("s1_target_free")
     ids, lens = torch.from_numpy(g["ids"]), torch.from_numpy(g["lengths"])
@@ -84,6 +107,10 @@ def test_sharded_inference_matches_unsharded_two_ranks(tmp_path):
         assert res[tag][0].shape == tuple(mel.shape), tag
         assert float(abs(res[tag][0] - mel.numpy()).max()) <= 1e-5, tag
         assert float(abs(res[tag][1] - audio.numpy()).max()) <= 1e-5, tag
+    mel1, audio1 = orc.inference(sd, orc.STAGE1, ids[:1], lens[:1], as_written=False)
+    assert bc["one_mel"].shape == tuple(mel1.shape)
+    assert float(abs(bc["one_mel"] - mel1.numpy()).max()) <= 1e-5
+    assert float(abs(bc["one_audio"] - audio1.numpy()).max()) <= 1e-5
 
 
 def test_shard_bounds_cover_batch():
