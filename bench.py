@@ -40,11 +40,27 @@ import ctypes
 import json
 import os
 import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
 
-import torch
+
+def _cpu_child_pin():
+    """CPU-baseline child (``bench.py --cpu-child SPEC``): pin this process to
+    the CPUs SPEC lists (one logical CPU per physical core) and bind one
+    OpenMP thread to each, before torch (and its OpenMP runtime) loads."""
+    spec = json.loads(sys.argv[sys.argv.index("--cpu-child") + 1])
+    os.sched_setaffinity(0, spec["cpus"])
+    n = str(len(spec["cpus"]))
+    os.environ.update(OMP_NUM_THREADS=n, MKL_NUM_THREADS=n, OMP_PROC_BIND="close", OMP_PLACES="threads",
+                      OMP_WAIT_POLICY="PASSIVE")
+
+
+if __name__ == "__main__" and "--cpu-child" in sys.argv:
+    _cpu_child_pin()
+
+import torch  # noqa: E402
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "m2-tts_amd" / "src"))
@@ -142,41 +158,107 @@ def host_info():
     return cpu_model, os.cpu_count(), affinity
 
 
-def cpu_baseline(workload: str, B: int, S: int, T: int, budget_s: float):
-    """Time the CPU oracle (the reference's op sequence) on a bounded sample of the workload."""
+def physical_cores():
+    """One logical CPU per physical core of this process's affinity mask, and
+    the sockets they sit on (sysfs topology)."""
+    chosen = {}
+    for c in sorted(os.sched_getaffinity(0)):
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            key = (int(open(base + "physical_package_id").read()), int(open(base + "core_id").read()))
+        except (OSError, ValueError):
+            key = (0, c)
+        chosen.setdefault(key, c)
+    return sorted(chosen.values()), len({k[0] for k in chosen})
+
+
+def cpu_measure(run, runs: int, min_s: float):
+    """Median / min / max over `runs` measurements of run()'s rate (calls/s),
+    each measurement timing whole calls for at least min_s seconds."""
+    rates = []
+    with torch.no_grad():
+        run()  # warm-up
+        for _ in range(runs):
+            n, t0 = 0, time.perf_counter()
+            while True:
+                run()
+                n += 1
+                el = time.perf_counter() - t0
+                if el >= min_s:
+                    break
+            rates.append(n / el)
+    rates.sort()
+    return rates[len(rates) // 2], rates[0], rates[-1], rates
+
+
+def cpu_child_main(spec):
+    """Runs in the pinned child: the CPU oracle (the reference's op sequence)
+    on both workloads of the headline configuration."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import m2tts_oracle as orc
-    threads = torch.get_num_threads()
+    torch.set_num_threads(len(spec["cpus"]))
+    B, S, T = spec["B"], spec["S"], spec["T"]
     torch.manual_seed(1234)
     from models.tts_model import M2TTSModel  # only for the seeded init (module construction on CPU)
     m = M2TTSModel(**STAGE1)
     sd = orc.pin_durations({k: v.detach().clone() for k, v in m.state_dict().items()})
     cfg = orc.STAGE1
     g = torch.Generator().manual_seed(0)
-    if workload == "vocoder":
-        mel = torch.randn(B, cfg.mel_channels, T, generator=g)
-        run = lambda: orc.vocoder(sd, mel)  # noqa: E731
-        desc = f"oracle SimpleVocoder single pass, B={B} mel [{B},{cfg.mel_channels},{T}]"
-    else:
-        ids = torch.randint(0, 42, (B, S), generator=g)
-        lens = torch.full((B,), S, dtype=torch.long)
-        run = lambda: orc.inference(sd, cfg, ids, lens, as_written=True)  # noqa: E731
-        desc = f"oracle M2TTSModel.inference as written (2 vocoder passes), B={B} S={S}"
-    with torch.no_grad():
-        run()  # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
-            run()
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= budget_s or n >= 200:
-                break
+    mel = torch.randn(B, cfg.mel_channels, T, generator=g)
+    ids = torch.randint(0, 42, (B, S), generator=g)
+    lens = torch.full((B,), S, dtype=torch.long)
+    out = {"torch_threads": torch.get_num_threads()}
+    if spec.get("ids_seed") is not None:
+        # the CPU path's frame counts for the pipeline line's batch (T equality, SURVEY.md 8d)
+        pids = torch.randint(0, 42, (B, S), generator=torch.Generator().manual_seed(spec["ids_seed"]))
+        with torch.no_grad():
+            enc, _ = orc.text_encoder(sd, cfg, pids, lens)
+            dur = orc.duration_predictor(sd, enc).double()
+        out["frames"] = {"cpu_T_per_utt": torch.trunc(dur).clamp(min=0).sum(1).to(torch.int64).tolist(),
+                         "min_duration_dist_to_int": float((dur - dur.round()).abs().min())}
+    for name, run in (("vocoder", lambda: orc.vocoder(sd, mel)),
+                      ("inference_as_written", lambda: orc.inference(sd, cfg, ids, lens, as_written=True))):
+        med, lo, hi, rates = cpu_measure(run, spec["runs"], spec["min_s"])
+        out[name] = {"median": med * B * 64 * T, "min": lo * B * 64 * T, "max": hi * B * 64 * T,
+                     "calls_per_s": [round(r, 3) for r in rates]}
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_seed=None):
+    """Time the CPU oracle (the reference's op sequence) on the
+    node's host cores: a child process pinned to one logical CPU per physical
+    core of this process's affinity mask, one OpenMP thread per core
+    (torch.set_num_threads(physical cores)), median of `runs` measurements
+    with the spread.  Two figures for the headline configuration: the
+    vocoder single pass (configs[1], the `value`) and M2TTSModel.inference as
+    written (2 vocoder passes, Python length-regulator loop)."""
+    cpus, sockets = physical_cores()
+    spec = {"cpus": cpus, "B": B, "S": S, "T": T, "runs": runs, "min_s": min_s, "ids_seed": ids_seed}
+    env = dict(os.environ)
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--cpu-child", json.dumps(spec)], env=env,
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": f"cpu baseline child failed (rc {r.returncode}): {r.stderr[-400:]}"}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
     cpu_model, ncpu, aff = host_info()
-    return {"value": samples_per(B, T) * n / el, "unit": "audio samples/s", "cores": threads, "kind": "port",
-            "host_logical_cpus": ncpu, "affinity_cpus": aff, "torch_threads": threads, "cpu_model": cpu_model,
-            "sample": f"{desc}; {n} runs in {el:.1f} s; torch {torch.__version__} CPU ops, {threads} intra-op "
-                      f"threads on {cpu_model} ({ncpu} logical CPUs on the host, {aff} in this process's "
-                      f"affinity mask)"}
+    voc, inf = res["vocoder"], res["inference_as_written"]
+    spread = lambda d: round((d["max"] - d["min"]) / d["median"], 3)  # noqa: E731
+    return {"value": voc["median"], "unit": "audio samples/s", "cores": len(cpus), "kind": "port",
+            "sockets": sockets, "host_logical_cpus": ncpu, "affinity_cpus": aff,
+            "torch_threads": res["torch_threads"], "pinned": "one OpenMP thread per physical core "
+            "(OMP_PROC_BIND=close on one logical CPU per core)", "cpu_model": cpu_model,
+            "stat": f"median of {runs} runs of >= {min_s} s", "min": voc["min"], "max": voc["max"],
+            "spread": spread(voc),
+            "sample": f"oracle SimpleVocoder single pass (the reference's ATen op sequence), B={B} mel [{B},64,{T}] "
+                      f"(configs[1]); torch {torch.__version__} CPU ops on {len(cpus)} physical cores "
+                      f"({sockets} sockets) of {cpu_model}",
+            "inference_as_written": {"value": inf["median"], "min": inf["min"], "max": inf["max"],
+                                     "spread": spread(inf), "unit": "audio samples/s",
+                                     "sample": f"oracle M2TTSModel.inference as written (2 vocoder passes, "
+                                               f"Python length-regulator loop), B={B} S={S} -> T={T}"},
+            "frames": res.get("frames"), "wall_s": round(time.perf_counter() - t0, 1)}
 
 
 def samples_per(B: int, T: int) -> int:
@@ -217,7 +299,7 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=32, help="utterances per GPU (vocoder / pipeline)")
     ap.add_argument("--phonemes", type=int, default=100)
     ap.add_argument("--s2-shape", default="8x500", help="BxT of the s2_vocoder workload")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="CPU baseline: measurements per workload (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline line only")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -407,11 +489,22 @@ def pipeline_line(cx: Ctx, B: int, S: int, args, settle_ms: float):
     steps = max(10, args.steps // 2)
     elapsed, _ = cx.timed(step, steps, max(3, args.warmup // 2))
     T = 5 * S
+    # the frame counts and how far the durations sit from the
+    # int() truncation points (a duration within ~1e-6 of an integer could
+    # flip a frame count between the GPU and the CPU path)
+    with torch.no_grad():
+        mel, _ = m.inference(ids, lens)
+        dur = m(ids, lens)["duration_pred"].double()
+    tot = torch.trunc(dur).clamp(min=0).sum(1).to(torch.int64).cpu()
+    frames = {"gpu_T_per_utt": tot.tolist(), "T": int(mel.shape[1]),
+              "T_is_batch_max": int(mel.shape[1]) == max(1, int(tot.max())),
+              "min_duration_dist_to_int": float((dur - dur.round()).abs().min()),
+              "ids_seed": 1000 + cx.rank}
     return {"value": round(samples_per(B, T) * steps * cx.world / elapsed, 1),
             "ms_per_step": round(elapsed / steps * 1e3, 5), "steps": steps, "settle_ms": round(settled, 1),
-            "scaling": "weak", "config": {"workload": "stage1_poc M2TTSModel.inference (configs[2])",
-                                          "per_gpu_batch": B, "global_batch": B * cx.world, "phonemes": S,
-                                          "mel_frames": T}}
+            "scaling": "weak", "frames": frames,
+            "config": {"workload": "stage1_poc M2TTSModel.inference (configs[2])",
+                       "per_gpu_batch": B, "global_batch": B * cx.world, "phonemes": S, "mel_frames": T}}
 
 
 def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, steps: int):
@@ -563,11 +656,20 @@ def run(args):
     out.update(extras)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("vocoder", "pipeline"):
-        out["cpu_baseline"] = cpu_baseline(wl, B, S, 5 * S, args.cpu_budget)
-        out["cpu_baseline"]["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
-        if not args.no_extras:
-            other = "pipeline" if wl == "vocoder" else "vocoder"
-            out["cpu_baseline_other"] = cpu_baseline(other, B, S, 5 * S, args.cpu_budget / 2)
+        pipe = out.get("pipeline") if wl == "vocoder" else head
+        cb = cpu_baseline(B, S, 5 * S, runs=args.cpu_runs,
+                          ids_seed=pipe["frames"]["ids_seed"] if isinstance(pipe, dict) and "frames" in pipe else None)
+        if "value" in cb:
+            cb["gpu_over_cpu"] = round(out["value"] / cb["value"], 1)
+            if isinstance(pipe, dict):
+                cb["inference_as_written"]["gpu_pipeline_over_cpu"] = round(
+                    pipe["value"] / cb["inference_as_written"]["value"], 1)
+                fr, cf = pipe.get("frames"), cb.pop("frames", None)
+                if fr and cf:  # T equality GPU vs the reference's CPU op sequence
+                    fr["cpu_T_per_utt_equal"] = fr["gpu_T_per_utt"] == cf["cpu_T_per_utt"]
+                    fr["cpu_min_duration_dist_to_int"] = cf["min_duration_dist_to_int"]
+                    fr.pop("gpu_T_per_utt")
+        out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
@@ -577,6 +679,8 @@ def run(args):
 
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
+    if "--cpu-child" in argv:
+        return cpu_child_main(json.loads(argv[argv.index("--cpu-child") + 1]))
     args = parse_args(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         launch_ranks(args, argv)

@@ -19,6 +19,13 @@
  *  - Return 0 on success; M2_E_* (<0) for argument/shape errors; a positive
  *    value is a hipError_t passed through.  m2_last_error() returns a
  *    thread-local message for the last failure on the calling thread.
+ *  - One stream per model handle: a model's calls must be ordered on one
+ *    stream (or externally synchronised).  The handle carries per-model
+ *    device state that successive calls hand over in stream order - the
+ *    split-f16 range flag (m2_model_check) and the work-queue counters of the
+ *    one-launch transformer layers - so two streams using one handle at the
+ *    same time may see each other's range flag and must not share it; create
+ *    one handle per stream instead (weights are packed per handle).
  */
 #ifndef M2TTS_HIP_H
 #define M2TTS_HIP_H
@@ -240,6 +247,14 @@ int32_t m2_conv1d(const float* x, const float* w, const float* b, const float* a
                   const float* beta, const float* res, int32_t ksize, int32_t act, int32_t B,
                   int32_t Cin, int32_t Cout, int32_t L, float* y, void* stream);
 
+/* m2_conv1d for any kernel size, dilation and zero padding (components.py:
+ * 143-200 ConvBlock(kernel_size), LightweightResBlock(kernel_size, dilation),
+ * tts_model.py:246,272 SimpleVocoder(kernel_size)): y [B,Cout,Lo] with
+ * Lo = L + 2*padding - dilation*(ksize-1); res (optional) needs Lo == L. */
+int32_t m2_conv1d_ex(const float* x, const float* w, const float* b, const float* alpha, const float* beta,
+                     const float* res, int32_t ksize, int32_t dilation, int32_t padding, int32_t act, int32_t B,
+                     int32_t Cin, int32_t Cout, int32_t L, float* y, void* stream);
+
 /* y = act(convT1d(x; w [Cin,Cout,2r], b, stride r, padding r/2)), r in {2,4};
  * x [B,Cin,L] -> y [B,Cout,r*L] (tts_model.py:255-263, 291). */
 int32_t m2_conv_transpose1d(const float* x, const float* w, const float* b, int32_t rate,
@@ -259,7 +274,8 @@ int32_t m2_layer_norm(const float* x, const float* gamma, const float* beta, int
 /* Attention core of MultiHeadAttention.forward (components.py:72-86):
  * qkv [B,N,3H] laid out (3, heads, hd) per row as the reference's reshape
  * implies; key_mask [B,N] uint8 or NULL (masked keys score -1e9);
- * out [B,N,H] (heads re-interleaved, before out_proj). */
+ * out [B,N,H] (heads re-interleaved, before out_proj).  head_dim 16/32/48/64
+ * run on the MFMA kernels, any other head_dim <= 256 on a generic fp32 one. */
 int32_t m2_attention(const float* qkv, const uint8_t* key_mask, int32_t B, int32_t N, int32_t H,
                      int32_t heads, float* out, void* stream);
 

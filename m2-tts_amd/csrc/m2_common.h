@@ -12,7 +12,7 @@ namespace m2 {
 constexpr int kWave = 64;            // CDNA wavefront
 constexpr float kLnEps = 1e-5f;      // nn.LayerNorm / BatchNorm1d default eps
 constexpr float kLeaky = 0.1f;       // F.leaky_relu slope used by the vocoder
-constexpr float kMaskFill = -1e9f;   // components.py:539
+constexpr float kMaskFill = -1e9f;   // components.py:81 (masked_fill_ value)
 
 enum Act : int { ACT_NONE = 0, ACT_LEAKY = 1, ACT_TANH = 2, ACT_RELU = 3, ACT_SOFTPLUS = 4 };
 

@@ -12,6 +12,7 @@
 
 #include "m2_common.h"
 #include "transformer_fused.h"
+#include "transformer_layer.h"
 #include "vocoder_fused.h"
 
 namespace m2 {
@@ -36,6 +37,8 @@ int32_t launch_add_pe(const float*, const float*, int, int, int, float*, hipStre
 int32_t launch_embed_pe_scaled(const int64_t*, const float*, const float*, int, int, int, int, float, float*, hipStream_t);
 int32_t launch_convT(const float*, const float*, const float*, int, int, int, int, int, int,
                      float*, hipStream_t);
+int32_t launch_conv_general(const float*, const float*, const float*, const float*, const float*, const float*, int,
+                            int, int, int, int, int, int, int, float*, hipStream_t);
 
 static thread_local std::string g_last_error;
 
@@ -185,6 +188,10 @@ struct m2_model {
     // exact-f32 attention for weights whose q/k/v bound leaves the f16 range
     int32_t* rflag_host = nullptr;
     int range_policy = 0;
+    // one-launch transformer layers: work-queue counters and the launch
+    // sequence whose parity picks their set (one stream per model)
+    unsigned* tflq = nullptr;
+    mutable unsigned tfl_seq = 0;
     bool att_f32 = false;
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
@@ -215,20 +222,35 @@ int32_t mask_kernel_launch(const int64_t* lengths, int B, int S, uint8_t* mask, 
     return M2_OK;
 }
 
+// Transformer stack scratch: the residual stream x and the padding mask, then
+// one region used either by the three-launch layers (qkv, att, hid) or by the
+// one-launch layers (two TflBufs sets, ping-pong between layers).
 struct TfBufs {
     float *x, *qkv, *att, *hid;
     uint8_t* mask;
+    TflBufs tfl[2];
 };
 
 template <typename A>
-void carve_tf(A& a, int B, int N, int H, TfBufs* out) {
+void carve_tf(A& a, int B, int N, int H, int heads, TfBufs* out) {
     const size_t R = (size_t)B * N;
     float* x = a.template take<float>(R * H);
-    float* qkv = a.template take<float>(R * 3 * H);
-    float* att = a.template take<float>(R * H);
-    float* hid = a.template take<float>(R * 2 * H);
     uint8_t* mask = a.template take<uint8_t>(R);
-    if (out) *out = TfBufs{x, qkv, att, hid, mask};
+    const size_t three = align_up(R * 3 * H * 4, 256) + align_up(R * H * 4, 256) + align_up(R * 2 * H * 4, 256);
+    const size_t one = tfl_supported(H, heads) ? 2 * align_up(tfl_bytes(B, N, H, heads), 256) : 0;
+    unsigned char* region = a.template take<unsigned char>(std::max(three, one));
+    if (!out) return;
+    *out = TfBufs{};
+    out->x = x;
+    out->mask = mask;
+    if (!region) return;
+    out->qkv = reinterpret_cast<float*>(region);
+    out->att = reinterpret_cast<float*>(region + align_up(R * 3 * H * 4, 256));
+    out->hid = reinterpret_cast<float*>(region + align_up(R * 3 * H * 4, 256) + align_up(R * H * 4, 256));
+    if (one) {
+        tfl_carve(region, B, N, H, heads, &out->tfl[0]);
+        tfl_carve(region + align_up(tfl_bytes(B, N, H, heads), 256), B, N, H, heads, &out->tfl[1]);
+    }
 }
 
 size_t vocoder_max_cl(const m2_config& c, int T) {
@@ -334,6 +356,64 @@ bool tf_chain(const m2_model* m) {
 // frame expansion fused in; tf_chain stacks only).
 bool tf_first_fused(const m2_model* m, const std::vector<m2_layer_w>& layers) {
     return tf_chain(m) && !layers.empty() && tf_src_fused_supported(m->cfg.hidden_dim, 3 * m->cfg.hidden_dim);
+}
+
+// The next launch's work queue (its parity alternates the counter sets).
+TflQueue tfl_queue(const m2_model* m) { return TflQueue{m->tflq, m->tfl_seq++}; }
+// A launch that failed may not have zeroed the next counter set: restart both.
+int32_t tfl_reset(const m2_model* m, hipStream_t st, int32_t rc) {
+    (void)hipMemsetAsync(m->tflq, 0, kTflQueueWords * sizeof(unsigned), st);
+    m->tfl_seq = 0;
+    return rc;
+}
+
+// One-launch layers (transformer_layer.hip) for a stack of this model:
+// heads == 2, H in {32, 64, 96}, the split-f16 transformer path.
+// M2_TF_LAYER=0 keeps the three-launch layers (A/B comparisons, tests).
+bool tfl_use(const m2_model* m, const std::vector<m2_layer_w>& layers) {
+    const char* e = std::getenv("M2_TF_LAYER");  // read per call: a process can switch (tests)
+    const bool on = !e || !*e || std::atoi(e) != 0;
+    return on && m->tfused && !m->att_f32 && !layers.empty() &&
+           tfl_supported(m->cfg.hidden_dim, m->cfg.num_heads);
+}
+
+// The layers of a stack whose first LN1 -> QKV (launch_tfl_first) already
+// wrote wb.tfl[0]; x0 = layer 0's input rows (residual), x = the output
+// stream.  The last layer also runs the final LN -> projection into fin_out
+// when its width has an instantiation (*fin_done).
+int32_t run_tfl(const m2_model* m, const std::vector<m2_layer_w>& layers, const float* x0, float* x, TfBufs& wb,
+                const int64_t* lengths, int B, int N, hipStream_t st, const float* fin_g = nullptr,
+                const float* fin_b = nullptr, const float* fin_W = nullptr, const float* fin_bias = nullptr,
+                int fin_N = 0, float* fin_out = nullptr, bool* fin_done = nullptr) {
+    const int H = m->cfg.hidden_dim, heads = m->cfg.num_heads, n = (int)layers.size();
+    if (fin_done) *fin_done = false;
+    const float* cur = x0;
+    for (int l = 0; l < n; ++l) {
+        const m2_layer_w& L = layers[l];
+        TflLayer w{L.out_p, L.out_b, L.n2_w, L.n2_b, L.ff1_p, L.ff1_b, L.ff2_p, L.ff2_b};
+        int next = 0, NN = 0;
+        float* z = nullptr;
+        if (l + 1 < n) {
+            next = 1;
+            w.gn = layers[l + 1].n1_w;
+            w.bn = layers[l + 1].n1_b;
+            w.Wn = layers[l + 1].qkv_p;
+        } else if (fin_W && tfl_proj_supported(H, fin_N)) {
+            next = 2;
+            w.gn = fin_g;
+            w.bn = fin_b;
+            w.Wn = fin_W;
+            w.bn2 = fin_bias;
+            NN = fin_N;
+            z = fin_out;
+        }
+        const int32_t rc = launch_tfl_layer(w, B, N, H, heads, lengths != nullptr, lengths, cur, x, wb.tfl[l & 1], next,
+                                            wb.tfl[(l + 1) & 1], NN, z, tfl_queue(m), st);
+        if (rc) return tfl_reset(m, st, rc);
+        if (next == 2 && fin_done) *fin_done = true;
+        cur = x;
+    }
+    return M2_OK;
 }
 
 int32_t run_stack(const m2_model* m, const std::vector<m2_layer_w>& layers, const float* x_in, float* x, TfBufs& wb,
@@ -846,6 +926,14 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
         m->rflag_host = static_cast<int32_t*>(h);
         m->vx.rflag = static_cast<int*>(d);
     }
+    // work-queue counters of the one-launch transformer layers (TflQueue)
+    e = hipMalloc(&m->tflq, kTflQueueWords * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemsetAsync(m->tflq, 0, kTflQueueWords * sizeof(unsigned), st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        m2_model_destroy(m);
+        return hip_status(e, "hipMalloc(tfl queue)");
+    }
     *out = m;
     return M2_OK;
 }
@@ -860,6 +948,7 @@ int32_t m2_model_destroy(m2_model* model) {
     if (model->tbuf) (void)hipFree(model->tbuf);
     if (model->mbuf) (void)hipFree(model->mbuf);
     if (model->rflag_host) (void)hipHostFree(model->rflag_host);
+    if (model->tflq) (void)hipFree(model->tflq);
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -876,8 +965,8 @@ size_t m2_workspace_bytes(const m2_model* model, int32_t B, int32_t S, int32_t T
     if (!model || B < 0 || S < 0 || T < 0) return 0;
     const int H = model->cfg.hidden_dim;
     Sizer a, b;
-    carve_tf(a, B, S, H, nullptr);
-    carve_tf(b, B, T, H, nullptr);
+    carve_tf(a, B, S, H, model->cfg.num_heads, nullptr);
+    carve_tf(b, B, T, H, model->cfg.num_heads, nullptr);
     return std::max(a.off, std::max(b.off, vocoder_ws_bytes(model, B, T))) + 256;
 }
 
@@ -892,13 +981,29 @@ int32_t text_encoder_layers(const m2_model* m, const int64_t* ids, const int64_t
     const int H = m->cfg.hidden_dim;
     Carve a(workspace, workspace_bytes);
     TfBufs wb;
-    carve_tf(a, B, S, H, &wb);
+    carve_tf(a, B, S, H, m->cfg.num_heads, &wb);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_text_encoder: workspace too small");
     *x_pre = wb.x;
     if (B == 0 || S == 0) return M2_OK;
     int32_t rc;
     const uint8_t* mask = nullptr;
     if (lengths) mask = out_mask ? out_mask : wb.mask;  // written by the embedding launch
+    if (tfl_use(m, m->enc)) {
+        const m2_layer_w& L0 = m->enc[0];
+        TflFirst f;
+        f.src = 1;
+        f.ids = ids;
+        f.emb = m->emb;
+        f.pe = m->pe;
+        f.vocab = m->cfg.vocab_size;
+        f.escale = (float)std::sqrt((double)H);  // as launch_embed_pe
+        f.lengths = lengths;
+        f.mask = out_mask;
+        if ((rc = launch_tfl_first(f, B, S, H, m->cfg.num_heads, lengths != nullptr, wb.x, L0.n1_w, L0.n1_b, L0.qkv_p,
+                                   wb.tfl[0], tfl_queue(m), st)))
+            return tfl_reset(m, st, rc);
+        return run_tfl(m, m->enc, wb.x, wb.x, wb, lengths, B, S, st);
+    }
     if (tf_first_fused(m, m->enc)) {
         const m2_layer_w& L0 = m->enc[0];
         if ((rc = launch_embed_ln_gemm(ids, m->emb, m->pe, B, S, H, m->cfg.vocab_size, lengths,
@@ -1055,10 +1160,33 @@ int32_t mel_decoder(const m2_model* m, float* x, int32_t B, int32_t T, float* ou
     const int H = m->cfg.hidden_dim;
     Carve a(workspace, workspace_bytes);
     TfBufs wb;
-    carve_tf(a, B, T, H, &wb);
+    carve_tf(a, B, T, H, m->cfg.num_heads, &wb);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_mel_decoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
     int32_t rc;
+    if (tfl_use(m, m->dec)) {
+        const m2_layer_w& L0 = m->dec[0];
+        TflFirst f;
+        if (enc) {  // the length regulator's expansion, built by the first launch into x
+            f.src = 2;
+            f.enc = enc;
+            f.cum = cum;
+            f.S = S;
+        } else {
+            f.src = 0;
+            f.x_in = x;
+        }
+        if ((rc = launch_tfl_first(f, B, T, H, m->cfg.num_heads, false, x, L0.n1_w, L0.n1_b, L0.qkv_p, wb.tfl[0],
+                                   tfl_queue(m), st)))
+            return tfl_reset(m, st, rc);
+        bool projected = false;
+        if ((rc = run_tfl(m, m->dec, x, wb.x, wb, nullptr, B, T, st, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b,
+                          m->cfg.mel_channels, out_mel, &projected)))
+            return rc;
+        if (projected) return M2_OK;
+        return launch_ln_gemm(wb.x, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b, ACT_NONE, B * T, H, m->cfg.mel_channels,
+                              out_mel, st);
+    }
     bool qkv_ready = false;
     if (enc) {
         if (tf_first_fused(m, m->dec)) {
@@ -1309,6 +1437,14 @@ int32_t m2_conv1d(const float* x, const float* w, const float* b, const float* a
     return launch_conv(x, w, b, alpha, beta, res, ksize, act, false, B, Cin, Cout, L, y, static_cast<hipStream_t>(stream));
 }
 
+int32_t m2_conv1d_ex(const float* x, const float* w, const float* b, const float* alpha, const float* beta,
+                     const float* res, int32_t ksize, int32_t dilation, int32_t padding, int32_t act, int32_t B,
+                     int32_t Cin, int32_t Cout, int32_t L, float* y, void* stream) {
+    M2_CHECK_ARG(x && w && b && y && B >= 0 && L >= 0, "m2_conv1d_ex: bad argument");
+    return launch_conv_general(x, w, b, alpha, beta, res, ksize, dilation, padding, act, B, Cin, Cout, L, y,
+                               static_cast<hipStream_t>(stream));
+}
+
 int32_t m2_conv_transpose1d(const float* x, const float* w, const float* b, int32_t rate,
                             int32_t act, int32_t B, int32_t Cin, int32_t Cout, int32_t L, float* y,
                             void* stream) {
@@ -1411,7 +1547,7 @@ int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, co
     // the regulated frames live after the decoder / vocoder scratch
     Carve w(workspace, workspace_bytes);
     Sizer sz_tf;
-    carve_tf(sz_tf, B, T, H, nullptr);
+    carve_tf(sz_tf, B, T, H, m->cfg.num_heads, nullptr);
     const size_t scratch = std::max(sz_tf.off, vocoder_ws_bytes(m, B, T));
     (void)w.take<char>(scratch);
     float* reg = w.take<float>((size_t)B * T * H);
@@ -1451,8 +1587,8 @@ size_t m2_inference_workspace_bytes(const m2_model* model, int32_t B, int32_t S,
     if (!model || B < 0 || S < 0 || T < 0) return 0;
     const int H = model->cfg.hidden_dim;
     Sizer a, b, d;
-    carve_tf(a, B, S, H, nullptr);
-    carve_tf(b, B, T, H, nullptr);
+    carve_tf(a, B, S, H, model->cfg.num_heads, nullptr);
+    carve_tf(b, B, T, H, model->cfg.num_heads, nullptr);
     d.off = std::max(b.off, vocoder_ws_bytes(model, B, T));
     (void)d.take<float>((size_t)B * T * H);
     return std::max(a.off, d.off) + 256;

@@ -839,14 +839,56 @@ static int32_t launch_att_split(dim3 grid, const float* qkv, const uint8_t* mask
         const char* e = std::getenv("M2_ATT_QT");
         return e ? std::atoi(e) : 0;
     }();
-    // (head_dim > 32: two tiles' registers spill past the 256-VGPR cap, 6-8x slower)
-    const bool qt2 = forced ? forced == 2 : (HD <= 32 && (long)cdiv(N, 128) * heads * B >= 256);
-    if (mask) {
-        if (qt2) return launch_att_split_qt<HD, 2, true>(N, heads, B, qkv, mask, H, scale, out, st);
-        return launch_att_split_qt<HD, 1, true>(N, heads, B, qkv, mask, H, scale, out, st);
+    // head_dim > 32: two tiles' registers spill past the 256-VGPR cap (400-432
+    // B/lane of scratch, 6-8x slower), so those instances are not compiled and
+    // M2_ATT_QT=2 is refused for them
+    if constexpr (HD <= 32) {
+        const bool qt2 = forced ? forced == 2 : (long)cdiv(N, 128) * heads * B >= 256;
+        if (qt2) {
+            if (mask) return launch_att_split_qt<HD, 2, true>(N, heads, B, qkv, mask, H, scale, out, st);
+            return launch_att_split_qt<HD, 2, false>(N, heads, B, qkv, mask, H, scale, out, st);
+        }
+    } else if (forced == 2) {
+        return fail(M2_E_SHAPE, "attention: M2_ATT_QT=2 is not available for head_dim > 32 (it spills)");
     }
-    if (qt2) return launch_att_split_qt<HD, 2, false>(N, heads, B, qkv, mask, H, scale, out, st);
+    if (mask) return launch_att_split_qt<HD, 1, true>(N, heads, B, qkv, mask, H, scale, out, st);
     return launch_att_split_qt<HD, 1, false>(N, heads, B, qkv, mask, H, scale, out, st);
+}
+
+// Any head_dim (the standalone MultiHeadAttention with head_dim outside the
+// MFMA instances 16 / 32 / 48 / 64, components.py:42-90): one query per lane,
+// the reference's max-subtracted softmax computed online in fp32, the query
+// row and its output accumulator in LDS (head_dim <= 256).
+__global__ __launch_bounds__(64) void attention_generic_kernel(const float* __restrict__ qkv,
+                                                               const uint8_t* __restrict__ key_mask, int N, int H,
+                                                               int hd, float scale, float* __restrict__ out) {
+    extern __shared__ float gsm[];
+    const int b = blockIdx.z, h = blockIdx.y, tid = threadIdx.x, q = blockIdx.x * 64 + tid;
+    float* qs = gsm + tid * hd;
+    float* as = gsm + 64 * hd + tid * hd;
+    const float* base = qkv + (size_t)b * N * 3 * H;
+    if (q >= N) return;
+    for (int d = 0; d < hd; ++d) {
+        qs[d] = base[(size_t)q * 3 * H + h * hd + d];
+        as[d] = 0.f;
+    }
+    float m = -INFINITY, l = 0.f;
+    for (int j = 0; j < N; ++j) {
+        const float* kr = base + (size_t)j * 3 * H + H + h * hd;
+        const float* vr = kr + H;
+        float dot = 0.f;
+        for (int d = 0; d < hd; ++d) dot = fmaf(qs[d], kr[d], dot);
+        float sc = dot * scale;
+        if (key_mask && key_mask[(size_t)b * N + j] == 0) sc = kMaskFill;
+        const float mn = fmaxf(m, sc);
+        const float corr = expf(m - mn), pj = expf(sc - mn);
+        l = l * corr + pj;
+        for (int d = 0; d < hd; ++d) as[d] = fmaf(pj, vr[d], as[d] * corr);
+        m = mn;
+    }
+    const float inv = 1.0f / l;
+    float* orow = out + ((size_t)b * N + q) * H + h * hd;
+    for (int d = 0; d < hd; ++d) orow[d] = as[d] * inv;
 }
 
 // ---------------------------------------------------------------------------
@@ -922,20 +964,32 @@ int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, in
     M2_CHECK_SHAPE(heads > 0 && H % heads == 0, "attention: H % heads != 0");
     const int hd = H / heads;
     if (B == 0 || N == 0) return M2_OK;
-    const float scale = (float)(1.0 / std::sqrt((double)hd));  // components.py:510, fp32 at the mul
-    // float4 reads of q/k/v rows: H and the head offsets must be 16-B aligned
-    M2_CHECK_SHAPE(H % 4 == 0, "attention: hidden_dim must be a multiple of 4");
+    const float scale = (float)(1.0 / std::sqrt((double)hd));  // components.py:52 (self.scale), fp32 at the mul
     dim3 grid(cdiv(N, 64), heads, B);
     // split-f16 MFMA by default; M2_ATT_F32=1: the exact-f32 MFMA kernel
     // (read per launch, so a process can switch: tests/test_gpu_parity.py)
     const char* env = std::getenv("M2_ATT_F32");
     const bool f32 = force_f32 || (env && *env && *env != '0');
+    // float4 reads of q/k/v rows in the MFMA kernels: H and the head offsets 16-B aligned
+    if (H % 4 != 0 || (hd != 16 && hd != 32 && hd != 48 && hd != 64)) {  // no MFMA instance: the generic kernel
+        M2_CHECK_SHAPE(hd <= 256, "attention: head_dim must be at most 256");
+        const size_t lds = (size_t)2 * 64 * hd * sizeof(float);
+        static bool attr = false;
+        if (!attr) {
+            M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attention_generic_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 256 * 4));
+            attr = true;
+        }
+        hipLaunchKernelGGL(attention_generic_kernel, grid, dim3(64), lds, st, qkv, mask, N, H, hd, scale, out);
+        M2_LAUNCHED("attention_generic_kernel");
+        return M2_OK;
+    }
     if (!f32) switch (hd) {
             case 16: return launch_att_split<16>(grid, qkv, mask, N, H, scale, out, st);
             case 32: return launch_att_split<32>(grid, qkv, mask, N, H, scale, out, st);
             case 48: return launch_att_split<48>(grid, qkv, mask, N, H, scale, out, st);
             case 64: return launch_att_split<64>(grid, qkv, mask, N, H, scale, out, st);
-            default: return fail(M2_E_SHAPE, "attention: head_dim must be 16, 32, 48 or 64");
+            default: break;
         }
     switch (hd) {
         case 16: hipLaunchKernelGGL(attention_kernel<16>, grid, dim3(256), 0, st, qkv, mask, N, H, scale, out); break;

@@ -1,0 +1,940 @@
+// One launch per pre-LN transformer layer (gfx950, split-f16 MFMA
+// v_mfma_f32_16x16x32_f16).
+//
+// layer_kernel computes, for a tile of 16 rows (queries) of ONE utterance:
+//   att = softmax(Q K^T * scale [+ -1e9 key mask]) V      both heads   (components.py:59-90)
+//   o   = x + att . Wo^T + bo                                           (components.py:86, 136-137)
+//   y   = o + W2 . relu(W1 . LN2(o) + b1) + b2                          (components.py:98-103, 139-140)
+// and then, on the same tile, the next launch's row-local work: the next
+// layer's LN1 -> QKV projection (components.py:55-56, 135), written straight
+// into the attention layouts below, or the decoder's final LN -> mel
+// projection (tts_model.py:225-228).  A stack of L layers is L + 1 launches
+// (the first LN1 -> QKV builds its own input rows: first_kernel), where the
+// three-launch form (ln_gemm / attention / post_attn, transformer_fused.hip)
+// needs 2L + 1, and the attention no longer re-splits K and V per query
+// block: the producing epilogue writes them as f16 hi/lo once.
+//
+// Attention layouts (TflBufs, one set per layer, ping-pong between layers):
+//   Q, K  [B*heads][npad][hi DP | lo DP] f16: one row per query / key, head
+//         dims padded to DP = 32 * ceil(hd / 32) with zeros; Q pre-scaled by
+//         scale * log2(e) when the attention is unmasked (the score is then the
+//         raw dot product, base 2);
+//   V^T   [B*heads][npad / 32][hd][hi 32 | lo 32] f16: per 32-key chunk, the
+//         keys of a row in the order the P^T fragment of the PV MFMA holds
+//         them (key 16 u + 4 g + e at position 8 g + 4 u + e).
+// A lane's MFMA operand is then one 16-B load: K rows are the A operand of
+// S^T = K . Q^T (16 keys x 32 dims), Q rows its B operand, V^T rows the A
+// operand of O^T += V^T . P^T.  These are L2-resident reads (the previous
+// launch wrote them); rows past N are zeros (the producing tiles write them).
+//
+// Workgroup = 8 waves, 16 rows of one utterance; the tiles of an utterance
+// get workgroup ids on one XCD (workgroup L runs on XCD L % 8) so its K / V
+// stay in that XCD's L2.  Attention: wave w = (head w / 4, key quarter w % 4)
+// takes the 32-key chunks c = w % 4 (mod 4) with its own online-softmax state
+// (the lazy rescaling of attention_split_kernel when unmasked); the four
+// quarters merge through LDS.  GEMMs: wave w computes the 16-column blocks
+// w, w + 8, ... as D^T = W . X^T (A = packed weights, B = split LDS rows), or
+// as D = X . W^T for the V columns, whose lanes then hold 4 consecutive keys
+// of one V^T row.  Arithmetic: every fp32 product as hi*hi + hi*lo + lo*hi
+// on f16 halves, LayerNorms / softmax / residuals in fp32.
+#include <cmath>
+#include <cstdlib>
+
+#include "m2_common.h"
+#include "transformer_layer.h"
+#include "vocoder_fused.h"  // split2u, vmax, vx_u32x4
+
+namespace m2 {
+namespace tfl {
+
+// Diagnostic build only (-DTFL_STAMPS, tools/probe/tfl_stamps.py): per-wave
+// s_memtime stamps at the phase boundaries of layer_kernel,
+// [workgroup][wave][16]; slots 14 / 15 = s_memrealtime (100 MHz) at start / end.
+#ifdef TFL_STAMPS
+__device__ unsigned long long g_tfl_stamps[4096][8][16];
+#define TSTAMP(i)                                                                                          \
+    do {                                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        unsigned long long _t;                                                                             \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                        \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) g_tfl_stamps[blockIdx.x][threadIdx.x >> 6][i] = _t; \
+    } while (0)
+#define TSTAMP_RT(i)                                                                                       \
+    do {                                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        unsigned long long _t;                                                                             \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+        __builtin_amdgcn_sched_barrier(0);                                                                 \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) g_tfl_stamps[blockIdx.x][threadIdx.x >> 6][i] = _t; \
+    } while (0)
+#else
+#define TSTAMP(i) \
+    do {          \
+    } while (0)
+#define TSTAMP_RT(i) \
+    do {             \
+    } while (0)
+#endif
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef vx_u32x4 u32x4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLazyT = 8.f;  // unmasked lazy rescale: weights stay <= 2^kLazyT
+constexpr int TQ = 16;         // rows (queries) per workgroup
+constexpr int NW = 8;          // waves per workgroup
+constexpr int KC = 32;         // keys per chunk
+constexpr int HEADS = 2;
+constexpr int WPH = NW / HEADS;  // waves per head (key quarters)
+
+__device__ __forceinline__ f32x4 mfma(u32x4 a, u32x4 b, f32x4 c) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+template <int HD>
+struct Geo {
+    static constexpr int KS = (HD + 31) / 32, DP = 32 * KS, MT = HD / 16;
+    static constexpr int QKROW = 4 * DP;    // bytes of a Q / K row
+    static constexpr int VROW = 128;        // bytes of a V^T row of one chunk
+    static constexpr int VCH = HD * VROW;   // bytes of a V^T chunk
+    static constexpr int XW = 2 + 4 * MT;   // merge record per lane (m, lsum, acc)
+};
+
+constexpr int srs(int K) { return 4 * K + 32; }  // split LDS row bytes (RS/16 = 2 mod 4: conflict-free b128 reads)
+constexpr int frs(int K) { return K + 4; }       // fp32 LDS row floats
+
+__device__ __forceinline__ float grp4_max(float x) {  // over the 4 lanes of one query (l, l^16, l^32, l^48)
+    x = vmax(x, __shfl_xor(x, 16));
+    return vmax(x, __shfl_xor(x, 32));
+}
+
+// An n-block's weight strip (pack_bfrag_split: [nb][ks][hi|lo][lane][8 f16]).
+template <int K>
+struct Strip {
+    u32x4 w[K / 32][2];
+    __device__ __forceinline__ void load(const u32x4* __restrict__ Wp, int nb) {
+        const u32x4* p = Wp + (size_t)nb * (K / 32) * 128 + (threadIdx.x & 63);
+#pragma unroll
+        for (int ks = 0; ks < K / 32; ++ks) {
+            w[ks][0] = p[ks * 128];
+            w[ks][1] = p[ks * 128 + 64];
+        }
+    }
+};
+
+// D^T = W . X^T over the 16 LDS rows X (split, stride srs(K)): lane (row
+// lane & 15) holds columns 4 (lane >> 4) + r of the block.
+template <int K>
+__device__ __forceinline__ f32x4 gemm_t(const unsigned char* X, const Strip<K>& st, f32x4 acc) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < K / 32; ++ks) {
+        const unsigned char* p = X + i * srs(K) + 2 * (32 * ks + 8 * g);
+        const u32x4 xh = *reinterpret_cast<const u32x4*>(p);
+        const u32x4 xl = *reinterpret_cast<const u32x4*>(p + 2 * K);
+        acc = mfma(st.w[ks][0], xh, acc);
+        acc = mfma(st.w[ks][0], xl, acc);
+        acc = mfma(st.w[ks][1], xh, acc);
+    }
+    return acc;
+}
+// D = X . W^T: lane holds rows 4 (lane >> 4) + r of column lane & 15.
+template <int K>
+__device__ __forceinline__ f32x4 gemm_n(const unsigned char* X, const Strip<K>& st, f32x4 acc) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < K / 32; ++ks) {
+        const unsigned char* p = X + i * srs(K) + 2 * (32 * ks + 8 * g);
+        const u32x4 xh = *reinterpret_cast<const u32x4*>(p);
+        const u32x4 xl = *reinterpret_cast<const u32x4*>(p + 2 * K);
+        acc = mfma(xh, st.w[ks][0], acc);
+        acc = mfma(xl, st.w[ks][0], acc);
+        acc = mfma(xh, st.w[ks][1], acc);
+    }
+    return acc;
+}
+
+// Four consecutive fp32 values -> their hi and lo f16 at p, p + 2K.
+template <int K>
+__device__ __forceinline__ void put_split4(unsigned char* p, float a, float b, float c, float d) {
+    unsigned h0, h1, l0, l1;
+    split2u(a, b, h0, l0);
+    split2u(c, d, h1, l1);
+    *reinterpret_cast<uint2*>(p) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(p + 2 * K) = uint2{l0, l1};
+}
+
+// LayerNorm (eps 1e-5, biased variance, affine) of the 16 fp32 LDS rows src
+// into split rows dst: 8 lanes per row, two-pass as nn.LayerNorm.
+template <int H>
+__device__ __forceinline__ void ln16(const float* src, unsigned char* dst, const float* __restrict__ g,
+                                     const float* __restrict__ b) {
+    constexpr int PER = H / 8;
+    static_assert(PER % 4 == 0, "H multiple of 32");
+    if (threadIdx.x >= 8 * TQ) return;
+    const int row = threadIdx.x >> 3, part = threadIdx.x & 7;
+    const float* xr = src + row * frs(H) + part * PER;
+    float v[PER];
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        const float4 t = *reinterpret_cast<const float4*>(xr + 4 * q);
+        v[4 * q] = t.x;
+        v[4 * q + 1] = t.y;
+        v[4 * q + 2] = t.z;
+        v[4 * q + 3] = t.w;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) s += v[k];
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    const float mean = s / (float)H;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const float d = v[k] - mean;
+        var += d * d;
+    }
+    var += __shfl_xor(var, 1);
+    var += __shfl_xor(var, 2);
+    var += __shfl_xor(var, 4);
+    const float rstd = 1.0f / sqrtf(var / (float)H + kLnEps);
+    unsigned char* yr = dst + row * srs(H) + 2 * part * PER;
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        float y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = part * PER + 4 * q + e;
+            y[e] = (v[4 * q + e] - mean) * rstd * g[k] + b[k];
+        }
+        put_split4<H>(yr + 8 * q, y[0], y[1], y[2], y[3]);
+    }
+}
+
+// Where a QKV projection's columns go (the attention layouts above).
+struct QkvOut {
+    unsigned char *q, *k, *v;
+    int npad, nch;
+    float qs;  // Q scale: scale * log2(e) for unmasked attention, else 1
+};
+
+// Q / K column block nb (< 2H/16) of the tile rows t0.. (D^T accumulator).
+template <int H, int HD>
+__device__ __forceinline__ void store_qk(const QkvOut& o, int b, int t0, int N, int nb, f32x4 acc) {
+    using G = Geo<HD>;
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const int which = nb / (H / 16), c0 = (nb - which * (H / 16)) * 16;
+    const int h = c0 / HD, dh = c0 - h * HD, d0 = dh + 4 * g;
+    const int t = t0 + i;
+    const bool live = t < N;
+    const float sc = which == 0 ? o.qs : 1.f;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = live ? acc[r] * sc : 0.f;
+    unsigned h0, h1, l0, l1;
+    split2u(v[0], v[1], h0, l0);
+    split2u(v[2], v[3], h1, l1);
+    unsigned char* row = (which ? o.k : o.q) + ((size_t)(b * HEADS + h) * o.npad + t) * G::QKROW;
+    *reinterpret_cast<uint2*>(row + 2 * d0) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(row + 2 * G::DP + 2 * d0) = uint2{l0, l1};
+    if constexpr (G::DP > HD) {
+        if (dh == HD - 16) {  // the head's last block also writes the zero padding dims
+            *reinterpret_cast<uint2*>(row + 2 * (HD + 4 * g)) = uint2{0u, 0u};
+            *reinterpret_cast<uint2*>(row + 2 * G::DP + 2 * (HD + 4 * g)) = uint2{0u, 0u};
+        }
+    }
+}
+
+// V column block nb (>= 2H/16) (D accumulator: rows t0 + 4g + r, column lane & 15).
+template <int H, int HD>
+__device__ __forceinline__ void store_v(const QkvOut& o, int b, int t0, int N, int nb, f32x4 acc) {
+    using G = Geo<HD>;
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const int c = (nb - 2 * (H / 16)) * 16 + i;
+    const int h = c / HD, d = c - h * HD;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (t0 + 4 * g + r < N) ? acc[r] : 0.f;
+    unsigned h0, h1, l0, l1;
+    split2u(v[0], v[1], h0, l0);
+    split2u(v[2], v[3], h1, l1);
+    const int p0 = 8 * g + 4 * ((t0 >> 4) & 1);  // keys 16u + 4g + e -> positions 8g + 4u + e
+    unsigned char* row = o.v + ((size_t)(b * HEADS + h) * o.nch + (t0 >> 5)) * G::VCH + d * G::VROW;
+    *reinterpret_cast<uint2*>(row + 2 * p0) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(row + 64 + 2 * p0) = uint2{l0, l1};
+}
+
+// The QKV projection of the tile's LN rows Xn into the attention layouts.
+template <int H, int HD>
+__device__ __forceinline__ void qkv_phase(const unsigned char* Xn, const u32x4* __restrict__ W, Strip<H>& cur,
+                                          const QkvOut& o, int b, int t0, int N) {
+    constexpr int NB = 3 * H / 16, NQK = 2 * H / 16;
+    const int wave = threadIdx.x >> 6;
+    const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int nb = wave; nb < NB; nb += NW) {
+        Strip<H> nxt;
+        if (nb + NW < NB) nxt.load(W, nb + NW);
+        if (nb < NQK) store_qk<H, HD>(o, b, t0, N, nb, gemm_t<H>(Xn, cur, z4));
+        else store_v<H, HD>(o, b, t0, N, nb, gemm_n<H>(Xn, cur, z4));
+        if (nb + NW < NB) cur = nxt;
+    }
+}
+
+// A tile wholly past the utterance's end: its rows of the next attention
+// buffers are zeros (no GEMM).
+template <int H, int HD>
+__device__ __forceinline__ void zero_tile(const QkvOut& o, int b, int t0) {
+    constexpr int NB = 3 * H / 16, NQK = 2 * H / 16;
+    const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = threadIdx.x >> 6; nb < NB; nb += NW) {
+        if (nb < NQK) store_qk<H, HD>(o, b, t0, 0, nb, z4);
+        else store_v<H, HD>(o, b, t0, 0, nb, z4);
+    }
+}
+
+// Utterance and tile of this workgroup (TflQueue): a claim on the queue of
+// the XCD the workgroup runs on - utterance b's tiles are in queue b % 8 - or,
+// when that queue is empty, on the next non-empty one.  The grid has exactly
+// one workgroup per tile and every queue scan ends with an empty queue, so
+// every tile is claimed once whatever the placement (XCD affinity only makes
+// it fast: a layer's K / V stay in the L2 of the XCD that wrote them).
+__device__ __forceinline__ void claim_tile(int B, int ntile, unsigned* __restrict__ cnt, unsigned seq, int* sh,
+                                           int* b, int* tile) {
+    if (threadIdx.x == 0) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        x &= 7;
+        unsigned* mine = cnt + (seq & 1) * 256;
+        if (blockIdx.x == 0)  // the next launch's set (the previous launch's, done by stream order)
+            for (int y = 0; y < 8; ++y)
+                __hip_atomic_store(cnt + ((seq + 1) & 1) * 256 + y * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int got = -1;
+        for (int k = 0; k < 8 && got < 0; ++k) {
+            const int y = (x + k) & 7;
+            const int n = (y < B ? (B - 1 - y) / 8 + 1 : 0) * ntile;
+            if (n == 0) continue;
+            const int i = (int)__hip_atomic_fetch_add(mine + y * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (i < n) got = (y + 8 * (i / ntile)) * ntile + (i - (i / ntile) * ntile);
+        }
+        *sh = got;
+    }
+    __syncthreads();
+    const int it = *sh;
+    *b = it / ntile;
+    *tile = it - *b * ntile;
+}
+
+// ---------------------------------------------------------------------------
+// Attention of the tile's 16 queries, both heads, over all N keys.  Leaves
+// the normalised output rows as split LDS rows A [16][srs(H)] (the out
+// projection's B operand).  The caller's `between` runs after the chunk loop,
+// before the merge (the first GEMM's weight strip is requested there).
+template <int H, int HD, bool MASKED, typename Between>
+__device__ __forceinline__ void attention_tile(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
+                                               const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
+                                               int len, float sl2, unsigned char* A, float* xs, Between between) {
+    using G = Geo<HD>;
+    constexpr int KS = G::KS, DP = G::DP, MT = G::MT, QKROW = G::QKROW, VCH = G::VCH, XW = G::XW;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, g = lane >> 4;
+    const int h = wave / WPH, kq = wave - h * WPH;
+    const int nch = npad / KC;
+    const size_t bh = (size_t)(b * HEADS + h);
+
+    // B = Q^T fragments: lane (query li, dims 32 ks + 8 g .. + 7)
+    u32x4 qh[KS], ql[KS];
+    {
+        const unsigned char* qp = qb + (bh * npad + t0 + li) * QKROW + 16 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            qh[ks] = *reinterpret_cast<const u32x4*>(qp + 64 * ks);
+            ql[ks] = *reinterpret_cast<const u32x4*>(qp + 2 * DP + 64 * ks);
+        }
+    }
+    // Chunk c's K rows and V^T block through a buffer descriptor whose record
+    // count is 0 past the last chunk: the prefetch of a chunk that does not
+    // exist is issued unconditionally (no branch around a load, so the
+    // compiler's vmcnt waits stay graded) and reads zeros without traffic.
+    const int koff = li * QKROW + 16 * g, voff = li * G::VROW + 16 * g;
+    struct Frag {
+        u32x4 kh[2][KS], kl[2][KS], vh[MT], vl[MT];
+    };
+    auto load = [&](Frag& f, int c) {
+        const bool ok = c < nch;
+        const auto rk = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<unsigned char*>(kb) + (bh * npad + (size_t)(ok ? c : 0) * KC) * QKROW, 0, ok ? KC * QKROW : 0,
+            0x00020000);
+        const auto rv = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<unsigned char*>(vb) + (bh * nch + (ok ? c : 0)) * VCH, 0, ok ? VCH : 0, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                f.kh[u][ks] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, koff + u * 16 * QKROW + 64 * ks, 0, 0));
+                f.kl[u][ks] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, koff + u * 16 * QKROW + 2 * DP + 64 * ks, 0, 0));
+            }
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            f.vh[t] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, voff + t * 16 * G::VROW, 0, 0));
+            f.vl[t] =
+                __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, voff + t * 16 * G::VROW + 64, 0, 0));
+        }
+    };
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = MASKED ? -INFINITY : 0.f, lsum = 0.f;
+    bool fresh = true;  // unmasked: no chunk processed yet (wave-uniform)
+
+    auto process = [&](const Frag& f, int c) {
+        const float nm = (MASKED || fresh) ? 0.f : -m;
+        float s[2][4];  // key 32 c + 16 u + 4 g + r of query li (base-2 score)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 st = f32x4{nm, nm, nm, nm};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                st = mfma(f.kh[u][ks], qh[ks], st);
+                st = mfma(f.kh[u][ks], ql[ks], st);
+                st = mfma(f.kl[u][ks], qh[ks], st);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[u][r] = st[r];
+        }
+        const int k0 = c * KC;
+        if constexpr (MASKED) {
+            // scores * scale, masked keys exactly the -1e9 fill, keys past N -inf
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = k0 + 16 * u + 4 * g + r;
+                    s[u][r] = key < len ? s[u][r] * sl2 : (key < N ? kMaskFill * kLog2e : -INFINITY);
+                }
+        } else if (N - k0 < KC) {  // the last chunk: keys past N score -inf (wave-uniform)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[u][r] = k0 + 16 * u + 4 * g + r < N ? s[u][r] : -INFINITY;
+        }
+        float cmax = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                           fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+        if constexpr (MASKED) {
+            const float mn = vmax(m, grp4_max(cmax));
+            const float corr = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first chunk -> 0
+            lsum *= corr;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[t] *= corr;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[u][r] -= mn;
+            m = mn;
+        } else {
+            const bool up = fresh || cmax > kLazyT;
+            if (__builtin_amdgcn_ballot_w64(up) != 0) {  // wave-uniform: move the base
+                const float cm = grp4_max(cmax);          // finite: every chunk has a live key
+                const float d = fresh ? cm : vmax(cm, 0.f);
+                m += d;
+                if (!fresh) {
+                    const float corr = __builtin_amdgcn_exp2f(-d);
+                    lsum *= corr;
+#pragma unroll
+                    for (int t = 0; t < MT; ++t) acc[t] *= corr;
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[u][r] -= d;
+            }
+            fresh = false;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                s[u][r] = __builtin_amdgcn_exp2f(s[u][r]);
+                lsum += s[u][r];
+            }
+        // B = P^T: lane (query li) holds keys 4g + e (u = 0) and 16 + 4g + e (u = 1)
+        unsigned ph[4], pl[4];
+        split2u(s[0][0], s[0][1], ph[0], pl[0]);
+        split2u(s[0][2], s[0][3], ph[1], pl[1]);
+        split2u(s[1][0], s[1][1], ph[2], pl[2]);
+        split2u(s[1][2], s[1][3], ph[3], pl[3]);
+        const u32x4 bh4 = u32x4{ph[0], ph[1], ph[2], ph[3]}, bl4 = u32x4{pl[0], pl[1], pl[2], pl[3]};
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            acc[t] = mfma(f.vh[t], bh4, acc[t]);
+            acc[t] = mfma(f.vh[t], bl4, acc[t]);
+            acc[t] = mfma(f.vl[t], bh4, acc[t]);
+        }
+    };
+
+    // chunks kq, kq + 4, ... through a two-slot register ring
+    const int nj = kq < nch ? (nch - kq + WPH - 1) / WPH : 0;
+    // The scheduling barriers keep each slot's loads in program order (slot 0
+    // before slot 1), so the wait at the top of an iteration is for the older
+    // slot only (vmcnt = one slot's loads); without them the scheduler put the
+    // first-consumed slot's loads last and the loop waited with vmcnt(0).
+    Frag f0, f1;
+    load(f0, kq);
+    __builtin_amdgcn_sched_barrier(0);
+    load(f1, kq + WPH);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+    for (int j = 0; j < nj; j += 2) {
+        process(f0, kq + WPH * j);
+        __builtin_amdgcn_sched_barrier(0);
+        load(f0, kq + WPH * (j + 2));
+        __builtin_amdgcn_sched_barrier(0);
+        if (j + 1 < nj) process(f1, kq + WPH * (j + 1));  // wave-uniform
+        __builtin_amdgcn_sched_barrier(0);
+        load(f1, kq + WPH * (j + 3));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    TSTAMP(1);
+    between();
+
+    // merge the four key quarters of each head through LDS
+    if (!MASKED && fresh) m = -INFINITY;  // this wave processed no chunk
+    float* xw = xs + (wave * 64 + lane) * XW;
+    xw[0] = m;
+    xw[1] = lsum;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xw[2 + 4 * t + r] = acc[t][r];
+    __syncthreads();
+    if (kq < MT) {  // wave (h, j = kq): output dims 16 j .. 16 j + 15 of head h
+        const int j = kq;
+        float mi[WPH], mx = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < WPH; ++q) {
+            mi[q] = xs[((h * WPH + q) * 64 + lane) * XW];
+            mx = vmax(mx, mi[q]);
+        }
+        float ls = 0.f, o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < WPH; ++q) {
+            const float* xq = xs + ((h * WPH + q) * 64 + lane) * XW;
+            const float fq = __builtin_amdgcn_exp2f(mi[q] - mx);
+            ls += xq[1] * fq;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] += xq[2 + 4 * j + r] * fq;
+        }
+        ls += __shfl_xor(ls, 16);
+        ls += __shfl_xor(ls, 32);
+        const float inv = 1.0f / ls;
+        put_split4<H>(A + li * srs(H) + 2 * (h * HD + 16 * j + 4 * g), o[0] * inv, o[1] * inv, o[2] * inv,
+                      o[3] * inv);
+    }
+    __syncthreads();
+    TSTAMP(2);
+}
+
+// ---------------------------------------------------------------------------
+struct LArgs {
+    int B, N, npad, ntile;
+    unsigned* qcnt;
+    unsigned qseq;
+    float sl2;  // scale * log2(e)
+    const int64_t* lengths;
+    const float* x_in;
+    float* x_out;
+    const unsigned char *q, *k, *v;
+    const u32x4 *Wo, *W1, *W2, *Wn;
+    const float *bo, *g2, *b2n, *b1, *b2, *gn, *bn, *bn2;
+    unsigned char *nq, *nk, *nv;
+    float* z;
+};
+
+template <int H, bool MASKED, int NEXT, int NN>
+__global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
+    constexpr int HD = H / HEADS, F = 2 * H;
+    __shared__ __attribute__((aligned(16))) unsigned char A[TQ * srs(H)];   // att, then LN2(o), LN(y) (split)
+    __shared__ __attribute__((aligned(16))) float O[TQ * frs(H)];           // o, then y (fp32)
+    __shared__ __attribute__((aligned(16))) unsigned char Hd[TQ * srs(F)];  // relu(FFN1) (split)
+    __shared__ __attribute__((aligned(16))) float xs[NW * 64 * Geo<HD>::XW];
+    // the layer's vectors, read once into LDS (their L2 latency otherwise sits
+    // in every LayerNorm and epilogue): bo | g2 | b2n | b1 [F] | b2 | gn | bn | bn2 [NN]
+    constexpr int VO = 0, VG2 = H, VB2N = 2 * H, VB1 = 3 * H, VB2 = 3 * H + F, VGN = 4 * H + F, VBN = 5 * H + F,
+                  VBN2 = 6 * H + F;
+    __shared__ __attribute__((aligned(16))) float vec[6 * H + F + (NN > 0 ? NN : 4)];
+    __shared__ int item;
+    int b, tile;
+    claim_tile(a.B, a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
+    const int t0 = tile * TQ, N = a.N;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
+    const QkvOut qo{a.nq, a.nk, a.nv, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
+    if (t0 >= N) {
+        if constexpr (NEXT == 1) zero_tile<H, HD>(qo, b, t0);
+        return;
+    }
+    for (int e = threadIdx.x; e < H; e += NW * 64) {
+        vec[VO + e] = a.bo[e];
+        vec[VG2 + e] = a.g2[e];
+        vec[VB2N + e] = a.b2n[e];
+        vec[VB2 + e] = a.b2[e];
+        if constexpr (NEXT != 0) {
+            vec[VGN + e] = a.gn[e];
+            vec[VBN + e] = a.bn[e];
+        }
+    }
+    for (int e = threadIdx.x; e < F; e += NW * 64) vec[VB1 + e] = a.b1[e];
+    if constexpr (NEXT == 2)
+        for (int e = threadIdx.x; e < NN; e += NW * 64) vec[VBN2 + e] = a.bn2[e];
+    TSTAMP_RT(14);
+    TSTAMP(0);
+    int len = N;
+    if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
+    Strip<H> so;
+    attention_tile<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs, [&] {
+        if (wave < H / 16) so.load(a.Wo, wave);
+    });
+    const size_t row0 = (size_t)b * N + t0;
+    const bool live = t0 + i < N;
+    // o = x + att . Wo^T + bo
+    if (wave < H / 16) {
+        const int nb = wave, col = nb * 16 + 4 * gq;
+        f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VO + col);
+        acc = gemm_t<H>(A, so, acc);
+        f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (live) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + i) * H + col);
+        *reinterpret_cast<f32x4*>(O + i * frs(H) + col) = x + acc;
+    }
+    Strip<H> s1;
+    if (wave < F / 16) s1.load(a.W1, wave);
+    __syncthreads();
+    TSTAMP(3);
+    ln16<H>(O, A, vec + VG2, vec + VB2N);
+    __syncthreads();
+    TSTAMP(4);
+    // h = relu(LN2(o) . W1^T + b1)
+#pragma unroll 1
+    for (int nb = wave; nb < F / 16; nb += NW) {
+        Strip<H> nxt;
+        if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
+        const int col = nb * 16 + 4 * gq;
+        f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
+        acc = gemm_t<H>(A, s1, acc);
+        put_split4<F>(Hd + i * srs(F) + 2 * col, acc[0] > 0.f ? acc[0] : 0.f, acc[1] > 0.f ? acc[1] : 0.f,
+                      acc[2] > 0.f ? acc[2] : 0.f, acc[3] > 0.f ? acc[3] : 0.f);
+        if (nb + NW < F / 16) s1 = nxt;
+    }
+    Strip<F> s2;
+    if (wave < H / 16) s2.load(a.W2, wave);
+    __syncthreads();
+    TSTAMP(5);
+    // y = o + h . W2^T + b2
+    if (wave < H / 16) {
+        const int col = wave * 16 + 4 * gq;
+        f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VB2 + col);
+        acc = gemm_t<F>(Hd, s2, acc);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(O + i * frs(H) + col) + acc;
+        if (live) *reinterpret_cast<f32x4*>(a.x_out + (row0 + i) * H + col) = y;
+        if constexpr (NEXT != 0) *reinterpret_cast<f32x4*>(O + i * frs(H) + col) = y;
+    }
+    if constexpr (NEXT == 1) {
+        Strip<H> sn;
+        if (wave < 3 * H / 16) sn.load(a.Wn, wave);
+        __syncthreads();
+        TSTAMP(6);
+        ln16<H>(O, A, vec + VGN, vec + VBN);
+        __syncthreads();
+        TSTAMP(7);
+        qkv_phase<H, HD>(A, a.Wn, sn, qo, b, t0, N);
+        TSTAMP(8);
+        TSTAMP_RT(15);
+    } else if constexpr (NEXT == 2) {
+        Strip<H> sn;
+        if (wave < NN / 16) sn.load(a.Wn, wave);
+        __syncthreads();
+        TSTAMP(6);
+        ln16<H>(O, A, vec + VGN, vec + VBN);
+        __syncthreads();
+        TSTAMP(7);
+#pragma unroll 1
+        for (int nb = wave; nb < NN / 16; nb += NW) {
+            Strip<H> nxt;
+            if (nb + NW < NN / 16) nxt.load(a.Wn, nb + NW);
+            const int col = nb * 16 + 4 * gq;
+            f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VBN2 + col);
+            acc = gemm_t<H>(A, sn, acc);
+            if (live) *reinterpret_cast<f32x4*>(a.z + (row0 + i) * NN + col) = acc;
+            if (nb + NW < NN / 16) sn = nxt;
+        }
+        TSTAMP(8);
+        TSTAMP_RT(15);
+    } else {
+        TSTAMP(6);
+        TSTAMP(7);
+        TSTAMP(8);
+        TSTAMP_RT(15);
+    }
+}
+
+// ---------------------------------------------------------------------------
+enum { SRC_X = 0, SRC_EMBED = 1, SRC_EXPAND = 2 };
+struct FArgs {
+    int B, N, npad, ntile;
+    unsigned* qcnt;
+    unsigned qseq;
+    float sl2;
+    const float* x_in;
+    const int64_t* ids;
+    const float *emb, *pe;
+    int vocab;
+    float escale;
+    const int64_t* lengths;
+    uint8_t* mask;
+    const float* enc;
+    const int32_t* cum;
+    int S;
+    float* x_out;
+    const float *g, *bln;
+    const u32x4* W;
+    unsigned char *q, *k, *v;
+};
+
+template <int H, int SRC, bool MASKED>
+__global__ __launch_bounds__(512, 2) void first_kernel(FArgs a) {
+    constexpr int HD = H / HEADS, H4 = H / 4;
+    __shared__ __attribute__((aligned(16))) float O[TQ * frs(H)];
+    __shared__ __attribute__((aligned(16))) unsigned char A[TQ * srs(H)];
+    __shared__ int sp[TQ];
+    __shared__ int item;
+    int b, tile;
+    claim_tile(a.B, a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
+    const int t0 = tile * TQ, N = a.N;
+    const int wave = threadIdx.x >> 6;
+    const QkvOut qo{a.q, a.k, a.v, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
+    if (t0 >= N) {
+        zero_tile<H, HD>(qo, b, t0);
+        return;
+    }
+    Strip<H> sq;
+    if (wave < 3 * H / 16) sq.load(a.W, wave);
+    __shared__ __attribute__((aligned(16))) float vec[2 * H];
+    for (int e = threadIdx.x; e < H; e += NW * 64) {
+        vec[e] = a.g[e];
+        vec[H + e] = a.bln[e];
+    }
+    if constexpr (SRC == SRC_EXPAND) {
+        // source phoneme of each frame: the smallest s with cum[s + 1] > t (-1: past the total)
+        if (threadIdx.x < TQ) {
+            const int t = t0 + threadIdx.x;
+            const int32_t* c = a.cum + (size_t)b * (a.S + 1);
+            int v = -1;
+            if (t < N && t < c[a.S]) {
+                int lo = 0, hi = a.S - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (c[mid + 1] > t) hi = mid;
+                    else lo = mid + 1;
+                }
+                v = b * a.S + lo;
+            }
+            sp[threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    for (int idx = threadIdx.x; idx < TQ * H4; idx += NW * 64) {
+        const int r = idx / H4, c = (idx - r * H4) * 4, t = t0 + r;
+        const size_t row = (size_t)b * N + t;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t < N) {
+            if constexpr (SRC == SRC_X) {
+                v = *reinterpret_cast<const float4*>(a.x_in + row * H + c);
+            } else if constexpr (SRC == SRC_EMBED) {
+                // tts_model.py:78-80: E[id] * sqrt(H) + pe[t]; ids outside the table read zeros
+                const int64_t id = a.ids[row];
+                float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (id >= 0 && id < a.vocab) e = *reinterpret_cast<const float4*>(a.emb + id * H + c);
+                const float4 p = *reinterpret_cast<const float4*>(a.pe + (size_t)t * H + c);
+                v = make_float4(__builtin_fmaf(e.x, a.escale, p.x), __builtin_fmaf(e.y, a.escale, p.y),
+                                __builtin_fmaf(e.z, a.escale, p.z), __builtin_fmaf(e.w, a.escale, p.w));
+                if (a.mask && c == 0) a.mask[row] = (int64_t)t < a.lengths[b] ? 1 : 0;  // components.py:236-240
+            } else {
+                const int q = sp[r];
+                if (q >= 0) v = *reinterpret_cast<const float4*>(a.enc + (size_t)q * H + c);
+            }
+            if constexpr (SRC != SRC_X) *reinterpret_cast<float4*>(a.x_out + row * H + c) = v;
+        }
+        *reinterpret_cast<float4*>(O + r * frs(H) + c) = v;
+    }
+    __syncthreads();
+    ln16<H>(O, A, vec, vec + H);
+    __syncthreads();
+    qkv_phase<H, HD>(A, a.W, sq, qo, b, t0, N);
+}
+
+}  // namespace tfl
+
+#ifdef TFL_STAMPS
+extern "C" int32_t m2_debug_stamps_tfl(void* host, size_t bytes) {
+    return (int32_t)hipMemcpyFromSymbol(host, HIP_SYMBOL(tfl::g_tfl_stamps),
+                                        bytes < sizeof(tfl::g_tfl_stamps) ? bytes : sizeof(tfl::g_tfl_stamps));
+}
+#endif
+
+// ---------------------------------------------------------------------------
+bool tfl_supported(int H, int heads) { return heads == 2 && (H == 32 || H == 64 || H == 96); }
+
+bool tfl_proj_supported(int H, int NN) {
+    return (H == 32 && (NN == 32 || NN == 64)) || (H == 64 && (NN == 64 || NN == 80)) ||
+           (H == 96 && (NN == 80 || NN == 96));
+}
+
+int tfl_npad(int N) { return (N + tfl::KC - 1) / tfl::KC * tfl::KC; }
+
+namespace {
+void tfl_sizes(int B, int N, int H, int heads, size_t* qk, size_t* v) {
+    const int HD = H / heads, DP = (HD + 31) / 32 * 32, npad = tfl_npad(N);
+    *qk = align_up((size_t)B * heads * npad * 4 * DP, 256);
+    *v = align_up((size_t)B * heads * (npad / tfl::KC) * HD * 128, 256);
+}
+}  // namespace
+
+size_t tfl_bytes(int B, int N, int H, int heads) {
+    size_t qk, v;
+    tfl_sizes(B, N, H, heads, &qk, &v);
+    return 2 * qk + v;
+}
+
+void tfl_carve(unsigned char* base, int B, int N, int H, int heads, TflBufs* out) {
+    size_t qk, v;
+    tfl_sizes(B, N, H, heads, &qk, &v);
+    *out = TflBufs{base, base + qk, base + 2 * qk};
+}
+
+namespace {
+dim3 tfl_grid(int B, int N) { return dim3(B * (tfl_npad(N) / tfl::TQ)); }
+float tfl_sl2(int H) {
+    const float scale = (float)(1.0 / std::sqrt((double)(H / tfl::HEADS)));  // components.py:52, fp32 at the mul
+    return scale * tfl::kLog2e;
+}
+}  // namespace
+
+int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool masked, float* x_out,
+                         const float* g, const float* bln, const float* Wqkv, const TflBufs& out, TflQueue q,
+                         hipStream_t st) {
+    M2_CHECK_SHAPE(tfl_supported(H, heads), "tfl: unsupported (hidden_dim, heads)");
+    M2_CHECK_ARG(q.cnt, "tfl: no work-queue counters");
+    if (B == 0 || N == 0) return M2_OK;
+    tfl::FArgs a{};
+    a.B = B;
+    a.N = N;
+    a.npad = tfl_npad(N);
+    a.ntile = a.npad / tfl::TQ;
+    a.qcnt = q.cnt;
+    a.qseq = q.seq;
+    a.sl2 = tfl_sl2(H);
+    a.x_in = f.x_in;
+    a.ids = f.ids;
+    a.emb = f.emb;
+    a.pe = f.pe;
+    a.vocab = f.vocab;
+    a.escale = f.escale;
+    a.lengths = f.lengths;
+    a.mask = f.lengths ? f.mask : nullptr;
+    a.enc = f.enc;
+    a.cum = f.cum;
+    a.S = f.S;
+    a.x_out = x_out;
+    a.g = g;
+    a.bln = bln;
+    a.W = reinterpret_cast<const vx_u32x4*>(Wqkv);
+    a.q = out.q;
+    a.k = out.k;
+    a.v = out.v;
+    const dim3 grid = tfl_grid(B, N), blk(tfl::NW * 64);
+#define M2_TFF(HH, SS, MM)                                                                      \
+    if (H == HH && f.src == SS && masked == MM) {                                               \
+        hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM>), grid, blk, 0, st, a);               \
+        M2_LAUNCHED("tfl first_kernel");                                                        \
+        return M2_OK;                                                                           \
+    }
+#define M2_TFF_H(HH)                  \
+    M2_TFF(HH, tfl::SRC_X, false)     \
+    M2_TFF(HH, tfl::SRC_X, true)      \
+    M2_TFF(HH, tfl::SRC_EMBED, false) \
+    M2_TFF(HH, tfl::SRC_EMBED, true)  \
+    M2_TFF(HH, tfl::SRC_EXPAND, false)
+    M2_TFF_H(32)
+    M2_TFF_H(64)
+    M2_TFF_H(96)
+#undef M2_TFF_H
+#undef M2_TFF
+    return fail(M2_E_SHAPE, "tfl first layer: unsupported (hidden_dim, row source, mask)");
+}
+
+int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool masked, const int64_t* lengths,
+                         const float* x_in, float* x_out, const TflBufs& in, int next, const TflBufs& out, int NN,
+                         float* z, TflQueue q, hipStream_t st) {
+    M2_CHECK_SHAPE(tfl_supported(H, heads), "tfl: unsupported (hidden_dim, heads)");
+    M2_CHECK_ARG(!masked || lengths, "tfl: masked attention needs lengths");
+    M2_CHECK_ARG(q.cnt, "tfl: no work-queue counters");
+    if (B == 0 || N == 0) return M2_OK;
+    auto u4 = [](const float* p) { return reinterpret_cast<const vx_u32x4*>(p); };
+    tfl::LArgs a{};
+    a.B = B;
+    a.N = N;
+    a.npad = tfl_npad(N);
+    a.ntile = a.npad / tfl::TQ;
+    a.qcnt = q.cnt;
+    a.qseq = q.seq;
+    a.sl2 = tfl_sl2(H);
+    a.lengths = lengths;
+    a.x_in = x_in;
+    a.x_out = x_out;
+    a.q = in.q;
+    a.k = in.k;
+    a.v = in.v;
+    a.Wo = u4(w.Wo);
+    a.W1 = u4(w.W1);
+    a.W2 = u4(w.W2);
+    a.Wn = u4(w.Wn);
+    a.bo = w.bo;
+    a.g2 = w.g2;
+    a.b2n = w.b2n;
+    a.b1 = w.b1;
+    a.b2 = w.b2;
+    a.gn = w.gn;
+    a.bn = w.bn;
+    a.bn2 = w.bn2;
+    a.nq = out.q;
+    a.nk = out.k;
+    a.nv = out.v;
+    a.z = z;
+    const dim3 grid = tfl_grid(B, N), blk(tfl::NW * 64);
+#define M2_TFL(HH, MM, NX, NNN)                                                                 \
+    if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
+        hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN>), grid, blk, 0, st, a);          \
+        M2_LAUNCHED("tfl layer_kernel");                                                        \
+        return M2_OK;                                                                           \
+    }
+#define M2_TFL_H(HH, P0, P1)     \
+    M2_TFL(HH, false, 0, 0)      \
+    M2_TFL(HH, false, 1, 0)      \
+    M2_TFL(HH, true, 0, 0)       \
+    M2_TFL(HH, true, 1, 0)       \
+    M2_TFL(HH, false, 2, P0)     \
+    M2_TFL(HH, false, 2, P1)
+    M2_TFL_H(32, 32, 64)
+    M2_TFL_H(64, 64, 80)
+    M2_TFL_H(96, 80, 96)
+#undef M2_TFL_H
+#undef M2_TFL
+    return fail(M2_E_SHAPE, "tfl layer: unsupported (hidden_dim, mask, next, projection width)");
+}
+
+}  // namespace m2

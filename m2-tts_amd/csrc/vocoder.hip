@@ -15,6 +15,8 @@
 //     ph + p <  r :  x[q]  * W[ph+p]    + x[q-1] * W[ph+p+r]
 //     ph + p >= r :  x[q+1]* W[ph+p-r]  + x[q]   * W[ph+p]
 // which is y[co,t] = b[co] + sum_ci sum_{i: k=t+p-i*r in [0,2r)} x[ci,i] W[ci,co,k].
+#include <climits>
+
 #include "m2_common.h"
 
 namespace m2 {
@@ -146,6 +148,49 @@ __global__ __launch_bounds__(256) void convT_kernel(const float* __restrict__ x,
     }
 }
 
+// Conv1d with any kernel size, dilation and zero padding (the standalone
+// components' general forms: LightweightResBlock(kernel_size, dilation),
+// ConvBlock(kernel_size), SimpleVocoder(kernel_size), components.py:143-200,
+// tts_model.py:246,272): y[co, t] = b[co] + sum_ci sum_j w[co, ci, j] *
+// x[ci, t - pad + j * dil], t < Lo = L + 2 pad - dil (K - 1), then the same
+// optional affine / activation / residual as conv_kernel.  Lanes own
+// consecutive output steps (coalesced along T), weights are wave-uniform.
+template <int CO_T>
+__global__ __launch_bounds__(256) void conv_general_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ alpha,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ res, int Cin, int Cout, int L,
+                                                           int Lo, int K, int dil, int pad, int act,
+                                                           float* __restrict__ y) {
+    const int b = blockIdx.z, co0 = blockIdx.y * CO_T;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= Lo) return;
+    const float* xb = x + (size_t)b * Cin * L;
+    float acc[CO_T];
+#pragma unroll
+    for (int c = 0; c < CO_T; ++c) acc[c] = 0.f;
+    for (int ci = 0; ci < Cin; ++ci) {
+        const float* xr = xb + (size_t)ci * L;
+        for (int j = 0; j < K; ++j) {
+            const int ti = t - pad + j * dil;
+            const float xv = (ti >= 0 && ti < L) ? xr[ti] : 0.f;
+#pragma unroll
+            for (int c = 0; c < CO_T; ++c) acc[c] = fmaf(w[((size_t)(co0 + c) * Cin + ci) * K + j], xv, acc[c]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < CO_T; ++c) {
+        const int co = co0 + c;
+        float v = acc[c] + bias[co];
+        if (alpha) v = v * alpha[co] + beta[co];
+        v = apply_act(v, act);
+        const size_t o = ((size_t)b * Cout + co) * Lo + t;
+        if (res) v = v + res[o];
+        y[o] = v;
+    }
+}
+
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kConvTT = 4;
@@ -206,6 +251,31 @@ int32_t launch_conv(const float* x, const float* w, const float* b, const float*
     if (ksize == 3) return conv_pick<3>(x, w, b, alpha, beta, res, act, x_transposed, B, Cin, Cout, L, y, st);
     if (ksize == 1) return conv_pick<1>(x, w, b, alpha, beta, res, act, x_transposed, B, Cin, Cout, L, y, st);
     return fail(M2_E_SHAPE, "conv: kernel size must be 1 or 3");
+}
+
+int32_t launch_conv_general(const float* x, const float* w, const float* b, const float* alpha, const float* beta,
+                            const float* res, int ksize, int dil, int pad, int act, int B, int Cin, int Cout, int L,
+                            float* y, hipStream_t st) {
+    M2_CHECK_SHAPE(Cin > 0 && Cout > 0 && ksize > 0 && dil > 0 && pad >= 0, "conv: bad kernel geometry");
+    M2_CHECK_ARG((alpha == nullptr) == (beta == nullptr), "conv: alpha and beta go together");
+    const long lo = (long)L + 2L * pad - (long)dil * (ksize - 1);
+    M2_CHECK_SHAPE(lo >= 0 && lo <= INT32_MAX, "conv: output length out of range");
+    const int Lo = (int)lo;
+    M2_CHECK_SHAPE(!res || Lo == L, "conv: a residual needs the output length to equal the input length");
+    if (B == 0 || Lo == 0) return M2_OK;
+    const int cot = Cout % 4 == 0 ? 4 : (Cout % 2 == 0 ? 2 : 1);
+    const dim3 grid(cdiv(Lo, 256), Cout / cot, B);
+    if (cot == 4)
+        hipLaunchKernelGGL((conv_general_kernel<4>), grid, dim3(256), 0, st, x, w, b, alpha, beta, res, Cin, Cout, L,
+                           Lo, ksize, dil, pad, act, y);
+    else if (cot == 2)
+        hipLaunchKernelGGL((conv_general_kernel<2>), grid, dim3(256), 0, st, x, w, b, alpha, beta, res, Cin, Cout, L,
+                           Lo, ksize, dil, pad, act, y);
+    else
+        hipLaunchKernelGGL((conv_general_kernel<1>), grid, dim3(256), 0, st, x, w, b, alpha, beta, res, Cin, Cout, L,
+                           Lo, ksize, dil, pad, act, y);
+    M2_LAUNCHED("conv_general_kernel");
+    return M2_OK;
 }
 
 int32_t launch_convT(const float* x, const float* w, const float* b, int rate, int act, int B,

@@ -82,17 +82,29 @@ def attention_core(qkv: Tensor, heads: int, key_mask: Optional[Tensor]) -> Tenso
 
 
 def conv1d(x: Tensor, weight: Tensor, bias: Tensor, *, act: int = ACT_NONE,
-           affine: Optional[tuple] = None, residual: Optional[Tensor] = None) -> Tensor:
-    """Conv1d(k=1|3, padding=k//2) [+ per-channel affine] [+ act] [+ residual], x [B,Cin,L]."""
+           affine: Optional[tuple] = None, residual: Optional[Tensor] = None, dilation: int = 1,
+           padding: Optional[int] = None) -> Tensor:
+    """Conv1d(k, dilation, zero padding (default k//2)) [+ per-channel affine]
+    [+ act] [+ residual], x [B,Cin,L] -> [B,Cout,L + 2 pad - dil (k - 1)].
+    k = 1 | 3 with dilation 1 and padding k//2 run the tiled kernel
+    (m2_conv1d); every other geometry the general one (m2_conv1d_ex)."""
     require_device(x, weight, what="conv1d")
     x = f32c(x)
     B, Cin, L = x.shape
     Cout, _, K = weight.shape
-    y = torch.empty(B, Cout, L, device=x.device, dtype=torch.float32)
+    pad = K // 2 if padding is None else int(padding)
+    Lo = L + 2 * pad - dilation * (K - 1)
+    if residual is not None and Lo != L:
+        raise RuntimeError(f"conv1d: output length {Lo} != input length {L}: the residual add has mismatched shapes")
+    y = torch.empty(B, Cout, max(Lo, 0), device=x.device, dtype=torch.float32)
     al, be = affine if affine is not None else (None, None)
     res = f32c(residual) if residual is not None else None
-    _lib.call("m2_conv1d", _ptr(x), _ptr(f32c(weight)), _ptr(f32c(bias)), _ptr(al), _ptr(be), _ptr(res), K, act,
-              B, Cin, Cout, L, _ptr(y), stream_handle(x.device))
+    if K in (1, 3) and dilation == 1 and pad == K // 2:
+        _lib.call("m2_conv1d", _ptr(x), _ptr(f32c(weight)), _ptr(f32c(bias)), _ptr(al), _ptr(be), _ptr(res), K, act,
+                  B, Cin, Cout, L, _ptr(y), stream_handle(x.device))
+    else:
+        _lib.call("m2_conv1d_ex", _ptr(x), _ptr(f32c(weight)), _ptr(f32c(bias)), _ptr(al), _ptr(be), _ptr(res), K,
+                  int(dilation), pad, act, B, Cin, Cout, L, _ptr(y), stream_handle(x.device))
     return y
 
 

@@ -126,12 +126,15 @@ class ConvBlock(nn.Module):
         _eval_only(self)
         n = self.norm
         affine = ops.batchnorm_eval_affine(n.weight, n.bias, n.running_mean, n.running_var, n.eps)
-        return ops.conv1d(x, self.conv.weight, self.conv.bias, affine=affine, act=ops.ACT_RELU)
+        return ops.conv1d(x, self.conv.weight, self.conv.bias, affine=affine, act=ops.ACT_RELU,
+                          padding=self.conv.padding[0])
 
 
 class LightweightResBlock(nn.Module):
-    """conv2(leaky(conv1(x), 0.1)) + x, both k=3 (reference components.py:177-200).
-    Only dilation 1 (the only value the reference vocoder uses) is implemented."""
+    """conv2(leaky(conv1(x), 0.1)) + x (reference components.py:177-200): conv1
+    with ``dilation`` and padding (k-1)*dilation//2, conv2 undilated.  An even
+    kernel size changes the length, so the residual add fails, as in the
+    reference."""
 
     def __init__(self, channels: int, kernel_size: int = 3, dilation: int = 1):
         super().__init__()
@@ -144,10 +147,9 @@ class LightweightResBlock(nn.Module):
         return (kernel_size - 1) * dilation // 2
 
     def forward(self, x: Tensor) -> Tensor:
-        if self.conv1.kernel_size[0] != 3 or self.conv1.dilation[0] != 1:
-            raise NotImplementedError("m2-tts_amd LightweightResBlock: kernel_size 3, dilation 1 only")
-        h = ops.conv1d(x, self.conv1.weight, self.conv1.bias, act=ops.ACT_LEAKY)
-        return ops.conv1d(h, self.conv2.weight, self.conv2.bias, residual=x)
+        h = ops.conv1d(x, self.conv1.weight, self.conv1.bias, act=ops.ACT_LEAKY, dilation=self.conv1.dilation[0],
+                       padding=self.conv1.padding[0])
+        return ops.conv1d(h, self.conv2.weight, self.conv2.bias, residual=x, padding=self.conv2.padding[0])
 
 
 class VariancePredictor(nn.Module):
@@ -162,7 +164,7 @@ class VariancePredictor(nn.Module):
     def forward(self, x: Tensor, _act: int = ops.ACT_NONE) -> Tensor:
         for blk in self.conv_layers:
             x = blk(x)
-        return ops.conv1d(x, self.projection.weight, self.projection.bias, act=_act)
+        return ops.conv1d(x, self.projection.weight, self.projection.bias, act=_act, padding=0)
 
 
 def create_padding_mask(lengths: Tensor, max_length: int) -> Tensor:

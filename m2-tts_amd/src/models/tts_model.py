@@ -154,13 +154,15 @@ class SimpleVocoder(nn.Module):
         hm = _owner_handle(self, "vocoder", mel.device)
         if hm is not None:
             return hm.vocoder(mel, layout_btm=False)
-        if self.input_conv.kernel_size[0] != 3:
-            raise NotImplementedError("m2-tts_amd SimpleVocoder: kernel_size 3 only")
-        x = ops.conv1d(mel, self.input_conv.weight, self.input_conv.bias)
+        # any kernel_size: input / output convs with padding k//2 and the
+        # resblocks' general form (an even k changes lengths and the resblock
+        # residual fails, as in the reference)
+        x = ops.conv1d(mel, self.input_conv.weight, self.input_conv.bias, padding=self.input_conv.padding[0])
         for r, up, rb in zip(UPSAMPLE_RATES, self.upsamples, self.resblocks):
             x = ops.conv_transpose1d(x, up.weight, up.bias, r, act=ops.ACT_LEAKY)
             x = rb(x)
-        return ops.conv1d(x, self.output_conv.weight, self.output_conv.bias, act=ops.ACT_TANH)
+        return ops.conv1d(x, self.output_conv.weight, self.output_conv.bias, act=ops.ACT_TANH,
+                          padding=self.output_conv.padding[0])
 
     def stream(self, mel: Tensor, chunk_frames: int = 256):
         """Yield the audio of mel [B, M, T] chunk by chunk ([B, 1, 64 n] for

@@ -35,7 +35,7 @@ Tensor = torch.Tensor
 UPSAMPLE_RATES = (4, 4, 2, 2)
 LN_EPS = 1e-5          # nn.LayerNorm default (components.py:136-137)
 BN_EPS = 1e-5          # nn.BatchNorm1d default (components.py:160)
-MASK_FILL = -1e9       # components.py:539 masked_fill value
+MASK_FILL = -1e9       # components.py:81 masked_fill_ value
 LEAKY = 0.1            # tts_model.py:291, components.py:198
 
 
@@ -115,10 +115,14 @@ def conv_block(sd: Dict[str, Tensor], p: str, x: Tensor) -> Tensor:
     return F.relu(x)
 
 
-def resblock(sd: Dict[str, Tensor], p: str, x: Tensor) -> Tensor:
-    """LightweightResBlock.forward, components.py:196-200 (dilation 1)."""
-    y = F.leaky_relu(F.conv1d(x, sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], padding=1), LEAKY)
-    y = F.conv1d(y, sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], padding=1)
+def resblock(sd: Dict[str, Tensor], p: str, x: Tensor, dilation: int = 1) -> Tensor:
+    """LightweightResBlock.forward, components.py:196-200: conv1 with
+    `dilation` and padding (k-1)*dilation//2 (components.py:180-189), conv2
+    undilated with padding (k-1)//2 (the vocoder uses k=3, dilation 1)."""
+    k = sd[p + ".conv1.weight"].shape[-1]
+    y = F.leaky_relu(F.conv1d(x, sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], padding=(k - 1) * dilation // 2,
+                              dilation=dilation), LEAKY)
+    y = F.conv1d(y, sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], padding=(k - 1) // 2)
     return y + x
 
 
@@ -185,12 +189,14 @@ def mel_decoder(sd: Dict[str, Tensor], cfg: OracleConfig, x: Tensor) -> Tensor:
 
 
 def vocoder(sd: Dict[str, Tensor], mel_bmt: Tensor) -> Tensor:
-    """SimpleVocoder.forward, tts_model.py:279-297; mel [B,M,T] -> audio [B,1,64T]."""
-    x = F.conv1d(mel_bmt, sd["vocoder.input_conv.weight"], sd["vocoder.input_conv.bias"], padding=1)
+    """SimpleVocoder.forward, tts_model.py:279-297; mel [B,M,T] -> audio [B,1,64T].
+    Convs pad kernel_size // 2 (tts_model.py:246, 272; kernel_size 3 in M2TTSModel)."""
+    ks = sd["vocoder.input_conv.weight"].shape[-1]
+    x = F.conv1d(mel_bmt, sd["vocoder.input_conv.weight"], sd["vocoder.input_conv.bias"], padding=ks // 2)
     for k, r in enumerate(UPSAMPLE_RATES):
         x = F.leaky_relu(conv_transpose(sd, f"vocoder.upsamples.{k}", x, r), LEAKY)
         x = resblock(sd, f"vocoder.resblocks.{k}", x)
-    return torch.tanh(F.conv1d(x, sd["vocoder.output_conv.weight"], sd["vocoder.output_conv.bias"], padding=1))
+    return torch.tanh(F.conv1d(x, sd["vocoder.output_conv.weight"], sd["vocoder.output_conv.bias"], padding=ks // 2))
 
 
 def forward(sd: Dict[str, Tensor], cfg: OracleConfig, ids: Tensor,

@@ -1,0 +1,66 @@
+// Per-CU read bandwidth of L2-resident data (the one-launch transformer
+// layer's K / V and weight reads): every workgroup of a 256-workgroup grid
+// (one per CU) reads `per_wg` bytes of a buffer that all workgroups on its
+// XCD share (workgroup L reads slice L % 8), 16-B loads, `inflight` loads per
+// lane in flight.  Prints GB/s per CU and chip-wide.
+//   hipcc --offload-arch=gfx950 -O3 tools/probe/l2bw.hip -o tools/probe/l2bw.bin
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int INF>
+__global__ __launch_bounds__(512) void rd(const u32x4* __restrict__ buf, size_t slice_elems, int per_wg_elems,
+                                          unsigned* __restrict__ out) {
+    const u32x4* p = buf + (size_t)(blockIdx.x & 7) * slice_elems;
+    unsigned acc = 0;
+    const int stride = blockDim.x * INF;
+    for (int base = threadIdx.x; base < per_wg_elems; base += stride) {
+        u32x4 v[INF];
+#pragma unroll
+        for (int i = 0; i < INF; ++i) {
+            const int e = base + i * blockDim.x;
+            v[i] = e < per_wg_elems ? p[e] : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int i = 0; i < INF; ++i) acc ^= v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+    if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
+int main(int argc, char** argv) {
+    const int per_wg = argc > 1 ? atoi(argv[1]) : 448 * 1024;
+    const int grid = argc > 2 ? atoi(argv[2]) : 256;
+    const int threads = argc > 3 ? atoi(argv[3]) : 512;
+    const size_t slice = (per_wg + 15) / 16;
+    u32x4* buf;
+    unsigned* out;
+    hipMalloc(&buf, slice * 8 * 16);
+    hipMalloc(&out, 4096 * 4);
+    hipMemset(buf, 1, slice * 8 * 16);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    for (int inf : {4, 8, 16}) {
+        auto launch = [&] {
+            if (inf == 4) hipLaunchKernelGGL(rd<4>, dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 8) hipLaunchKernelGGL(rd<8>, dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 16) hipLaunchKernelGGL(rd<16>, dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+        };
+        for (int i = 0; i < 50; ++i) launch();
+        hipDeviceSynchronize();
+        const int n = 200;
+        hipEventRecord(a);
+        for (int i = 0; i < n; ++i) launch();
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        const double us = ms * 1e3 / n;
+        const double per_cu = (double)per_wg / (us * 1e-6) / 1e9;
+        printf("per_wg %d B, grid %d x %d threads, %2d loads/lane in flight: %.2f us/launch, %.1f GB/s per WG, %.2f TB/s chip\n",
+               per_wg, grid, threads, inf, us, per_cu, per_cu * grid / 1e3);
+    }
+    return 0;
+}

@@ -19,8 +19,10 @@ def summarize(path, steps=20):
     en = [int(r["End_Timestamp"]) for r in rows]
     # a step starts at the embedding kernel (first kernel of m2_inference_front;
     # with the fused first layer, ln_gemm_kernel<..., SRC_EMBED = 1>)
+    # (one-launch layers: m2::tfl::first_kernel<H, SRC_EMBED = 1, ...>)
     starts = [i for i, n in enumerate(names) if "embed" in n or (n.startswith("m2::tfx::ln_gemm_kernel") and
-                                                                   n.endswith(", 1>"))]
+                                                                   n.endswith(", 1>")) or
+              (n.startswith("m2::tfl::first_kernel") and ", 1," in n)]
     starts = starts[-steps - 1:]
     per = {}
     spans, busy = [], []
