@@ -507,7 +507,7 @@ def pipeline_line(cx: Ctx, B: int, S: int, args, settle_ms: float):
                        "per_gpu_batch": B, "global_batch": B * cx.world, "phonemes": S, "mel_frames": T}}
 
 
-def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, steps: int):
+def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, steps: int, share: bool = False):
     """stage2 inference over a global batch of Bg utterances sharded across the
     ranks (configs[3] / [4]): one m2_inference_front + RCCL all_reduce(MAX) +
     m2_inference_back + all_gather of mel / audio per step."""
@@ -521,7 +521,8 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
         lens = torch.full((Bg,), S, dtype=torch.long, device=cx.dev)
         st = hip_stages(m)
         # the global batch's mel / audio are gathered to rank 0 (RCCL gather over xGMI)
-        step = lambda: sharded_inference(st, ids, lens, gather_to=0)  # noqa: E731
+        # share: one rank's two-phase flow (front, T exchange, back) timed alone
+        step = lambda: sharded_inference(st, ids, lens, gather_to=0, one_call_world1=not share)  # noqa: E731
         mel, audio = step()
         T = 5 * S  # pinned durations: every utterance has 5 frames per phoneme
         if cx.rank == 0:
@@ -631,7 +632,8 @@ def run(args):
         if world == 1:
             # the per-GPU share of configs[3] at N=8 (8 utterances), run alone:
             # what bounds a small per-GPU batch (host phases vs GPU-elapsed)
-            extras["s2_b8_per_gpu_share"] = sharded_line(cx, 8, 100, 0, args, 100.0, max(20, args.steps // 2))
+            extras["s2_b8_per_gpu_share"] = sharded_line(cx, 8, 100, 0, args, 100.0, max(20, args.steps // 2),
+                                                         share=True)
         if wl != "s2_longform":
             extras["s2_longform_sharded"] = sharded_line(cx, 128, 520, 256, args, 100.0, max(3, args.steps // 40))
 

@@ -14,18 +14,25 @@
 // needs 2L + 1, and the attention no longer re-splits K and V per query
 // block: the producing epilogue writes them as f16 hi/lo once.
 //
-// Attention layouts (TflBufs, one set per layer, ping-pong between layers):
-//   Q, K  [B*heads][npad][hi DP | lo DP] f16: one row per query / key, head
-//         dims padded to DP = 32 * ceil(hd / 32) with zeros; Q pre-scaled by
+// Attention layouts (TflBufs, one set per layer, ping-pong between layers),
+// all in MFMA-fragment order: a 1-KB fragment holds the 16 B of each of the 64
+// lanes of one v_mfma_f32_16x16x32_f16 operand, lane-contiguous, so every
+// operand load of the consumer is one 1-KB contiguous wave read (a load of 16
+// rows x 64 B - the row-major form - ran at 34 GB/s per CU against 82 GB/s
+// contiguous from L2, tools/probe/l2bw.hip):
+//   Q, K  [B*heads][npad/16 row blocks][KS k-steps][hi|lo][lane][8 f16]: lane
+//         (row li, group g) of k-step ks holds dims 32 ks + 8 g .. + 7 of row
+//         16 blk + li; dims padded to DP = 32 * KS with zeros; Q pre-scaled by
 //         scale * log2(e) when the attention is unmasked (the score is then the
 //         raw dot product, base 2);
-//   V^T   [B*heads][npad / 32][hd][hi 32 | lo 32] f16: per 32-key chunk, the
-//         keys of a row in the order the P^T fragment of the PV MFMA holds
+//   V^T   [B*heads][npad/32 chunks][hd/16 blocks][hi|lo][lane][8 f16]: lane
+//         (dim 16 t + li, group g) holds the chunk's keys at positions
+//         8 g .. + 7, keys in the order the P^T fragment of the PV MFMA holds
 //         them (key 16 u + 4 g + e at position 8 g + 4 u + e).
-// A lane's MFMA operand is then one 16-B load: K rows are the A operand of
-// S^T = K . Q^T (16 keys x 32 dims), Q rows its B operand, V^T rows the A
-// operand of O^T += V^T . P^T.  These are L2-resident reads (the previous
-// launch wrote them); rows past N are zeros (the producing tiles write them).
+// K fragments are the A operand of S^T = K . Q^T (16 keys x 32 dims), Q
+// fragments its B operand, V^T fragments the A operand of O^T += V^T . P^T.
+// These are L2-resident reads (the previous launch wrote them); rows past N
+// are zeros (the producing tiles write them).
 //
 // Workgroup = 8 waves, 16 rows of one utterance; the tiles of an utterance
 // get workgroup ids on one XCD (workgroup L runs on XCD L % 8) so its K / V
@@ -96,10 +103,9 @@ __device__ __forceinline__ f32x4 mfma(u32x4 a, u32x4 b, f32x4 c) {
 template <int HD>
 struct Geo {
     static constexpr int KS = (HD + 31) / 32, DP = 32 * KS, MT = HD / 16;
-    static constexpr int QKROW = 4 * DP;    // bytes of a Q / K row
-    static constexpr int VROW = 128;        // bytes of a V^T row of one chunk
-    static constexpr int VCH = HD * VROW;   // bytes of a V^T chunk
-    static constexpr int XW = 2 + 4 * MT;   // merge record per lane (m, lsum, acc)
+    static constexpr int QKBLK = KS * 2048;  // bytes of a 16-row Q / K block (KS k-steps x hi|lo x 1 KB)
+    static constexpr int VCH = MT * 2048;    // bytes of a V^T chunk (MT d-blocks x hi|lo x 1 KB)
+    static constexpr int XW = 2 + 4 * MT;    // merge record per lane (m, lsum, acc)
 };
 
 constexpr int srs(int K) { return 4 * K + 32; }  // split LDS row bytes (RS/16 = 2 mod 4: conflict-free b128 reads)
@@ -124,36 +130,49 @@ struct Strip {
     }
 };
 
-// D^T = W . X^T over the 16 LDS rows X (split, stride srs(K)): lane (row
-// lane & 15) holds columns 4 (lane >> 4) + r of the block.
-template <int K>
-__device__ __forceinline__ f32x4 gemm_t(const unsigned char* X, const Strip<K>& st, f32x4 acc) {
+// D^T = W . X^T over RB 16-row blocks of the LDS rows X (split, stride
+// srs(K)): acc[rb] lane (row rb*16 + (lane & 15)) holds columns 4 (lane >> 4)
+// + r of the block; every weight fragment feeds the RB blocks.
+template <int K, int RB>
+__device__ __forceinline__ void gemm_t(const unsigned char* X, const Strip<K>& st, f32x4 (&acc)[RB]) {
     const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
 #pragma unroll
     for (int ks = 0; ks < K / 32; ++ks) {
-        const unsigned char* p = X + i * srs(K) + 2 * (32 * ks + 8 * g);
-        const u32x4 xh = *reinterpret_cast<const u32x4*>(p);
-        const u32x4 xl = *reinterpret_cast<const u32x4*>(p + 2 * K);
-        acc = mfma(st.w[ks][0], xh, acc);
-        acc = mfma(st.w[ks][0], xl, acc);
-        acc = mfma(st.w[ks][1], xh, acc);
+        u32x4 xh[RB], xl[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const unsigned char* p = X + (rb * 16 + i) * srs(K) + 2 * (32 * ks + 8 * g);
+            xh[rb] = *reinterpret_cast<const u32x4*>(p);
+            xl[rb] = *reinterpret_cast<const u32x4*>(p + 2 * K);
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma(st.w[ks][0], xh[rb], acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma(st.w[ks][0], xl[rb], acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma(st.w[ks][1], xh[rb], acc[rb]);
     }
-    return acc;
 }
-// D = X . W^T: lane holds rows 4 (lane >> 4) + r of column lane & 15.
-template <int K>
-__device__ __forceinline__ f32x4 gemm_n(const unsigned char* X, const Strip<K>& st, f32x4 acc) {
+// D = X . W^T: acc[rb] lane holds rows rb*16 + 4 (lane >> 4) + r of column lane & 15.
+template <int K, int RB>
+__device__ __forceinline__ void gemm_n(const unsigned char* X, const Strip<K>& st, f32x4 (&acc)[RB]) {
     const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
 #pragma unroll
     for (int ks = 0; ks < K / 32; ++ks) {
-        const unsigned char* p = X + i * srs(K) + 2 * (32 * ks + 8 * g);
-        const u32x4 xh = *reinterpret_cast<const u32x4*>(p);
-        const u32x4 xl = *reinterpret_cast<const u32x4*>(p + 2 * K);
-        acc = mfma(xh, st.w[ks][0], acc);
-        acc = mfma(xl, st.w[ks][0], acc);
-        acc = mfma(xh, st.w[ks][1], acc);
+        u32x4 xh[RB], xl[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const unsigned char* p = X + (rb * 16 + i) * srs(K) + 2 * (32 * ks + 8 * g);
+            xh[rb] = *reinterpret_cast<const u32x4*>(p);
+            xl[rb] = *reinterpret_cast<const u32x4*>(p + 2 * K);
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma(xh[rb], st.w[ks][0], acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma(xl[rb], st.w[ks][0], acc[rb]);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = mfma(xh[rb], st.w[ks][1], acc[rb]);
     }
-    return acc;
 }
 
 // Four consecutive fp32 values -> their hi and lo f16 at p, p + 2K.
@@ -166,14 +185,13 @@ __device__ __forceinline__ void put_split4(unsigned char* p, float a, float b, f
     *reinterpret_cast<uint2*>(p + 2 * K) = uint2{l0, l1};
 }
 
-// LayerNorm (eps 1e-5, biased variance, affine) of the 16 fp32 LDS rows src
-// into split rows dst: 8 lanes per row, two-pass as nn.LayerNorm.
-template <int H>
-__device__ __forceinline__ void ln16(const float* src, unsigned char* dst, const float* __restrict__ g,
-                                     const float* __restrict__ b) {
+// LayerNorm (eps 1e-5, biased variance, affine) of R fp32 LDS rows src into
+// split rows dst: 8 lanes per row, two-pass as nn.LayerNorm; g, b in LDS.
+template <int H, int R>
+__device__ __forceinline__ void ln_rows(const float* src, unsigned char* dst, const float* g, const float* b) {
     constexpr int PER = H / 8;
     static_assert(PER % 4 == 0, "H multiple of 32");
-    if (threadIdx.x >= 8 * TQ) return;
+    if (threadIdx.x >= 8 * R) return;
     const int row = threadIdx.x >> 3, part = threadIdx.x & 7;
     const float* xr = src + row * frs(H) + part * PER;
     float v[PER];
@@ -222,7 +240,7 @@ struct QkvOut {
     float qs;  // Q scale: scale * log2(e) for unmasked attention, else 1
 };
 
-// Q / K column block nb (< 2H/16) of the tile rows t0.. (D^T accumulator).
+// Q / K column block nb (< 2H/16) of the 16 rows t0.. (D^T accumulator).
 template <int H, int HD>
 __device__ __forceinline__ void store_qk(const QkvOut& o, int b, int t0, int N, int nb, f32x4 acc) {
     using G = Geo<HD>;
@@ -238,18 +256,24 @@ __device__ __forceinline__ void store_qk(const QkvOut& o, int b, int t0, int N, 
     unsigned h0, h1, l0, l1;
     split2u(v[0], v[1], h0, l0);
     split2u(v[2], v[3], h1, l1);
-    unsigned char* row = (which ? o.k : o.q) + ((size_t)(b * HEADS + h) * o.npad + t) * G::QKROW;
-    *reinterpret_cast<uint2*>(row + 2 * d0) = uint2{h0, h1};
-    *reinterpret_cast<uint2*>(row + 2 * G::DP + 2 * d0) = uint2{l0, l1};
+    // fragment order: dims d0 .. d0+3 of row t are half (d0 % 8) / 4 of lane
+    // ((d0 % 32) / 8) * 16 + t % 16 in k-step d0 / 32 of row block t / 16
+    unsigned char* blk = (which ? o.k : o.q) + ((size_t)(b * HEADS + h) * (o.npad / 16) + t / 16) * G::QKBLK;
+    auto piece = [&](int d) { return blk + (d / 32) * 2048 + ((((d & 31) >> 3) * 16 + (t & 15)) * 16) + ((d & 7) >> 2) * 8; };
+    unsigned char* ph = piece(d0);
+    *reinterpret_cast<uint2*>(ph) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(ph + 1024) = uint2{l0, l1};
     if constexpr (G::DP > HD) {
         if (dh == HD - 16) {  // the head's last block also writes the zero padding dims
-            *reinterpret_cast<uint2*>(row + 2 * (HD + 4 * g)) = uint2{0u, 0u};
-            *reinterpret_cast<uint2*>(row + 2 * G::DP + 2 * (HD + 4 * g)) = uint2{0u, 0u};
+            unsigned char* pz = piece(HD + 4 * g);
+            *reinterpret_cast<uint2*>(pz) = uint2{0u, 0u};
+            *reinterpret_cast<uint2*>(pz + 1024) = uint2{0u, 0u};
         }
     }
 }
 
-// V column block nb (>= 2H/16) (D accumulator: rows t0 + 4g + r, column lane & 15).
+// V column block nb (>= 2H/16) of the 16 rows t0.. (D accumulator: rows
+// t0 + 4g + r, column lane & 15).
 template <int H, int HD>
 __device__ __forceinline__ void store_v(const QkvOut& o, int b, int t0, int N, int nb, f32x4 acc) {
     using G = Geo<HD>;
@@ -262,39 +286,52 @@ __device__ __forceinline__ void store_v(const QkvOut& o, int b, int t0, int N, i
     unsigned h0, h1, l0, l1;
     split2u(v[0], v[1], h0, l0);
     split2u(v[2], v[3], h1, l1);
-    const int p0 = 8 * g + 4 * ((t0 >> 4) & 1);  // keys 16u + 4g + e -> positions 8g + 4u + e
-    unsigned char* row = o.v + ((size_t)(b * HEADS + h) * o.nch + (t0 >> 5)) * G::VCH + d * G::VROW;
-    *reinterpret_cast<uint2*>(row + 2 * p0) = uint2{h0, h1};
-    *reinterpret_cast<uint2*>(row + 64 + 2 * p0) = uint2{l0, l1};
+    // keys 16u + 4g + e (u = row block within the chunk) -> positions 8g + 4u + e:
+    // half u of lane g * 16 + d % 16 of d-block d / 16
+    unsigned char* pc = o.v + ((size_t)(b * HEADS + h) * o.nch + (t0 >> 5)) * G::VCH + (d >> 4) * 2048 +
+                        (g * 16 + (d & 15)) * 16 + ((t0 >> 4) & 1) * 8;
+    *reinterpret_cast<uint2*>(pc) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(pc + 1024) = uint2{l0, l1};
 }
 
-// The QKV projection of the tile's LN rows Xn into the attention layouts.
-template <int H, int HD>
+// The QKV projection of the tile's LN rows Xn (16 RB rows from t0) into the
+// attention layouts.
+template <int H, int HD, int RB>
 __device__ __forceinline__ void qkv_phase(const unsigned char* Xn, const u32x4* __restrict__ W, Strip<H>& cur,
                                           const QkvOut& o, int b, int t0, int N) {
     constexpr int NB = 3 * H / 16, NQK = 2 * H / 16;
     const int wave = threadIdx.x >> 6;
-    const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
     for (int nb = wave; nb < NB; nb += NW) {
         Strip<H> nxt;
         if (nb + NW < NB) nxt.load(W, nb + NW);
-        if (nb < NQK) store_qk<H, HD>(o, b, t0, N, nb, gemm_t<H>(Xn, cur, z4));
-        else store_v<H, HD>(o, b, t0, N, nb, gemm_n<H>(Xn, cur, z4));
+        f32x4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (nb < NQK) {
+            gemm_t<H, RB>(Xn, cur, acc);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) store_qk<H, HD>(o, b, t0 + 16 * rb, N, nb, acc[rb]);
+        } else {
+            gemm_n<H, RB>(Xn, cur, acc);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) store_v<H, HD>(o, b, t0 + 16 * rb, N, nb, acc[rb]);
+        }
         if (nb + NW < NB) cur = nxt;
     }
 }
 
 // A tile wholly past the utterance's end: its rows of the next attention
 // buffers are zeros (no GEMM).
-template <int H, int HD>
+template <int H, int HD, int RB>
 __device__ __forceinline__ void zero_tile(const QkvOut& o, int b, int t0) {
     constexpr int NB = 3 * H / 16, NQK = 2 * H / 16;
     const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int nb = threadIdx.x >> 6; nb < NB; nb += NW) {
-        if (nb < NQK) store_qk<H, HD>(o, b, t0, 0, nb, z4);
-        else store_v<H, HD>(o, b, t0, 0, nb, z4);
-    }
+    for (int nb = threadIdx.x >> 6; nb < NB; nb += NW)
+        for (int rb = 0; rb < RB; ++rb) {
+            if (nb < NQK) store_qk<H, HD>(o, b, t0 + 16 * rb, 0, nb, z4);
+            else store_v<H, HD>(o, b, t0 + 16 * rb, 0, nb, z4);
+        }
 }
 
 // Utterance and tile of this workgroup (TflQueue): a claim on the queue of
@@ -324,51 +361,56 @@ __device__ __forceinline__ void claim_tile(int B, int ntile, unsigned* __restric
         *sh = got;
     }
     __syncthreads();
-    const int it = *sh;
-    *b = it / ntile;
-    *tile = it - *b * ntile;
+    // wave-uniform in an SGPR: every address derived from b (the K / V buffer
+    // descriptors in particular) stays scalar - a VGPR-held b turns each buffer
+    // load into a readfirstlane waterfall loop
+    const int it = __builtin_amdgcn_readfirstlane(*sh);
+    *b = __builtin_amdgcn_readfirstlane(it / ntile);
+    *tile = __builtin_amdgcn_readfirstlane(it - (it / ntile) * ntile);
 }
 
 // ---------------------------------------------------------------------------
-// Attention of the tile's 16 queries, both heads, over all N keys.  Leaves
-// the normalised output rows as split LDS rows A [16][srs(H)] (the out
-// projection's B operand).  The caller's `between` runs after the chunk loop,
-// before the merge (the first GEMM's weight strip is requested there).
-template <int H, int HD, bool MASKED, typename Between>
+// Attention of the tile's 16 RB queries (RB 16-query blocks share every K / V
+// fragment), both heads, over all N keys.  Leaves the normalised output rows
+// as split LDS rows A [16 RB][srs(H)] (the out projection's B operand).  The
+// caller's `between` runs after the chunk loop, before the merge (the first
+// GEMM's weight strip is requested there).
+template <int H, int HD, bool MASKED, int RB, typename Between>
 __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
                                                const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
                                                int len, float sl2, unsigned char* A, float* xs, Between between) {
     using G = Geo<HD>;
-    constexpr int KS = G::KS, DP = G::DP, MT = G::MT, QKROW = G::QKROW, VCH = G::VCH, XW = G::XW;
+    constexpr int KS = G::KS, MT = G::MT, QKBLK = G::QKBLK, VCH = G::VCH, XW = G::XW;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, g = lane >> 4;
     const int h = wave / WPH, kq = wave - h * WPH;
     const int nch = npad / KC;
-    const size_t bh = (size_t)(b * HEADS + h);
+    const size_t bh = (size_t)__builtin_amdgcn_readfirstlane(b * HEADS + h);
 
-    // B = Q^T fragments: lane (query li, dims 32 ks + 8 g .. + 7)
-    u32x4 qh[KS], ql[KS];
-    {
-        const unsigned char* qp = qb + (bh * npad + t0 + li) * QKROW + 16 * g;
+    // B = Q^T fragments: lane (query li of block qt, dims 32 ks + 8 g .. + 7)
+    u32x4 qh[RB][KS], ql[RB][KS];
+#pragma unroll
+    for (int qt = 0; qt < RB; ++qt) {
+        const unsigned char* qp = qb + (bh * (npad / 16) + t0 / 16 + qt) * QKBLK + 16 * lane;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            qh[ks] = *reinterpret_cast<const u32x4*>(qp + 64 * ks);
-            ql[ks] = *reinterpret_cast<const u32x4*>(qp + 2 * DP + 64 * ks);
+            qh[qt][ks] = *reinterpret_cast<const u32x4*>(qp + 2048 * ks);
+            ql[qt][ks] = *reinterpret_cast<const u32x4*>(qp + 2048 * ks + 1024);
         }
     }
-    // Chunk c's K rows and V^T block through a buffer descriptor whose record
-    // count is 0 past the last chunk: the prefetch of a chunk that does not
-    // exist is issued unconditionally (no branch around a load, so the
+    // Chunk c's K fragments and V^T fragments through a buffer descriptor whose
+    // record count is 0 past the last chunk: the prefetch of a chunk that does
+    // not exist is issued unconditionally (no branch around a load, so the
     // compiler's vmcnt waits stay graded) and reads zeros without traffic.
-    const int koff = li * QKROW + 16 * g, voff = li * G::VROW + 16 * g;
+    const int loff = 16 * lane;
     struct Frag {
         u32x4 kh[2][KS], kl[2][KS], vh[MT], vl[MT];
     };
     auto load = [&](Frag& f, int c) {
         const bool ok = c < nch;
         const auto rk = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<unsigned char*>(kb) + (bh * npad + (size_t)(ok ? c : 0) * KC) * QKROW, 0, ok ? KC * QKROW : 0,
-            0x00020000);
+            const_cast<unsigned char*>(kb) + (bh * (npad / 16) + (size_t)(ok ? c : 0) * 2) * QKBLK, 0,
+            ok ? 2 * QKBLK : 0, 0x00020000);
         const auto rv = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<unsigned char*>(vb) + (bh * nch + (ok ? c : 0)) * VCH, 0, ok ? VCH : 0, 0x00020000);
 #pragma unroll
@@ -376,38 +418,45 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 f.kh[u][ks] = __builtin_bit_cast(
-                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, koff + u * 16 * QKROW + 64 * ks, 0, 0));
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff + u * QKBLK + 2048 * ks, 0, 0));
                 f.kl[u][ks] = __builtin_bit_cast(
-                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, koff + u * 16 * QKROW + 2 * DP + 64 * ks, 0, 0));
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff + u * QKBLK + 2048 * ks + 1024, 0, 0));
             }
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
-            f.vh[t] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, voff + t * 16 * G::VROW, 0, 0));
-            f.vl[t] =
-                __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, voff + t * 16 * G::VROW + 64, 0, 0));
+            f.vh[t] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, loff + t * 2048, 0, 0));
+            f.vl[t] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, loff + t * 2048 + 1024, 0, 0));
         }
     };
 
-    f32x4 acc[MT];
+    f32x4 acc[RB][MT];
+    float m[RB], lsum[RB];
 #pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = MASKED ? -INFINITY : 0.f, lsum = 0.f;
+    for (int qt = 0; qt < RB; ++qt) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        m[qt] = MASKED ? -INFINITY : 0.f;
+        lsum[qt] = 0.f;
+    }
     bool fresh = true;  // unmasked: no chunk processed yet (wave-uniform)
 
     auto process = [&](const Frag& f, int c) {
-        const float nm = (MASKED || fresh) ? 0.f : -m;
-        float s[2][4];  // key 32 c + 16 u + 4 g + r of query li (base-2 score)
+        float s[RB][2][4];  // key 32 c + 16 u + 4 g + r of query li of block qt (base-2 score)
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            f32x4 st = f32x4{nm, nm, nm, nm};
+        for (int qt = 0; qt < RB; ++qt) {
+            const float nm = (MASKED || fresh) ? 0.f : -m[qt];
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                st = mfma(f.kh[u][ks], qh[ks], st);
-                st = mfma(f.kh[u][ks], ql[ks], st);
-                st = mfma(f.kl[u][ks], qh[ks], st);
+            for (int u = 0; u < 2; ++u) {
+                f32x4 st = f32x4{nm, nm, nm, nm};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    st = mfma(f.kh[u][ks], qh[qt][ks], st);
+                    st = mfma(f.kh[u][ks], ql[qt][ks], st);
+                    st = mfma(f.kl[u][ks], qh[qt][ks], st);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[qt][u][r] = st[r];
             }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[u][r] = st[r];
         }
         const int k0 = c * KC;
         if constexpr (MASKED) {
@@ -417,74 +466,95 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int key = k0 + 16 * u + 4 * g + r;
-                    s[u][r] = key < len ? s[u][r] * sl2 : (key < N ? kMaskFill * kLog2e : -INFINITY);
+#pragma unroll
+                    for (int qt = 0; qt < RB; ++qt)
+                        s[qt][u][r] = key < len ? s[qt][u][r] * sl2 : (key < N ? kMaskFill * kLog2e : -INFINITY);
                 }
         } else if (N - k0 < KC) {  // the last chunk: keys past N score -inf (wave-uniform)
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) s[u][r] = k0 + 16 * u + 4 * g + r < N ? s[u][r] : -INFINITY;
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int qt = 0; qt < RB; ++qt)
+                        s[qt][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qt][u][r] : -INFINITY;
         }
-        float cmax = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
-                           fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+        float cmax[RB];
+#pragma unroll
+        for (int qt = 0; qt < RB; ++qt)
+            cmax[qt] = fmaxf(fmaxf(fmaxf(s[qt][0][0], s[qt][0][1]), fmaxf(s[qt][0][2], s[qt][0][3])),
+                             fmaxf(fmaxf(s[qt][1][0], s[qt][1][1]), fmaxf(s[qt][1][2], s[qt][1][3])));
         if constexpr (MASKED) {
-            const float mn = vmax(m, grp4_max(cmax));
-            const float corr = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first chunk -> 0
-            lsum *= corr;
 #pragma unroll
-            for (int t = 0; t < MT; ++t) acc[t] *= corr;
+            for (int qt = 0; qt < RB; ++qt) {
+                const float mn = vmax(m[qt], grp4_max(cmax[qt]));
+                const float corr = __builtin_amdgcn_exp2f(m[qt] - mn);  // m = -inf on the first chunk -> 0
+                lsum[qt] *= corr;
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[u][r] -= mn;
-            m = mn;
-        } else {
-            const bool up = fresh || cmax > kLazyT;
-            if (__builtin_amdgcn_ballot_w64(up) != 0) {  // wave-uniform: move the base
-                const float cm = grp4_max(cmax);          // finite: every chunk has a live key
-                const float d = fresh ? cm : vmax(cm, 0.f);
-                m += d;
-                if (!fresh) {
-                    const float corr = __builtin_amdgcn_exp2f(-d);
-                    lsum *= corr;
-#pragma unroll
-                    for (int t = 0; t < MT; ++t) acc[t] *= corr;
-                }
+                for (int t = 0; t < MT; ++t) acc[qt][t] *= corr;
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) s[u][r] -= d;
+                    for (int r = 0; r < 4; ++r) s[qt][u][r] -= mn;
+                m[qt] = mn;
+            }
+        } else {
+            bool up = fresh;
+#pragma unroll
+            for (int qt = 0; qt < RB; ++qt) up = up || cmax[qt] > kLazyT;
+            if (__builtin_amdgcn_ballot_w64(up) != 0) {  // wave-uniform: move the base
+#pragma unroll
+                for (int qt = 0; qt < RB; ++qt) {
+                    const float cm = grp4_max(cmax[qt]);  // finite: every chunk has a live key
+                    const float d = fresh ? cm : vmax(cm, 0.f);
+                    m[qt] += d;
+                    if (!fresh) {
+                        const float corr = __builtin_amdgcn_exp2f(-d);
+                        lsum[qt] *= corr;
+#pragma unroll
+                        for (int t = 0; t < MT; ++t) acc[qt][t] *= corr;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[qt][u][r] -= d;
+                }
             }
             fresh = false;
         }
+        u32x4 bh4[RB], bl4[RB];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int qt = 0; qt < RB; ++qt) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                s[u][r] = __builtin_amdgcn_exp2f(s[u][r]);
-                lsum += s[u][r];
-            }
-        // B = P^T: lane (query li) holds keys 4g + e (u = 0) and 16 + 4g + e (u = 1)
-        unsigned ph[4], pl[4];
-        split2u(s[0][0], s[0][1], ph[0], pl[0]);
-        split2u(s[0][2], s[0][3], ph[1], pl[1]);
-        split2u(s[1][0], s[1][1], ph[2], pl[2]);
-        split2u(s[1][2], s[1][3], ph[3], pl[3]);
-        const u32x4 bh4 = u32x4{ph[0], ph[1], ph[2], ph[3]}, bl4 = u32x4{pl[0], pl[1], pl[2], pl[3]};
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            acc[t] = mfma(f.vh[t], bh4, acc[t]);
-            acc[t] = mfma(f.vh[t], bl4, acc[t]);
-            acc[t] = mfma(f.vl[t], bh4, acc[t]);
+                for (int r = 0; r < 4; ++r) {
+                    s[qt][u][r] = __builtin_amdgcn_exp2f(s[qt][u][r]);
+                    lsum[qt] += s[qt][u][r];
+                }
+            // B = P^T: lane (query li) holds keys 4g + e (u = 0) and 16 + 4g + e (u = 1)
+            unsigned ph[4], pl[4];
+            split2u(s[qt][0][0], s[qt][0][1], ph[0], pl[0]);
+            split2u(s[qt][0][2], s[qt][0][3], ph[1], pl[1]);
+            split2u(s[qt][1][0], s[qt][1][1], ph[2], pl[2]);
+            split2u(s[qt][1][2], s[qt][1][3], ph[3], pl[3]);
+            bh4[qt] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+            bl4[qt] = u32x4{pl[0], pl[1], pl[2], pl[3]};
         }
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int qt = 0; qt < RB; ++qt) {
+                acc[qt][t] = mfma(f.vh[t], bh4[qt], acc[qt][t]);
+                acc[qt][t] = mfma(f.vh[t], bl4[qt], acc[qt][t]);
+                acc[qt][t] = mfma(f.vl[t], bh4[qt], acc[qt][t]);
+            }
     };
 
-    // chunks kq, kq + 4, ... through a two-slot register ring
+    // chunks kq, kq + 4, ... through a two-slot register ring.  The scheduling
+    // barriers keep each slot's loads in program order (slot 0 before slot 1),
+    // so the wait at the top of an iteration is for the older slot only.
     const int nj = kq < nch ? (nch - kq + WPH - 1) / WPH : 0;
-    // The scheduling barriers keep each slot's loads in program order (slot 0
-    // before slot 1), so the wait at the top of an iteration is for the older
-    // slot only (vmcnt = one slot's loads); without them the scheduler put the
-    // first-consumed slot's loads last and the loop waited with vmcnt(0).
     Frag f0, f1;
     load(f0, kq);
     __builtin_amdgcn_sched_barrier(0);
@@ -505,37 +575,46 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
     between();
 
     // merge the four key quarters of each head through LDS
-    if (!MASKED && fresh) m = -INFINITY;  // this wave processed no chunk
-    float* xw = xs + (wave * 64 + lane) * XW;
-    xw[0] = m;
-    xw[1] = lsum;
+    if (!MASKED && fresh) {  // this wave processed no chunk
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+        for (int qt = 0; qt < RB; ++qt) m[qt] = -INFINITY;
+    }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xw[2 + 4 * t + r] = acc[t][r];
+    for (int qt = 0; qt < RB; ++qt) {
+        float* xw = xs + ((wave * RB + qt) * 64 + lane) * XW;
+        xw[0] = m[qt];
+        xw[1] = lsum[qt];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xw[2 + 4 * t + r] = acc[qt][t][r];
+    }
     __syncthreads();
     if (kq < MT) {  // wave (h, j = kq): output dims 16 j .. 16 j + 15 of head h
         const int j = kq;
-        float mi[WPH], mx = -INFINITY;
 #pragma unroll
-        for (int q = 0; q < WPH; ++q) {
-            mi[q] = xs[((h * WPH + q) * 64 + lane) * XW];
-            mx = vmax(mx, mi[q]);
+        for (int qt = 0; qt < RB; ++qt) {
+            float mi[WPH], mx = -INFINITY;
+#pragma unroll
+            for (int q = 0; q < WPH; ++q) {
+                mi[q] = xs[(((h * WPH + q) * RB + qt) * 64 + lane) * XW];
+                mx = vmax(mx, mi[q]);
+            }
+            float ls = 0.f, o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < WPH; ++q) {
+                const float* xq = xs + (((h * WPH + q) * RB + qt) * 64 + lane) * XW;
+                const float fq = __builtin_amdgcn_exp2f(mi[q] - mx);
+                ls += xq[1] * fq;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] += xq[2 + 4 * j + r] * fq;
+            }
+            ls += __shfl_xor(ls, 16);
+            ls += __shfl_xor(ls, 32);
+            const float inv = 1.0f / ls;
+            put_split4<H>(A + (16 * qt + li) * srs(H) + 2 * (h * HD + 16 * j + 4 * g), o[0] * inv, o[1] * inv,
+                          o[2] * inv, o[3] * inv);
         }
-        float ls = 0.f, o[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < WPH; ++q) {
-            const float* xq = xs + ((h * WPH + q) * 64 + lane) * XW;
-            const float fq = __builtin_amdgcn_exp2f(mi[q] - mx);
-            ls += xq[1] * fq;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] += xq[2 + 4 * j + r] * fq;
-        }
-        ls += __shfl_xor(ls, 16);
-        ls += __shfl_xor(ls, 32);
-        const float inv = 1.0f / ls;
-        put_split4<H>(A + li * srs(H) + 2 * (h * HD + 16 * j + 4 * g), o[0] * inv, o[1] * inv, o[2] * inv,
-                      o[3] * inv);
     }
     __syncthreads();
     TSTAMP(2);
@@ -557,13 +636,16 @@ struct LArgs {
     float* z;
 };
 
-template <int H, bool MASKED, int NEXT, int NN>
+// RB = 1 (16-row tiles) while the grid fits one round of the CUs, else 2
+// (32-row tiles: every K / V and weight fragment a workgroup reads serves
+// twice the rows).
+template <int H, bool MASKED, int NEXT, int NN, int RB>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
-    constexpr int HD = H / HEADS, F = 2 * H;
-    __shared__ __attribute__((aligned(16))) unsigned char A[TQ * srs(H)];   // att, then LN2(o), LN(y) (split)
-    __shared__ __attribute__((aligned(16))) float O[TQ * frs(H)];           // o, then y (fp32)
-    __shared__ __attribute__((aligned(16))) unsigned char Hd[TQ * srs(F)];  // relu(FFN1) (split)
-    __shared__ __attribute__((aligned(16))) float xs[NW * 64 * Geo<HD>::XW];
+    constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
+    __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att, then LN2(o), LN(y) (split)
+    __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];           // o, then y (fp32)
+    __shared__ __attribute__((aligned(16))) unsigned char Hd[TR * srs(F)];  // relu(FFN1) (split)
+    __shared__ __attribute__((aligned(16))) float xs[NW * RB * 64 * Geo<HD>::XW];
     // the layer's vectors, read once into LDS (their L2 latency otherwise sits
     // in every LayerNorm and epilogue): bo | g2 | b2n | b1 [F] | b2 | gn | bn | bn2 [NN]
     constexpr int VO = 0, VG2 = H, VB2N = 2 * H, VB1 = 3 * H, VB2 = 3 * H + F, VGN = 4 * H + F, VBN = 5 * H + F,
@@ -572,11 +654,11 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     __shared__ int item;
     int b, tile;
     claim_tile(a.B, a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
-    const int t0 = tile * TQ, N = a.N;
+    const int t0 = tile * TR, N = a.N;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     const QkvOut qo{a.nq, a.nk, a.nv, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
     if (t0 >= N) {
-        if constexpr (NEXT == 1) zero_tile<H, HD>(qo, b, t0);
+        if constexpr (NEXT == 1) zero_tile<H, HD, RB>(qo, b, t0);
         return;
     }
     for (int e = threadIdx.x; e < H; e += NW * 64) {
@@ -597,25 +679,30 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     int len = N;
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
-    attention_tile<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs, [&] {
+    attention_tile<H, HD, MASKED, RB>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs, [&] {
         if (wave < H / 16) so.load(a.Wo, wave);
     });
     const size_t row0 = (size_t)b * N + t0;
-    const bool live = t0 + i < N;
     // o = x + att . Wo^T + bo
     if (wave < H / 16) {
-        const int nb = wave, col = nb * 16 + 4 * gq;
-        f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VO + col);
-        acc = gemm_t<H>(A, so, acc);
-        f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (live) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + i) * H + col);
-        *reinterpret_cast<f32x4*>(O + i * frs(H) + col) = x + acc;
+        const int col = wave * 16 + 4 * gq;
+        f32x4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VO + col);
+        gemm_t<H, RB>(A, so, acc);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int rr = rb * 16 + i;
+            f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (t0 + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
+            *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = x + acc[rb];
+        }
     }
     Strip<H> s1;
     if (wave < F / 16) s1.load(a.W1, wave);
     __syncthreads();
     TSTAMP(3);
-    ln16<H>(O, A, vec + VG2, vec + VB2N);
+    ln_rows<H, TR>(O, A, vec + VG2, vec + VB2N);
     __syncthreads();
     TSTAMP(4);
     // h = relu(LN2(o) . W1^T + b1)
@@ -624,10 +711,15 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         Strip<H> nxt;
         if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
         const int col = nb * 16 + 4 * gq;
-        f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
-        acc = gemm_t<H>(A, s1, acc);
-        put_split4<F>(Hd + i * srs(F) + 2 * col, acc[0] > 0.f ? acc[0] : 0.f, acc[1] > 0.f ? acc[1] : 0.f,
-                      acc[2] > 0.f ? acc[2] : 0.f, acc[3] > 0.f ? acc[3] : 0.f);
+        f32x4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
+        gemm_t<H, RB>(A, s1, acc);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+            put_split4<F>(Hd + (rb * 16 + i) * srs(F) + 2 * col, acc[rb][0] > 0.f ? acc[rb][0] : 0.f,
+                          acc[rb][1] > 0.f ? acc[rb][1] : 0.f, acc[rb][2] > 0.f ? acc[rb][2] : 0.f,
+                          acc[rb][3] > 0.f ? acc[rb][3] : 0.f);
         if (nb + NW < F / 16) s1 = nxt;
     }
     Strip<F> s2;
@@ -637,21 +729,27 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     // y = o + h . W2^T + b2
     if (wave < H / 16) {
         const int col = wave * 16 + 4 * gq;
-        f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VB2 + col);
-        acc = gemm_t<F>(Hd, s2, acc);
-        const f32x4 y = *reinterpret_cast<const f32x4*>(O + i * frs(H) + col) + acc;
-        if (live) *reinterpret_cast<f32x4*>(a.x_out + (row0 + i) * H + col) = y;
-        if constexpr (NEXT != 0) *reinterpret_cast<f32x4*>(O + i * frs(H) + col) = y;
+        f32x4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB2 + col);
+        gemm_t<F, RB>(Hd, s2, acc);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int rr = rb * 16 + i;
+            const f32x4 y = *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
+            if (t0 + rr < N) *reinterpret_cast<f32x4*>(a.x_out + (row0 + rr) * H + col) = y;
+            if constexpr (NEXT != 0) *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = y;
+        }
     }
     if constexpr (NEXT == 1) {
         Strip<H> sn;
         if (wave < 3 * H / 16) sn.load(a.Wn, wave);
         __syncthreads();
         TSTAMP(6);
-        ln16<H>(O, A, vec + VGN, vec + VBN);
+        ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
         __syncthreads();
         TSTAMP(7);
-        qkv_phase<H, HD>(A, a.Wn, sn, qo, b, t0, N);
+        qkv_phase<H, HD, RB>(A, a.Wn, sn, qo, b, t0, N);
         TSTAMP(8);
         TSTAMP_RT(15);
     } else if constexpr (NEXT == 2) {
@@ -659,7 +757,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         if (wave < NN / 16) sn.load(a.Wn, wave);
         __syncthreads();
         TSTAMP(6);
-        ln16<H>(O, A, vec + VGN, vec + VBN);
+        ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
         __syncthreads();
         TSTAMP(7);
 #pragma unroll 1
@@ -667,9 +765,15 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
             Strip<H> nxt;
             if (nb + NW < NN / 16) nxt.load(a.Wn, nb + NW);
             const int col = nb * 16 + 4 * gq;
-            f32x4 acc = *reinterpret_cast<const f32x4*>(vec + VBN2 + col);
-            acc = gemm_t<H>(A, sn, acc);
-            if (live) *reinterpret_cast<f32x4*>(a.z + (row0 + i) * NN + col) = acc;
+            f32x4 acc[RB];
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VBN2 + col);
+            gemm_t<H, RB>(A, sn, acc);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) {
+                const int rr = rb * 16 + i;
+                if (t0 + rr < N) *reinterpret_cast<f32x4*>(a.z + (row0 + rr) * NN + col) = acc[rb];
+            }
             if (nb + NW < NN / 16) sn = nxt;
         }
         TSTAMP(8);
@@ -705,34 +809,43 @@ struct FArgs {
     unsigned char *q, *k, *v;
 };
 
-template <int H, int SRC, bool MASKED>
+template <int H, int SRC, bool MASKED, int RB>
 __global__ __launch_bounds__(512, 2) void first_kernel(FArgs a) {
-    constexpr int HD = H / HEADS, H4 = H / 4;
-    __shared__ __attribute__((aligned(16))) float O[TQ * frs(H)];
-    __shared__ __attribute__((aligned(16))) unsigned char A[TQ * srs(H)];
-    __shared__ int sp[TQ];
+    constexpr int HD = H / HEADS, H4 = H / 4, TR = 16 * RB;
+    __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];
+    __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];
+    __shared__ __attribute__((aligned(16))) float vec[2 * H];
+    __shared__ int sp[TR];
     __shared__ int item;
     int b, tile;
     claim_tile(a.B, a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
-    const int t0 = tile * TQ, N = a.N;
+    const int t0 = tile * TR, N = a.N;
     const int wave = threadIdx.x >> 6;
     const QkvOut qo{a.q, a.k, a.v, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
     if (t0 >= N) {
-        zero_tile<H, HD>(qo, b, t0);
+        zero_tile<H, HD, RB>(qo, b, t0);
         return;
     }
     Strip<H> sq;
     if (wave < 3 * H / 16) sq.load(a.W, wave);
-    __shared__ __attribute__((aligned(16))) float vec[2 * H];
     for (int e = threadIdx.x; e < H; e += NW * 64) {
         vec[e] = a.g[e];
         vec[H + e] = a.bln[e];
     }
     if constexpr (SRC == SRC_EXPAND) {
-        // source phoneme of each frame: the smallest s with cum[s + 1] > t (-1: past the total)
-        if (threadIdx.x < TQ) {
+        // source phoneme of each frame: the smallest s with cum[s + 1] > t (-1:
+        // past the total); the utterance's prefix sums are searched in LDS
+        // (one coalesced load instead of a chain of dependent L2 reads)
+        constexpr int CS = 1024;
+        __shared__ int32_t cs[CS];
+        const int32_t* cg = a.cum + (size_t)b * (a.S + 1);
+        const bool in_lds = a.S + 1 <= CS;
+        if (in_lds)
+            for (int k = threadIdx.x; k <= a.S; k += NW * 64) cs[k] = cg[k];
+        __syncthreads();
+        if (threadIdx.x < TR) {
+            const int32_t* c = in_lds ? cs : cg;
             const int t = t0 + threadIdx.x;
-            const int32_t* c = a.cum + (size_t)b * (a.S + 1);
             int v = -1;
             if (t < N && t < c[a.S]) {
                 int lo = 0, hi = a.S - 1;
@@ -747,7 +860,7 @@ __global__ __launch_bounds__(512, 2) void first_kernel(FArgs a) {
         }
         __syncthreads();
     }
-    for (int idx = threadIdx.x; idx < TQ * H4; idx += NW * 64) {
+    for (int idx = threadIdx.x; idx < TR * H4; idx += NW * 64) {
         const int r = idx / H4, c = (idx - r * H4) * 4, t = t0 + r;
         const size_t row = (size_t)b * N + t;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -772,9 +885,9 @@ __global__ __launch_bounds__(512, 2) void first_kernel(FArgs a) {
         *reinterpret_cast<float4*>(O + r * frs(H) + c) = v;
     }
     __syncthreads();
-    ln16<H>(O, A, vec, vec + H);
+    ln_rows<H, TR>(O, A, vec, vec + H);
     __syncthreads();
-    qkv_phase<H, HD>(A, a.W, sq, qo, b, t0, N);
+    qkv_phase<H, HD, RB>(A, a.W, sq, qo, b, t0, N);
 }
 
 }  // namespace tfl
@@ -798,9 +911,9 @@ int tfl_npad(int N) { return (N + tfl::KC - 1) / tfl::KC * tfl::KC; }
 
 namespace {
 void tfl_sizes(int B, int N, int H, int heads, size_t* qk, size_t* v) {
-    const int HD = H / heads, DP = (HD + 31) / 32 * 32, npad = tfl_npad(N);
-    *qk = align_up((size_t)B * heads * npad * 4 * DP, 256);
-    *v = align_up((size_t)B * heads * (npad / tfl::KC) * HD * 128, 256);
+    const int HD = H / heads, KS = (HD + 31) / 32, npad = tfl_npad(N);
+    *qk = align_up((size_t)B * heads * (npad / 16) * KS * 2048, 256);
+    *v = align_up((size_t)B * heads * (npad / tfl::KC) * (HD / 16) * 2048, 256);
 }
 }  // namespace
 
@@ -817,7 +930,15 @@ void tfl_carve(unsigned char* base, int B, int N, int H, int heads, TflBufs* out
 }
 
 namespace {
-dim3 tfl_grid(int B, int N) { return dim3(B * (tfl_npad(N) / tfl::TQ)); }
+// Rows per workgroup: 16 while one round of the 256 CUs holds the grid, else
+// 32 (half the K / V and weight bytes per row).  M2_TFL_RB=1|2 forces one.
+int tfl_rb(int B, int N) {
+    const char* e = std::getenv("M2_TFL_RB");  // per call: tests switch it
+    const int forced = e ? std::atoi(e) : 0;
+    if (forced == 1 || forced == 2) return forced;
+    return (long)B * (tfl_npad(N) / tfl::TQ) > 256 ? 2 : 1;
+}
+dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
 float tfl_sl2(int H) {
     const float scale = (float)(1.0 / std::sqrt((double)(H / tfl::HEADS)));  // components.py:52, fp32 at the mul
     return scale * tfl::kLog2e;
@@ -834,7 +955,8 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.B = B;
     a.N = N;
     a.npad = tfl_npad(N);
-    a.ntile = a.npad / tfl::TQ;
+    const int rb = tfl_rb(B, N);
+    a.ntile = a.npad / (tfl::TQ * rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
     a.sl2 = tfl_sl2(H);
@@ -856,10 +978,11 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.q = out.q;
     a.k = out.k;
     a.v = out.v;
-    const dim3 grid = tfl_grid(B, N), blk(tfl::NW * 64);
+    const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
 #define M2_TFF(HH, SS, MM)                                                                      \
     if (H == HH && f.src == SS && masked == MM) {                                               \
-        hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM>), grid, blk, 0, st, a);               \
+        if (rb == 2) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 2>), grid, blk, 0, st, a);  \
+        else hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 1>), grid, blk, 0, st, a);          \
         M2_LAUNCHED("tfl first_kernel");                                                        \
         return M2_OK;                                                                           \
     }
@@ -889,7 +1012,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.B = B;
     a.N = N;
     a.npad = tfl_npad(N);
-    a.ntile = a.npad / tfl::TQ;
+    const int rb = tfl_rb(B, N);
+    a.ntile = a.npad / (tfl::TQ * rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
     a.sl2 = tfl_sl2(H);
@@ -915,10 +1039,11 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nk = out.k;
     a.nv = out.v;
     a.z = z;
-    const dim3 grid = tfl_grid(B, N), blk(tfl::NW * 64);
+    const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN>), grid, blk, 0, st, a);          \
+        if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2>), grid, blk, 0, st, a);  \
+        else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 1>), grid, blk, 0, st, a);          \
         M2_LAUNCHED("tfl layer_kernel");                                                        \
         return M2_OK;                                                                           \
     }

@@ -87,6 +87,12 @@ class HipStages:
         hm, st = state
         return hm.inference_back(st, T)
 
+    def both(self, ids: Tensor, lens: Optional[Tensor], scale: float) -> Tuple[Tensor, Tensor]:
+        """Both phases with no collective between them (world 1): the one-call
+        m2_inference (the back half is launched from C right after the T_max
+        read, no Python between the phases)."""
+        return self.model._hip(ids.device).inference(ids, lens, scale)
+
 
 def hip_stages(model) -> HipStages:
     return HipStages(model)
@@ -194,7 +200,7 @@ class PendingGather:
 def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Optional[Tensor],
                       duration_scale: float = 1.0, group=None, gather: bool = True,
                       gather_to: Optional[int] = None, src: Optional[int] = None,
-                      async_gather: bool = False):
+                      async_gather: bool = False, one_call_world1: bool = True):
     """M2TTSModel.inference (tts_model.py:402-438) over a global batch sharded by
     utterance.
 
@@ -208,7 +214,9 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
     with ``gather_to=r`` on rank r only, None elsewhere), else this rank's
     shard and its bounds.  ``async_gather`` (with ``gather``) leaves the
     gather in flight and returns a PendingGather, so the next step's work
-    overlaps it; call ``.wait()`` for the tensors."""
+    overlaps it; call ``.wait()`` for the tensors.  At world 1 the two phases
+    run as one library call (``one_call_world1``; False keeps the two-phase
+    form the ranks of a multi-GPU job run, e.g. to time one rank's share)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     if src is not None and world > 1:
@@ -217,6 +225,14 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
     lo, hi = shard_bounds(B, world, rank)
     ids = phoneme_ids[lo:hi]
     lens = phoneme_lengths[lo:hi] if phoneme_lengths is not None else None
+    if one_call_world1 and world == 1 and hi > lo and hasattr(stages, "both"):
+        with torch.no_grad():
+            mel, audio = stages.both(ids, lens, duration_scale)
+        if async_gather and gather:
+            out = PendingGather(None, None, None, None)
+            out._out = (mel, audio)
+            return out
+        return (mel, audio) if gather else (mel, audio, (lo, hi))
     with torch.no_grad():
         state, t_local = stages.front(ids, lens, duration_scale) if hi > lo else (None, 0)
         M = stages.mel_channels()

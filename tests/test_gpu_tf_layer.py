@@ -28,9 +28,17 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
+@pytest.fixture(params=["auto", "1", "2"])
+def rows_per_tile(request, monkeypatch):
+    """16- and 32-row workgroup tiles (M2_TFL_RB), and the per-call choice."""
+    if request.param != "auto":
+        monkeypatch.setenv("M2_TFL_RB", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("stage", STAGES)
 @pytest.mark.parametrize("B,S", [(1, 1), (2, 15), (3, 16), (1, 17), (9, 31), (2, 32), (5, 33), (17, 47), (4, 100)])
-def test_text_encoder_edges(gpu, stage, B, S):
+def test_text_encoder_edges(gpu, stage, B, S, rows_per_tile):
     cfg = stage_config(stage)
     sd = golden_state(stage)
     m = build_model(stage, gpu)
@@ -51,7 +59,7 @@ def test_text_encoder_edges(gpu, stage, B, S):
 
 @pytest.mark.parametrize("stage", STAGES)
 @pytest.mark.parametrize("B,T", [(1, 1), (2, 16), (3, 17), (1, 31), (9, 32), (2, 33), (5, 63), (1, 500), (3, 257)])
-def test_mel_decoder_edges(gpu, stage, B, T):
+def test_mel_decoder_edges(gpu, stage, B, T, rows_per_tile):
     cfg = stage_config(stage)
     sd = golden_state(stage)
     m = build_model(stage, gpu)

@@ -10,17 +10,27 @@
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <int INF>
+// ROWS = 0: a wave-instruction reads 1 KB contiguous (lane i: element base + i);
+// ROWS = 1: 16 rows of 64 B, rows 256 B apart (lane (i, g): row i, 16 g) -
+// the one-launch layer's K-fragment pattern; a wave covers 4 such blocks
+// (the row's 4 x 64 B) before moving on.
+template <int INF, int ROWS>
 __global__ __launch_bounds__(512) void rd(const u32x4* __restrict__ buf, size_t slice_elems, int per_wg_elems,
                                           unsigned* __restrict__ out) {
     const u32x4* p = buf + (size_t)(blockIdx.x & 7) * slice_elems;
     unsigned acc = 0;
     const int stride = blockDim.x * INF;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int base = threadIdx.x; base < per_wg_elems; base += stride) {
         u32x4 v[INF];
 #pragma unroll
         for (int i = 0; i < INF; ++i) {
-            const int e = base + i * blockDim.x;
+            int e = base + i * blockDim.x;
+            if (ROWS) {
+                const int ins = (base - threadIdx.x) / 64 + w + i * (blockDim.x / 64);  // wave-instruction index
+                const int blk = ins >> 2, part = ins & 3;                               // 16-row block, 64-B column
+                e = blk * 256 + (lane & 15) * 16 + part * 4 + (lane >> 4);              // 16-B elements
+            }
             v[i] = e < per_wg_elems ? p[e] : u32x4{0, 0, 0, 0};
         }
 #pragma unroll
@@ -42,11 +52,14 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int inf : {4, 8, 16}) {
+    for (int inf : {4, 8, 16, -4, -8, -16}) {
         auto launch = [&] {
-            if (inf == 4) hipLaunchKernelGGL(rd<4>, dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
-            if (inf == 8) hipLaunchKernelGGL(rd<8>, dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
-            if (inf == 16) hipLaunchKernelGGL(rd<16>, dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 4) hipLaunchKernelGGL((rd<4, 0>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 8) hipLaunchKernelGGL((rd<8, 0>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 16) hipLaunchKernelGGL((rd<16, 0>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == -4) hipLaunchKernelGGL((rd<4, 1>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == -8) hipLaunchKernelGGL((rd<8, 1>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == -16) hipLaunchKernelGGL((rd<16, 1>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
         };
         for (int i = 0; i < 50; ++i) launch();
         hipDeviceSynchronize();
@@ -59,8 +72,9 @@ int main(int argc, char** argv) {
         hipEventElapsedTime(&ms, a, b);
         const double us = ms * 1e3 / n;
         const double per_cu = (double)per_wg / (us * 1e-6) / 1e9;
-        printf("per_wg %d B, grid %d x %d threads, %2d loads/lane in flight: %.2f us/launch, %.1f GB/s per WG, %.2f TB/s chip\n",
-               per_wg, grid, threads, inf, us, per_cu, per_cu * grid / 1e3);
+        printf("per_wg %d B, grid %d x %d threads, %s, %2d loads/lane in flight: %.2f us/launch, %.1f GB/s per WG, %.2f TB/s chip\n",
+               per_wg, grid, threads, inf > 0 ? "contiguous 1 KB" : "16 rows x 64 B", inf > 0 ? inf : -inf, us, per_cu,
+               per_cu * grid / 1e3);
     }
     return 0;
 }

@@ -30,12 +30,14 @@ def summarize(path, steps=20):
         spans.append((st[b] - st[a]) / 1e3)
         busy.append(sum(en[i] - st[i] for i in range(a, b)) / 1e3)
         for i in range(a, b):
-            per.setdefault((i - a, names[i]), []).append((en[i] - st[i]) / 1e3)
+            gap = (st[i] - en[i - 1]) / 1e3 if i > a else 0.0
+            per.setdefault((i - a, names[i]), []).append(((en[i] - st[i]) / 1e3, (st[i] - st[a]) / 1e3, gap))
     n = len(spans)
     print(f"steps {n}: span median {sorted(spans)[n // 2]:.1f} us, kernel-busy median {sorted(busy)[n // 2]:.1f} us")
+    print("  #  duration  start@   gap-before (medians, us)")
     for (i, nm), v in sorted(per.items()):
-        v.sort()
-        print(f"{i:3d} {v[len(v) // 2]:7.2f} us  {nm}")
+        med = [sorted(c)[len(c) // 2] for c in zip(*v)]
+        print(f"{i:3d} {med[0]:7.2f} {med[1]:8.1f} {med[2]:7.2f}  {nm}")
 
 
 def main():
@@ -54,10 +56,14 @@ def main():
     ids = torch.randint(0, 42, (B, 100), generator=g).to(dev)
     lens = torch.full((B,), 100, dtype=torch.long, device=dev)
     hm = m._hip(dev)
+    one = len(sys.argv) > 2 and sys.argv[2] == "one"  # the one-call m2_inference
     with torch.no_grad():
         for _ in range(200):
-            state, tl = hm.inference_front(ids, lens, 1.0)
-            hm.inference_back(state, max(1, tl))
+            if one:
+                hm.inference(ids, lens, 1.0)
+            else:
+                state, tl = hm.inference_front(ids, lens, 1.0)
+                hm.inference_back(state, max(1, tl))
     torch.cuda.synchronize()
     print("done")
 
