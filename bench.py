@@ -172,6 +172,22 @@ def physical_cores():
     return sorted(chosen.values()), len({k[0] for k in chosen})
 
 
+def cpu_quota():
+    """CPUs' worth of time this process's cgroup may use (cgroup v2 cpu.max or
+    v1 cfs quota / period), or None when unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_measure(run, runs: int, min_s: float):
     """Median / min / max over `runs` measurements of run()'s rate (calls/s),
     each measurement timing whole calls for at least min_s seconds."""
@@ -232,7 +248,12 @@ def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_
     with the spread.  Two figures for the headline configuration: the
     vocoder single pass (configs[1], the `value`) and M2TTSModel.inference as
     written (2 vocoder passes, Python length-regulator loop)."""
-    cpus, sockets = physical_cores()
+    phys, sockets = physical_cores()
+    quota = cpu_quota()
+    # threads beyond the job's CPU quota only queue behind the throttle (and
+    # make the figure swing with the neighbours' load): one per physical core,
+    # capped at the quota
+    cpus = phys[:max(1, int(quota))] if quota is not None else phys
     spec = {"cpus": cpus, "B": B, "S": S, "T": T, "runs": runs, "min_s": min_s, "ids_seed": ids_seed}
     env = dict(os.environ)
     env.pop("HIP_VISIBLE_DEVICES", None)
@@ -247,13 +268,14 @@ def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_
     spread = lambda d: round((d["max"] - d["min"]) / d["median"], 3)  # noqa: E731
     return {"value": voc["median"], "unit": "audio samples/s", "cores": len(cpus), "kind": "port",
             "sockets": sockets, "host_logical_cpus": ncpu, "affinity_cpus": aff,
+            "physical_cores_in_affinity": len(phys), "cgroup_cpu_quota": quota,
             "torch_threads": res["torch_threads"], "pinned": "one OpenMP thread per physical core "
             "(OMP_PROC_BIND=close on one logical CPU per core)", "cpu_model": cpu_model,
             "stat": f"median of {runs} runs of >= {min_s} s", "min": voc["min"], "max": voc["max"],
             "spread": spread(voc),
             "sample": f"oracle SimpleVocoder single pass (the reference's ATen op sequence), B={B} mel [{B},64,{T}] "
                       f"(configs[1]); torch {torch.__version__} CPU ops on {len(cpus)} physical cores "
-                      f"({sockets} sockets) of {cpu_model}",
+                      f"(of {len(phys)} on {sockets} sockets; job CPU quota {quota}) of {cpu_model}",
             "inference_as_written": {"value": inf["median"], "min": inf["min"], "max": inf["max"],
                                      "spread": spread(inf), "unit": "audio samples/s",
                                      "sample": f"oracle M2TTSModel.inference as written (2 vocoder passes, "
@@ -341,7 +363,12 @@ class Ctx:
 
     def model(self, stage: str):
         if stage not in self.models:
-            self.models[stage] = fixture_model(STAGE1 if stage == "s1" else STAGE2, self.dev)
+            m = fixture_model(STAGE1 if stage == "s1" else STAGE2, self.dev)
+            # throughput lines: the asynchronous "report" range policy (a non-finite
+            # split-f16 result raises on the next call); the default "fallback"
+            # policy's per-call cost is its own line (vocoder_default_policy)
+            m.set_range_policy("report")
+            self.models[stage] = m
         return self.models[stage]
 
     def barrier(self):
@@ -464,10 +491,23 @@ def vocoder_line(cx: Ctx, stage: str, B: int, T: int, args, settle_ms: float, se
                 "dtype_peak_note": note}
     flop_s = vocoder_flops_per_sample(cfg["vocoder_channels"], cfg["mel_channels"])
     voc_s = ms * 1e-3
+    # north_star "rocprof GB/s vs peak" for the whole vocoder step: the three
+    # kernels' PMC bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
+    # correction, profiles/traffic.json) / this run's step time
+    hbm = None
+    if stage == "s1" and path == 2 and B == 32 and T == 500:
+        per = [traffic_for(d["kernel"])[0] for d in per_kernel]
+        if per and all(v is not None for v in per):
+            gbs = sum(per) / voc_s / 1e9
+            hbm = {"hbm_gbs": round(gbs, 1), "frac_of_8tbs": round(gbs / HBM_PEAK_GBS, 4),
+                   "bytes_per_step": sum(per),
+                   "def": "sum over the 3 vocoder kernels of PMC bytes per launch (2*FETCH_SIZE + WRITE_SIZE, "
+                          "static: " + (traffic_for("_source")[0] or "profiles/traffic.json") + ") / this run's "
+                          "ms_per_step, against 8 TB/s"}
     out = {"value": round(value, 1), "ms_per_step": round(ms, 5), "dtype": dtype, "settle_ms": round(settled, 1),
            "config": {"stage": stage, "per_gpu_batch": B, "mel_frames": T, "audio_samples_per_utt": 64 * T},
            "roofline": roof, "vocoder_kernels": per_kernel,
-           "vocoder_flop_per_sample": flop_s,
+           "vocoder_flop_per_sample": flop_s, "vocoder_hbm": hbm,
            "vocoder_tflops": round(value / cx.world * flop_s / 1e12, 3),
            # SURVEY.md 8d "MRF HBM fraction": sum of the 4 resblocks' per-kernel algorithmic
            # bytes / the whole fused vocoder's time per step / 8 TB/s (the resblocks are fused
@@ -477,6 +517,28 @@ def vocoder_line(cx: Ctx, stage: str, B: int, T: int, args, settle_ms: float, se
            "fp32_valu_fraction": round(value / cx.world * flop_s / (FP32_PEAK_TFLOPS * 1e12), 4),
            "fp32_valu_fraction_def": "algorithmic vocoder FLOP/s / 157.3 TF (MI355X fp32 vector peak)"}
     return out
+
+
+def default_policy_line(cx: Ctx, B: int, T: int, args, report_ms: float):
+    """The headline vocoder workload on the public default range policy
+    ("fallback": each call waits for its audio and re-runs it on the exact-f32
+    kernels if it came out non-finite) - the cost of that per-call host
+    synchronisation against the asynchronous "report" policy of the headline."""
+    m = cx.model("s1")
+    g = torch.Generator().manual_seed(1000 + cx.rank)
+    mel = torch.randn(B, STAGE1["mel_channels"], T, generator=g).to(cx.dev)
+    m.set_range_policy("fallback")
+    try:
+        step = lambda: m.vocoder(mel)  # noqa: E731
+        cx.settle(step, 50.0)
+        steps = max(10, args.steps // 2)
+        elapsed, _ = cx.timed(step, steps, 3)
+    finally:
+        m.set_range_policy("report")
+    ms = elapsed / steps * 1e3
+    return {"value": round(samples_per(B, T) * steps * cx.world / elapsed, 1), "ms_per_step": round(ms, 5),
+            "steps": steps, "range_policy": "fallback",
+            "per_call_cost_ms_vs_report": round(ms - report_ms, 5)}
 
 
 def pipeline_line(cx: Ctx, B: int, S: int, args, settle_ms: float):
@@ -618,6 +680,7 @@ def run(args):
         if wl != "pipeline":
             extras["pipeline"] = pipeline_line(cx, B, S, args, 100.0)
         if wl == "vocoder":
+            extras["vocoder_default_policy"] = default_policy_line(cx, B, 5 * S, args, head["ms_per_step"])
             f32 = vocoder_line(cx, "s1", B, 5 * S, args, 100.0, 1000, f32=True)
             extras["vocoder_exact_f32"] = {k: f32[k] for k in ("value", "ms_per_step", "dtype", "roofline",
                                                               "vocoder_kernels", "vocoder_tflops")}
@@ -649,9 +712,10 @@ def run(args):
                                       if head.get("scaling", "weak") == "weak" else
                                       f"utterance-sharded x{world} (RCCL all_reduce + all_gather)")},
            "settle_ms": head["settle_ms"],
+           "range_policy": "report (asynchronous; the default fallback policy: vocoder_default_policy)",
            "rtf_x_realtime": round(head["value"] / SAMPLE_RATE, 1),
            "rtf_x_realtime_per_gpu": round(head["value"] / SAMPLE_RATE / world, 1)}
-    for k in ("roofline", "vocoder_kernels", "vocoder_flop_per_sample", "vocoder_tflops", "mrf_hbm_fraction",
+    for k in ("roofline", "vocoder_kernels", "vocoder_hbm", "vocoder_flop_per_sample", "vocoder_tflops", "mrf_hbm_fraction",
               "mrf_hbm_fraction_def", "fp32_valu_fraction", "fp32_valu_fraction_def", "rank0_phase_ms"):
         if k in head:
             out[k] = head[k]

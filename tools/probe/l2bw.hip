@@ -31,6 +31,10 @@ __global__ __launch_bounds__(512) void rd(const u32x4* __restrict__ buf, size_t 
                 const int blk = ins >> 2, part = ins & 3;                               // 16-row block, 64-B column
                 e = blk * 256 + (lane & 15) * 16 + part * 4 + (lane >> 4);              // 16-B elements
             }
+            if (ROWS == 2) {  // rotated start: workgroup k of an XCD begins k/32 of the way in
+                const int rot = (int)(((long long)(blockIdx.x >> 3) * per_wg_elems / 32) & ~63);
+                e = e < per_wg_elems ? (e + rot) % per_wg_elems : e;
+            }
             v[i] = e < per_wg_elems ? p[e] : u32x4{0, 0, 0, 0};
         }
 #pragma unroll
@@ -52,7 +56,7 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int inf : {4, 8, 16, -4, -8, -16}) {
+    for (int inf : {4, 8, 16, -4, -8, 104, 108, 116}) {
         auto launch = [&] {
             if (inf == 4) hipLaunchKernelGGL((rd<4, 0>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
             if (inf == 8) hipLaunchKernelGGL((rd<8, 0>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
@@ -60,6 +64,9 @@ int main(int argc, char** argv) {
             if (inf == -4) hipLaunchKernelGGL((rd<4, 1>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
             if (inf == -8) hipLaunchKernelGGL((rd<8, 1>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
             if (inf == -16) hipLaunchKernelGGL((rd<16, 1>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 104) hipLaunchKernelGGL((rd<4, 2>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 108) hipLaunchKernelGGL((rd<8, 2>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 116) hipLaunchKernelGGL((rd<16, 2>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
         };
         for (int i = 0; i < 50; ++i) launch();
         hipDeviceSynchronize();
@@ -73,7 +80,8 @@ int main(int argc, char** argv) {
         const double us = ms * 1e3 / n;
         const double per_cu = (double)per_wg / (us * 1e-6) / 1e9;
         printf("per_wg %d B, grid %d x %d threads, %s, %2d loads/lane in flight: %.2f us/launch, %.1f GB/s per WG, %.2f TB/s chip\n",
-               per_wg, grid, threads, inf > 0 ? "contiguous 1 KB" : "16 rows x 64 B", inf > 0 ? inf : -inf, us, per_cu,
+               per_wg, grid, threads, inf > 100 ? "rotated 1 KB" : inf > 0 ? "contiguous 1 KB" : "16 rows x 64 B",
+               inf > 100 ? inf - 100 : inf > 0 ? inf : -inf, us, per_cu,
                per_cu * grid / 1e3);
     }
     return 0;

@@ -65,6 +65,15 @@ def main():
             d = (cur[ok] - prev[ok]).max(axis=1)
             print(f"   {NAMES[i - 1]:16s} {np.median(d):8.0f} cycles  (p90 {np.percentile(d, 90):8.0f}, WGs {ok.sum()})")
             prev = np.where(cur != 0, cur, prev)
+        s0, s1, s2 = st[:, :, 0], st[:, :, 1], st[:, :, 2]
+        ok = (s1 != 0).all(axis=1) & (s2 != 0).all(axis=1)
+        if ok.any():
+            spread = s1[ok].max(axis=1) - s1[ok].min(axis=1)
+            after = s2[ok].max(axis=1) - s1[ok].max(axis=1)
+            att = s1[ok] - s0[ok]
+            print(f"   attention-end spread over waves {np.median(spread):8.0f} cycles; merge after the last wave "
+                  f"{np.median(after):8.0f}; per-wave attention min/median/max {np.median(att.min(axis=1)):.0f} / "
+                  f"{np.median(np.median(att, axis=1)):.0f} / {np.median(att.max(axis=1)):.0f}")
         last = max(i for i in range(1, 9) if (st[:, :, i] != 0).all(axis=1).any())
         tot = (st[:, :, last] - st[:, :, 0]).max(axis=1)
         print(f"   total            {np.median(tot):8.0f} cycles")

@@ -1,0 +1,9 @@
+# Round 3 checkpoint: CPU quota of the box, the -m gpu suite + driver-form bench,
+# kernel stats + PMC passes of the headline vocoder and the B=8 stage2 step.
+set -u
+mkdir -p gpurun_out
+{ cat /sys/fs/cgroup/cpu.max 2>&1; nproc; python3 -c 'import os; print(len(os.sched_getaffinity(0)))'; } > gpurun_out/r03j_cpu.txt
+cat gpurun_out/r03j_cpu.txt
+bash tools/gpu_check.sh r03j &&
+tools/profile_gpu.sh r03j_vocoder &&
+python3 tools/pmc_summary.py gpurun_out/prof_r03j_vocoder > gpurun_out/r03j_vocoder_pmc.txt
