@@ -521,9 +521,10 @@ def vocoder_line(cx: Ctx, stage: str, B: int, T: int, args, settle_ms: float, se
 
 def default_policy_line(cx: Ctx, B: int, T: int, args, report_ms: float):
     """The headline vocoder workload on the public default range policy
-    ("fallback": each call waits for its audio and re-runs it on the exact-f32
-    kernels if it came out non-finite) - the cost of that per-call host
-    synchronisation against the asynchronous "report" policy of the headline."""
+    ("fallback": a call whose split audio came out non-finite is re-run on the
+    exact-f32 kernels, enqueued behind the split ones on the device and
+    returning at once when not needed) - the cost of those launches against
+    the "report" policy of the headline."""
     m = cx.model("s1")
     g = torch.Generator().manual_seed(1000 + cx.rank)
     mel = torch.randn(B, STAGE1["mel_channels"], T, generator=g).to(cx.dev)

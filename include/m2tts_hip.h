@@ -176,9 +176,14 @@ size_t m2_vocoder_chunk_workspace_bytes(const m2_model* model, int32_t B, int32_
  *     next m2_vocoder / m2_inference* call on the model returns M2_E_RANGE
  *     (and clears the flag); m2_model_check synchronises `stream` and
  *     reports it at once (*flagged = 1, flag cleared).
- *   policy 1 (fallback): m2_vocoder synchronises after its kernels and, when
- *     the flag is up, recomputes the call on the exact-f32 kernels (the
- *     reference's fp32 result, non-finite only if the reference's is). */
+ *   policy 1 (fallback): the call is recomputed on the exact-f32 kernels
+ *     when its split audio came out non-finite (the reference's fp32 result,
+ *     non-finite only if the reference's is).  With the fused vocoder kernels
+ *     (the model's own shapes) this happens on the device, without a host
+ *     wait: the split kernels raise a device flag word and the exact-f32
+ *     kernels, enqueued behind them, return at once unless it is raised (two
+ *     words alternate between calls; the next call's first kernel zeroes the
+ *     other).  Otherwise m2_vocoder synchronises `stream` and re-runs. */
 int32_t m2_set_range_policy(m2_model* model, int32_t policy);
 int32_t m2_model_check(m2_model* model, void* stream, int32_t* flagged);
 

@@ -187,6 +187,12 @@ struct m2_model {
     // device address), what a raised flag does (m2_set_range_policy), and the
     // exact-f32 attention for weights whose q/k/v bound leaves the f16 range
     int32_t* rflag_host = nullptr;
+    // range policy 1 on the fused vocoders: two device flag words used by
+    // alternate calls (rseq parity) - the split kernels raise the call's word,
+    // the exact-f32 redo kernels run only when it is raised, and the next
+    // call's head kernel zeroes it
+    int* rflag_dev = nullptr;
+    mutable unsigned rseq = 0;
     int range_policy = 0;
     // one-launch transformer layers: work-queue counters and the launch
     // sequence whose parity picks their set (one stream per model)
@@ -925,6 +931,15 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
         std::memset(h, 0, 64);
         m->rflag_host = static_cast<int32_t*>(h);
         m->vx.rflag = static_cast<int*>(d);
+        void* dv = nullptr;
+        e = hipMalloc(&dv, 64);
+        if (e == hipSuccess) e = hipMemsetAsync(dv, 0, 64, st);
+        if (e != hipSuccess) {
+            if (dv) (void)hipFree(dv);
+            m2_model_destroy(m);
+            return hip_status(e, "hipMalloc(range flags)");
+        }
+        m->rflag_dev = static_cast<int*>(dv);
     }
     // work-queue counters of the one-launch transformer layers (TflQueue)
     e = hipMalloc(&m->tflq, kTflQueueWords * sizeof(unsigned));
@@ -948,6 +963,7 @@ int32_t m2_model_destroy(m2_model* model) {
     if (model->tbuf) (void)hipFree(model->tbuf);
     if (model->mbuf) (void)hipFree(model->mbuf);
     if (model->rflag_host) (void)hipHostFree(model->rflag_host);
+    if (model->rflag_dev) (void)hipFree(model->rflag_dev);
     if (model->tflq) (void)hipFree(model->tflq);
     hipError_t e = hipFree(model->buf);
     delete model;
@@ -1225,7 +1241,7 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
 
 namespace {
 int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                    float* const* buf, hipStream_t st, bool x3);
+                    float* const* buf, hipStream_t st, bool x3, int redo = -1);
 
 // Audio samples [64 f0, 64 f1) of every utterance of a T-frame mel, computed
 // over the window [f0 - halo, f1 + halo) clipped to [0, T): the window's mel
@@ -1233,7 +1249,8 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
 // call, and the centre of its audio copied to out (row pitch out_pitch floats,
 // utterance b's chunk at out + b * out_pitch).
 int32_t vocoder_window(const m2_model* m, const float* mel, int32_t layout, int32_t B, int32_t T, int32_t f0,
-                       int32_t f1, float* out, size_t out_pitch, const ChunkBufs& c, hipStream_t st, bool x3) {
+                       int32_t f1, float* out, size_t out_pitch, const ChunkBufs& c, hipStream_t st, bool x3,
+                       int redo = -1) {
     const int M = m->cfg.mel_channels;
     const int w0 = std::max(0, f0 - kVocHalo), w1 = std::min(T, f1 + kVocHalo), W = w1 - w0;
     if (layout == 1)  // [B,T,M]: utterance b's window is W*M contiguous floats
@@ -1242,16 +1259,17 @@ int32_t vocoder_window(const m2_model* m, const float* mel, int32_t layout, int3
     else  // [B,M,T]: one W-float row per (utterance, channel)
         M2_HIP(hipMemcpy2DAsync(c.mel, (size_t)W * 4, mel + w0, (size_t)T * 4, (size_t)W * 4, (size_t)B * M,
                                 hipMemcpyDeviceToDevice, st));
-    int32_t rc = vocoder_run(m, c.mel, layout, B, W, c.audio, c.voc, st, x3);
+    int32_t rc = vocoder_run(m, c.mel, layout, B, W, c.audio, c.voc, st, x3, redo);
     if (rc) return rc;
     M2_HIP(hipMemcpy2DAsync(out, out_pitch * 4, c.audio + (size_t)64 * (f0 - w0), (size_t)64 * W * 4,
                             (size_t)64 * (f1 - f0) * 4, B, hipMemcpyDeviceToDevice, st));
     return M2_OK;
 }
 
-// One m2_vocoder call on the split (x3) or exact-f32 kernels.
+// One m2_vocoder call on the split (x3) or exact-f32 kernels; redo >= 0: the
+// on-device range redo with flag word redo (vocoder_run).
 int32_t vocoder_call(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                     void* workspace, size_t workspace_bytes, hipStream_t st, bool x3) {
+                     void* workspace, size_t workspace_bytes, hipStream_t st, bool x3, int redo = -1) {
     Carve a(workspace, workspace_bytes);
     if (m->chunk_frames > 0 && T > m->chunk_frames) {  // streamed: chunk by chunk into out_audio
         ChunkBufs c;
@@ -1261,7 +1279,7 @@ int32_t vocoder_call(const m2_model* m, const float* mel, int32_t mel_layout, in
         for (int f0 = 0; f0 < T; f0 += m->chunk_frames) {
             const int f1 = std::min(T, f0 + m->chunk_frames);
             const int32_t rc = vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_audio + (size_t)64 * f0,
-                                              (size_t)64 * T, c, st, x3);
+                                              (size_t)64 * T, c, st, x3, redo);
             if (rc) return rc;
         }
         return M2_OK;
@@ -1270,7 +1288,7 @@ int32_t vocoder_call(const m2_model* m, const float* mel, int32_t mel_layout, in
     carve_voc(a, m->cfg, B, T, buf);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
-    return vocoder_run(m, mel, mel_layout, B, T, out_audio, buf, st, x3);
+    return vocoder_run(m, mel, mel_layout, B, T, out_audio, buf, st, x3, redo);
 }
 
 // Sticky range error of an earlier call (policy 0), returned and cleared on entry.
@@ -1285,8 +1303,15 @@ int32_t range_entry(const m2_model* m, const char* what) {
     return M2_OK;
 }
 
-// Policy 1: wait for the call, and re-run it on the exact-f32 kernels if its
-// audio came out non-finite.
+// Policy 1 on the fused vocoders: the flag word of this call for an on-device
+// redo (vocoder_run), or -1 (the host-side fallback below).
+int device_redo_word(const m2_model* m, bool x3) {
+    if (m->range_policy != 1 || !x3 || !m->fused || !m->rflag_dev) return -1;
+    return (int)(m->rseq++ & 1u);
+}
+
+// Policy 1 otherwise: wait for the call, and re-run it on the exact-f32
+// kernels if its audio came out non-finite.
 template <typename F>
 int32_t range_fallback(const m2_model* m, hipStream_t st, bool x3, F redo) {
     if (m->range_policy != 1 || !x3 || !m->rflag_host) return M2_OK;
@@ -1307,7 +1332,9 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
     int32_t rc = range_entry(m, "m2_vocoder");
     if (rc) return rc;
     const bool x3 = m->x3;
-    if ((rc = vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, x3))) return rc;
+    const int redo = device_redo_word(m, x3);
+    if ((rc = vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, x3, redo))) return rc;
+    if (redo >= 0) return M2_OK;
     return range_fallback(m, st, x3, [&] {
         return vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, false);
     });
@@ -1327,8 +1354,10 @@ int32_t m2_vocoder_chunk(const m2_model* m, const float* mel, int32_t mel_layout
     if (B == 0) return M2_OK;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const bool x3 = m->x3;
-    if ((rc = vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_chunk, (size_t)64 * (f1 - f0), c, st, x3)))
+    const int redo = device_redo_word(m, x3);
+    if ((rc = vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_chunk, (size_t)64 * (f1 - f0), c, st, x3, redo)))
         return rc;
+    if (redo >= 0) return M2_OK;
     return range_fallback(m, st, x3, [&] {
         return vocoder_window(m, mel, mel_layout, B, T, f0, f1, out_chunk, (size_t)64 * (f1 - f0), c, st, false);
     });
@@ -1378,8 +1407,12 @@ int32_t m2_vocoder_select(m2_model* m, int32_t path) {
 }  // extern "C"
 
 namespace {
+// redo >= 0 (range policy 1, x3): the split kernels raise flag word `redo`
+// instead of the host-mapped flag, and the exact-f32 kernels follow, each
+// workgroup returning at once unless that word is raised - a call whose split
+// audio came out non-finite is recomputed on the device, with no host wait.
 int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                    float* const* buf, hipStream_t st, bool x3) {
+                    float* const* buf, hipStream_t st, bool x3, int redo) {
     int32_t rc;
     if (m->fused) {
         const int call = m->prof_calls;
@@ -1391,6 +1424,18 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
             const size_t slot = (size_t)call * kVocKernels + kidx;
             (void)hipEventRecord(begin ? m->prof_begin[slot] : m->prof_end[slot], st);
         };
+        if (x3 && redo >= 0) {
+            VocX vx = m->vx;
+            vx.rflag = m->rflag_dev + redo;
+            vx.rclear = m->rflag_dev + (redo ^ 1);
+            if ((rc = launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vx,
+                                        buf[0], buf[1], out_audio, st, mark)))
+                return rc;
+            VocW wg = m->vw;
+            wg.guard = m->rflag_dev + redo;
+            return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, wg,
+                                        buf[0], buf[1], out_audio, st, [](int, bool) {});
+        }
         if (x3)
             return launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vx,
                                      buf[0], buf[1], out_audio, st, mark);

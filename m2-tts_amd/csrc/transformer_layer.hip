@@ -20,11 +20,18 @@
 // operand load of the consumer is one 1-KB contiguous wave read (a load of 16
 // rows x 64 B - the row-major form - ran at 34 GB/s per CU against 82 GB/s
 // contiguous from L2, tools/probe/l2bw.hip):
-//   Q, K  [B*heads][npad/16 row blocks][KS k-steps][hi|lo][lane][8 f16]: lane
-//         (row li, group g) of k-step ks holds dims 32 ks + 8 g .. + 7 of row
-//         16 blk + li; dims padded to DP = 32 * KS with zeros; Q pre-scaled by
-//         scale * log2(e) when the attention is unmasked (the score is then the
-//         raw dot product, base 2);
+//   Q, K  [B*heads][npad/16 row blocks][KS k-steps][hi|lo][lane][8 f16]
+//         [KT tail steps][hi|lo][lane < 32][8 f16]: lane (row li, group g) of
+//         k-step ks holds dims 32 ks + 8 g .. + 7 of row 16 blk + li (the
+//         operands of v_mfma_f32_16x16x32_f16); a head_dim that is an odd
+//         multiple of 16 (48, 16) ends in a 16-dim tail step stored for lane
+//         groups 0, 1 only (512 B per plane): the lanes of groups 2, 3 take
+//         zeros from an out-of-range buffer offset, so no zero padding is
+//         stored or read (the MFMAs still run K = 32: a K = 16 MFMA chained
+//         with K = 32 ones on one accumulator gave wrong scores, the hazard
+//         DESIGN.md notes in round 2); Q pre-scaled by scale * log2(e)
+//         when the attention is unmasked (the score is then the raw dot
+//         product, base 2);
 //   V^T   [B*heads][npad/32 chunks][hd/16 blocks][hi|lo][lane][8 f16]: lane
 //         (dim 16 t + li, group g) holds the chunk's keys at positions
 //         8 g .. + 7, keys in the order the P^T fragment of the PV MFMA holds
@@ -99,11 +106,17 @@ __device__ __forceinline__ f32x4 mfma(u32x4 a, u32x4 b, f32x4 c) {
     typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
 }
+// Byte offset of this lane's tail-step piece in a block (lane groups 0, 1),
+// or one past any buffer record for groups 2, 3 (a raw buffer load there
+// returns zeros).
+__device__ __forceinline__ int tail_off(int lane) { return lane < 32 ? 16 * lane : 0x40000000; }
 
 template <int HD>
 struct Geo {
-    static constexpr int KS = (HD + 31) / 32, DP = 32 * KS, MT = HD / 16;
-    static constexpr int QKBLK = KS * 2048;  // bytes of a 16-row Q / K block (KS k-steps x hi|lo x 1 KB)
+    static constexpr int KS = HD / 32, KT = (HD % 32) / 16, MT = HD / 16;
+    static constexpr int KSA = KS > 0 ? KS : 1;  // array extent
+    static constexpr int TAIL = KS * 2048;       // byte offset of the tail step (hi 512 B | lo 512 B)
+    static constexpr int QKBLK = KS * 2048 + KT * 1024;  // bytes of a 16-row Q / K block
     static constexpr int VCH = MT * 2048;    // bytes of a V^T chunk (MT d-blocks x hi|lo x 1 KB)
     static constexpr int XW = 2 + 4 * MT;    // merge record per lane (m, lsum, acc)
 };
@@ -259,16 +272,14 @@ __device__ __forceinline__ void store_qk(const QkvOut& o, int b, int t0, int N, 
     // fragment order: dims d0 .. d0+3 of row t are half (d0 % 8) / 4 of lane
     // ((d0 % 32) / 8) * 16 + t % 16 in k-step d0 / 32 of row block t / 16
     unsigned char* blk = (which ? o.k : o.q) + ((size_t)(b * HEADS + h) * (o.npad / 16) + t / 16) * G::QKBLK;
-    auto piece = [&](int d) { return blk + (d / 32) * 2048 + ((((d & 31) >> 3) * 16 + (t & 15)) * 16) + ((d & 7) >> 2) * 8; };
-    unsigned char* ph = piece(d0);
-    *reinterpret_cast<uint2*>(ph) = uint2{h0, h1};
-    *reinterpret_cast<uint2*>(ph + 1024) = uint2{l0, l1};
-    if constexpr (G::DP > HD) {
-        if (dh == HD - 16) {  // the head's last block also writes the zero padding dims
-            unsigned char* pz = piece(HD + 4 * g);
-            *reinterpret_cast<uint2*>(pz) = uint2{0u, 0u};
-            *reinterpret_cast<uint2*>(pz + 1024) = uint2{0u, 0u};
-        }
+    if (d0 < 32 * G::KS) {
+        unsigned char* ph = blk + (d0 / 32) * 2048 + ((((d0 & 31) >> 3) * 16 + (t & 15)) * 16) + ((d0 & 7) >> 2) * 8;
+        *reinterpret_cast<uint2*>(ph) = uint2{h0, h1};
+        *reinterpret_cast<uint2*>(ph + 1024) = uint2{l0, l1};
+    } else {  // tail step: lane ((d0 - 32 KS) / 8) * 16 + t % 16, half (d0 % 8) / 4
+        unsigned char* ph = blk + G::TAIL + (((d0 - 32 * G::KS) >> 3) * 16 + (t & 15)) * 16 + ((d0 & 7) >> 2) * 8;
+        *reinterpret_cast<uint2*>(ph) = uint2{h0, h1};
+        *reinterpret_cast<uint2*>(ph + 512) = uint2{l0, l1};
     }
 }
 
@@ -380,15 +391,15 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
                                                const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
                                                int len, float sl2, unsigned char* A, float* xs, Between between) {
     using G = Geo<HD>;
-    constexpr int KS = G::KS, MT = G::MT, QKBLK = G::QKBLK, VCH = G::VCH, XW = G::XW;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, VCH = G::VCH, XW = G::XW;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, g = lane >> 4;
     const int h = wave / WPH, kq = wave - h * WPH;
-    const int nch = npad / KC;
+    const int nch = npad / KC, nchl = (N + KC - 1) / KC;  // layout chunks, chunks holding live keys
     const size_t bh = (size_t)__builtin_amdgcn_readfirstlane(b * HEADS + h);
 
     // B = Q^T fragments: lane (query li of block qt, dims 32 ks + 8 g .. + 7)
-    u32x4 qh[RB][KS], ql[RB][KS];
+    u32x4 qh[RB][KSA], ql[RB][KSA], qxh[RB], qxl[RB];
 #pragma unroll
     for (int qt = 0; qt < RB; ++qt) {
         const unsigned char* qp = qb + (bh * (npad / 16) + t0 / 16 + qt) * QKBLK + 16 * lane;
@@ -397,17 +408,22 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
             qh[qt][ks] = *reinterpret_cast<const u32x4*>(qp + 2048 * ks);
             ql[qt][ks] = *reinterpret_cast<const u32x4*>(qp + 2048 * ks + 1024);
         }
+        if constexpr (KT) {
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            qxh[qt] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp + G::TAIL) : z;
+            qxl[qt] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp + G::TAIL + 512) : z;
+        }
     }
     // Chunk c's K fragments and V^T fragments through a buffer descriptor whose
     // record count is 0 past the last chunk: the prefetch of a chunk that does
     // not exist is issued unconditionally (no branch around a load, so the
     // compiler's vmcnt waits stay graded) and reads zeros without traffic.
-    const int loff = 16 * lane;
+    const int loff = 16 * lane, toff = tail_off(lane);
     struct Frag {
-        u32x4 kh[2][KS], kl[2][KS], vh[MT], vl[MT];
+        u32x4 kh[2][KSA], kl[2][KSA], kxh[2], kxl[2], vh[MT], vl[MT];
     };
     auto load = [&](Frag& f, int c) {
-        const bool ok = c < nch;
+        const bool ok = c < nchl;
         const auto rk = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<unsigned char*>(kb) + (bh * (npad / 16) + (size_t)(ok ? c : 0) * 2) * QKBLK, 0,
             ok ? 2 * QKBLK : 0, 0x00020000);
@@ -421,6 +437,14 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
                     u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff + u * QKBLK + 2048 * ks, 0, 0));
                 f.kl[u][ks] = __builtin_bit_cast(
                     u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff + u * QKBLK + 2048 * ks + 1024, 0, 0));
+            }
+        if constexpr (KT)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f.kxh[u] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, toff, u * QKBLK + G::TAIL, 0));
+                f.kxl[u] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, toff, u * QKBLK + G::TAIL + 512, 0));
             }
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -453,6 +477,11 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
                     st = mfma(f.kh[u][ks], qh[qt][ks], st);
                     st = mfma(f.kh[u][ks], ql[qt][ks], st);
                     st = mfma(f.kl[u][ks], qh[qt][ks], st);
+                }
+                if constexpr (KT) {
+                    st = mfma(f.kxh[u], qxh[qt], st);
+                    st = mfma(f.kxh[u], qxl[qt], st);
+                    st = mfma(f.kxl[u], qxh[qt], st);
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) s[qt][u][r] = st[r];
@@ -554,7 +583,7 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
     // chunks kq, kq + 4, ... through a two-slot register ring.  The scheduling
     // barriers keep each slot's loads in program order (slot 0 before slot 1),
     // so the wait at the top of an iteration is for the older slot only.
-    const int nj = kq < nch ? (nch - kq + WPH - 1) / WPH : 0;
+    const int nj = kq < nchl ? (nchl - kq + WPH - 1) / WPH : 0;
     Frag f0, f1;
     load(f0, kq);
     __builtin_amdgcn_sched_barrier(0);
@@ -621,6 +650,211 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Attention of a 64-row tile for large grids: wave w = (head w / 4, query
+// block w % 4) owns 16 queries of one head over ALL keys (its own online
+// softmax, no merge), and the workgroup stages each 32-key chunk's K and V^T
+// fragments of both heads in LDS once (one 1-KB contiguous wave read per
+// piece, 3 per thread for head_dim 48), shared by the four waves of the head.
+// The key-quarter form above reads every K / V byte from L2 once per 16 or 32
+// queries and is bound by the CU's L2 read rate (~37 B/clk, tools/probe/
+// l2bw.hip); this one reads it once per 64 queries and then from LDS.  Two
+// LDS buffers, two register sets: chunk c + 2 is in flight from L2 while c is
+// computed and c + 1 goes to LDS; one barrier per chunk.  Leaves the
+// normalised rows in A (split, stride srs(H)); `ring` is 2 * chunk bytes.
+template <int HD>
+struct QsGeo {
+    using G = Geo<HD>;
+    static constexpr int KB = 2 * G::QKBLK;      // one head's K of a chunk (two 16-key blocks)
+    static constexpr int HB = KB + G::VCH;       // one head's K and V^T
+    static constexpr int CB = 2 * HB;            // a chunk, both heads
+    static constexpr int PPT = CB / (16 * NW * 64);  // 16-B pieces per thread
+    static_assert(CB % (16 * NW * 64) == 0, "chunk bytes a multiple of one 512-thread b128 round");
+};
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int H, int HD, bool MASKED>
+__device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
+                                                 const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
+                                                 int len, float sl2, unsigned char* A, unsigned char* ring) {
+    using G = Geo<HD>;
+    using Q = QsGeo<HD>;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, PPT = Q::PPT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, g = lane >> 4;
+    const int h = wave / WPH, qblk = wave - h * WPH;
+    const int nch = npad / KC, nchl = (N + KC - 1) / KC;
+
+    // B = Q^T fragments of this wave's 16 queries
+    u32x4 qh[KSA], ql[KSA], qxh, qxl;
+    {
+        const unsigned char* qp =
+            qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + qblk) * QKBLK + 16 * lane;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            qh[ks] = *reinterpret_cast<const u32x4*>(qp + 2048 * ks);
+            ql[ks] = *reinterpret_cast<const u32x4*>(qp + 2048 * ks + 1024);
+        }
+        if constexpr (KT) {
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            qxh = lane < 32 ? *reinterpret_cast<const u32x4*>(qp + G::TAIL) : z;
+            qxl = lane < 32 ? *reinterpret_cast<const u32x4*>(qp + G::TAIL + 512) : z;
+        }
+    }
+    // the global source of piece p (16 B) of chunk c: [head][K blocks | V^T chunk]
+    const unsigned char* src[PPT];
+    int step[PPT];  // bytes from chunk c to c + 1 of that piece
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int o = 16 * (tid + NW * 64 * i), hh = o / Q::HB, r = o - hh * Q::HB;
+        const size_t bh = (size_t)b * HEADS + hh;
+        if (r < Q::KB) {
+            src[i] = kb + bh * (npad / 16) * QKBLK + r;
+            step[i] = 2 * QKBLK;
+        } else {
+            src[i] = vb + bh * nch * G::VCH + (r - Q::KB);
+            step[i] = G::VCH;
+        }
+    }
+    u32x4 pre[2][PPT];
+    auto gload = [&](u32x4 (&d)[PPT], int c) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) d[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)c * step[i]);
+    };
+    auto lstore = [&](const u32x4 (&d)[PPT], int buf) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * CB + 16 * (tid + NW * 64 * i)) = d[i];
+    };
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = MASKED ? -INFINITY : 0.f, lsum = 0.f;
+    bool fresh = true;
+
+    auto process = [&](const unsigned char* cb, int c) {
+        const unsigned char* kp = cb + h * Q::HB + 16 * lane;
+        const unsigned char* vp = kp + Q::KB;
+        float s[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float nm = (MASKED || fresh) ? 0.f : -m;
+            f32x4 st = f32x4{nm, nm, nm, nm};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + 2048 * ks);
+                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + 2048 * ks + 1024);
+                st = mfma(kh, qh[ks], st);
+                st = mfma(kh, ql[ks], st);
+                st = mfma(kl, qh[ks], st);
+            }
+            if constexpr (KT) {  // lanes of groups 2, 3 read the lo plane: their Q operand is zero
+                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + G::TAIL);
+                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
+                st = mfma(kxh, qxh, st);
+                st = mfma(kxh, qxl, st);
+                st = mfma(kxl, qxh, st);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[u][r] = st[r];
+        }
+        const int k0 = c * KC;
+        if constexpr (MASKED) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = k0 + 16 * u + 4 * g + r;
+                    s[u][r] = key < len ? s[u][r] * sl2 : (key < N ? kMaskFill * kLog2e : -INFINITY);
+                }
+        } else if (N - k0 < KC) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[u][r] = k0 + 16 * u + 4 * g + r < N ? s[u][r] : -INFINITY;
+        }
+        const float cmax = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                                 fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+        if constexpr (MASKED) {
+            const float mn = vmax(m, grp4_max(cmax));
+            const float corr = __builtin_amdgcn_exp2f(m - mn);
+            lsum *= corr;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[t] *= corr;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[u][r] -= mn;
+            m = mn;
+        } else {
+            if (__builtin_amdgcn_ballot_w64(fresh || cmax > kLazyT) != 0) {  // wave-uniform: move the base
+                const float cm = grp4_max(cmax);
+                const float d = fresh ? cm : vmax(cm, 0.f);
+                m += d;
+                if (!fresh) {
+                    const float corr = __builtin_amdgcn_exp2f(-d);
+                    lsum *= corr;
+#pragma unroll
+                    for (int t = 0; t < MT; ++t) acc[t] *= corr;
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[u][r] -= d;
+            }
+            fresh = false;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                s[u][r] = __builtin_amdgcn_exp2f(s[u][r]);
+                lsum += s[u][r];
+            }
+        unsigned ph[4], pl[4];
+        split2u(s[0][0], s[0][1], ph[0], pl[0]);
+        split2u(s[0][2], s[0][3], ph[1], pl[1]);
+        split2u(s[1][0], s[1][1], ph[2], pl[2]);
+        split2u(s[1][2], s[1][3], ph[3], pl[3]);
+        const u32x4 bh4 = u32x4{ph[0], ph[1], ph[2], ph[3]}, bl4 = u32x4{pl[0], pl[1], pl[2], pl[3]};
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+            const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+            acc[t] = mfma(vh, bh4, acc[t]);
+            acc[t] = mfma(vh, bl4, acc[t]);
+            acc[t] = mfma(vl, bh4, acc[t]);
+        }
+    };
+
+    gload(pre[0], 0);
+    if (1 < nchl) gload(pre[1], 1);
+    lstore(pre[0], 0);
+    lds_barrier();
+#pragma unroll 1
+    for (int c = 0; c < nchl; c += 2) {
+        // even chunk c from buffer 0; c + 1 goes to buffer 1, c + 2 is requested
+        if (c + 1 < nchl) lstore(pre[1], 1);
+        if (c + 2 < nchl) gload(pre[0], c + 2);
+        process(ring, c);
+        lds_barrier();
+        if (c + 1 >= nchl) break;
+        if (c + 2 < nchl) lstore(pre[0], 0);
+        if (c + 3 < nchl) gload(pre[1], c + 3);
+        process(ring + CB, c + 1);
+        lds_barrier();
+    }
+    TSTAMP(1);
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    const float inv = 1.0f / lsum;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+        put_split4<H>(A + (16 * qblk + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), acc[t][0] * inv, acc[t][1] * inv,
+                      acc[t][2] * inv, acc[t][3] * inv);
+}
+
+// ---------------------------------------------------------------------------
 struct LArgs {
     int B, N, npad, ntile;
     unsigned* qcnt;
@@ -642,10 +876,16 @@ struct LArgs {
 template <int H, bool MASKED, int NEXT, int NN, int RB>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
+    constexpr bool QS = RB == 4;  // 64-row tiles: attention_qsplit
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att, then LN2(o), LN(y) (split)
-    __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];           // o, then y (fp32)
-    __shared__ __attribute__((aligned(16))) unsigned char Hd[TR * srs(F)];  // relu(FFN1) (split)
-    __shared__ __attribute__((aligned(16))) float xs[NW * RB * 64 * Geo<HD>::XW];
+    // the attention's scratch (key-quarter merge records / the K-V chunk ring)
+    // and, after it, o / y (fp32, O) and relu(FFN1) (split, Hd)
+    constexpr int OB = TR * frs(H) * 4, HB = TR * srs(F);
+    constexpr int XB = QS ? 2 * QsGeo<HD>::CB : NW * RB * 64 * Geo<HD>::XW * 4;
+    __shared__ __attribute__((aligned(16))) unsigned char U[OB + HB > XB ? OB + HB : XB];
+    float* const O = reinterpret_cast<float*>(U);
+    unsigned char* const Hd = U + OB;
+    float* const xs = reinterpret_cast<float*>(U);
     // the layer's vectors, read once into LDS (their L2 latency otherwise sits
     // in every LayerNorm and epilogue): bo | g2 | b2n | b1 [F] | b2 | gn | bn | bn2 [NN]
     constexpr int VO = 0, VG2 = H, VB2N = 2 * H, VB1 = 3 * H, VB2 = 3 * H + F, VGN = 4 * H + F, VBN = 5 * H + F,
@@ -679,9 +919,16 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     int len = N;
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
-    attention_tile<H, HD, MASKED, RB>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs, [&] {
+    if constexpr (QS) {
+        attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         if (wave < H / 16) so.load(a.Wo, wave);
-    });
+        __syncthreads();
+        TSTAMP(2);
+    } else {
+        attention_tile<H, HD, MASKED, RB>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs, [&] {
+            if (wave < H / 16) so.load(a.Wo, wave);
+        });
+    }
     const size_t row0 = (size_t)b * N + t0;
     // o = x + att . Wo^T + bo
     if (wave < H / 16) {
@@ -907,12 +1154,13 @@ bool tfl_proj_supported(int H, int NN) {
            (H == 96 && (NN == 80 || NN == 96));
 }
 
-int tfl_npad(int N) { return (N + tfl::KC - 1) / tfl::KC * tfl::KC; }
+// a multiple of 64 so that 16-, 32- and 64-row tiles all cover [0, npad) exactly
+int tfl_npad(int N) { return (N + 63) / 64 * 64; }
 
 namespace {
 void tfl_sizes(int B, int N, int H, int heads, size_t* qk, size_t* v) {
-    const int HD = H / heads, KS = (HD + 31) / 32, npad = tfl_npad(N);
-    *qk = align_up((size_t)B * heads * (npad / 16) * KS * 2048, 256);
+    const int HD = H / heads, npad = tfl_npad(N);
+    *qk = align_up((size_t)B * heads * (npad / 16) * ((HD / 32) * 2048 + ((HD % 32) / 16) * 1024), 256);
     *v = align_up((size_t)B * heads * (npad / tfl::KC) * (HD / 16) * 2048, 256);
 }
 }  // namespace
@@ -930,13 +1178,16 @@ void tfl_carve(unsigned char* base, int B, int N, int H, int heads, TflBufs* out
 }
 
 namespace {
-// Rows per workgroup: 16 while one round of the 256 CUs holds the grid, else
-// 32 (half the K / V and weight bytes per row).  M2_TFL_RB=1|2 forces one.
+// Rows per workgroup of the layer launches: 64 (query-split attention, K / V
+// staged in LDS) once the 64-row tiles alone fill the 256 CUs; else 16 while
+// one round of the CUs holds the 16-row grid, else 32.  M2_TFL_RB=1|2|4
+// forces one.  The first (LN1 -> QKV) launch has no attention: at most 32.
 int tfl_rb(int B, int N) {
     const char* e = std::getenv("M2_TFL_RB");  // per call: tests switch it
     const int forced = e ? std::atoi(e) : 0;
-    if (forced == 1 || forced == 2) return forced;
-    return (long)B * (tfl_npad(N) / tfl::TQ) > 256 ? 2 : 1;
+    if (forced == 1 || forced == 2 || forced == 4) return forced;
+    const long tiles16 = (long)B * (tfl_npad(N) / tfl::TQ);
+    return tiles16 >= 4 * 256 ? 4 : (tiles16 > 256 ? 2 : 1);
 }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
 float tfl_sl2(int H) {
@@ -955,7 +1206,7 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.B = B;
     a.N = N;
     a.npad = tfl_npad(N);
-    const int rb = tfl_rb(B, N);
+    const int rb = tfl_rb(B, N) > 1 ? 2 : 1;
     a.ntile = a.npad / (tfl::TQ * rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
@@ -1042,7 +1293,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2>), grid, blk, 0, st, a);  \
+        if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
+        else if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2>), grid, blk, 0, st, a);  \
         else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 1>), grid, blk, 0, st, a);          \
         M2_LAUNCHED("tfl layer_kernel");                                                        \
         return M2_OK;                                                                           \

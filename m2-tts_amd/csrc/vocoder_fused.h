@@ -15,6 +15,10 @@ struct VocW {
     const float *wt[4], *bt[4];
     const float *w1[4], *b1[4], *w2[4], *b2[4];
     const float *wo, *bo;
+    // device word; when set, every workgroup returns at once unless it is
+    // non-zero (the range policy's on-device redo of a split-path call whose
+    // audio came out non-finite)
+    const int* guard = nullptr;
 };
 
 bool vocoder_fused_supported(int M, int C);
@@ -113,8 +117,12 @@ struct VocX {
     const float* hcb;
     const float* hce;
     // set to 1 (vector store) by the last kernel when an audio sample is not
-    // finite; host-mapped (m2_model_check)
+    // finite; host-mapped (m2_model_check), or a device word of the range
+    // policy's on-device redo
     int* rflag;
+    // zeroed by the head kernel's first thread when set (the on-device redo's
+    // other flag word, whose last readers ran in the previous call)
+    int* rclear = nullptr;
 };
 
 // Non-finite output check of the split path's last kernel: any NaN among the

@@ -384,6 +384,7 @@ __device__ unsigned long long g_stamps[3][4096][16][16];
 template <class Cfg, bool TRANS>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(const float* __restrict__ mel, int T,
                                                                              VocW w, float* __restrict__ U1) {
+    if (w.guard && *w.guard == 0) return;  // guarded redo, not needed
     constexpr int M = Cfg::M, C = Cfg::C, TF = Cfg::TF;
     using Pl = HeadPlan<M, C, TF, Cfg::CP>;
     constexpr int C1 = Pl::C1;
@@ -423,6 +424,7 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(co
 template <class Cfg>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(const float* __restrict__ U1, int L1,
                                                                             VocW w, float* __restrict__ U2) {
+    if (w.guard && *w.guard == 0) return;  // guarded redo, not needed
     constexpr int CI = Cfg::C / 2, W = Cfg::W2;
     using Pl = MidPlan<CI, W>;
     constexpr int CO = Pl::CO;
@@ -458,6 +460,7 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(con
 template <class Cfg>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(const float* __restrict__ U2, int L2,
                                                                              VocW w, float* __restrict__ audio) {
+    if (w.guard && *w.guard == 0) return;  // guarded redo, not needed
     constexpr int CI = Cfg::C / 4, W = Cfg::W3;
     using Pl = TailPlan<CI, W>;
     constexpr int C3 = Pl::C3, C4 = Pl::C4;

@@ -942,6 +942,8 @@ constexpr bool head_planar() {
 template <class Cfg, bool TRANS, bool COMP = false>
 __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const float* __restrict__ mel, int T,
                                                                             VocX w, unsigned char* __restrict__ U1) {
+    if (w.rclear && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        *reinterpret_cast<volatile int*>(w.rclear) = 0;
     constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
     using Pl = HeadPlan<MP, C, TF, head_planar<Cfg>()>;
     constexpr int C1 = Pl::C1;

@@ -207,8 +207,9 @@ class HipModel:
     def set_range_policy(self, policy: str):
         """What a non-finite split-path result does (m2_set_range_policy):
         "report" - the next call raises M2Error (M2_E_RANGE), check() reports
-        it at once; "fallback" - each vocoder call waits for its kernels and
-        re-runs on the exact-f32 kernels when its audio is not finite."""
+        it at once; "fallback" - a call whose audio is not finite is re-run on
+        the exact-f32 kernels (on the device, no host wait, for the fused
+        vocoders; otherwise after a stream synchronisation)."""
         if policy not in RANGE_POLICIES:
             raise ValueError(f"range policy {policy!r}: expected one of {sorted(RANGE_POLICIES)}")
         _lib.call("m2_set_range_policy", self.handle, RANGE_POLICIES[policy])

@@ -244,11 +244,14 @@ class M2TTSModel(nn.Module):
         """The split-f16 vocoder carries fp32 values as f16 hi/lo pairs; an
         input or activation of magnitude >= 65520 turns its audio non-finite
         (never silently wrong).  "fallback" (the default, also without this
-        call; M2_RANGE_POLICY overrides it for new handles): every vocoder
-        call waits for its result and recomputes it on the exact-f32 kernels
-        when it is not finite, so a call never returns non-finite audio for an
-        input the reference's fp32 path handles (costs one host
-        synchronisation per call: bench.py's ``vocoder_default_policy``).
+        call; M2_RANGE_POLICY overrides it for new handles): a vocoder call
+        whose split audio is not finite is recomputed on the exact-f32 kernels
+        before anything behind it on the stream runs, so a call never returns
+        non-finite audio for an input the reference's fp32 path handles - on
+        the device, without a host wait (the exact kernels are enqueued behind
+        the split ones and return at once unless the call was flagged; their
+        empty launches are the per-call cost, bench.py's
+        ``vocoder_default_policy``).
         "report" (opt-in, what the throughput benchmarks use): asynchronous -
         the next call raises, check_numerics() reports it at once."""
         if policy not in runtime.RANGE_POLICIES:

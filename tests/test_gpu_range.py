@@ -97,6 +97,43 @@ def test_default_policy_inference_never_nan(gpu, stage):
 
 
 @pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_fallback_on_device_alternating_calls(gpu, stage):
+    """The "fallback" policy's on-device redo (two flag words used by
+    alternate calls, the next call's head kernel zeroing the other): any
+    sequence of overflowing and ordinary calls gives, call by call, the
+    exact-f32 audio for the former and the split-path audio for the latter,
+    with nothing left pending."""
+    ok, bad = _mel(stage, 30, 1.0).to(gpu), _mel(stage, 30, 1e6, seed=6).to(gpu)
+    ref = build_model(stage, gpu)
+    ref.set_range_policy("report")
+    split_ok = ref.vocoder(ok)
+    ref.set_vocoder_precision("f32")
+    exact_bad = ref.vocoder(bad)
+    m = build_model(stage, gpu)
+    m.set_range_policy("fallback")
+    for x in ("bad", "ok", "bad", "bad", "ok", "ok", "bad", "ok"):
+        out = m.vocoder(bad if x == "bad" else ok)
+        assert torch.equal(out, exact_bad if x == "bad" else split_ok), x
+    torch.cuda.synchronize()
+    m.check_numerics()
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_fallback_on_device_chunked(gpu, stage):
+    """Streamed (chunked) vocoding with an overflowing stretch in one window:
+    finite audio within the waveform bound of the oracle."""
+    mel = _mel(stage, 70, 1.0)
+    mel[:, :, 30:34] *= 1e6
+    m = build_model(stage, gpu)
+    m.set_range_policy("fallback")
+    m.set_vocoder_chunking(16)
+    out = m.vocoder(mel.to(gpu))
+    assert torch.isfinite(out).all()
+    assert rms(out, orc.vocoder(golden_state(stage), mel)) <= AUDIO_RMS_TOL
+    m.check_numerics()
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
 @pytest.mark.parametrize("scale", [1e-3, 1e-6])
 def test_tiny_mel_within_bound(gpu, stage, scale):
     """Mel values whose lo halves are f16 subnormals (or zero): the absolute

@@ -28,9 +28,11 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
-@pytest.fixture(params=["auto", "1", "2"])
+@pytest.fixture(params=["auto", "1", "2", "4"])
 def rows_per_tile(request, monkeypatch):
-    """16- and 32-row workgroup tiles (M2_TFL_RB), and the per-call choice."""
+    """16- and 32-row workgroup tiles with key-quarter attention, 64-row tiles
+    with query-split attention (K / V staged in LDS) (M2_TFL_RB), and the
+    per-call choice."""
     if request.param != "auto":
         monkeypatch.setenv("M2_TFL_RB", request.param)
     return request.param
@@ -58,7 +60,8 @@ def test_text_encoder_edges(gpu, stage, B, S, rows_per_tile):
 
 
 @pytest.mark.parametrize("stage", STAGES)
-@pytest.mark.parametrize("B,T", [(1, 1), (2, 16), (3, 17), (1, 31), (9, 32), (2, 33), (5, 63), (1, 500), (3, 257)])
+@pytest.mark.parametrize("B,T", [(1, 1), (2, 16), (3, 17), (1, 31), (9, 32), (2, 33), (5, 63), (1, 64), (2, 65),
+                                 (1, 500), (3, 257)])
 def test_mel_decoder_edges(gpu, stage, B, T, rows_per_tile):
     cfg = stage_config(stage)
     sd = golden_state(stage)
@@ -104,3 +107,23 @@ def test_inference_ragged_batch_not_multiple_of_8(gpu, stage):
     assert mel.shape == ref_mel.shape
     assert maxabs(mel, ref_mel) <= MEL_MAXABS_TOL
     assert float(((audio.cpu().double() - ref_audio.double()) ** 2).mean().sqrt()) <= 1e-4
+
+
+@pytest.mark.parametrize("stage", STAGES)
+def test_large_grid_query_split_auto(gpu, stage):
+    """Grids of >= 1024 16-row tiles pick the 64-row query-split attention by
+    themselves: the decoder (unmasked, B=64 T=250) and the text encoder
+    (masked, ragged, B=128 S=130) against the oracle."""
+    cfg = stage_config(stage)
+    sd = golden_state(stage)
+    m = build_model(stage, gpu)
+    x = torch.randn(64, 250, cfg.hidden_dim, generator=torch.Generator().manual_seed(5))
+    mel = m.decoder(x.to(gpu))
+    assert maxabs(mel, orc.mel_decoder(sd, cfg, x)) <= DEC_TOL
+    g = torch.Generator().manual_seed(6)
+    ids = torch.randint(0, 42, (128, 130), generator=g)
+    lens = torch.randint(0, 131, (128,), generator=g)
+    enc, mask = m.text_encoder(ids.to(gpu), lens.to(gpu))
+    ref, ref_mask = orc.text_encoder(sd, cfg, ids, lens)
+    assert maxabs(enc, ref) <= ENC_TOL
+    assert torch.equal(mask.cpu(), ref_mask)

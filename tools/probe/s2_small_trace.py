@@ -13,6 +13,7 @@ ROOT = Path(__file__).resolve().parent.parent.parent
 
 
 def summarize(path, steps=20):
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else steps
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"].split("(")[0].replace("void ", "")[:70] for r in rows]
     st = [int(r["Start_Timestamp"]) for r in rows]
@@ -53,12 +54,14 @@ def main():
     m = bench.fixture_model(bench.STAGE2, dev)
     g = torch.Generator().manual_seed(2024)
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    ids = torch.randint(0, 42, (B, 100), generator=g).to(dev)
-    lens = torch.full((B,), 100, dtype=torch.long, device=dev)
+    S = int(sys.argv[3]) if len(sys.argv) > 3 else 100
+    ids = torch.randint(0, 42, (B, S), generator=g).to(dev)
+    lens = torch.full((B,), S, dtype=torch.long, device=dev)
+    m.set_range_policy("report")
     hm = m._hip(dev)
     one = len(sys.argv) > 2 and sys.argv[2] == "one"  # the one-call m2_inference
     with torch.no_grad():
-        for _ in range(200):
+        for _ in range(200 if S <= 100 else 30):
             if one:
                 hm.inference(ids, lens, 1.0)
             else:
