@@ -652,22 +652,25 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
 // ---------------------------------------------------------------------------
 // Attention of a 64-row tile for large grids: wave w = (head w / 4, query
 // block w % 4) owns 16 queries of one head over ALL keys (its own online
-// softmax, no merge), and the workgroup stages each 32-key chunk's K and V^T
-// fragments of both heads in LDS once (one 1-KB contiguous wave read per
-// piece, 3 per thread for head_dim 48), shared by the four waves of the head.
-// The key-quarter form above reads every K / V byte from L2 once per 16 or 32
-// queries and is bound by the CU's L2 read rate (~37 B/clk, tools/probe/
-// l2bw.hip); this one reads it once per 64 queries and then from LDS.  Two
-// LDS buffers, two register sets: chunk c + 2 is in flight from L2 while c is
-// computed and c + 1 goes to LDS; one barrier per chunk.  Leaves the
-// normalised rows in A (split, stride srs(H)); `ring` is 2 * chunk bytes.
+// softmax, no merge), and the workgroup stages the K and V^T fragments of
+// both heads in LDS once per 64 keys (two 32-key chunks: one 1-KB contiguous
+// wave read per piece, 6 per thread for head_dim 48), shared by the four waves
+// of a head.  The key-quarter form above reads every K / V byte from L2 once
+// per 16 or 32 queries and is bound by the CU's L2 read rate (~37 B/clk,
+// tools/probe/l2bw.hip); this one reads it once per 64 queries and then from
+// LDS.  Per 64 keys: the QK^T MFMAs of both chunks (four independent
+// accumulators), one softmax update, the PV MFMAs; two LDS buffers and one
+// register set - keys 64 (p + 2) are in flight from L2 while p is computed and
+// p + 1 goes to LDS; one barrier per 64 keys.  Leaves the normalised rows in A
+// (split, stride srs(H)); `ring` is 2 * 2 chunks.
 template <int HD>
 struct QsGeo {
     using G = Geo<HD>;
     static constexpr int KB = 2 * G::QKBLK;      // one head's K of a chunk (two 16-key blocks)
     static constexpr int HB = KB + G::VCH;       // one head's K and V^T
     static constexpr int CB = 2 * HB;            // a chunk, both heads
-    static constexpr int PPT = CB / (16 * NW * 64);  // 16-B pieces per thread
+    static constexpr int SB = 2 * CB;            // 64 keys
+    static constexpr int PPT = SB / (16 * NW * 64);  // 16-B pieces per thread
     static_assert(CB % (16 * NW * 64) == 0, "chunk bytes a multiple of one 512-thread b128 round");
 };
 
@@ -679,11 +682,12 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
                                                  int len, float sl2, unsigned char* A, unsigned char* ring) {
     using G = Geo<HD>;
     using Q = QsGeo<HD>;
-    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, PPT = Q::PPT;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
+    constexpr int PPT = Q::PPT;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, g = lane >> 4;
     const int h = wave / WPH, qblk = wave - h * WPH;
-    const int nch = npad / KC, nchl = (N + KC - 1) / KC;
+    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);  // layout chunks (even), 64-key steps
 
     // B = Q^T fragments of this wave's 16 queries
     u32x4 qh[KSA], ql[KSA], qxh, qxl;
@@ -701,29 +705,29 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
             qxl = lane < 32 ? *reinterpret_cast<const u32x4*>(qp + G::TAIL + 512) : z;
         }
     }
-    // the global source of piece p (16 B) of chunk c: [head][K blocks | V^T chunk]
+    // the global source of piece i (16 B) of 64-key step 0: [chunk][head][K blocks | V^T chunk]
     const unsigned char* src[PPT];
-    int step[PPT];  // bytes from chunk c to c + 1 of that piece
+    int step[PPT];  // bytes from one 64-key step to the next for that piece
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-        const int o = 16 * (tid + NW * 64 * i), hh = o / Q::HB, r = o - hh * Q::HB;
+        const int o = 16 * (tid + NW * 64 * i), j = o / CB, oc = o - j * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
         const size_t bh = (size_t)b * HEADS + hh;
         if (r < Q::KB) {
-            src[i] = kb + bh * (npad / 16) * QKBLK + r;
-            step[i] = 2 * QKBLK;
+            src[i] = kb + (bh * (npad / 16) + 2 * j) * QKBLK + r;
+            step[i] = 4 * QKBLK;
         } else {
-            src[i] = vb + bh * nch * G::VCH + (r - Q::KB);
-            step[i] = G::VCH;
+            src[i] = vb + (bh * nch + j) * G::VCH + (r - Q::KB);
+            step[i] = 2 * G::VCH;
         }
     }
-    u32x4 pre[2][PPT];
-    auto gload = [&](u32x4 (&d)[PPT], int c) {
+    u32x4 pre[PPT];
+    auto gload = [&](int p) {
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) d[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)c * step[i]);
+        for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * step[i]);
     };
-    auto lstore = [&](const u32x4 (&d)[PPT], int buf) {
+    auto lstore = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * CB + 16 * (tid + NW * 64 * i)) = d[i];
+        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
     };
 
     f32x4 acc[MT];
@@ -732,116 +736,123 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
     float m = MASKED ? -INFINITY : 0.f, lsum = 0.f;
     bool fresh = true;
 
-    auto process = [&](const unsigned char* cb, int c) {
-        const unsigned char* kp = cb + h * Q::HB + 16 * lane;
-        const unsigned char* vp = kp + Q::KB;
-        float s[2][4];
+    // keys 64 p + 32 j + 16 u + 4 g + r, j = chunk of the step, u = 16-key block
+    auto process = [&](const unsigned char* sb, int p) {
+        float s[2][2][4];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const float nm = (MASKED || fresh) ? 0.f : -m;
-            f32x4 st = f32x4{nm, nm, nm, nm};
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + 2048 * ks);
-                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + 2048 * ks + 1024);
-                st = mfma(kh, qh[ks], st);
-                st = mfma(kh, ql[ks], st);
-                st = mfma(kl, qh[ks], st);
+            for (int u = 0; u < 2; ++u) {
+                const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
+                f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
+                    const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
+                    st = mfma(kh, qh[ks], st);
+                    st = mfma(kh, ql[ks], st);
+                    st = mfma(kl, qh[ks], st);
+                }
+                if constexpr (KT) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
+                    const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
+                    const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
+                    st = mfma(kxh, qxh, st);
+                    st = mfma(kxh, qxl, st);
+                    st = mfma(kxl, qxh, st);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[j][u][r] = st[r];
             }
-            if constexpr (KT) {  // lanes of groups 2, 3 read the lo plane: their Q operand is zero
-                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + G::TAIL);
-                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
-                st = mfma(kxh, qxh, st);
-                st = mfma(kxh, qxl, st);
-                st = mfma(kxl, qxh, st);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[u][r] = st[r];
-        }
-        const int k0 = c * KC;
+        const int k0 = p * 2 * KC;
         if constexpr (MASKED) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = k0 + 16 * u + 4 * g + r;
-                    s[u][r] = key < len ? s[u][r] * sl2 : (key < N ? kMaskFill * kLog2e : -INFINITY);
-                }
-        } else if (N - k0 < KC) {
+                for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+                    for (int r = 0; r < 4; ++r) {
+                        const int key = k0 + 32 * j + 16 * u + 4 * g + r;
+                        s[j][u][r] = key < len ? s[j][u][r] * sl2 : (key < N ? kMaskFill * kLog2e : -INFINITY);
+                    }
+        } else if (N - k0 < 2 * KC) {  // the last step: keys past N score -inf (wave-uniform)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) s[u][r] = k0 + 16 * u + 4 * g + r < N ? s[u][r] : -INFINITY;
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        s[j][u][r] = k0 + 32 * j + 16 * u + 4 * g + r < N ? s[j][u][r] : -INFINITY;
         }
-        const float cmax = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
-                                 fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+        float cmax = s[0][0][0];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cmax = fmaxf(cmax, s[j][u][r]);
         if constexpr (MASKED) {
             const float mn = vmax(m, grp4_max(cmax));
             const float corr = __builtin_amdgcn_exp2f(m - mn);
             lsum *= corr;
 #pragma unroll
             for (int t = 0; t < MT; ++t) acc[t] *= corr;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[u][r] -= mn;
             m = mn;
         } else {
-            if (__builtin_amdgcn_ballot_w64(fresh || cmax > kLazyT) != 0) {  // wave-uniform: move the base
-                const float cm = grp4_max(cmax);
-                const float d = fresh ? cm : vmax(cm, 0.f);
-                m += d;
+            // lazy base (attention_split_kernel): move it only on the first step or
+            // when a score exceeds it by more than 2^kLazyT (wave-uniform)
+            const float rel = cmax - m;
+            if (__builtin_amdgcn_ballot_w64(fresh || rel > kLazyT) != 0) {
+                const float cm = grp4_max(cmax);  // finite: the step's first chunk has a live key
+                const float mn = fresh ? cm : vmax(cm, m);
                 if (!fresh) {
-                    const float corr = __builtin_amdgcn_exp2f(-d);
+                    const float corr = __builtin_amdgcn_exp2f(m - mn);
                     lsum *= corr;
 #pragma unroll
                     for (int t = 0; t < MT; ++t) acc[t] *= corr;
                 }
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s[u][r] -= d;
+                m = mn;
             }
             fresh = false;
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                s[u][r] = __builtin_amdgcn_exp2f(s[u][r]);
-                lsum += s[u][r];
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    s[j][u][r] = __builtin_amdgcn_exp2f(s[j][u][r] - m);
+                    lsum += s[j][u][r];
+                }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            unsigned ph[4], pl[4];
+            split2u(s[j][0][0], s[j][0][1], ph[0], pl[0]);
+            split2u(s[j][0][2], s[j][0][3], ph[1], pl[1]);
+            split2u(s[j][1][0], s[j][1][1], ph[2], pl[2]);
+            split2u(s[j][1][2], s[j][1][3], ph[3], pl[3]);
+            const u32x4 bh4 = u32x4{ph[0], ph[1], ph[2], ph[3]}, bl4 = u32x4{pl[0], pl[1], pl[2], pl[3]};
+            const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+                const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+                acc[t] = mfma(vh, bh4, acc[t]);
+                acc[t] = mfma(vh, bl4, acc[t]);
+                acc[t] = mfma(vl, bh4, acc[t]);
             }
-        unsigned ph[4], pl[4];
-        split2u(s[0][0], s[0][1], ph[0], pl[0]);
-        split2u(s[0][2], s[0][3], ph[1], pl[1]);
-        split2u(s[1][0], s[1][1], ph[2], pl[2]);
-        split2u(s[1][2], s[1][3], ph[3], pl[3]);
-        const u32x4 bh4 = u32x4{ph[0], ph[1], ph[2], ph[3]}, bl4 = u32x4{pl[0], pl[1], pl[2], pl[3]};
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
-            const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
-            acc[t] = mfma(vh, bh4, acc[t]);
-            acc[t] = mfma(vh, bl4, acc[t]);
-            acc[t] = mfma(vl, bh4, acc[t]);
         }
     };
 
-    gload(pre[0], 0);
-    if (1 < nchl) gload(pre[1], 1);
-    lstore(pre[0], 0);
+    gload(0);
+    lstore(0);
+    if (1 < nsc) gload(1);
     lds_barrier();
 #pragma unroll 1
-    for (int c = 0; c < nchl; c += 2) {
-        // even chunk c from buffer 0; c + 1 goes to buffer 1, c + 2 is requested
-        if (c + 1 < nchl) lstore(pre[1], 1);
-        if (c + 2 < nchl) gload(pre[0], c + 2);
-        process(ring, c);
-        lds_barrier();
-        if (c + 1 >= nchl) break;
-        if (c + 2 < nchl) lstore(pre[0], 0);
-        if (c + 3 < nchl) gload(pre[1], c + 3);
-        process(ring + CB, c + 1);
+    for (int p = 0; p < nsc; ++p) {
+        // step p from buffer p & 1; p + 1 goes to the other buffer, p + 2 is requested
+        if (p + 1 < nsc) lstore((p + 1) & 1);
+        if (p + 2 < nsc) gload(p + 2);
+        process(ring + (p & 1) * SB, p);
         lds_barrier();
     }
     TSTAMP(1);
@@ -881,7 +892,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     // the attention's scratch (key-quarter merge records / the K-V chunk ring)
     // and, after it, o / y (fp32, O) and relu(FFN1) (split, Hd)
     constexpr int OB = TR * frs(H) * 4, HB = TR * srs(F);
-    constexpr int XB = QS ? 2 * QsGeo<HD>::CB : NW * RB * 64 * Geo<HD>::XW * 4;
+    constexpr int XB = QS ? 2 * QsGeo<HD>::SB : NW * RB * 64 * Geo<HD>::XW * 4;
     __shared__ __attribute__((aligned(16))) unsigned char U[OB + HB > XB ? OB + HB : XB];
     float* const O = reinterpret_cast<float*>(U);
     unsigned char* const Hd = U + OB;
