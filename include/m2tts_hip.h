@@ -215,17 +215,46 @@ int32_t m2_inference_back(const m2_model* model, int32_t B, int32_t S, int32_t T
                           float* out_audio, void* workspace, size_t workspace_bytes,
                           void* stream);
 
-/* Both halves in ONE call when the outputs fit: after T = max(1, T_max) is
- * known, the back half runs straight away if mel_buf (mel_cap floats) holds
- * B*T*M, audio_buf (audio_cap floats) holds B*64*T and the workspace holds
- * m2_inference_workspace_bytes(B,S,T); the outputs are written contiguously
- * from the start of the buffers ([B,T,M] and [B,1,64T]) and *launched = 1.
- * Otherwise *launched = 0 and the caller allocates for *host_T and calls
- * m2_inference_back (the front buffer holds the hand-off). */
+/* Both halves in ONE call when the outputs fit.  The buffers give a frame
+ * capacity T_cap = min(mel_cap / (B*M), audio_cap / (B*64)) (if the workspace
+ * holds m2_inference_workspace_bytes(B,S,T_cap)); with one, and when
+ * m2_inference_dev_supported(model, T_cap), the back half is enqueued right
+ * behind the count kernel BEFORE the host reads T_max, its grids sized for
+ * T_cap and its kernels taking T = max(1, T_max) from the device (the host
+ * wait then overlaps the decoder instead of idling the GPU); otherwise it is
+ * enqueued after the read, if B*T*M / B*64*T fit.  The outputs are written
+ * contiguously from the start of the buffers ([B,T,M] and [B,1,64T]) and
+ * *launched = 1.  When T exceeds the capacity (the speculative launches then
+ * did nothing) *launched = 0 and the caller allocates for *host_T and calls
+ * m2_inference_back (the front buffer holds the hand-off).
+ * M2_SPECULATIVE=0 in the environment turns the device-side frame count off. */
 int32_t m2_inference(const m2_model* model, const int64_t* ids, const int64_t* lengths, int32_t B,
                      int32_t S, float scale, void* front, size_t front_bytes, void* workspace,
                      size_t workspace_bytes, float* mel_buf, size_t mel_cap, float* audio_buf,
                      size_t audio_cap, int32_t* host_T, int32_t* launched, void* stream);
+
+/* Device-side frame count for sharded inference (no host read between the
+ * halves): m2_inference_front_dev writes this shard's T_max to the device word
+ * dev_Tmax (e.g. the payload of the ranks' all-reduce(MAX)) without waiting;
+ * m2_inference_back_dev launches the back half for a capacity of T_cap frames
+ * and takes T = max(1, *dev_T) from the device; when T > T_cap it does
+ * nothing (the caller reads T and runs m2_inference_back).  Outputs as
+ * m2_inference's.  m2_inference_dev_supported: 1 when this model's back half
+ * can run so at T_cap (one-launch decoder layers with the fused mel
+ * projection, the fused unchunked vocoder).  The back half's first launch
+ * posts T = max(1, *dev_T) (also when it exceeds T_cap) to a host-mapped word
+ * of the model: m2_frames_wait blocks until the post of the model's latest
+ * m2_inference_back_dev call is visible and returns that T (no stream
+ * synchronisation, no copy: the back half keeps running). */
+int32_t m2_inference_dev_supported(const m2_model* model, int32_t T_cap);
+int32_t m2_inference_front_dev(const m2_model* model, const int64_t* ids, const int64_t* lengths,
+                               int32_t B, int32_t S, float scale, void* front, size_t front_bytes,
+                               void* workspace, size_t workspace_bytes, int32_t* dev_Tmax, void* stream);
+int32_t m2_inference_back_dev(const m2_model* model, int32_t B, int32_t S, int32_t T_cap,
+                              const int32_t* dev_T, const void* front, size_t front_bytes,
+                              float* out_mel, float* out_audio, void* workspace,
+                              size_t workspace_bytes, void* stream);
+int32_t m2_frames_wait(const m2_model* model, void* stream, int32_t* host_T);
 
 /* ---- kernel-level entry points (for the components API and tests) ---------*/
 

@@ -262,8 +262,10 @@ __global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ 
                 const int32_t tm = sat32(part[0]);
                 *Tmax = tm;
                 __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(mbox + 1, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(mbox, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (mbox) {  // null: T_max stays on the device (m2_inference_front_dev)
+                    __hip_atomic_store(mbox + 1, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(mbox, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
     }

@@ -58,6 +58,17 @@ __device__ __forceinline__ float act_t(float v) {
     else return v;
 }
 
+// Device-resident frame count of a speculatively launched back half
+// (m2_inference with a known capacity, m2_inference_back_dev): the launch's
+// grid covers `cap` frames; the kernels read T_max from the device word the
+// length regulator (or the ranks' all-reduce) wrote and use T = max(1, T_max)
+// (tts_model.py:158-160), or 0 - nothing to do - when T exceeds the capacity
+// (the host then re-runs the back half for the real T).
+__device__ __forceinline__ int dev_frames(const int32_t* p, int cap) {
+    const int t = max(1, *p);
+    return t <= cap ? t : 0;
+}
+
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 

@@ -198,6 +198,13 @@ struct m2_model {
     // sequence whose parity picks their set (one stream per model)
     unsigned* tflq = nullptr;
     mutable unsigned tfl_seq = 0;
+    // device-T path: the count kernel's ticket word (after the queue words in
+    // tflq) and the host-mapped [seq, T] pair the back half's first launch
+    // posts (m2_frames_wait)
+    unsigned* cnt_ticket = nullptr;
+    int32_t* fpost_host = nullptr;
+    int32_t* fpost_dev = nullptr;
+    mutable int32_t fpost_seq = 0;
     bool att_f32 = false;
     // measurement: per m2_vocoder call, an event pair around each fused kernel
     mutable std::vector<hipEvent_t> prof_begin, prof_end;  // [call][kernel]
@@ -390,7 +397,7 @@ bool tfl_use(const m2_model* m, const std::vector<m2_layer_w>& layers) {
 int32_t run_tfl(const m2_model* m, const std::vector<m2_layer_w>& layers, const float* x0, float* x, TfBufs& wb,
                 const int64_t* lengths, int B, int N, hipStream_t st, const float* fin_g = nullptr,
                 const float* fin_b = nullptr, const float* fin_W = nullptr, const float* fin_bias = nullptr,
-                int fin_N = 0, float* fin_out = nullptr, bool* fin_done = nullptr) {
+                int fin_N = 0, float* fin_out = nullptr, bool* fin_done = nullptr, const int32_t* dN = nullptr) {
     const int H = m->cfg.hidden_dim, heads = m->cfg.num_heads, n = (int)layers.size();
     if (fin_done) *fin_done = false;
     const float* cur = x0;
@@ -414,7 +421,7 @@ int32_t run_tfl(const m2_model* m, const std::vector<m2_layer_w>& layers, const 
             z = fin_out;
         }
         const int32_t rc = launch_tfl_layer(w, B, N, H, heads, lengths != nullptr, lengths, cur, x, wb.tfl[l & 1], next,
-                                            wb.tfl[(l + 1) & 1], NN, z, tfl_queue(m), st);
+                                            wb.tfl[(l + 1) & 1], NN, z, tfl_queue(m), st, dN);
         if (rc) return tfl_reset(m, st, rc);
         if (next == 2 && fin_done) *fin_done = true;
         cur = x;
@@ -942,8 +949,21 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
         m->rflag_dev = static_cast<int*>(dv);
     }
     // work-queue counters of the one-launch transformer layers (TflQueue)
-    e = hipMalloc(&m->tflq, kTflQueueWords * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemsetAsync(m->tflq, 0, kTflQueueWords * sizeof(unsigned), st);
+    // (+ 16 words: the count kernel's ticket of the device-T front half)
+    e = hipMalloc(&m->tflq, (kTflQueueWords + 16) * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemsetAsync(m->tflq, 0, (kTflQueueWords + 16) * sizeof(unsigned), st);
+    if (e == hipSuccess) m->cnt_ticket = m->tflq + kTflQueueWords;
+    if (e == hipSuccess) {
+        void* h = nullptr;
+        e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
+        if (e == hipSuccess) {
+            std::memset(h, 0, 64);
+            m->fpost_host = static_cast<int32_t*>(h);
+            void* d = nullptr;
+            e = hipHostGetDevicePointer(&d, h, 0);
+            m->fpost_dev = static_cast<int32_t*>(d);
+        }
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         m2_model_destroy(m);
@@ -965,6 +985,7 @@ int32_t m2_model_destroy(m2_model* model) {
     if (model->rflag_host) (void)hipHostFree(model->rflag_host);
     if (model->rflag_dev) (void)hipFree(model->rflag_dev);
     if (model->tflq) (void)hipFree(model->tflq);
+    if (model->fpost_host) (void)hipHostFree(model->fpost_host);
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -1172,7 +1193,7 @@ namespace {
 // LN1 -> QKV launch when tf_first_fused (else a separate lr_expand launch).
 int32_t mel_decoder(const m2_model* m, float* x, int32_t B, int32_t T, float* out_mel, void* workspace,
                     size_t workspace_bytes, hipStream_t st, const float* enc = nullptr, const int32_t* cum = nullptr,
-                    int32_t S = 0) {
+                    int32_t S = 0, const int32_t* dT = nullptr) {
     const int H = m->cfg.hidden_dim;
     Carve a(workspace, workspace_bytes);
     TfBufs wb;
@@ -1180,9 +1201,19 @@ int32_t mel_decoder(const m2_model* m, float* x, int32_t B, int32_t T, float* ou
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_mel_decoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
     int32_t rc;
+    // dT: T is the capacity of a speculative launch (spec_ok: one-launch
+    // layers with the mel projection fused into the last one)
+    M2_CHECK_ARG(!dT || (tfl_use(m, m->dec) && tfl_proj_supported(H, m->cfg.mel_channels)),
+                 "mel decoder: a device frame count needs the one-launch layers");
     if (tfl_use(m, m->dec)) {
         const m2_layer_w& L0 = m->dec[0];
         TflFirst f;
+        f.dN = dT;
+        if (dT) {  // the first launch posts T for the host (m2_frames_wait)
+            m->fpost_seq = m->fpost_seq == INT_MAX ? 1 : m->fpost_seq + 1;
+            f.post = m->fpost_dev;
+            f.post_seq = m->fpost_seq;
+        }
         if (enc) {  // the length regulator's expansion, built by the first launch into x
             f.src = 2;
             f.enc = enc;
@@ -1197,7 +1228,7 @@ int32_t mel_decoder(const m2_model* m, float* x, int32_t B, int32_t T, float* ou
             return tfl_reset(m, st, rc);
         bool projected = false;
         if ((rc = run_tfl(m, m->dec, x, wb.x, wb, nullptr, B, T, st, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b,
-                          m->cfg.mel_channels, out_mel, &projected)))
+                          m->cfg.mel_channels, out_mel, &projected, dT)))
             return rc;
         if (projected) return M2_OK;
         return launch_ln_gemm(wb.x, m->dec_nw, m->dec_nb, m->mel_p, m->mel_b, ACT_NONE, B * T, H, m->cfg.mel_channels,
@@ -1241,7 +1272,7 @@ int32_t m2_mel_decoder(const m2_model* m, const float* x, int32_t B, int32_t T, 
 
 namespace {
 int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                    float* const* buf, hipStream_t st, bool x3, int redo = -1);
+                    float* const* buf, hipStream_t st, bool x3, int redo = -1, const int32_t* dT = nullptr);
 
 // Audio samples [64 f0, 64 f1) of every utterance of a T-frame mel, computed
 // over the window [f0 - halo, f1 + halo) clipped to [0, T): the window's mel
@@ -1269,8 +1300,11 @@ int32_t vocoder_window(const m2_model* m, const float* mel, int32_t layout, int3
 // One m2_vocoder call on the split (x3) or exact-f32 kernels; redo >= 0: the
 // on-device range redo with flag word redo (vocoder_run).
 int32_t vocoder_call(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                     void* workspace, size_t workspace_bytes, hipStream_t st, bool x3, int redo = -1) {
+                     void* workspace, size_t workspace_bytes, hipStream_t st, bool x3, int redo = -1,
+                     const int32_t* dT = nullptr) {
     Carve a(workspace, workspace_bytes);
+    M2_CHECK_ARG(!dT || (m->fused && !(m->chunk_frames > 0 && T > m->chunk_frames)),
+                 "m2_vocoder: a device frame count needs the fused, unchunked vocoder");
     if (m->chunk_frames > 0 && T > m->chunk_frames) {  // streamed: chunk by chunk into out_audio
         ChunkBufs c;
         carve_chunked(a, m->cfg, B, T, m->chunk_frames, &c);
@@ -1288,7 +1322,7 @@ int32_t vocoder_call(const m2_model* m, const float* mel, int32_t mel_layout, in
     carve_voc(a, m->cfg, B, T, buf);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_vocoder: workspace too small");
     if (B == 0 || T == 0) return M2_OK;
-    return vocoder_run(m, mel, mel_layout, B, T, out_audio, buf, st, x3, redo);
+    return vocoder_run(m, mel, mel_layout, B, T, out_audio, buf, st, x3, redo, dT);
 }
 
 // Sticky range error of an earlier call (policy 0), returned and cleared on entry.
@@ -1320,12 +1354,10 @@ int32_t range_fallback(const m2_model* m, hipStream_t st, bool x3, F redo) {
     __atomic_store_n(m->rflag_host, 0, __ATOMIC_RELEASE);
     return redo();
 }
-}  // namespace
 
-extern "C" {
-
-int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T,
-                   float* out_audio, void* workspace, size_t workspace_bytes, void* stream) {
+// m2_vocoder; dT: T is the capacity of a speculative launch (dev_frames)
+int32_t vocoder_entry(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
+                      void* workspace, size_t workspace_bytes, void* stream, const int32_t* dT = nullptr) {
     M2_CHECK_ARG(m && mel && out_audio && B >= 0 && T >= 0, "m2_vocoder: bad argument");
     M2_CHECK_ARG(mel_layout == 0 || mel_layout == 1, "m2_vocoder: mel_layout must be 0 or 1");
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1333,11 +1365,20 @@ int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int3
     if (rc) return rc;
     const bool x3 = m->x3;
     const int redo = device_redo_word(m, x3);
-    if ((rc = vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, x3, redo))) return rc;
+    if ((rc = vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, x3, redo, dT)))
+        return rc;
     if (redo >= 0) return M2_OK;
     return range_fallback(m, st, x3, [&] {
-        return vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, false);
+        return vocoder_call(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, st, false, -1, dT);
     });
+}
+}  // namespace
+
+extern "C" {
+
+int32_t m2_vocoder(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T,
+                   float* out_audio, void* workspace, size_t workspace_bytes, void* stream) {
+    return vocoder_entry(m, mel, mel_layout, B, T, out_audio, workspace, workspace_bytes, stream);
 }
 
 int32_t m2_vocoder_chunk(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, int32_t f0,
@@ -1412,7 +1453,7 @@ namespace {
 // workgroup returning at once unless that word is raised - a call whose split
 // audio came out non-finite is recomputed on the device, with no host wait.
 int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int32_t B, int32_t T, float* out_audio,
-                    float* const* buf, hipStream_t st, bool x3, int redo) {
+                    float* const* buf, hipStream_t st, bool x3, int redo, const int32_t* dT) {
     int32_t rc;
     if (m->fused) {
         const int call = m->prof_calls;
@@ -1424,24 +1465,26 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
             const size_t slot = (size_t)call * kVocKernels + kidx;
             (void)hipEventRecord(begin ? m->prof_begin[slot] : m->prof_end[slot], st);
         };
+        VocX vx = m->vx;
+        VocW vw = m->vw;
+        vx.dT = vw.dT = dT;
         if (x3 && redo >= 0) {
-            VocX vx = m->vx;
             vx.rflag = m->rflag_dev + redo;
             vx.rclear = m->rflag_dev + (redo ^ 1);
             if ((rc = launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vx,
                                         buf[0], buf[1], out_audio, st, mark)))
                 return rc;
-            VocW wg = m->vw;
-            wg.guard = m->rflag_dev + redo;
-            return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, wg,
+            vw.guard = m->rflag_dev + redo;
+            return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vw,
                                         buf[0], buf[1], out_audio, st, [](int, bool) {});
         }
         if (x3)
-            return launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vx,
+            return launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vx,
                                      buf[0], buf[1], out_audio, st, mark);
-        return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, m->vw,
+        return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vw,
                                     buf[0], buf[1], out_audio, st, mark);
     }
+    M2_CHECK_ARG(!dT, "m2_vocoder: a device frame count needs the fused vocoder");
     int ch = m->cfg.vocoder_channels, L = T;
     float *cur = buf[0], *up = buf[1], *tmp = buf[2];
     if ((rc = launch_conv(mel, m->vin_w, m->vin_b, nullptr, nullptr, nullptr, 3, ACT_NONE, mel_layout == 1, B, m->cfg.mel_channels, ch, L, cur, st))) return rc;
@@ -1550,37 +1593,54 @@ size_t m2_front_bytes(const m2_model* model, int32_t B, int32_t S) {
     return a.off + 256;
 }
 
-int32_t m2_inference_front(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S,
-                           float scale, void* front, size_t front_bytes, void* workspace, size_t workspace_bytes,
-                           int32_t* host_Tmax, void* stream) {
-    M2_CHECK_ARG(m && host_Tmax && B >= 0 && S >= 0, "m2_inference_front: bad argument");
+}  // extern "C"
+
+namespace {
+// The front half up to the frame counts: encoder, durations (into f), then
+// count(f) launches the length regulator's count kernel (which writes T_max).
+template <typename Count>
+int32_t front_run(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S, void* front,
+                  size_t front_bytes, void* workspace, size_t workspace_bytes, hipStream_t st, FrontBufs* f,
+                  Count count) {
+    M2_CHECK_ARG(m && B >= 0 && S >= 0, "m2_inference_front: bad argument");
     M2_CHECK_ARG(ids || B * S == 0, "m2_inference_front: null ids");
     if (int32_t rc0 = range_entry(m, "m2_inference")) return rc0;
     Carve a(front, front_bytes);
-    FrontBufs f;
-    carve_front(a, B, S, m->cfg.hidden_dim, &f);
+    carve_front(a, B, S, m->cfg.hidden_dim, f);
     if (!a.ok) return fail(M2_E_WORKSPACE, "m2_inference_front: front buffer too small");
     int32_t rc;
     if (B > 0 && S > 0) {
         M2_CHECK_SHAPE(S <= m->cfg.max_positions, "m2_inference: sequence longer than the positional table");
-        hipStream_t st = static_cast<hipStream_t>(stream);
         float* x = nullptr;
-        if ((rc = text_encoder_layers(m, ids, lengths, B, S, lengths ? f.mask : nullptr, workspace, workspace_bytes,
+        if ((rc = text_encoder_layers(m, ids, lengths, B, S, lengths ? f->mask : nullptr, workspace, workspace_bytes,
                                       st, &x)))
             return rc;
         // the encoder's final LayerNorm runs inside the duration kernel, which
         // also stores the normalised encoder output (f.enc)
-        if ((rc = launch_duration(x, B, S, m->cfg.hidden_dim, m->dur, f.dur, st, m->enc_nw, m->enc_nb, f.enc)))
+        if ((rc = launch_duration(x, B, S, m->cfg.hidden_dim, m->dur, f->dur, st, m->enc_nw, m->enc_nb, f->enc)))
             return rc;
     }
     // A frame-count epilogue fused into the duration kernel (per-utterance
     // tickets, one L2 write-back per workgroup) measured 5 us slower than
     // this separate count kernel (tools/probe/count_fusion_ab.py, r17).
-    return m2_length_regulator_count_sync(f.dur, 0, scale, B, S, f.cum, f.tot, f.tmax, host_Tmax, stream);
+    return count(*f);
 }
 
-int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, const void* front, size_t front_bytes,
-                          float* out_mel, float* out_audio, void* workspace, size_t workspace_bytes, void* stream) {
+// The back half can run from a device-resident frame count with its grids
+// sized for T_cap frames: the one-launch decoder layers with the mel
+// projection fused into the last one, and the fused (unchunked) vocoder.
+bool dev_back_ok(const m2_model* m, int32_t T_cap) {
+    const char* e = std::getenv("M2_SPECULATIVE");  // 0: host-side T only (A/B, tests; read per call)
+    if (e && *e && std::atoi(e) == 0) return false;
+    return T_cap > 0 && tfl_use(m, m->dec) && tfl_proj_supported(m->cfg.hidden_dim, m->cfg.mel_channels) &&
+           m->fused && !(m->chunk_frames > 0 && T_cap > m->chunk_frames);
+}
+
+// expansion to T frames + decoder + vocoder; dT: T is the capacity and the
+// kernels take the frame count from the device word (dev_frames)
+int32_t back_run(const m2_model* m, int32_t B, int32_t S, int32_t T, const int32_t* dT, const void* front,
+                 size_t front_bytes, float* out_mel, float* out_audio, void* workspace, size_t workspace_bytes,
+                 void* stream) {
     M2_CHECK_ARG(m && B >= 0 && S >= 0 && T >= 0, "m2_inference_back: bad argument");
     if (B == 0 || T == 0) return M2_OK;
     M2_CHECK_ARG(out_mel && out_audio, "m2_inference_back: null output");
@@ -1600,9 +1660,78 @@ int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, co
     int32_t rc;
     // frame expansion + decoder (the expansion fused into the first layer's launch)
     if ((rc = mel_decoder(m, reg, B, T, out_mel, workspace, scratch, static_cast<hipStream_t>(stream), f.enc, f.cum,
-                          S)))
+                          S, dT)))
         return rc;
-    return m2_vocoder(m, out_mel, 1, B, T, out_audio, workspace, scratch, stream);
+    return vocoder_entry(m, out_mel, 1, B, T, out_audio, workspace, scratch, stream, dT);
+}
+}  // namespace
+
+extern "C" {
+
+int32_t m2_inference_front(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S,
+                           float scale, void* front, size_t front_bytes, void* workspace, size_t workspace_bytes,
+                           int32_t* host_Tmax, void* stream) {
+    M2_CHECK_ARG(host_Tmax, "m2_inference_front: bad argument");
+    FrontBufs f;
+    return front_run(m, ids, lengths, B, S, front, front_bytes, workspace, workspace_bytes,
+                     static_cast<hipStream_t>(stream), &f, [&](FrontBufs& fb) {
+                         return m2_length_regulator_count_sync(fb.dur, 0, scale, B, S, fb.cum, fb.tot, fb.tmax,
+                                                               host_Tmax, stream);
+                     });
+}
+
+int32_t m2_inference_front_dev(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S,
+                               float scale, void* front, size_t front_bytes, void* workspace, size_t workspace_bytes,
+                               int32_t* dev_Tmax, void* stream) {
+    M2_CHECK_ARG(dev_Tmax, "m2_inference_front_dev: null T_max word");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    FrontBufs f;
+    return front_run(m, ids, lengths, B, S, front, front_bytes, workspace, workspace_bytes, st, &f,
+                     [&](FrontBufs& fb) -> int32_t {
+                         if (B == 0) {
+                             M2_HIP(hipMemsetAsync(dev_Tmax, 0, sizeof(int32_t), st));
+                             return M2_OK;
+                         }
+                         return launch_lr_count_sync(fb.dur, 0, scale, B, S, fb.cum, fb.tot, dev_Tmax,
+                                                     m->cnt_ticket, nullptr, 0, st);
+                     });
+}
+
+int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, const void* front, size_t front_bytes,
+                          float* out_mel, float* out_audio, void* workspace, size_t workspace_bytes, void* stream) {
+    return back_run(m, B, S, T, nullptr, front, front_bytes, out_mel, out_audio, workspace, workspace_bytes, stream);
+}
+
+int32_t m2_inference_dev_supported(const m2_model* m, int32_t T_cap) { return m && dev_back_ok(m, T_cap) ? 1 : 0; }
+
+int32_t m2_inference_back_dev(const m2_model* m, int32_t B, int32_t S, int32_t T_cap, const int32_t* dev_T,
+                              const void* front, size_t front_bytes, float* out_mel, float* out_audio,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+    M2_CHECK_ARG(m && dev_T && T_cap > 0, "m2_inference_back_dev: bad argument");
+    M2_CHECK_ARG(dev_back_ok(m, T_cap), "m2_inference_back_dev: this model's back half needs the host-side frame "
+                                        "count (m2_inference_dev_supported is 0)");
+    return back_run(m, B, S, T_cap, dev_T, front, front_bytes, out_mel, out_audio, workspace, workspace_bytes, stream);
+}
+
+int32_t m2_frames_wait(const m2_model* m, void* stream, int32_t* host_T) {
+    M2_CHECK_ARG(m && host_T, "m2_frames_wait: bad argument");
+    M2_CHECK_ARG(m->fpost_seq > 0, "m2_frames_wait: no m2_inference_back_dev call to wait for");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int32_t seq = m->fpost_seq;
+    for (unsigned i = 1;; ++i) {
+        if (__atomic_load_n(m->fpost_host, __ATOMIC_ACQUIRE) == seq) break;
+        if ((i & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(m->fpost_host, __ATOMIC_ACQUIRE) == seq) break;
+                return fail(M2_E_INTERNAL, "m2_frames_wait: stream idle but T not posted");
+            }
+            if (e != hipErrorNotReady) return hip_status(e, "m2_frames_wait");
+        }
+        _mm_pause();
+    }
+    *host_T = __atomic_load_n(m->fpost_host + 1, __ATOMIC_RELAXED);
+    return M2_OK;
 }
 
 int32_t m2_inference(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S, float scale,
@@ -1611,12 +1740,52 @@ int32_t m2_inference(const m2_model* m, const int64_t* ids, const int64_t* lengt
                      void* stream) {
     M2_CHECK_ARG(m && host_T && launched, "m2_inference: bad argument");
     *launched = 0;
-    int32_t tmax = 0, rc;
-    if ((rc = m2_inference_front(m, ids, lengths, B, S, scale, front, front_bytes, workspace, workspace_bytes, &tmax,
-                                 stream)))
-        return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // The capacity the caller's buffers give: with one, the back half is
+    // enqueued right behind the count kernel, before the host reads T_max,
+    // its kernels taking the frame count from the device (dev_frames) - the
+    // host wait overlaps the decoder instead of idling the GPU.
+    int32_t cap = 0;
+    if (B > 0 && mel_buf && audio_buf) {
+        const size_t c1 = mel_cap / ((size_t)B * m->cfg.mel_channels), c2 = audio_cap / ((size_t)B * 64);
+        cap = (int32_t)std::min<size_t>(std::min(c1, c2), (size_t)kMaxFrames);
+        if (cap > 0 && m2_inference_workspace_bytes(m, B, S, cap) > workspace_bytes) cap = 0;
+    }
+    const bool spec = cap > 0 && S > 0 && dev_back_ok(m, cap);
+    int32_t rc, tmax = 0;
+    FrontBufs f;
+    if (!spec) {
+        if ((rc = m2_inference_front(m, ids, lengths, B, S, scale, front, front_bytes, workspace, workspace_bytes,
+                                     &tmax, stream)))
+            return rc;
+    } else {
+        int dev = 0;
+        if ((rc = stream_device(st, &dev))) return rc;
+        std::lock_guard<std::mutex> lk(g_mb_mu);
+        LrMailbox* mb = nullptr;
+        if ((rc = mailbox_for(dev, &mb))) return rc;
+        int32_t seq = 0;
+        if ((rc = front_run(m, ids, lengths, B, S, front, front_bytes, workspace, workspace_bytes, st, &f,
+                            [&](FrontBufs& fb) {
+                                mb->seq = mb->seq == INT_MAX ? 1 : mb->seq + 1;
+                                seq = mb->seq;
+                                return launch_lr_count_sync(fb.dur, 0, scale, B, S, fb.cum, fb.tot, fb.tmax, mb->ticket,
+                                                            mb->dev, seq, st);
+                            })))
+            return rc;
+        if ((rc = back_run(m, B, S, cap, f.tmax, front, front_bytes, mel_buf, audio_buf, workspace, workspace_bytes,
+                           stream)))
+            return rc;
+        if ((rc = mailbox_wait(mb, seq, st, &tmax, "m2_inference"))) return rc;
+        M2_CHECK_SHAPE(tmax <= kMaxFrames, "length regulator: an utterance's frame count exceeds 2^24 (the "
+                                           "durations times duration_scale are out of range)");
+    }
     const int32_t T = std::max(1, tmax);  // tts_model.py:158-160
     *host_T = T;
+    if (spec) {  // done unless T outgrew the capacity (then the launches did nothing)
+        *launched = T <= cap ? 1 : 0;
+        return M2_OK;
+    }
     const size_t need_mel = (size_t)B * T * m->cfg.mel_channels, need_audio = (size_t)B * 64 * T;
     if (!mel_buf || !audio_buf || need_mel > mel_cap || need_audio > audio_cap ||
         m2_inference_workspace_bytes(m, B, S, T) > workspace_bytes)

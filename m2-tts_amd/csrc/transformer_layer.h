@@ -54,6 +54,11 @@ struct TflFirst {
     const float* enc = nullptr;
     const int32_t* cum = nullptr;
     int S = 0;
+    const int32_t* dN = nullptr;  // device frame count (dev_frames): N is then the capacity
+    // with dN: [seq, T] posted to this host-mapped pair (T = max(1, *dN), also
+    // past the capacity) so the host learns T without a copy or a stream sync
+    int32_t* post = nullptr;
+    int32_t post_seq = 0;
 };
 int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool masked, float* x_out,
                          const float* g, const float* bln, const float* Wqkv, const TflBufs& out, TflQueue q,
@@ -69,6 +74,6 @@ struct TflLayer {
 };
 int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool masked, const int64_t* lengths,
                          const float* x_in, float* x_out, const TflBufs& in, int next, const TflBufs& out,
-                         int NN, float* z, TflQueue q, hipStream_t st);
+                         int NN, float* z, TflQueue q, hipStream_t st, const int32_t* dN = nullptr);
 
 }  // namespace m2

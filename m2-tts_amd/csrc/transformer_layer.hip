@@ -868,6 +868,7 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
 // ---------------------------------------------------------------------------
 struct LArgs {
     int B, N, npad, ntile;
+    const int32_t* dN;  // device frame count (dev_frames; N is then the capacity)
     unsigned* qcnt;
     unsigned qseq;
     float sl2;  // scale * log2(e)
@@ -905,7 +906,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     __shared__ int item;
     int b, tile;
     claim_tile(a.B, a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
-    const int t0 = tile * TR, N = a.N;
+    const int t0 = tile * TR, N = a.dN ? dev_frames(a.dN, a.N) : a.N;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     const QkvOut qo{a.nq, a.nk, a.nv, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
     if (t0 >= N) {
@@ -1048,6 +1049,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
 enum { SRC_X = 0, SRC_EMBED = 1, SRC_EXPAND = 2 };
 struct FArgs {
     int B, N, npad, ntile;
+    const int32_t* dN;  // device frame count (dev_frames; N is then the capacity)
     unsigned* qcnt;
     unsigned qseq;
     float sl2;
@@ -1061,6 +1063,8 @@ struct FArgs {
     const float* enc;
     const int32_t* cum;
     int S;
+    int32_t* post;
+    int32_t post_seq;
     float* x_out;
     const float *g, *bln;
     const u32x4* W;
@@ -1075,9 +1079,13 @@ __global__ __launch_bounds__(512, 2) void first_kernel(FArgs a) {
     __shared__ __attribute__((aligned(16))) float vec[2 * H];
     __shared__ int sp[TR];
     __shared__ int item;
+    if (a.post && blockIdx.x == 0 && threadIdx.x == 0) {  // the frame count for the host (TflFirst::post)
+        __hip_atomic_store(a.post + 1, max(1, *a.dN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.post, a.post_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     int b, tile;
     claim_tile(a.B, a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
-    const int t0 = tile * TR, N = a.N;
+    const int t0 = tile * TR, N = a.dN ? dev_frames(a.dN, a.N) : a.N;
     const int wave = threadIdx.x >> 6;
     const QkvOut qo{a.q, a.k, a.v, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
     if (t0 >= N) {
@@ -1233,6 +1241,9 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.enc = f.enc;
     a.cum = f.cum;
     a.S = f.S;
+    a.dN = f.dN;
+    a.post = f.dN ? f.post : nullptr;
+    a.post_seq = f.post_seq;
     a.x_out = x_out;
     a.g = g;
     a.bln = bln;
@@ -1264,7 +1275,7 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
 
 int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool masked, const int64_t* lengths,
                          const float* x_in, float* x_out, const TflBufs& in, int next, const TflBufs& out, int NN,
-                         float* z, TflQueue q, hipStream_t st) {
+                         float* z, TflQueue q, hipStream_t st, const int32_t* dN) {
     M2_CHECK_SHAPE(tfl_supported(H, heads), "tfl: unsupported (hidden_dim, heads)");
     M2_CHECK_ARG(!masked || lengths, "tfl: masked attention needs lengths");
     M2_CHECK_ARG(q.cnt, "tfl: no work-queue counters");
@@ -1273,6 +1284,7 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     tfl::LArgs a{};
     a.B = B;
     a.N = N;
+    a.dN = dN;
     a.npad = tfl_npad(N);
     const int rb = tfl_rb(B, N);
     a.ntile = a.npad / (tfl::TQ * rb);

@@ -19,6 +19,8 @@ struct VocW {
     // non-zero (the range policy's on-device redo of a split-path call whose
     // audio came out non-finite)
     const int* guard = nullptr;
+    // device frame count (dev_frames); T of the launch = capacity when set
+    const int32_t* dT = nullptr;
 };
 
 bool vocoder_fused_supported(int M, int C);
@@ -123,6 +125,9 @@ struct VocX {
     // zeroed by the head kernel's first thread when set (the on-device redo's
     // other flag word, whose last readers ran in the previous call)
     int* rclear = nullptr;
+    // device frame count (dev_frames): when set, the T passed to the launches
+    // is the capacity their grids cover
+    const int32_t* dT = nullptr;
 };
 
 // Non-finite output check of the split path's last kernel: any NaN among the
@@ -196,8 +201,9 @@ struct MidpSrc {
     const float *wt, *bt, *w1, *b1, *w2, *b2;
 };
 bool pack_midp(const MidpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
+// dT (dev_frames): when set, L1 is the capacity (4 x capacity frames)
 int32_t launch_vocoder_midp(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2,
-                            hipStream_t st);
+                            hipStream_t st, const int32_t* dT = nullptr);
 extern const char* const kVocMidpKernelName;
 
 // Raw fp32 reference weights of the five tail modules (host pointers).
@@ -208,13 +214,13 @@ struct TailpSrc {
 // happen for the stage1 shapes; the x3 tail is kept then).
 bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                             int* rflag, hipStream_t st);
+                             int* rflag, hipStream_t st, const int32_t* dT = nullptr);
 extern const char* const kVocTailpKernelName;
 // The same five modules at stage2 widths (C = 256: U2 64 channels) for the
 // pipelined stage2 tail (vocoder_tailp2.hip, two waves per layer).
 bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
 int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                              int* rflag, hipStream_t st);
+                              int* rflag, hipStream_t st, const int32_t* dT = nullptr);
 extern const char* const kVocTailp2KernelName;
 
 bool vocoder_x3_supported(int M, int C);

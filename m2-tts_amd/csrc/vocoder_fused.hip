@@ -390,6 +390,10 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(co
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.y, f0 = blockIdx.x * TF;
+    if (w.dT) {  // speculative launch: T was the capacity
+        T = dev_frames(w.dT, T);
+        if (f0 >= T) return;
+    }
     __shared__ int ctr[8];  // per-layer work counters (32 B: keeps the dynamic LDS base 16-B aligned)
     if (threadIdx.x < 8) ctr[threadIdx.x] = 0;
     LB melw{lds, Pl::P_MEL, f0 - 3};
@@ -430,6 +434,10 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(con
     constexpr int CO = Pl::CO;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.y, p0 = blockIdx.x * W;
+    if (w.dT) {  // speculative launch: L1 was the capacity
+        L1 = 4 * dev_frames(w.dT, L1 / 4);
+        if (p0 >= L1) return;
+    }
     __shared__ int ctr[8];  // per-layer work counters (32 B: keeps the dynamic LDS base 16-B aligned)
     if (threadIdx.x < 8) ctr[threadIdx.x] = 0;
     const int L2 = 4 * L1;
@@ -466,6 +474,10 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(co
     constexpr int C3 = Pl::C3, C4 = Pl::C4;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.y, p0 = blockIdx.x * W;
+    if (w.dT) {  // speculative launch: L2 was the capacity
+        L2 = 16 * dev_frames(w.dT, L2 / 16);
+        if (p0 >= L2) return;
+    }
     __shared__ int ctr[8];  // per-layer work counters (32 B: keeps the dynamic LDS base 16-B aligned)
     if (threadIdx.x < 8) ctr[threadIdx.x] = 0;
     const int L3 = 2 * L2, L4 = 4 * L2;

@@ -244,9 +244,14 @@ template <int NCH>
 __global__ __launch_bounds__(NWAVES * 64, 4) void midp_kernel(const unsigned char* __restrict__ U1, int L1,
                                                                const u32x4* __restrict__ W,
                                                                const float* __restrict__ bias,
-                                                               unsigned char* __restrict__ U2) {
+                                                               unsigned char* __restrict__ U2,
+                                                               const int32_t* __restrict__ dT) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
+    if (dT) {  // speculative launch: L1 was the capacity
+        L1 = 4 * dev_frames(dT, L1 / 4);
+        if (qa >= L1) return;
+    }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool edge = qa < 16 || qa + 16 * NCH + 16 > L1;
     unsigned char* u2row = U2 + (size_t)b * 4 * L1 * 128;
@@ -273,7 +278,8 @@ __global__ __launch_bounds__(NWAVES * 64, 4) void midp_kernel(const unsigned cha
 }
 
 template <int NCH>
-int32_t launch(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2, hipStream_t st) {
+int32_t launch(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2, hipStream_t st,
+               const int32_t* dT) {
     static bool attr = false;
     if (!attr) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(midp_kernel<NCH>),
@@ -281,7 +287,7 @@ int32_t launch(const void* U1, int L1, int B, const vx_u32x4* W, const float* bi
         attr = true;
     }
     hipLaunchKernelGGL((midp_kernel<NCH>), dim3(cdiv(L1, 16 * NCH), B), dim3(NWAVES * 64), LDS_BYTES, st,
-                       static_cast<const unsigned char*>(U1), L1, W, bias, static_cast<unsigned char*>(U2));
+                       static_cast<const unsigned char*>(U1), L1, W, bias, static_cast<unsigned char*>(U2), dT);
     M2_LAUNCHED("midp_kernel");
     return M2_OK;
 }
@@ -291,16 +297,16 @@ int32_t launch(const void* U1, int L1, int B, const vx_u32x4* W, const float* bi
 const char* const kVocMidpKernelName = "midp_kernel (ConvT2 + ResBlock2, pipelined)";
 
 int32_t launch_vocoder_midp(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2,
-                            hipStream_t st) {
+                            hipStream_t st, const int32_t* dT) {
     if (B == 0 || L1 == 0) return M2_OK;
     static const int nch = [] {
         const char* e = std::getenv("M2_MIDP_NCH");
         const int v = e ? std::atoi(e) : 16;
         return (v == 8 || v == 32) ? v : 16;
     }();
-    if (nch == 8) return mp::launch<8>(U1, L1, B, W, bias, U2, st);
-    if (nch == 32) return mp::launch<32>(U1, L1, B, W, bias, U2, st);
-    return mp::launch<16>(U1, L1, B, W, bias, U2, st);
+    if (nch == 8) return mp::launch<8>(U1, L1, B, W, bias, U2, st, dT);
+    if (nch == 32) return mp::launch<32>(U1, L1, B, W, bias, U2, st, dT);
+    return mp::launch<16>(U1, L1, B, W, bias, U2, st, dT);
 }
 
 // ---------------------------------------------------------------------------

@@ -521,9 +521,14 @@ template <int NCH, int NL>
 __global__ __launch_bounds__(nwaves(NL) * 64, 6) void tailp_kernel(const unsigned char* __restrict__ U2, int L2,
                                                                     const u32x4* __restrict__ W,
                                                                     const float* __restrict__ bias,
-                                                                    float* __restrict__ audio, int* rflag) {
+                                                                    float* __restrict__ audio, int* rflag,
+                                                                    const int32_t* __restrict__ dT) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
+    if (dT) {  // speculative launch: L2 was the capacity
+        L2 = 16 * dev_frames(dT, L2 / 16);
+        if (qa >= L2) return;
+    }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
     float* arow = audio + (size_t)b * 4 * L2;
@@ -563,7 +568,7 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 6) void tailp_kernel(const unsigne
 
 template <int NCH, int NL>
 int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
-               hipStream_t st) {
+               hipStream_t st, const int32_t* dT) {
     static bool attr = false;
     if (!attr) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp_kernel<NCH, NL>),
@@ -571,17 +576,17 @@ int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bi
         attr = true;
     }
     hipLaunchKernelGGL((tailp_kernel<NCH, NL>), dim3(cdiv(L2, 16 * NCH), B), dim3(nwaves(NL) * 64), lds_bytes(NL),
-                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
+                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag, dT);
     M2_LAUNCHED("tailp_kernel");
     return M2_OK;
 }
 
 template <int NL>
 int32_t launch_nl(int nch, const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                  int* rflag, hipStream_t st) {
-    if (nch == 21) return launch<21, NL>(U2, L2, B, W, bias, audio, rflag, st);
-    if (nch == 48) return launch<48, NL>(U2, L2, B, W, bias, audio, rflag, st);
-    return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st);
+                  int* rflag, hipStream_t st, const int32_t* dT) {
+    if (nch == 21) return launch<21, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+    if (nch == 48) return launch<48, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+    return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
 }
 
 }  // namespace tp
@@ -597,7 +602,7 @@ const char* const kVocTailpKernelName =
     "tailp_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, pipelined)";
 
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                             int* rflag, hipStream_t st) {
+                             int* rflag, hipStream_t st, const int32_t* dT) {
     if (B == 0 || L2 == 0) return M2_OK;
     // Strip length: the shortest instantiated NCH that covers an utterance in
     // at most floor(768 / B) strips, so the grid is about one round of three
@@ -620,8 +625,8 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
     // classes of 18/21/16/12 MFMAs instead of 18/24/16/9 and measured the same:
     // the step is latency-bound, not bound by one SIMD's MFMA pipe.)
     const bool seven = std::getenv("M2_TAILP_SEVEN") != nullptr;
-    return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st)
-                 : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st);
+    return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT)
+                 : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT);
 }
 
 // ---------------------------------------------------------------------------

@@ -448,9 +448,14 @@ template <int NCH, int NL>
 __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsigned char* __restrict__ U2, int L2,
                                                                      const u32x4* __restrict__ W,
                                                                      const float* __restrict__ bias,
-                                                                     float* __restrict__ audio, int* rflag) {
+                                                                     float* __restrict__ audio, int* rflag,
+                                                                     const int32_t* __restrict__ dT) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
+    if (dT) {  // speculative launch: L2 was the capacity
+        L2 = 16 * dev_frames(dT, L2 / 16);
+        if (qa >= L2) return;
+    }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
     float* arow = audio + (size_t)b * 4 * L2;
@@ -497,7 +502,7 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsign
 
 template <int NCH, int NL>
 int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
-               hipStream_t st) {
+               hipStream_t st, const int32_t* dT) {
     static bool attr = false;
     if (!attr) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp2_kernel<NCH, NL>),
@@ -505,21 +510,21 @@ int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bi
         attr = true;
     }
     hipLaunchKernelGGL((tailp2_kernel<NCH, NL>), dim3(cdiv(L2, 16 * NCH), B), dim3(nwaves(NL) * 64), lds_bytes(NL),
-                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag);
+                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag, dT);
     M2_LAUNCHED("tailp2_kernel");
     return M2_OK;
 }
 
 template <int NL>
 int32_t launch_nl(int nch, const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                  int* rflag, hipStream_t st) {
+                  int* rflag, hipStream_t st, const int32_t* dT) {
     switch (nch) {
-        case 8: return launch<8, NL>(U2, L2, B, W, bias, audio, rflag, st);
-        case 16: return launch<16, NL>(U2, L2, B, W, bias, audio, rflag, st);
-        case 32: return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st);
-        case 64: return launch<64, NL>(U2, L2, B, W, bias, audio, rflag, st);
-        case 128: return launch<128, NL>(U2, L2, B, W, bias, audio, rflag, st);
-        default: return launch<192, NL>(U2, L2, B, W, bias, audio, rflag, st);
+        case 8: return launch<8, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+        case 16: return launch<16, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+        case 32: return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+        case 64: return launch<64, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+        case 128: return launch<128, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+        default: return launch<192, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
     }
 }
 
@@ -529,7 +534,7 @@ const char* const kVocTailp2KernelName =
     "tailp2_kernel (stage2 ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, pipelined)";
 
 int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                              int* rflag, hipStream_t st) {
+                              int* rflag, hipStream_t st, const int32_t* dT) {
     if (B == 0 || L2 == 0) return M2_OK;
     // Strip length: the instantiated NCH minimising rounds x (NCH + NL pipeline
     // steps) at one workgroup per CU.  M2_TAILP2_NCH forces one;
@@ -553,8 +558,8 @@ int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, 
             if (best < 0 || cost < best) best = cost, nch = n;
         }
     }
-    return seven ? tp2::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st)
-                 : tp2::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st);
+    return seven ? tp2::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT)
+                 : tp2::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT);
 }
 
 // ---------------------------------------------------------------------------

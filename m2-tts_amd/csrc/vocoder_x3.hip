@@ -945,6 +945,10 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     if (w.rclear && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         *reinterpret_cast<volatile int*>(w.rclear) = 0;
     constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
+    if (w.dT) {  // speculative launch: T was the capacity
+        T = dev_frames(w.dT, T);
+        if ((int)blockIdx.x * TF >= T) return;
+    }
     using Pl = HeadPlan<MP, C, TF, head_planar<Cfg>()>;
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1154,6 +1158,10 @@ __global__ __launch_bounds__(Cfg::MW * 64, Cfg::MMIN) void x3_mid_kernel(const u
     constexpr int CO = Pl::CO;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, p0 = blockIdx.x * W;
+    if (w.dT) {  // speculative launch: L1 was the capacity
+        L1 = 4 * dev_frames(w.dT, L1 / 4);
+        if (p0 >= L1) return;
+    }
     const int L2 = 4 * L1;
     XW inw{lds, p0 - 2};
     XW hw{lds, 4 * p0 - 1};
@@ -1188,6 +1196,10 @@ __global__ __launch_bounds__(Cfg::TW * 64, Cfg::TMIN) void x3_tail_kernel(const 
     constexpr int C3 = Pl::C3, C4 = Pl::C4;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, p0 = blockIdx.x * W;
+    if (w.dT) {  // speculative launch: L2 was the capacity
+        L2 = 16 * dev_frames(w.dT, L2 / 16);
+        if (p0 >= L2) return;
+    }
     const int L3 = 2 * L2, L4 = 4 * L2;
     unsigned char* ra = lds;
     unsigned char* rb = lds + Pl::RA;
@@ -1341,7 +1353,7 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     M2_LAUNCHED("x3_head_kernel");
     mark(1, true);
     if (w.mp) {  // stage1: the pipelined mid stage (vocoder_midp.hip)
-        const int32_t rc = launch_vocoder_midp(u1, 4 * T, B, w.mp, w.mpb, u2, st);
+        const int32_t rc = launch_vocoder_midp(u1, 4 * T, B, w.mp, w.mpb, u2, st, w.dT);
         if (rc) return rc;
     } else if (S2 && alt_mid) {
         hipLaunchKernelGGL((x3_mid_kernel<CfgS2Alt>), dim3(cdiv(4 * T, CfgS2Alt::W2), B), dim3(Cfg::MW * 64),
@@ -1355,12 +1367,12 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     mark(1, false);
     mark(2, true);
     if (w.tp2) {  // stage2: the pipelined tail (vocoder_tailp2.hip)
-        const int32_t rc = launch_vocoder_tailp2(u2, 16 * T, B, w.tp2, w.tp2b, audio, w.rflag, st);
+        const int32_t rc = launch_vocoder_tailp2(u2, 16 * T, B, w.tp2, w.tp2b, audio, w.rflag, st, w.dT);
         mark(2, false);
         return rc;
     }
     if (w.tp) {  // stage1: the pipelined tail (vocoder_tailp.hip)
-        const int32_t rc = launch_vocoder_tailp(u2, 16 * T, B, w.tp, w.tpb, audio, w.rflag, st);
+        const int32_t rc = launch_vocoder_tailp(u2, 16 * T, B, w.tp, w.tpb, audio, w.rflag, st, w.dT);
         mark(2, false);
         return rc;
     }

@@ -87,6 +87,12 @@ _SIGNATURES = {
     "m2_inference": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, c_vp, c_size, c_vp, c_size, c_vp,
                              c_size, c_vp, c_vp, c_vp]),
     "m2_inference_back": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_size, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "m2_inference_dev_supported": (c_i32, [c_vp, c_i32]),
+    "m2_frames_wait": (c_i32, [c_vp, c_vp, c_vp]),
+    "m2_inference_front_dev": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_size, c_vp, c_size, c_vp,
+                                       c_vp]),
+    "m2_inference_back_dev": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp, c_vp, c_vp, c_size,
+                                      c_vp]),
 }
 
 # act codes (m2_common.h Act)

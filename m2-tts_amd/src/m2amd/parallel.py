@@ -18,9 +18,20 @@ Payloads are KB..MB, so the path is latency-bound; weights are replicated.
 
 A step is two phases around the all-reduce: ``front`` (encoder, durations,
 frame counts -> local T_max) and ``back`` (expansion to the global T, decoder,
-vocoder).  On the GPU each phase is ONE library call (m2_inference_front /
-m2_inference_back); the oracle-backed ``Stages`` used by the CPU tests compose
-the same phases from per-stage functions.
+vocoder).  On the GPU each phase is ONE library call; the oracle-backed
+``Stages`` used by the CPU tests compose the same phases from per-stage
+functions.
+
+On the GPU the frame count normally never visits the host between the phases
+(device-T path): m2_inference_front_dev writes the shard's T_max into a device
+word, the RCCL all-reduce(MAX) runs on that word in stream order, and
+m2_inference_back_dev launches the back half with grids sized for a frame
+capacity learnt from earlier steps (the global T rounded up to 32 frames, the
+same on every rank), its kernels reading T from the word.  The gather is
+enqueued right behind it on buffers laid out for that capacity; the host reads
+T (posted to host-mapped memory by the back half's first launch) only to shape
+the outputs.  A step whose T exceeds the capacity re-runs its back
+half and gather for the exact T (every rank sees the same T and capacity).
 """
 from __future__ import annotations
 
@@ -68,10 +79,28 @@ class Stages:
 
 class HipStages:
     """The MI355X phases: one m2_inference_front and one m2_inference_back call
-    per step on the model's packed handle (models/tts_model.py)."""
+    per step on the model's packed handle (models/tts_model.py), or their
+    device-T forms (m2_inference_front_dev / m2_inference_back_dev)."""
 
     def __init__(self, model):
         self.model = model
+        # frame capacity of the device-T path per (global B, S, duration_scale):
+        # the last global T rounded up to 32 frames - identical on every rank
+        self.tcap = {}
+
+    def dev_ok(self, device: torch.device, T_cap: int) -> bool:
+        return self.model._hip(device).dev_supported(T_cap)
+
+    def front_dev(self, ids: Tensor, lens: Optional[Tensor], scale: float, tword: Tensor) -> Any:
+        hm = self.model._hip(ids.device)
+        return hm, hm.inference_front_dev(ids, lens, scale, tword)
+
+    def back_dev(self, state: Any, T_cap: int, tword: Tensor, mel_out: Tensor, audio_out: Tensor) -> None:
+        hm, st = state
+        hm.inference_back_dev(st, T_cap, tword, mel_out, audio_out)
+
+    def frames_wait(self, state: Any) -> int:
+        return state[0].frames_wait()
 
     def mel_channels(self) -> int:
         return int(self.model._m2_cfg.mel_channels)
@@ -181,8 +210,12 @@ class PendingGather:
     def __init__(self, finish: Callable, mel_shape, audio_shape, audio_dtype):
         self._finish, self._ms, self._as, self._ad = finish, mel_shape, audio_shape, audio_dtype
         self._out = None
+        self._assemble = None  # device-T path: waits and returns (mel, audio) itself
 
     def wait(self):
+        if self._assemble is not None:
+            self._out = self._assemble()
+            self._assemble = None
         if self._finish is not None:
             g = self._finish()
             self._finish = None
@@ -197,10 +230,89 @@ class PendingGather:
         return self._out
 
 
+def _learn_cap(caps: dict, key, T: int) -> None:
+    cap = caps.get(key, 0)
+    if T > cap or 2 * T < cap:
+        caps[key] = (T + 31) // 32 * 32
+
+
+def _sharded_dev(stages, ids, lens, scale, B, lo, hi, world, group, cap, key, gather, gather_to, async_gather):
+    """One step of the device-T path (module docstring); None when T outgrew
+    the capacity (the caller re-runs the step's back half on the host path)."""
+    dev = ids.device
+    M = stages.mel_channels()
+    b = hi - lo
+    nccl = world > 1 and dist.get_backend(group) == "nccl"
+    tw = torch.empty(1, dtype=torch.int32, device=dev)
+    state = stages.front_dev(ids[lo:hi], lens[lo:hi] if lens is not None else None, scale, tw) if b else None
+    if not b:
+        tw.zero_()
+    if world > 1:
+        if nccl:  # RCCL on the device word, in stream order: no host read
+            dist.all_reduce(tw, op=dist.ReduceOp.MAX, group=group)
+        else:  # gloo (tests): staged through the host
+            t = tw.cpu()
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            tw.copy_(t)
+    rows = -(-B // world) if (gather and world > 1) else b
+    moff = (rows * cap * M + 63) // 64 * 64
+    buf = torch.empty(moff + rows * 64 * cap, dtype=torch.float32, device=dev)
+    if b:
+        stages.back_dev(state, cap, tw, buf[: b * cap * M], buf[moff: moff + b * 64 * cap])
+    parts, work = None, None
+    if gather and world > 1:
+        me = dist.get_rank(group)
+        dst = None if gather_to is None else (dist.get_global_rank(group, gather_to) if group is not None
+                                              else gather_to)
+        if gather_to is None or me == gather_to:
+            parts = [torch.empty_like(buf) for _ in range(world)]
+        if gather_to is None:
+            work = dist.all_gather(parts, buf, group=group, async_op=async_gather)
+        else:
+            work = dist.gather(buf, parts, dst=dst, group=group, async_op=async_gather)
+    # T as the back half's first launch posted it (the back half keeps running);
+    # a rank with an empty shard reads the word
+    T = stages.frames_wait(state) if b else max(1, int(tw.item()))
+    _learn_cap(stages.tcap, key, T)
+    if T > cap:
+        if async_gather and work is not None:
+            work.wait()
+        return None
+
+    def view(flat, n):
+        return flat[: n * T * M].view(n, T, M), flat[moff: moff + n * 64 * T].view(n, 1, 64 * T)
+
+    if not gather or world == 1:
+        mel, audio = view(buf, b)
+        if not gather:
+            return mel, audio, (lo, hi)
+        if async_gather:
+            out = PendingGather(None, None, None, None)
+            out._out = (mel, audio)
+            return out
+        return mel, audio
+
+    counts = [shard_bounds(B, world, r)[1] - shard_bounds(B, world, r)[0] for r in range(world)]
+
+    def finish():
+        if async_gather and work is not None:
+            work.wait()
+        if parts is None:
+            return None, None
+        vs = [view(parts[r], counts[r]) for r in range(world) if counts[r]]
+        return torch.cat([v[0] for v in vs]), torch.cat([v[1] for v in vs])
+
+    if async_gather:
+        out = PendingGather(None, None, None, None)
+        out._assemble = finish
+        return out
+    return finish()
+
+
 def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Optional[Tensor],
                       duration_scale: float = 1.0, group=None, gather: bool = True,
                       gather_to: Optional[int] = None, src: Optional[int] = None,
-                      async_gather: bool = False, one_call_world1: bool = True):
+                      async_gather: bool = False, one_call_world1: bool = True, device_T: bool = True):
     """M2TTSModel.inference (tts_model.py:402-438) over a global batch sharded by
     utterance.
 
@@ -216,7 +328,10 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
     gather in flight and returns a PendingGather, so the next step's work
     overlaps it; call ``.wait()`` for the tensors.  At world 1 the two phases
     run as one library call (``one_call_world1``; False keeps the two-phase
-    form the ranks of a multi-GPU job run, e.g. to time one rank's share)."""
+    form the ranks of a multi-GPU job run, e.g. to time one rank's share).
+    ``device_T`` (stages with ``front_dev``, CUDA inputs): the frame count
+    stays on the device between the phases once a capacity is known (module
+    docstring); the first step of a (B, S) shape runs the host path."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     if src is not None and world > 1:
@@ -225,6 +340,17 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
     lo, hi = shard_bounds(B, world, rank)
     ids = phoneme_ids[lo:hi]
     lens = phoneme_lengths[lo:hi] if phoneme_lengths is not None else None
+    key = (B, phoneme_ids.shape[1], float(duration_scale))
+    use_dev = device_T and hasattr(stages, "front_dev") and phoneme_ids.is_cuda and \
+        not (one_call_world1 and world == 1 and hi > lo and hasattr(stages, "both"))
+    if use_dev:
+        cap = stages.tcap.get(key, 0)
+        if cap > 0 and stages.dev_ok(phoneme_ids.device, cap):
+            with torch.no_grad():
+                out = _sharded_dev(stages, phoneme_ids, phoneme_lengths, duration_scale, B, lo, hi, world, group,
+                                   cap, key, gather, gather_to, async_gather)
+            if out is not None:
+                return out
     if one_call_world1 and world == 1 and hi > lo and hasattr(stages, "both"):
         with torch.no_grad():
             mel, audio = stages.both(ids, lens, duration_scale)
@@ -243,6 +369,8 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
             t_local, M = (int(v) for v in t.tolist())
         T = max(1, t_local)  # all-empty batch -> one zero frame (tts_model.py:158-160)
+        if hasattr(stages, "tcap"):
+            _learn_cap(stages.tcap, key, T)
         if hi > lo:
             mel, audio = stages.back(state, T)
         else:

@@ -196,6 +196,54 @@ class HipModel:
                   audio.data_ptr(), ws.data_ptr(), ws.numel(), stream_handle(self.device))
         return mel, audio
 
+    # ------------------------------------------------- device-side frame count
+    def dev_supported(self, T_cap: int) -> bool:
+        """True when the back half can take its frame count from the device
+        at a capacity of T_cap frames (m2_inference_dev_supported)."""
+        return T_cap > 0 and bool(_lib.load().m2_inference_dev_supported(self.handle, int(T_cap)))
+
+    def inference_front_dev(self, ids: Tensor, lengths: Optional[Tensor], scale: float, tword: Tensor) -> Tuple:
+        """Front half with no host read (m2_inference_front_dev): this shard's
+        T_max goes to the device word tword[0] (int32, e.g. the payload of the
+        ranks' all-reduce), stream-ordered.  Returns the hand-off state."""
+        require_device(ids, lengths, tword, what="M2TTSModel")
+        if tword.dtype != torch.int32 or not tword.is_contiguous():
+            raise ValueError("inference_front_dev: tword must be a contiguous int32 device tensor")
+        ids = ids.to(torch.int64).contiguous()
+        B, S = ids.shape
+        lens = lengths.to(torch.int64).contiguous() if lengths is not None else None
+        front = self._scratch("_front", self._size("m2_front_bytes", B, S))
+        ws = self._scratch("_ws", self._size("m2_inference_workspace_bytes", B, S, 0))
+        _lib.call("m2_inference_front_dev", self.handle, ids.data_ptr(), None if lens is None else lens.data_ptr(),
+                  B, S, float(scale), front.data_ptr(), front.numel(), ws.data_ptr(), ws.numel(), tword.data_ptr(),
+                  stream_handle(self.device))
+        return (B, S, front, ids, lens)
+
+    def inference_back_dev(self, state: Tuple, T_cap: int, tword: Tensor, mel_out: Tensor,
+                           audio_out: Tensor) -> None:
+        """Back half for a capacity of T_cap frames taking T = max(1, tword[0])
+        from the device (m2_inference_back_dev): mel [B,T,M] written at the
+        start of mel_out (>= B*T_cap*M floats), audio [B,1,64T] at the start
+        of audio_out (>= B*64*T_cap floats).  Nothing is written when
+        T > T_cap (the caller then runs inference_back(T))."""
+        B, S, front, _ids, _lens = state
+        for t, n in ((mel_out, B * T_cap * self.M), (audio_out, B * 64 * T_cap)):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < n or t.data_ptr() % 16:
+                raise ValueError("inference_back_dev: output buffers must be 16-B aligned contiguous float32 "
+                                 "tensors of B*T_cap*M and B*64*T_cap elements")
+        ws = self._scratch("_ws", self._size("m2_inference_workspace_bytes", B, S, T_cap))
+        _lib.call("m2_inference_back_dev", self.handle, B, S, int(T_cap), tword.data_ptr(), front.data_ptr(),
+                  front.numel(), mel_out.data_ptr(), audio_out.data_ptr(), ws.data_ptr(), ws.numel(),
+                  stream_handle(self.device))
+
+    def frames_wait(self) -> int:
+        """T of this model's latest inference_back_dev call, as its first
+        launch posted it (m2_frames_wait): blocks until that launch has run,
+        not until the back half is done."""
+        T = ctypes.c_int32(0)
+        _lib.call("m2_frames_wait", self.handle, stream_handle(self.device), ctypes.byref(T))
+        return int(T.value)
+
     # ------------------------------------------------------------------ vocoder modes
     def vocoder_select(self, path: int):
         """1 = exact-f32 MFMA kernels, 2 = split-f16 MFMA kernels (m2_vocoder_select)."""

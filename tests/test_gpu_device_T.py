@@ -1,0 +1,184 @@
+"""GPU: the device-side frame count (speculative back half).
+
+m2_inference enqueues the expansion / decoder / vocoder right behind the count
+kernel, before the host reads T_max, with grids sized for the frame capacity
+of the caller's buffers; the kernels take T = max(1, T_max) from the device
+(dev_frames) and do nothing when T outgrows the capacity.  The sharded path's
+m2_inference_front_dev / m2_inference_back_dev keep T on the device across the
+ranks' all-reduce.  Checked against the host-T path (M2_SPECULATIVE=0 /
+m2_inference_back at the exact T) bit for bit, the fixtures and the oracle
+(reference: tts_model.py:158-176 - T is the batch maximum, max(1, .))."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import m2tts_oracle as orc
+from conftest import AUDIO_RMS_TOL, MEL_MAXABS_TOL, golden, golden_state, maxabs, rms, stage_config
+
+pytestmark = pytest.mark.gpu
+
+
+def build_model(stage, dev):
+    from models.tts_model import M2TTSModel
+    m = M2TTSModel(**stage_config(stage).as_dict())
+    m.load_state_dict(golden_state(stage))
+    return m.to(dev).eval()
+
+
+def _host_path(m, ids, lens, scale, monkeypatch):
+    monkeypatch.setenv("M2_SPECULATIVE", "0")
+    try:
+        return m.inference(ids, lens, duration_scale=scale)
+    finally:
+        monkeypatch.delenv("M2_SPECULATIVE")
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_speculative_inference_equals_host_path(gpu, stage, monkeypatch):
+    """A sequence of calls whose T shrinks under the capacity, grows past it
+    (the speculative launches do nothing; the call finishes at the exact T)
+    and repeats: every result equals the host-T path bit for bit."""
+    m = build_model(stage, gpu)
+    hm = m._hip(gpu)
+    g = torch.Generator().manual_seed(5)
+    B, S = 6, 40
+    ids = torch.randint(0, 42, (B, S), generator=g).to(gpu)
+    lens = torch.tensor([40, 13, 27, 40, 1, 33]).to(gpu)
+    seen_spec = False
+    for scale in (1.0, 1.0, 0.8, 0.6, 1.4, 1.4, 1.0):
+        cap = hm._tcap.get((B, S), 0)
+        mel, audio = m.inference(ids, lens, duration_scale=scale)
+        hmel, haudio = _host_path(m, ids, lens, scale, monkeypatch)
+        assert mel.shape == hmel.shape and audio.shape == haudio.shape
+        assert torch.equal(mel, hmel) and torch.equal(audio, haudio), (scale, cap, mel.shape)
+        seen_spec |= 0 < mel.shape[1] <= cap
+    assert seen_spec
+
+
+def test_speculative_inference_fixture_and_oracle(gpu):
+    """configs[3]'s fixture batch (B=64, S=100) on the speculative path: the
+    reference fingerprints and the oracle on three rows."""
+    from test_gpu_parity import _check_fingerprint
+    fp = golden("fp_s2_B64_S100")
+    m = build_model("s2", gpu)
+    ids, lens = torch.from_numpy(fp["ids"]).to(gpu), torch.from_numpy(fp["lengths"]).to(gpu)
+    m.inference(ids, lens)  # learns the capacity
+    assert m._hip(gpu)._tcap[tuple(ids.shape)] > 0
+    mel, audio = m.inference(ids, lens)
+    _check_fingerprint(fp, mel, audio)
+    rows = [1, 40]
+    ref_mel, ref_audio = orc.inference(golden_state("s2"), stage_config("s2"), ids[rows].cpu(), lens[rows].cpu(),
+                                       as_written=False)
+    assert maxabs(mel[rows], ref_mel) <= MEL_MAXABS_TOL
+    assert rms(audio[rows], ref_audio) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_back_dev_direct(gpu, stage):
+    """HipModel.inference_front_dev / inference_back_dev: T from the device
+    word at capacities T, T + 5 and 2T equal inference_back at the exact T;
+    a capacity under T leaves the outputs untouched."""
+    m = build_model(stage, gpu)
+    hm = m._hip(gpu)
+    M = stage_config(stage).mel_channels
+    g = torch.Generator().manual_seed(9)
+    ids = torch.randint(0, 42, (3, 24), generator=g).to(gpu)
+    lens = torch.tensor([24, 9, 17]).to(gpu)
+    st, T = hm.inference_front(ids, lens, 1.0)
+    rmel, raudio = hm.inference_back(st, max(1, T))
+    T = max(1, T)
+    for cap in (T, T + 5, 2 * T, T - 1):
+        if cap <= 0 or not hm.dev_supported(cap):
+            continue
+        tw = torch.empty(1, dtype=torch.int32, device=gpu)
+        st = hm.inference_front_dev(ids, lens, 1.0, tw)
+        mel_out = torch.full((3 * cap * M,), float("nan"), device=gpu)
+        audio_out = torch.full((3 * 64 * cap,), float("nan"), device=gpu)
+        hm.inference_back_dev(st, cap, tw, mel_out, audio_out)
+        assert hm.frames_wait() == T  # posted by the first launch, also past the capacity
+        torch.cuda.synchronize()
+        assert int(tw.item()) == T
+        if cap < T:
+            assert torch.isnan(mel_out).all() and torch.isnan(audio_out).all()
+            continue
+        assert torch.equal(mel_out[: 3 * T * M].view(3, T, M), rmel)
+        assert torch.equal(audio_out[: 3 * 64 * T].view(3, 1, 64 * T), raudio)
+
+
+@pytest.mark.parametrize("B", [8, 64])
+def test_sharded_device_T_world1(gpu, B):
+    """sharded_inference(..., one_call_world1=False) - the flow of one rank of
+    a multi-GPU job: the first step learns the capacity on the host path, the
+    next ones keep T on the device; bit for bit equal to inference()."""
+    from m2amd.parallel import hip_stages, sharded_inference
+    m = build_model("s2", gpu)
+    st = hip_stages(m)
+    g = torch.Generator().manual_seed(B)
+    ids = torch.randint(0, 42, (B, 100), generator=g).to(gpu)
+    lens = torch.randint(20, 101, (B,), generator=g).to(gpu)
+    ref_mel, ref_audio = m.inference(ids, lens)
+    for _ in range(3):
+        mel, audio = sharded_inference(st, ids, lens, gather_to=0, one_call_world1=False)
+        assert torch.equal(mel, ref_mel) and torch.equal(audio, ref_audio)
+    assert st.tcap[(B, 100, 1.0)] >= ref_mel.shape[1]
+    pend = sharded_inference(st, ids, lens, one_call_world1=False, async_gather=True)
+    mel, audio = pend.wait()
+    assert torch.equal(mel, ref_mel) and torch.equal(audio, ref_audio)
+    mel, audio, (lo, hi) = sharded_inference(st, ids, lens, gather=False, one_call_world1=False)
+    assert (lo, hi) == (0, B) and torch.equal(mel, ref_mel)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dev_worker(rank, world, port, outfile):
+    """Two gloo ranks sharing cuda:0 on the device-T path (gloo stages the
+    one-word all-reduce through the host); a batch smaller than the world on
+    the last step gives rank 1 an empty shard."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from m2amd.parallel import hip_stages, sharded_inference
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        m = build_model("s1", dev)
+        st = hip_stages(m)
+        g = torch.Generator().manual_seed(21)
+        ids = torch.randint(0, 42, (5, 30), generator=g)
+        lens = torch.tensor([30, 12, 25, 7, 30])
+        outs = {}
+        for i, scale in enumerate((1.0, 1.0, 0.7, 1.6, 1.0)):
+            mel, audio = sharded_inference(st, ids.to(dev), lens.to(dev), duration_scale=scale)
+            outs[f"mel{i}"], outs[f"audio{i}"] = mel.cpu().numpy(), audio.cpu().numpy()
+        for i in range(2):  # B = 1 < world: rank 1's shard is empty
+            mel, audio = sharded_inference(st, ids[:1].to(dev), lens[:1].to(dev))
+            outs[f"one{i}"] = mel.cpu().numpy()
+        if rank == 0:
+            np.savez(outfile, ids=ids.numpy(), lens=lens.numpy(), **outs)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_device_T_two_ranks_gloo(gpu, tmp_path):
+    import torch.multiprocessing as mp
+    outfile = str(tmp_path / "dev.npz")
+    mp.spawn(_dev_worker, args=(2, _free_port(), outfile), nprocs=2, join=True)
+    z = np.load(outfile)
+    m = build_model("s1", gpu)
+    ids, lens = torch.from_numpy(z["ids"]).to(gpu), torch.from_numpy(z["lens"]).to(gpu)
+    for i, scale in enumerate((1.0, 1.0, 0.7, 1.6, 1.0)):
+        mel, audio = m.inference(ids, lens, duration_scale=scale)
+        assert torch.equal(torch.from_numpy(z[f"mel{i}"]), mel.cpu()), i
+        assert torch.equal(torch.from_numpy(z[f"audio{i}"]), audio.cpu()), i
+    mel1, _ = m.inference(ids[:1], lens[:1])
+    for i in range(2):
+        assert torch.equal(torch.from_numpy(z[f"one{i}"]), mel1.cpu())

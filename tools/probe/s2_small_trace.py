@@ -59,10 +59,16 @@ def main():
     lens = torch.full((B,), S, dtype=torch.long, device=dev)
     m.set_range_policy("report")
     hm = m._hip(dev)
-    one = len(sys.argv) > 2 and sys.argv[2] == "one"  # the one-call m2_inference
+    mode = sys.argv[2] if len(sys.argv) > 2 else "two"
+    one = mode == "one"  # the one-call m2_inference (speculative back half)
+    if mode == "dev":  # one rank's sharded flow on the device-T path
+        from m2amd.parallel import hip_stages, sharded_inference
+        st = hip_stages(m)
     with torch.no_grad():
         for _ in range(200 if S <= 100 else 30):
-            if one:
+            if mode == "dev":
+                sharded_inference(st, ids, lens, gather_to=0, one_call_world1=False)
+            elif one:
                 hm.inference(ids, lens, 1.0)
             else:
                 state, tl = hm.inference_front(ids, lens, 1.0)
