@@ -570,11 +570,15 @@ def pipeline_line(cx: Ctx, B: int, S: int, args, settle_ms: float):
                        "per_gpu_batch": B, "global_batch": B * cx.world, "phonemes": S, "mel_frames": T}}
 
 
-def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, steps: int, share: bool = False):
+def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, steps: int, share: bool = False,
+                 depth: int = 1):
     """stage2 inference over a global batch of Bg utterances sharded across the
-    ranks (configs[3] / [4]): one m2_inference_front + RCCL all_reduce(MAX) +
-    m2_inference_back + all_gather of mel / audio per step."""
-    from m2amd.parallel import hip_stages, shard_bounds, sharded_inference
+    ranks (configs[3] / [4]): per step the front half (T_max into a device
+    word), RCCL all_reduce(MAX) of that word, the back half reading T from it
+    and a gather of mel / audio to rank 0.  depth > 1: ShardedPipeline with
+    that many global batches in flight per rank (one stream and model handle
+    per lane; step i + 1's front half beside step i's back half and gather)."""
+    from m2amd.parallel import ShardedPipeline, hip_stages, shard_bounds, sharded_inference
     import torch.distributed as td
     m = cx.model("s2")
     m.set_vocoder_chunking(chunk)
@@ -585,8 +589,21 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
         st = hip_stages(m)
         # the global batch's mel / audio are gathered to rank 0 (RCCL gather over xGMI)
         # share: one rank's two-phase flow (front, T exchange, back) timed alone
-        step = lambda: sharded_inference(st, ids, lens, gather_to=0, one_call_world1=not share)  # noqa: E731
-        mel, audio = step()
+        if depth > 1:
+            pipe = ShardedPipeline(m, depth=depth, gather_to=0)
+            prev = [None]
+
+            def step():
+                r = pipe.submit(ids, lens)
+                if prev[0] is not None:
+                    prev[0].wait()
+                prev[0] = r
+                return r
+
+            mel, audio = pipe.submit(ids, lens).wait()
+        else:
+            step = lambda: sharded_inference(st, ids, lens, gather_to=0, one_call_world1=not share)  # noqa: E731
+            mel, audio = step()
         T = 5 * S  # pinned durations: every utterance has 5 frames per phoneme
         if cx.rank == 0:
             assert mel.shape == (Bg, T, 80) and audio.shape == (Bg, 1, 64 * T)
@@ -623,7 +640,7 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
     finally:
         m.set_vocoder_chunking(0)
     return {"value": round(samples_per(Bg, T) * steps / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
-            "steps": steps, "settle_ms": round(settled, 1), "scaling": "strong",
+            "steps": steps, "settle_ms": round(settled, 1), "scaling": "strong", "in_flight": depth,
             "rtf_x_realtime": round(samples_per(Bg, T) * steps / elapsed / SAMPLE_RATE, 1),
             "config": {"stage": "stage2_quality", "global_batch": Bg, "per_gpu_batch": hi - lo, "phonemes": S,
                        "mel_frames": T, "vocoder_chunk_frames": chunk, "n_ranks": cx.world,
@@ -698,6 +715,12 @@ def run(args):
             # what bounds a small per-GPU batch (host phases vs GPU-elapsed)
             extras["s2_b8_per_gpu_share"] = sharded_line(cx, 8, 100, 0, args, 100.0, max(20, args.steps // 2),
                                                          share=True)
+            # the same share with two global batches in flight (ShardedPipeline)
+            extras["s2_b8_per_gpu_share_2inflight"] = sharded_line(cx, 8, 100, 0, args, 100.0,
+                                                                   max(20, args.steps // 2), share=True, depth=2)
+        if wl != "s2_b64":
+            extras["s2_b64_sharded_2inflight"] = sharded_line(cx, 64, 100, 0, args, 100.0, max(10, args.steps // 4),
+                                                              depth=2)
         if wl != "s2_longform":
             extras["s2_longform_sharded"] = sharded_line(cx, 128, 520, 256, args, 100.0, max(3, args.steps // 40))
 

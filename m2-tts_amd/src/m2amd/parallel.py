@@ -26,8 +26,8 @@ On the GPU the frame count normally never visits the host between the phases
 (device-T path): m2_inference_front_dev writes the shard's T_max into a device
 word, the RCCL all-reduce(MAX) runs on that word in stream order, and
 m2_inference_back_dev launches the back half with grids sized for a frame
-capacity learnt from earlier steps (the global T rounded up to 32 frames, the
-same on every rank), its kernels reading T from the word.  The gather is
+capacity learnt from earlier steps (the last global T that exceeded it or fell
+under half of it - the same on every rank), its kernels reading T from the word.  The gather is
 enqueued right behind it on buffers laid out for that capacity; the host reads
 T (posted to host-mapped memory by the back half's first launch) only to shape
 the outputs.  A step whose T exceeds the capacity re-runs its back
@@ -80,27 +80,16 @@ class Stages:
 class HipStages:
     """The MI355X phases: one m2_inference_front and one m2_inference_back call
     per step on the model's packed handle (models/tts_model.py), or their
-    device-T forms (m2_inference_front_dev / m2_inference_back_dev)."""
+    device-T forms (m2_inference_front_dev / m2_inference_back_dev).  ``lane``
+    picks a handle of its own (ShardedPipeline: one per stream)."""
 
-    def __init__(self, model):
+    def __init__(self, model, lane: int = 0, tcap: Optional[dict] = None):
         self.model = model
+        self.lane = lane
         # frame capacity of the device-T path per (global B, S, duration_scale):
-        # the last global T rounded up to 32 frames - identical on every rank
-        self.tcap = {}
-
-    def dev_ok(self, device: torch.device, T_cap: int) -> bool:
-        return self.model._hip(device).dev_supported(T_cap)
-
-    def front_dev(self, ids: Tensor, lens: Optional[Tensor], scale: float, tword: Tensor) -> Any:
-        hm = self.model._hip(ids.device)
-        return hm, hm.inference_front_dev(ids, lens, scale, tword)
-
-    def back_dev(self, state: Any, T_cap: int, tword: Tensor, mel_out: Tensor, audio_out: Tensor) -> None:
-        hm, st = state
-        hm.inference_back_dev(st, T_cap, tword, mel_out, audio_out)
-
-    def frames_wait(self, state: Any) -> int:
-        return state[0].frames_wait()
+        # the last global T that exceeded it or fell under half of it -
+        # identical on every rank
+        self.tcap = {} if tcap is None else tcap
 
     def mel_channels(self) -> int:
         return int(self.model._m2_cfg.mel_channels)
@@ -108,7 +97,7 @@ class HipStages:
     def front(self, ids: Tensor, lens: Optional[Tensor], scale: float) -> Tuple[Any, int]:
         # one handle lookup per step (its weight-identity check walks every
         # parameter, ~25 us of host time): the back half reuses this handle
-        hm = self.model._hip(ids.device)
+        hm = self.model._hip(ids.device, self.lane)
         state, t = hm.inference_front(ids, lens, scale)
         return (hm, state), t
 
@@ -120,7 +109,12 @@ class HipStages:
         """Both phases with no collective between them (world 1): the one-call
         m2_inference (the back half is launched from C right after the T_max
         read, no Python between the phases)."""
-        return self.model._hip(ids.device).inference(ids, lens, scale)
+        return self.model._hip(ids.device, self.lane).inference(ids, lens, scale)
+
+    def dev_handle(self, device: torch.device, T_cap: int):
+        """The HipModel of the device-T path at capacity T_cap, or None."""
+        hm = self.model._hip(device, self.lane)
+        return hm if hm.dev_supported(T_cap) else None
 
 
 def hip_stages(model) -> HipStages:
@@ -233,18 +227,18 @@ class PendingGather:
 def _learn_cap(caps: dict, key, T: int) -> None:
     cap = caps.get(key, 0)
     if T > cap or 2 * T < cap:
-        caps[key] = (T + 31) // 32 * 32
+        caps[key] = T  # exact: launch configurations chosen from the capacity are T's own
 
 
-def _sharded_dev(stages, ids, lens, scale, B, lo, hi, world, group, cap, key, gather, gather_to, async_gather):
-    """One step of the device-T path (module docstring); None when T outgrew
-    the capacity (the caller re-runs the step's back half on the host path)."""
+def _sharded_dev(stages, hm, ids, lens, scale, B, lo, hi, world, group, cap, key, gather, gather_to, async_gather):
+    """One step of the device-T path (module docstring) on HipModel hm; None
+    when T outgrew the capacity (the caller re-runs the step on the host path)."""
     dev = ids.device
     M = stages.mel_channels()
     b = hi - lo
     nccl = world > 1 and dist.get_backend(group) == "nccl"
     tw = torch.empty(1, dtype=torch.int32, device=dev)
-    state = stages.front_dev(ids[lo:hi], lens[lo:hi] if lens is not None else None, scale, tw) if b else None
+    state = hm.inference_front_dev(ids[lo:hi], lens[lo:hi] if lens is not None else None, scale, tw) if b else None
     if not b:
         tw.zero_()
     if world > 1:
@@ -258,7 +252,7 @@ def _sharded_dev(stages, ids, lens, scale, B, lo, hi, world, group, cap, key, ga
     moff = (rows * cap * M + 63) // 64 * 64
     buf = torch.empty(moff + rows * 64 * cap, dtype=torch.float32, device=dev)
     if b:
-        stages.back_dev(state, cap, tw, buf[: b * cap * M], buf[moff: moff + b * 64 * cap])
+        hm.inference_back_dev(state, cap, tw, buf[: b * cap * M], buf[moff: moff + b * 64 * cap])
     parts, work = None, None
     if gather and world > 1:
         me = dist.get_rank(group)
@@ -272,7 +266,7 @@ def _sharded_dev(stages, ids, lens, scale, B, lo, hi, world, group, cap, key, ga
             work = dist.gather(buf, parts, dst=dst, group=group, async_op=async_gather)
     # T as the back half's first launch posted it (the back half keeps running);
     # a rank with an empty shard reads the word
-    T = stages.frames_wait(state) if b else max(1, int(tw.item()))
+    T = hm.frames_wait() if b else max(1, int(tw.item()))
     _learn_cap(stages.tcap, key, T)
     if T > cap:
         if async_gather and work is not None:
@@ -341,14 +335,15 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
     ids = phoneme_ids[lo:hi]
     lens = phoneme_lengths[lo:hi] if phoneme_lengths is not None else None
     key = (B, phoneme_ids.shape[1], float(duration_scale))
-    use_dev = device_T and hasattr(stages, "front_dev") and phoneme_ids.is_cuda and \
+    use_dev = device_T and hasattr(stages, "dev_handle") and phoneme_ids.is_cuda and \
         not (one_call_world1 and world == 1 and hi > lo and hasattr(stages, "both"))
     if use_dev:
         cap = stages.tcap.get(key, 0)
-        if cap > 0 and stages.dev_ok(phoneme_ids.device, cap):
+        hm = stages.dev_handle(phoneme_ids.device, cap) if cap > 0 else None
+        if hm is not None:
             with torch.no_grad():
-                out = _sharded_dev(stages, phoneme_ids, phoneme_lengths, duration_scale, B, lo, hi, world, group,
-                                   cap, key, gather, gather_to, async_gather)
+                out = _sharded_dev(stages, hm, phoneme_ids, phoneme_lengths, duration_scale, B, lo, hi, world,
+                                   group, cap, key, gather, gather_to, async_gather)
             if out is not None:
                 return out
     if one_call_world1 and world == 1 and hi > lo and hasattr(stages, "both"):
@@ -389,3 +384,56 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
     fin = _gather_shards(both, B, world, group, gather_to, async_op=async_gather)
     pend = PendingGather(fin if async_gather else (lambda: fin), (B, T, M), (B, 1, 64 * T), audio.dtype)
     return pend if async_gather else pend.wait()
+
+
+class _LaneResult:
+    """A pipelined step's (mel, audio): ``wait()`` joins the lane's stream into
+    the caller's and returns them (None on non-destination ranks)."""
+
+    def __init__(self, out, stream, caller):
+        self._out, self._stream, self._caller = out, stream, caller
+        self._res = None
+
+    def wait(self):
+        if self._out is not None:
+            r = self._out.wait() if isinstance(self._out, PendingGather) else self._out
+            self._caller.wait_stream(self._stream)
+            for t in r:
+                if t is not None:
+                    t.record_stream(self._caller)
+            self._res, self._out = r, None
+        return self._res
+
+
+class ShardedPipeline:
+    """Sharded inference with ``depth`` global batches in flight per rank.
+
+    Each lane has its own model handle and HIP stream; ``submit`` runs one
+    step (sharded_inference on the device-T path, gather left in flight) on
+    the next lane and returns at once with a _LaneResult.  Step i + 1's
+    front half (encoder, durations: small launches that leave most CUs idle
+    at a per-GPU share of 8 utterances) then runs beside step i's decoder and
+    vocoder, and step i's gather beside step i + 1's compute.  Every rank
+    submits the same sequence, so the lanes' collectives are issued in the
+    same order everywhere (torch's process group runs them on one
+    communicator stream).  Results are identical to sharded_inference."""
+
+    def __init__(self, model, depth: int = 2, group=None, gather_to: Optional[int] = 0):
+        tcap: dict = {}
+        self.lanes = [(HipStages(model, lane=i, tcap=tcap), torch.cuda.Stream()) for i in range(depth)]
+        self.group, self.gather_to = group, gather_to
+        self._next = 0
+
+    def submit(self, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor],
+               duration_scale: float = 1.0) -> _LaneResult:
+        st, stream = self.lanes[self._next % len(self.lanes)]
+        self._next += 1
+        caller = torch.cuda.current_stream(phoneme_ids.device)
+        stream.wait_stream(caller)  # the inputs were produced on the caller's stream
+        for t in (phoneme_ids, phoneme_lengths):
+            if t is not None:
+                t.record_stream(stream)
+        with torch.cuda.stream(stream):
+            out = sharded_inference(st, phoneme_ids, phoneme_lengths, duration_scale, group=self.group,
+                                    gather_to=self.gather_to, async_gather=True, one_call_world1=False)
+        return _LaneResult(out, stream, caller)

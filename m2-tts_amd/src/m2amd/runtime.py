@@ -126,10 +126,12 @@ class HipModel:
         expansion, decoder and vocoder enqueued from C right after the read.
 
         The outputs are allocated before T is known, for a frame capacity per
-        (B, S) learnt from earlier calls (T rounded up to 32 frames; shrunk
-        when T falls under half of it); the result is the contiguous [B,T,M] /
-        [B,1,64T] prefix of those buffers.  A call whose T exceeds the capacity
-        allocates exactly and finishes with m2_inference_back."""
+        (B, S) learnt from earlier calls (the last T that exceeded it, or fell
+        under half of it); the result is the contiguous [B,T,M] / [B,1,64T]
+        prefix of those buffers.  With a capacity the back half is enqueued
+        before the host reads T (kernels take T from the device).  A call whose
+        T exceeds the capacity allocates exactly and finishes with
+        m2_inference_back."""
         require_device(ids, lengths, what="M2TTSModel")
         if ids.dtype != torch.int64 or not ids.is_contiguous():
             ids = ids.to(torch.int64).contiguous()
@@ -165,7 +167,9 @@ class HipModel:
             _lib.check(lib.m2_inference_back(self.handle, B, S, T, front.data_ptr(), front.numel(), mel.data_ptr(),
                                              audio.data_ptr(), ws.data_ptr(), ws.numel(), st), "m2_inference_back")
         if T > cap or 2 * T < cap:
-            self._tcap[(B, S)] = (T + 31) // 32 * 32
+            # the exact T: the launch configurations chosen from the capacity
+            # (e.g. the stage1 tail's strip length) are then those of T itself
+            self._tcap[(B, S)] = T
         return mel, audio
 
     def inference_front(self, ids: Tensor, lengths: Optional[Tensor], scale: float) -> Tuple[Tuple, int]:
@@ -371,14 +375,16 @@ def default_range_policy() -> str:
 
 
 class HandleCache:
-    """Per-device HipModel for one nn.Module, rebuilt when its weights change."""
+    """Per-device HipModel for one nn.Module, rebuilt when its weights change.
+    ``lane`` > 0 gives further handles of the same weights (one per stream of a
+    pipelined caller: a handle's device state is ordered on one stream)."""
 
     def __init__(self):
-        self._entries: Dict[torch.device, Tuple[Tuple, HipModel]] = {}
+        self._entries: Dict[Tuple[torch.device, int], Tuple[Tuple, HipModel]] = {}
 
-    def get(self, module: torch.nn.Module, cfg: _lib.M2Config, device: torch.device) -> HipModel:
+    def get(self, module: torch.nn.Module, cfg: _lib.M2Config, device: torch.device, lane: int = 0) -> HipModel:
         key = state_key(module)
-        ent = self._entries.get(device)
+        ent = self._entries.get((device, lane))
         if ent is not None and ent[0] == key:
             return ent[1]
         hm = HipModel(module.state_dict(), cfg, device)
@@ -390,7 +396,7 @@ class HandleCache:
         if path:
             hm.vocoder_select(path)
         hm.set_range_policy(module.__dict__.get("_m2_range_policy") or default_range_policy())
-        self._entries[device] = (key, hm)
+        self._entries[(device, lane)] = (key, hm)
         return hm
 
     def handles(self):

@@ -222,12 +222,12 @@ class M2TTSModel(nn.Module):
                 self.eval()
                 return
 
-    def _hip(self, device: torch.device):
+    def _hip(self, device: torch.device, lane: int = 0):
         cache = _HANDLES.get(self)
         if cache is None:
             cache = HandleCache()
             _HANDLES[self] = cache
-        return cache.get(self, self._m2_cfg, device)
+        return cache.get(self, self._m2_cfg, device, lane)
 
     def set_vocoder_chunking(self, chunk_frames: int = 256):
         """Stream the vocoder in chunks of ``chunk_frames`` mel frames inside

@@ -182,3 +182,31 @@ def test_sharded_device_T_two_ranks_gloo(gpu, tmp_path):
     mel1, _ = m.inference(ids[:1], lens[:1])
     for i in range(2):
         assert torch.equal(torch.from_numpy(z[f"one{i}"]), mel1.cpu())
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_sharded_pipeline_world1(gpu, depth):
+    """ShardedPipeline: several global batches in flight on their own streams
+    and handles; each result equals inference() on its inputs bit for bit
+    (batches alternate between two inputs of different T, so lanes also
+    cross the capacity bookkeeping)."""
+    from m2amd.parallel import ShardedPipeline
+    m = build_model("s2", gpu)
+    g = torch.Generator().manual_seed(depth)
+    batches = []
+    for k in range(2):
+        ids = torch.randint(0, 42, (8, 100), generator=g).to(gpu)
+        lens = torch.randint(30 + 40 * k, 101, (8,), generator=g).to(gpu)
+        batches.append((ids, lens, m.inference(ids, lens)))
+    pipe = ShardedPipeline(m, depth=depth)
+    pend = []
+    for i in range(7):
+        ids, lens, _ = batches[i % 2]
+        pend.append((pipe.submit(ids, lens), i % 2))
+        if len(pend) > depth:
+            r, k = pend.pop(0)
+            mel, audio = r.wait()
+            assert torch.equal(mel, batches[k][2][0]) and torch.equal(audio, batches[k][2][1])
+    for r, k in pend:
+        mel, audio = r.wait()
+        assert torch.equal(mel, batches[k][2][0]) and torch.equal(audio, batches[k][2][1])
