@@ -385,9 +385,17 @@ class Ctx:
         return float(t.item())
 
     def settle(self, fn, ms: float) -> float:
-        """Run fn untimed for about `ms` milliseconds of wall time (clock settling)."""
+        """Run fn untimed for about `ms` milliseconds of wall time (clock settling).
+        With several ranks the ranks agree on every further iteration (fn may
+        hold collectives: a rank that stopped alone would leave the others
+        waiting in one)."""
         t0 = time.perf_counter()
-        while (time.perf_counter() - t0) * 1e3 < ms:
+        while True:
+            go = (time.perf_counter() - t0) * 1e3 < ms
+            if self.dist:
+                go = self.max_over_ranks(1.0 if go else 0.0) > 0.5
+            if not go:
+                break
             fn()
             torch.cuda.synchronize(self.dev)
         return (time.perf_counter() - t0) * 1e3
@@ -653,6 +661,21 @@ def sharded_line(cx: Ctx, Bg: int, S: int, chunk: int, args, settle_ms: float, s
                                       "around each half (GPU time incl. any launch gaps)"}}
 
 
+class _Progress(dict):
+    """The extras dict; every line stored prints a progress note to stderr (a
+    multi-line run is otherwise silent until its one JSON line)."""
+
+    def __init__(self, rank: int):
+        super().__init__()
+        self.rank, self.t0 = rank, time.perf_counter()
+
+    def __setitem__(self, key, value):
+        super().__setitem__(key, value)
+        ms = value.get("ms_per_step") if isinstance(value, dict) else None
+        print(f"[bench rank {self.rank}] {key}: {ms} ms/step ({time.perf_counter() - self.t0:.1f} s)",
+              file=sys.stderr, flush=True)
+
+
 def run(args):
     if args.dry_run:
         return dry_run(args)
@@ -675,7 +698,7 @@ def run(args):
     cx.backend = "RCCL" if args.dist_backend == "nccl" else "gloo"
     B, S = args.batch, args.phonemes
     wl = args.workload
-    extras = {}
+    extras = _Progress(rank)
 
     if wl == "vocoder":
         head = vocoder_line(cx, "s1", B, 5 * S, args, args.settle_ms, 1000)
@@ -694,6 +717,7 @@ def run(args):
         desc = f"stage2_quality M2TTSModel.inference global B={Bg} S={Sg} sharded x{world} ({wl}, configs[" \
                f"{3 if wl == 's2_b64' else 4}])"
 
+    print(f"[bench rank {rank}] {wl}: {head['ms_per_step']} ms/step", file=sys.stderr, flush=True)
     if not args.no_extras:
         if wl != "pipeline":
             extras["pipeline"] = pipeline_line(cx, B, S, args, 100.0)

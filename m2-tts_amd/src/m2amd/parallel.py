@@ -396,7 +396,10 @@ class _LaneResult:
 
     def wait(self):
         if self._out is not None:
-            r = self._out.wait() if isinstance(self._out, PendingGather) else self._out
+            # the gather's wait and the assembly of rank 0's outputs run on the
+            # lane's stream, where the gathered buffers were allocated
+            with torch.cuda.stream(self._stream):
+                r = self._out.wait() if isinstance(self._out, PendingGather) else self._out
             self._caller.wait_stream(self._stream)
             for t in r:
                 if t is not None:
