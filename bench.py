@@ -245,7 +245,7 @@ def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_
     node's host cores: a child process pinned to one logical CPU per physical
     core of this process's affinity mask, one OpenMP thread per core
     (torch.set_num_threads(physical cores)), median of `runs` measurements
-    with the spread.  Two figures for the headline configuration: the
+    with the spread (value = the best run).  Two figures for the headline configuration: the
     vocoder single pass (configs[1], the `value`) and M2TTSModel.inference as
     written (2 vocoder passes, Python length-regulator loop)."""
     phys, sockets = physical_cores()
@@ -266,17 +266,23 @@ def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_
     cpu_model, ncpu, aff = host_info()
     voc, inf = res["vocoder"], res["inference_as_written"]
     spread = lambda d: round((d["max"] - d["min"]) / d["median"], 3)  # noqa: E731
-    return {"value": voc["median"], "unit": "audio samples/s", "cores": len(cpus), "kind": "port",
+    # value = the best of the runs: other tenants' load on the shared host only
+    # slows a run down, so the fastest is the most repeatable figure (and the
+    # conservative one for the GPU / CPU ratio); the median is reported beside it
+    return {"value": voc["max"], "median": voc["median"], "unit": "audio samples/s", "cores": len(cpus),
+            "kind": "port",
             "sockets": sockets, "host_logical_cpus": ncpu, "affinity_cpus": aff,
             "physical_cores_in_affinity": len(phys), "cgroup_cpu_quota": quota,
             "torch_threads": res["torch_threads"], "pinned": "one OpenMP thread per physical core "
             "(OMP_PROC_BIND=close on one logical CPU per core)", "cpu_model": cpu_model,
-            "stat": f"median of {runs} runs of >= {min_s} s", "min": voc["min"], "max": voc["max"],
+            "stat": f"best of {runs} runs of >= {min_s} s (median, min, max beside it)", "min": voc["min"],
+            "max": voc["max"],
             "spread": spread(voc),
             "sample": f"oracle SimpleVocoder single pass (the reference's ATen op sequence), B={B} mel [{B},64,{T}] "
                       f"(configs[1]); torch {torch.__version__} CPU ops on {len(cpus)} physical cores "
                       f"(of {len(phys)} on {sockets} sockets; job CPU quota {quota}) of {cpu_model}",
-            "inference_as_written": {"value": inf["median"], "min": inf["min"], "max": inf["max"],
+            "inference_as_written": {"value": inf["max"], "median": inf["median"], "min": inf["min"],
+                                     "max": inf["max"],
                                      "spread": spread(inf), "unit": "audio samples/s",
                                      "sample": f"oracle M2TTSModel.inference as written (2 vocoder passes, "
                                                f"Python length-regulator loop), B={B} S={S} -> T={T}"},
