@@ -1225,7 +1225,10 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.B = B;
     a.N = N;
     a.npad = tfl_npad(N);
-    const int rb = tfl_rb(B, N) > 1 ? 2 : 1;
+    // rows per workgroup: the layers' choice, 64-row tiles only with
+    // M2_TFL_FIRST_RB=4 (A/B; read per call)
+    const char* fe = std::getenv("M2_TFL_FIRST_RB");
+    const int rl = tfl_rb(B, N), rb = rl > 2 ? ((fe && std::atoi(fe) == 4) ? 4 : 2) : rl;
     a.ntile = a.npad / (tfl::TQ * rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
@@ -1254,7 +1257,8 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
 #define M2_TFF(HH, SS, MM)                                                                      \
     if (H == HH && f.src == SS && masked == MM) {                                               \
-        if (rb == 2) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 2>), grid, blk, 0, st, a);  \
+        if (rb == 4) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 4>), grid, blk, 0, st, a);  \
+        else if (rb == 2) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 2>), grid, blk, 0, st, a);  \
         else hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 1>), grid, blk, 0, st, a);          \
         M2_LAUNCHED("tfl first_kernel");                                                        \
         return M2_OK;                                                                           \

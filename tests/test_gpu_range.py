@@ -90,6 +90,10 @@ def test_default_policy_inference_never_nan(gpu, stage):
     ref_mel, ref_audio = orc.inference(sd, stage_config(stage), ids, lens, as_written=False)
     assert maxabs(mel, ref_mel) <= MEL_MAXABS_TOL
     assert rms(audio, ref_audio) <= AUDIO_RMS_TOL
+    # the second call of the shape runs the speculative back half (T from the
+    # device, the redo kernels sized for the capacity): the same audio
+    mel2, audio2 = m.inference(ids.to(gpu), lens.to(gpu))
+    assert torch.equal(mel2, mel) and torch.equal(audio2, audio)
     m.set_vocoder_precision("f32")
     _, exact = m.inference(ids.to(gpu), lens.to(gpu))
     assert torch.equal(audio, exact)
@@ -181,3 +185,10 @@ def test_frame_count_overflow_is_an_error(gpu):
         m.inference(torch.from_numpy(g["ids"]).to(gpu), torch.from_numpy(g["lengths"]).to(gpu), duration_scale=1e7)
     mel, _ = m.inference(torch.from_numpy(g["ids"]).to(gpu), torch.from_numpy(g["lengths"]).to(gpu))
     assert mel.shape == tuple(g["mel"].shape)  # the mailbox protocol is intact after the error
+    # with a capacity learnt the back half is launched before the count is
+    # known: the overflowing call still raises (its launches did nothing) and
+    # the next call is intact
+    with pytest.raises(M2Error, match="status -2"):
+        m.inference(torch.from_numpy(g["ids"]).to(gpu), torch.from_numpy(g["lengths"]).to(gpu), duration_scale=1e7)
+    mel2, _ = m.inference(torch.from_numpy(g["ids"]).to(gpu), torch.from_numpy(g["lengths"]).to(gpu))
+    assert torch.equal(mel2, mel)
