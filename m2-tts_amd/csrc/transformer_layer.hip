@@ -679,8 +679,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 template <int H, int HD, bool MASKED>
 __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
                                                  const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
-                                                 int len, float sl2, unsigned char* A, unsigned char* ring,
-                                                 int prio = 0) {
+                                                 int len, float sl2, unsigned char* A, unsigned char* ring) {
     using G = Geo<HD>;
     using Q = QsGeo<HD>;
     constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
@@ -848,10 +847,10 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
     lstore(0);
     if (1 < nsc) gload(1);
     lds_barrier();
-    // prio (A/B, M2_TFL_PRIO=1): head 0's waves issue first on their SIMD (the
-    // head-1 wave of the same query block shares it), so one wave's MFMA phase
-    // can fall on the other's softmax (VALU) phase
-    if (prio && h == 0) __builtin_amdgcn_s_setprio(1);
+    // (Head 0's waves at a higher issue priority than the head-1 wave of the
+    // same query block on their SIMD, so that one wave's MFMA phase could fall
+    // on the other's softmax phase: no change at B=64 T=500, B=16 T=2600 or
+    // stage1 B=32, in-process A/B, profiles/r03/ab/r03x_ab.txt.)
 #pragma unroll 1
     for (int p = 0; p < nsc; ++p) {
         // step p from buffer p & 1; p + 1 goes to the other buffer, p + 2 is requested
@@ -860,7 +859,6 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
         process(ring + (p & 1) * SB, p);
         lds_barrier();
     }
-    if (prio && h == 0) __builtin_amdgcn_s_setprio(0);
     TSTAMP(1);
     lsum += __shfl_xor(lsum, 16);
     lsum += __shfl_xor(lsum, 32);
@@ -874,7 +872,6 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
 // ---------------------------------------------------------------------------
 struct LArgs {
     int B, N, npad, ntile;
-    int prio;  // attention_qsplit's wave priorities (A/B switch)
     const int32_t* dN;  // device frame count (dev_frames; N is then the capacity)
     unsigned* qcnt;
     unsigned qseq;
@@ -939,7 +936,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
     if constexpr (QS) {
-        attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U, a.prio);
+        attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         if (wave < H / 16) so.load(a.Wo, wave);
         __syncthreads();
         TSTAMP(2);
@@ -1232,10 +1229,10 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.B = B;
     a.N = N;
     a.npad = tfl_npad(N);
-    // rows per workgroup: the layers' choice, 64-row tiles only with
-    // M2_TFL_FIRST_RB=4 (A/B; read per call)
-    const char* fe = std::getenv("M2_TFL_FIRST_RB");
-    const int rl = tfl_rb(B, N), rb = rl > 2 ? ((fe && std::atoi(fe) == 4) ? 4 : 2) : rl;
+    // rows per workgroup: the layers' choice up to 32 (64-row tiles made this
+    // launch 23 % faster but the step 1.4 % slower at stage2 B=64, in-process
+    // A/B, profiles/r03/ab/r03x_ab.txt)
+    const int rb = tfl_rb(B, N) > 1 ? 2 : 1;
     a.ntile = a.npad / (tfl::TQ * rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
@@ -1264,8 +1261,7 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
 #define M2_TFF(HH, SS, MM)                                                                      \
     if (H == HH && f.src == SS && masked == MM) {                                               \
-        if (rb == 4) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 4>), grid, blk, 0, st, a);  \
-        else if (rb == 2) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 2>), grid, blk, 0, st, a);  \
+        if (rb == 2) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 2>), grid, blk, 0, st, a);  \
         else hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 1>), grid, blk, 0, st, a);          \
         M2_LAUNCHED("tfl first_kernel");                                                        \
         return M2_OK;                                                                           \
@@ -1296,8 +1292,6 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.B = B;
     a.N = N;
     a.dN = dN;
-    const char* pe = std::getenv("M2_TFL_PRIO");  // read per call (A/B)
-    a.prio = pe && std::atoi(pe) == 1;
     a.npad = tfl_npad(N);
     const int rb = tfl_rb(B, N);
     a.ntile = a.npad / (tfl::TQ * rb);
