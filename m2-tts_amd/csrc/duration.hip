@@ -36,6 +36,16 @@ constexpr int DUR_TS = 14;
 constexpr int DUR_WAVES = 8;
 
 typedef float dur_f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;  // global (never flat) agent-scope accesses
+
+// The frame count fused into the duration kernel (duration_kernel<H, LN, true>)
+struct DurCount {
+    float scale;
+    int32_t *cum, *T, *Tmax;
+    unsigned* ticket;  // zero between calls (the last workgroup resets it)
+    int32_t* mbox;     // host-mapped (seq, T_max) mailbox or null
+    int32_t seq;
+};
 
 __device__ __forceinline__ int frames_from(float d, float scale) {
     const float v = d * scale;                       // fp32 product, as dur*scale
@@ -103,18 +113,83 @@ __device__ __forceinline__ void dur_conv_mfma(const float* in, const DurW<H>& W,
     }
 }
 
+__device__ __forceinline__ int32_t sat32(long long v) { return (int32_t)min(v, (long long)INT32_MAX); }
+
+// The length regulator's frame count run by the duration kernel's last
+// workgroup: the same arithmetic as lr_count_kernel<true> - frames_from per
+// phoneme, 64-bit prefix sums saturated at INT32_MAX into cum[b, 0..S], totals
+// T[b], Tmax, the ticket reset for the next call and the optional host mailbox
+// post.  The durations were stored sc1 by the other workgroups of this launch,
+// so every load of them is an sc1 load; the whole batch's frame counts are
+// fetched in one pass (8 loads in flight per lane) into LDS, then one wave per
+// utterance scans them.  B * S <= kDurCountMax.
+constexpr int kDurCountMax = 8192;
+__device__ __forceinline__ float dur_ld(const float* d, size_t i) {
+    return __uint_as_float(__hip_atomic_load((gu32*)(d + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ void count_frames(const float* __restrict__ dur, int B, int S, const DurCount& dc) {
+    __shared__ int32_t fr[kDurCountMax];
+    __shared__ long long wmax[DUR_WAVES];
+    constexpr int NT = 64 * DUR_WAVES, U = 8;
+    const int n = B * S, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i0 = threadIdx.x; i0 < n; i0 += U * NT) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = i0 + u * NT < n ? dur_ld(dur, (size_t)i0 + u * NT) : 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * NT < n) fr[i0 + u * NT] = frames_from(v[u], dc.scale);
+    }
+    __syncthreads();
+    const int per = (S + 63) / 64, lo = min(S, lane * per), hi = min(S, lo + per);
+    long long mx = 0;
+    for (int b = wave; b < B; b += DUR_WAVES) {
+        const int32_t* f = fr + b * S;
+        long long sum = 0;
+        for (int s = lo; s < hi; ++s) sum += f[s];
+        long long inc = sum;  // inclusive scan over the wave's lanes
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const long long v = __shfl_up(inc, off);
+            if (lane >= off) inc += v;
+        }
+        long long run = inc - sum;
+        int32_t* c = dc.cum + (size_t)b * (S + 1);
+        if (lane == 0) c[0] = 0;
+        for (int s = lo; s < hi; ++s) {
+            run += f[s];
+            c[s + 1] = sat32(run);
+        }
+        const long long total = __shfl(inc, 63);
+        if (lane == 0) dc.T[b] = sat32(total);
+        mx = max(mx, total);
+    }
+    if (lane == 0) wmax[wave] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < DUR_WAVES; ++w) mx = max(mx, wmax[w]);
+        const int32_t tm = sat32(mx);
+        *dc.Tmax = tm;
+        __hip_atomic_store((gu32*)dc.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dc.mbox) {  // null: T_max stays on the device (m2_inference_front_dev)
+            __hip_atomic_store(dc.mbox + 1, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(dc.mbox, dc.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // LN: `enc` is the encoder's last layer output BEFORE its final LayerNorm
 // (tts_model.py:87); each workgroup normalises its rows while loading them
 // (one wave per row, the halo rows redundantly) and stores its own 14
 // normalised rows to enc_out - the encoder output the length regulator
 // expands - in place of a separate layer_norm_kernel launch.
-template <int H, bool LN>
+template <int H, bool LN, bool COUNT>
 __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ enc, int S, const float4* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ a1, const float* __restrict__ c1, const float4* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ a2, const float* __restrict__ c2,
     const float* __restrict__ pw, const float* __restrict__ pb, float* __restrict__ dur,
-    const float* __restrict__ lng, const float* __restrict__ lnb, float* __restrict__ enc_out) {
+    const float* __restrict__ lng, const float* __restrict__ lnb, float* __restrict__ enc_out, DurCount dc) {
     constexpr int XS = H + 2, NT = 64 * DUR_WAVES;
     __shared__ float X[18 * XS];   // positions s0-2 .. s0+15
     __shared__ float Y1[18 * XS];  // s0-1 .. s0+14 (+2 zero rows read by conv2's unused rows)
@@ -184,8 +259,28 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
             const float x = acc + pb[0];
             // F.softplus(beta=1, threshold=20)
             const float d = x > 20.f ? x : log1pf(expf(x));
-            dur[(size_t)b * S + s] = d;
+            if constexpr (COUNT)  // write-through (sc1): the last workgroup reads it in this launch
+                __hip_atomic_store((gu32*)(dur + (size_t)b * S + s), __float_as_uint(d), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            else
+                dur[(size_t)b * S + s] = d;
         }
+    }
+    if constexpr (COUNT) {
+        // hand-off to the last workgroup (MI355X_MICROARCH.md, inter-workgroup
+        // visibility, table row 1): every storing wave drains its sc1 stores,
+        // the barrier orders them before lane 0's ticket add, and the workgroup
+        // whose add returns the last ticket reads every duration with sc1 loads
+        // (no fences: no L2 write-back per workgroup, which made round 1's
+        // fused form slower than the separate count kernel)
+        __shared__ int last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+            last = __hip_atomic_fetch_add((gu32*)dc.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   gridDim.x * gridDim.y - 1;
+        __syncthreads();
+        if (last) count_frames(dur, gridDim.y, S, dc);
     }
 }
 
@@ -203,8 +298,6 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
 // Frame counts are clamped to 2^30 per phoneme and summed in 64 bits; the
 // stored prefix sums and totals saturate at INT32_MAX (the host rejects a
 // T_max above m2's frame limit with M2_E_SHAPE instead of wrapping).
-__device__ __forceinline__ int32_t sat32(long long v) { return (int32_t)min(v, (long long)INT32_MAX); }
-
 template <bool SYNC>
 __global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ dur, int is_int,
                                                        float scale, int S, int32_t* __restrict__ cum,
@@ -321,19 +414,23 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict_
 
 // ---------------------------------------------------------------------------
 // p: w1 (packed), b1, alpha1, beta1, w2 (packed), b2, alpha2, beta2, proj_w, proj_b
-int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st,
-                        const float* ln_g, const float* ln_b, float* enc_out) {
+namespace {
+int32_t duration_launch(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st,
+                        const float* ln_g, const float* ln_b, float* enc_out, const DurCount* dc) {
     if (B == 0 || S == 0) return M2_OK;
     const dim3 grid(cdiv(S, DUR_TS), B), blk(64 * DUR_WAVES);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
-#define M2_DUR(HH)                                                                                           \
-    case HH:                                                                                                 \
-        if (enc_out)                                                                                         \
-            hipLaunchKernelGGL((duration_kernel<HH, true>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], \
-                               p[3], f4(p[4]), p[5], p[6], p[7], p[8], p[9], dur, ln_g, ln_b, enc_out);     \
-        else                                                                                                 \
-            hipLaunchKernelGGL((duration_kernel<HH, false>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], \
-                               p[3], f4(p[4]), p[5], p[6], p[7], p[8], p[9], dur, nullptr, nullptr, nullptr); \
+    const DurCount none{};
+#define M2_DUR_L(HH, LL, CC)                                                                                       \
+    hipLaunchKernelGGL((duration_kernel<HH, LL, CC>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], p[3],         \
+                       f4(p[4]), p[5], p[6], p[7], p[8], p[9], dur, LL ? ln_g : nullptr, LL ? ln_b : nullptr,        \
+                       LL ? enc_out : nullptr, dc ? *dc : none)
+#define M2_DUR(HH)                                            \
+    case HH:                                                  \
+        if (enc_out && dc) M2_DUR_L(HH, true, true);          \
+        else if (enc_out) M2_DUR_L(HH, true, false);          \
+        else if (dc) M2_DUR_L(HH, false, true);               \
+        else M2_DUR_L(HH, false, false);                      \
         break;
     switch (H) {
         M2_DUR(32)
@@ -343,8 +440,29 @@ int32_t launch_duration(const float* enc, int B, int S, int H, const float* cons
         default: return fail(M2_E_SHAPE, "duration: hidden_dim must be 32, 64, 96 or 128");
     }
 #undef M2_DUR
+#undef M2_DUR_L
     M2_LAUNCHED("duration_kernel");
     return M2_OK;
+}
+}  // namespace
+
+// p: w1 (packed), b1, alpha1, beta1, w2 (packed), b2, alpha2, beta2, proj_w, proj_b
+int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st,
+                        const float* ln_g, const float* ln_b, float* enc_out) {
+    return duration_launch(enc, B, S, H, p, dur, st, ln_g, ln_b, enc_out, nullptr);
+}
+
+// The same launch with the length regulator's count (lr_count_kernel<true>'s
+// outputs: cum, T, Tmax, ticket reset, mailbox post) run by its last
+// workgroup - one launch fewer per inference.  0 < B * S <= kDurCountMax.
+bool duration_count_fusable(int B, int S) { return B > 0 && S > 0 && (long)B * S <= kDurCountMax; }
+
+int32_t launch_duration_count(const float* enc, int B, int S, int H, const float* const* p, float* dur,
+                              hipStream_t st, const float* ln_g, const float* ln_b, float* enc_out, float scale,
+                              int32_t* cum, int32_t* T, int32_t* Tmax, unsigned* ticket, int32_t* mbox, int32_t seq) {
+    M2_CHECK_ARG(B > 0 && S > 0 && (long)B * S <= kDurCountMax, "duration + count: batch too large to fuse");
+    const DurCount dc{scale, cum, T, Tmax, ticket, mbox, seq};
+    return duration_launch(enc, B, S, H, p, dur, st, ln_g, ln_b, enc_out, &dc);
 }
 
 int32_t launch_lr_count(const void* dur, int is_int, float scale, int B, int S, int32_t* cum,

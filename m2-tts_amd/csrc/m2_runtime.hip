@@ -27,6 +27,9 @@ int32_t launch_linear(const float*, const float*, const float*, const float*, co
 int32_t launch_attention(const float*, const uint8_t*, int, int, int, int, float*, hipStream_t, bool force_f32 = false);
 int32_t launch_duration(const float*, int, int, int, const float* const*, float*, hipStream_t,
                         const float* ln_g = nullptr, const float* ln_b = nullptr, float* enc_out = nullptr);
+int32_t launch_duration_count(const float*, int, int, int, const float* const*, float*, hipStream_t, const float*,
+                              const float*, float*, float, int32_t*, int32_t*, int32_t*, unsigned*, int32_t*, int32_t);
+bool duration_count_fusable(int, int);
 int32_t launch_lr_count(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int32_t launch_lr_count_sync(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, unsigned*, int32_t*,
                              int32_t, hipStream_t);
@@ -1597,11 +1600,32 @@ size_t m2_front_bytes(const m2_model* model, int32_t B, int32_t S) {
 
 namespace {
 // The front half up to the frame counts: encoder, durations (into f), then
-// count(f) launches the length regulator's count kernel (which writes T_max).
+// the frame counts.  With `fuse` (and a batch small enough, fuse_count) the
+// duration kernel's last workgroup runs the count itself: T_max into fuse->Tmax, the ticket
+// fuse->ticket, the optional mailbox post; otherwise count(f) launches the
+// length regulator's count kernel.
+struct CountFuse {
+    float scale;
+    int32_t* Tmax;  // null: the front buffer's own T_max word
+    unsigned* ticket;
+    int32_t* mbox;
+    int32_t seq;
+};
+// Default: fused for B * S <= 2048.  The last workgroup's count is serial
+// work behind every other workgroup: at stage2 B=8 S=100 the step is 1.9 %
+// shorter fused (duration 13.3 -> 15.7 us, the 5 us count launch gone), at
+// stage1 B=32 and stage2 B=64 S=100 it measured +0.3 / +0.7 % (in-process
+// A/B, profiles/r03/r03aa_ab.txt).  M2_DUR_COUNT=1 fuses up to the kernel's
+// limit (8192), =0 never.
+bool fuse_count(int B, int S) {
+    const char* e = std::getenv("M2_DUR_COUNT");  // read per call (tests and A/B switch it)
+    if (e && *e) return std::atoi(e) != 0 && duration_count_fusable(B, S);
+    return (long)B * S <= 2048 && duration_count_fusable(B, S);
+}
 template <typename Count>
 int32_t front_run(const m2_model* m, const int64_t* ids, const int64_t* lengths, int32_t B, int32_t S, void* front,
                   size_t front_bytes, void* workspace, size_t workspace_bytes, hipStream_t st, FrontBufs* f,
-                  Count count) {
+                  Count count, const CountFuse* fuse = nullptr) {
     M2_CHECK_ARG(m && B >= 0 && S >= 0, "m2_inference_front: bad argument");
     M2_CHECK_ARG(ids || B * S == 0, "m2_inference_front: null ids");
     if (int32_t rc0 = range_entry(m, "m2_inference")) return rc0;
@@ -1617,12 +1641,17 @@ int32_t front_run(const m2_model* m, const int64_t* ids, const int64_t* lengths,
             return rc;
         // the encoder's final LayerNorm runs inside the duration kernel, which
         // also stores the normalised encoder output (f.enc)
+        if (fuse && fuse_count(B, S))
+            return launch_duration_count(x, B, S, m->cfg.hidden_dim, m->dur, f->dur, st, m->enc_nw, m->enc_nb, f->enc,
+                                         fuse->scale, f->cum, f->tot, fuse->Tmax ? fuse->Tmax : f->tmax,
+                                         fuse->ticket, fuse->mbox, fuse->seq);
         if ((rc = launch_duration(x, B, S, m->cfg.hidden_dim, m->dur, f->dur, st, m->enc_nw, m->enc_nb, f->enc)))
             return rc;
     }
-    // A frame-count epilogue fused into the duration kernel (per-utterance
-    // tickets, one L2 write-back per workgroup) measured 5 us slower than
-    // this separate count kernel (tools/probe/count_fusion_ab.py, r17).
+    // Round 1's fused count (per-utterance tickets behind release fences: one
+    // L2 write-back per workgroup) measured 5 us slower than this separate
+    // kernel (tools/probe/count_fusion_ab.py, r17); the fused form above hands
+    // the durations over with write-through stores instead.
     return count(*f);
 }
 
@@ -1686,6 +1715,7 @@ int32_t m2_inference_front_dev(const m2_model* m, const int64_t* ids, const int6
     M2_CHECK_ARG(dev_Tmax, "m2_inference_front_dev: null T_max word");
     hipStream_t st = static_cast<hipStream_t>(stream);
     FrontBufs f;
+    const CountFuse cf{scale, dev_Tmax, m->cnt_ticket, nullptr, 0};
     return front_run(m, ids, lengths, B, S, front, front_bytes, workspace, workspace_bytes, st, &f,
                      [&](FrontBufs& fb) -> int32_t {
                          if (B == 0) {
@@ -1694,7 +1724,7 @@ int32_t m2_inference_front_dev(const m2_model* m, const int64_t* ids, const int6
                          }
                          return launch_lr_count_sync(fb.dur, 0, scale, B, S, fb.cum, fb.tot, dev_Tmax,
                                                      m->cnt_ticket, nullptr, 0, st);
-                     });
+                     }, &cf);
 }
 
 int32_t m2_inference_back(const m2_model* m, int32_t B, int32_t S, int32_t T, const void* front, size_t front_bytes,
@@ -1764,14 +1794,14 @@ int32_t m2_inference(const m2_model* m, const int64_t* ids, const int64_t* lengt
         std::lock_guard<std::mutex> lk(g_mb_mu);
         LrMailbox* mb = nullptr;
         if ((rc = mailbox_for(dev, &mb))) return rc;
-        int32_t seq = 0;
+        mb->seq = mb->seq == INT_MAX ? 1 : mb->seq + 1;
+        const int32_t seq = mb->seq;
+        const CountFuse cf{scale, nullptr, mb->ticket, mb->dev, seq};
         if ((rc = front_run(m, ids, lengths, B, S, front, front_bytes, workspace, workspace_bytes, st, &f,
                             [&](FrontBufs& fb) {
-                                mb->seq = mb->seq == INT_MAX ? 1 : mb->seq + 1;
-                                seq = mb->seq;
                                 return launch_lr_count_sync(fb.dur, 0, scale, B, S, fb.cum, fb.tot, fb.tmax, mb->ticket,
                                                             mb->dev, seq, st);
-                            })))
+                            }, &cf)))
             return rc;
         if ((rc = back_run(m, B, S, cap, f.tmax, front, front_bytes, mel_buf, audio_buf, workspace, workspace_bytes,
                            stream)))

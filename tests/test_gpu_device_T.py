@@ -210,3 +210,39 @@ def test_sharded_pipeline_world1(gpu, depth):
     for r, k in pend:
         mel, audio = r.wait()
         assert torch.equal(mel, batches[k][2][0]) and torch.equal(audio, batches[k][2][1])
+
+
+@pytest.mark.parametrize("stage,B,S,scale", [("s2", 8, 100, 1.0), ("s1", 64, 128, 1.0), ("s1", 65, 128, 1.0),
+                                             ("s2", 3, 700, 1.7), ("s1", 5, 40, 0.0), ("s1", 1, 1, 1.0),
+                                             ("s2", 16, 100, 0.45)])
+def test_fused_frame_count_equals_count_kernel(gpu, stage, B, S, scale, monkeypatch):
+    """The frame count run by the duration kernel's last workgroup (durations
+    handed over with write-through stores and a ticket; M2_DUR_COUNT=1 forces
+    it up to B*S = 8192, the default fuses up to 2048) leaves the front buffer - durations, prefix sums,
+    totals - and the T_max word bit for bit as the separate count kernel
+    (M2_DUR_COUNT=0) does, over repeated calls (the ticket is reset by the
+    last workgroup) and ragged lengths (tts_model.py:146-166)."""
+    m = build_model(stage, gpu)
+    hm = m._hip(gpu)
+    g = torch.Generator().manual_seed(B * 1000 + S)
+    ids = torch.randint(0, 42, (B, S), generator=g).to(gpu)
+    lens = torch.randint(1, S + 1, (B,), generator=g).to(gpu)
+    res = {}
+    for mode in ("0", "1", "1", "0", "1"):
+        monkeypatch.setenv("M2_DUR_COUNT", mode)
+        tword = torch.full((1,), -7, dtype=torch.int32, device=gpu)
+        state = hm.inference_front_dev(ids, lens, scale, tword)
+        torch.cuda.synchronize(gpu)
+        got = (state[2].clone(), int(tword.item()))
+        if mode in res:
+            assert torch.equal(got[0], res[mode][0]) and got[1] == res[mode][1]
+        res[mode] = got
+    assert torch.equal(res["0"][0], res["1"][0])
+    assert res["0"][1] == res["1"][1] >= 0
+    # and through the whole one-call inference (mailbox post from the fused count)
+    monkeypatch.setenv("M2_DUR_COUNT", "0")
+    mel0, audio0 = m.inference(ids, lens, duration_scale=scale)
+    monkeypatch.setenv("M2_DUR_COUNT", "1")
+    for _ in range(2):
+        mel1, audio1 = m.inference(ids, lens, duration_scale=scale)
+        assert torch.equal(mel0, mel1) and torch.equal(audio0, audio1)
