@@ -869,6 +869,256 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
                       acc[t][2] * inv, acc[t][3] * inv);
 }
 
+// The same 64-row tile with each wave on TWO 16-query blocks and ONE 32-key
+// chunk of every 64-key step: wave w = (head w / 4, query pair (w / 2) % 2,
+// chunk w % 2).  Every K / V^T fragment a wave reads from LDS then feeds the
+// MFMAs of both query blocks, so the workgroup reads half the LDS bytes per
+// step of attention_qsplit (8 waves x one chunk instead of 8 waves x both
+// chunks of its head); the MFMA count is the same.  Each wave keeps an online
+// softmax per query block over its chunks; the two chunk waves of a (head,
+// query pair) merge through LDS at the end (each finalises one block).  A
+// chunk wholly past N is skipped (wave-uniform), so a wave may see no key:
+// its record then carries m = -inf and weight 0.
+template <int H, int HD, bool MASKED>
+__device__ __forceinline__ void attention_qsplit2(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
+                                                  const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
+                                                  int len, float sl2, unsigned char* A, unsigned char* ring) {
+    using G = Geo<HD>;
+    using Q = QsGeo<HD>;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
+    constexpr int PPT = Q::PPT, RW = 2 + 4 * MT;  // merge record floats per lane
+    static_assert(NW * RW * 64 * 4 <= 2 * SB, "merge records fit the ring");
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, g = lane >> 4;
+    const int h = wave >> 2, qp = (wave >> 1) & 1, j = wave & 1;
+    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
+
+    // B = Q^T fragments of this wave's two 16-query blocks 2 qp, 2 qp + 1
+    u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+        const unsigned char* qp8 =
+            qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + 2 * qp + qq) * QKBLK + 16 * lane;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            qh[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks);
+            ql[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024);
+        }
+        if constexpr (KT) {
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            qxh[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
+            qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
+        }
+    }
+    // the staging of a 64-key step into LDS: as attention_qsplit
+    const unsigned char* src[PPT];
+    int step[PPT];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int o = 16 * (tid + NW * 64 * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
+        const size_t bh = (size_t)b * HEADS + hh;
+        if (r < Q::KB) {
+            src[i] = kb + (bh * (npad / 16) + 2 * jj) * QKBLK + r;
+            step[i] = 4 * QKBLK;
+        } else {
+            src[i] = vb + (bh * nch + jj) * G::VCH + (r - Q::KB);
+            step[i] = 2 * G::VCH;
+        }
+    }
+    u32x4 pre[PPT];
+    auto gload = [&](int p) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * step[i]);
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
+    };
+
+    f32x4 acc[2][MT];
+    float m[2], lsum[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        m[qq] = MASKED ? -INFINITY : 0.f;
+        lsum[qq] = 0.f;
+    }
+    bool fresh = true;  // no chunk processed yet (wave-uniform)
+
+    // keys 64 p + 32 j + 16 u + 4 g + r of query li of block qq
+    auto process = [&](const unsigned char* sb, int p) {
+        float s[2][2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
+            f32x4 st[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
+                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kh, qh[qq][ks], st[qq]);
+                    st[qq] = mfma(kh, ql[qq][ks], st[qq]);
+                    st[qq] = mfma(kl, qh[qq][ks], st[qq]);
+                }
+            }
+            if constexpr (KT) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
+                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
+                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kxh, qxh[qq], st[qq]);
+                    st[qq] = mfma(kxh, qxl[qq], st[qq]);
+                    st[qq] = mfma(kxl, qxh[qq], st[qq]);
+                }
+            }
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
+        }
+        const int k0 = p * 2 * KC + j * KC;
+        if constexpr (MASKED) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = k0 + 16 * u + 4 * g + r;
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq)
+                        s[qq][u][r] = key < len ? s[qq][u][r] * sl2 : (key < N ? kMaskFill * kLog2e : -INFINITY);
+                }
+        } else if (N - k0 < KC) {  // the chunk straddles N: keys past N score -inf (wave-uniform)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq)
+                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
+        }
+        float cmax[2];
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq)
+            cmax[qq] = fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
+                             fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+        if constexpr (MASKED) {
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float mn = vmax(m[qq], grp4_max(cmax[qq]));  // finite: the chunk holds a key < N
+                const float corr = __builtin_amdgcn_exp2f(m[qq] - mn);  // m = -inf on the first chunk -> 0
+                lsum[qq] *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+                m[qq] = mn;
+            }
+        } else {
+            // lazy base (attention_split_kernel): moved only on the first chunk or
+            // when a score exceeds it by more than 2^kLazyT (wave-uniform)
+            bool up = fresh;
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) up = up || cmax[qq] - m[qq] > kLazyT;
+            if (__builtin_amdgcn_ballot_w64(up) != 0) {
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    const float cm = grp4_max(cmax[qq]);  // finite: the chunk holds a key < N
+                    const float mn = fresh ? cm : vmax(cm, m[qq]);
+                    if (!fresh) {
+                        const float corr = __builtin_amdgcn_exp2f(m[qq] - mn);
+                        lsum[qq] *= corr;
+#pragma unroll
+                        for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+                    }
+                    m[qq] = mn;
+                }
+            }
+        }
+        fresh = false;
+        u32x4 bh4[2], bl4[2];
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    s[qq][u][r] = __builtin_amdgcn_exp2f(s[qq][u][r] - m[qq]);
+                    lsum[qq] += s[qq][u][r];
+                }
+            // B = P^T: lane (query li) holds keys 4g + e (u = 0) and 16 + 4g + e (u = 1)
+            unsigned ph[4], pl[4];
+            split2u(s[qq][0][0], s[qq][0][1], ph[0], pl[0]);
+            split2u(s[qq][0][2], s[qq][0][3], ph[1], pl[1]);
+            split2u(s[qq][1][0], s[qq][1][1], ph[2], pl[2]);
+            split2u(s[qq][1][2], s[qq][1][3], ph[3], pl[3]);
+            bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+            bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+        }
+        const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+            const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
+            }
+        }
+    };
+
+    gload(0);
+    lstore(0);
+    if (1 < nsc) gload(1);
+    lds_barrier();
+#pragma unroll 1
+    for (int p = 0; p < nsc; ++p) {
+        // step p from buffer p & 1; p + 1 goes to the other buffer, p + 2 is requested
+        if (p + 1 < nsc) lstore((p + 1) & 1);
+        if (p + 2 < nsc) gload(p + 2);
+        if (2 * KC * p + KC * j < N) process(ring + (p & 1) * SB, p);  // wave-uniform
+        lds_barrier();
+    }
+    TSTAMP(1);
+    if (fresh) {  // this wave saw no key
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) m[qq] = -INFINITY;
+    }
+    // merge the two chunk waves of (h, qp): wave j finalises block 2 qp + j and
+    // hands its state of the other block to its partner (wave ^ 1)
+    float* rec = reinterpret_cast<float*>(ring);
+    {
+        const int qo = 1 - j;
+        float* w = rec + (size_t)wave * RW * 64 + lane;
+        w[0] = m[qo];
+        w[64] = lsum[qo];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qo][t][r];
+    }
+    __syncthreads();
+    const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
+    const float mo = o[0], mm = j ? m[1] : m[0];
+    const float mx = vmax(mm, mo);  // finite: chunk 0 of step 0 holds key 0 < N
+    const float fm = __builtin_amdgcn_exp2f(mm - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
+    float ls = (j ? lsum[1] : lsum[0]) * fm + o[64] * fo;
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    const float inv = 1.0f / ls;
+    const int qblk = 2 * qp + j;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        const f32x4 a = j ? acc[1][t] : acc[0][t];
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (a[r] * fm + o[(2 + 4 * t + r) * 64] * fo) * inv;
+        put_split4<H>(A + (16 * qblk + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2], v[3]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 struct LArgs {
     int B, N, npad, ntile;
@@ -889,7 +1139,7 @@ struct LArgs {
 // RB = 1 (16-row tiles) while the grid fits one round of the CUs, else 2
 // (32-row tiles: every K / V and weight fragment a workgroup reads serves
 // twice the rows).
-template <int H, bool MASKED, int NEXT, int NN, int RB>
+template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
     constexpr bool QS = RB == 4;  // 64-row tiles: attention_qsplit
@@ -936,7 +1186,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
     if constexpr (QS) {
-        attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        else attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         if (wave < H / 16) so.load(a.Wo, wave);
         __syncthreads();
         TSTAMP(2);
@@ -1212,6 +1463,12 @@ int tfl_rb(int B, int N) {
     const long tiles16 = (long)B * (tfl_npad(N) / tfl::TQ);
     return tiles16 >= 4 * 256 ? 4 : (tiles16 > 256 ? 2 : 1);
 }
+// 64-row tiles: two query blocks per wave (attention_qsplit2) unless
+// M2_TFL_QS2=0 (read per call: A/B and tests switch it)
+bool tfl_qs2() {
+    const char* e = std::getenv("M2_TFL_QS2");
+    return !(e && *e && std::atoi(e) == 0);
+}
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
 float tfl_sl2(int H) {
     const float scale = (float)(1.0 / std::sqrt((double)(H / tfl::HEADS)));  // components.py:52, fp32 at the mul
@@ -1321,9 +1578,11 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nv = out.v;
     a.z = z;
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
+    const bool qs2 = tfl_qs2();
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
+        else if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
         else if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2>), grid, blk, 0, st, a);  \
         else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 1>), grid, blk, 0, st, a);          \
         M2_LAUNCHED("tfl layer_kernel");                                                        \
