@@ -879,6 +879,11 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
 // query pair) merge through LDS at the end (each finalises one block).  A
 // chunk wholly past N is skipped (wave-uniform), so a wave may see no key:
 // its record then carries m = -inf and weight 0.
+template <int V>
+struct CI {
+    static constexpr int value = V;
+};
+
 template <int H, int HD, bool MASKED>
 __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
                                                   const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
@@ -1087,10 +1092,12 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
         for (int qq = 0; qq < 2; ++qq) m[qq] = -INFINITY;
     }
     // merge the two chunk waves of (h, qp): wave j finalises block 2 qp + j and
-    // hands its state of the other block to its partner (wave ^ 1)
+    // hands its state of the other block to its partner (wave ^ 1).  The block
+    // index is a compile-time constant in each branch (a runtime index into
+    // the register arrays would move them to scratch or LDS).
     float* rec = reinterpret_cast<float*>(ring);
-    {
-        const int qo = 1 - j;
+    auto put = [&](auto J) {
+        constexpr int qo = 1 - decltype(J)::value;
         float* w = rec + (size_t)wave * RW * 64 + lane;
         w[0] = m[qo];
         w[64] = lsum[qo];
@@ -1098,25 +1105,31 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
         for (int t = 0; t < MT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qo][t][r];
-    }
+    };
+    auto fin = [&](auto J) {
+        constexpr int qq = decltype(J)::value;
+        const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
+        const float mo = o[0];
+        const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
+        const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
+        float ls = lsum[qq] * fm + o[64] * fo;
+        ls += __shfl_xor(ls, 16);
+        ls += __shfl_xor(ls, 32);
+        const float inv = 1.0f / ls;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (acc[qq][t][r] * fm + o[(2 + 4 * t + r) * 64] * fo) * inv;
+            put_split4<H>(A + (16 * (2 * qp + qq) + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2],
+                          v[3]);
+        }
+    };
+    if (j) put(CI<1>{});
+    else put(CI<0>{});
     __syncthreads();
-    const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
-    const float mo = o[0], mm = j ? m[1] : m[0];
-    const float mx = vmax(mm, mo);  // finite: chunk 0 of step 0 holds key 0 < N
-    const float fm = __builtin_amdgcn_exp2f(mm - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
-    float ls = (j ? lsum[1] : lsum[0]) * fm + o[64] * fo;
-    ls += __shfl_xor(ls, 16);
-    ls += __shfl_xor(ls, 32);
-    const float inv = 1.0f / ls;
-    const int qblk = 2 * qp + j;
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-        const f32x4 a = j ? acc[1][t] : acc[0][t];
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (a[r] * fm + o[(2 + 4 * t + r) * 64] * fo) * inv;
-        put_split4<H>(A + (16 * qblk + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2], v[3]);
-    }
+    if (j) fin(CI<1>{});
+    else fin(CI<0>{});
 }
 
 // ---------------------------------------------------------------------------
@@ -1463,11 +1476,16 @@ int tfl_rb(int B, int N) {
     const long tiles16 = (long)B * (tfl_npad(N) / tfl::TQ);
     return tiles16 >= 4 * 256 ? 4 : (tiles16 > 256 ? 2 : 1);
 }
-// 64-row tiles: two query blocks per wave (attention_qsplit2) unless
-// M2_TFL_QS2=0 (read per call: A/B and tests switch it)
-bool tfl_qs2() {
+// 64-row tiles: two query blocks per wave (attention_qsplit2) at head_dim 48
+// (stage2: B=128 T=2600 decoder layer 1614 -> 1547 us per launch, step
+// -0.7 %; at stage2 B=64 T=500 level), the one-block form at head_dim 32
+// (stage1 B=32 pipeline +0.6 % with two blocks, in-process A/Bs,
+// profiles/r03/r03ab_*, r03ad_ab.txt).  M2_TFL_QS2=0|1 forces either (read per
+// call: A/B and tests switch it).
+bool tfl_qs2(int H) {
     const char* e = std::getenv("M2_TFL_QS2");
-    return !(e && *e && std::atoi(e) == 0);
+    if (e && *e) return std::atoi(e) != 0;
+    return H / tfl::HEADS >= 48;
 }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
 float tfl_sl2(int H) {
@@ -1578,7 +1596,7 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nv = out.v;
     a.z = z;
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
-    const bool qs2 = tfl_qs2();
+    const bool qs2 = tfl_qs2(H);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
         if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
