@@ -11,6 +11,7 @@
 // phoneme; here it is one scan kernel and one gather kernel, and the only
 // host round trip left is the caller's read of T_max to size the output.
 #include <algorithm>
+#include <cstdlib>
 
 #include "m2_common.h"
 
@@ -80,7 +81,7 @@ __device__ __forceinline__ void dur_wload(const float4* __restrict__ Wp, DurW<H>
     }
 }
 
-template <int H>
+template <int H, int RBK>
 __device__ __forceinline__ void dur_conv_mfma(const float* in, const DurW<H>& W, const float* __restrict__ b,
                                               const float* __restrict__ a, const float* __restrict__ c, float* out,
                                               int pos0, int S) {
@@ -88,28 +89,36 @@ __device__ __forceinline__ void dur_conv_mfma(const float* in, const DurW<H>& W,
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
     if (wave < H / 16) {
         const int nb = wave;
-        dur_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        // RBK 16-position row blocks share every weight fragment (independent
+        // accumulation chains)
+        dur_f32x4 acc[RBK];
+#pragma unroll
+        for (int rb = 0; rb < RBK; ++rb) acc[rb] = dur_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int tap = 0; tap < 3; ++tap) {
-            const float* x0 = in + (i + tap) * XS + g;
 #pragma unroll
             for (int s4 = 0; s4 < H / 16; ++s4) {
                 const float4 w = W.w[tap * (H / 16) + s4];
                 const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[(4 * s4 + q) * 4], wv[q], acc, 0, 0, 0);
+#pragma unroll
+                    for (int rb = 0; rb < RBK; ++rb)
+                        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            in[(16 * rb + i + tap) * XS + g + (4 * s4 + q) * 4], wv[q], acc[rb], 0, 0, 0);
             }
         }
         const int co = nb * 16 + i;
         const float bb = b[co], aa = a[co], cc = c[co];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 4 * g + r, s = pos0 + row;
-            float v = (acc[r] + bb) * aa + cc;
-            v = v > 0.f ? v : 0.f;
-            out[row * XS + co] = (s >= 0 && s < S) ? v : 0.f;
-        }
+        for (int rb = 0; rb < RBK; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * rb + 4 * g + r, s = pos0 + row;
+                float v = (acc[rb][r] + bb) * aa + cc;
+                v = v > 0.f ? v : 0.f;
+                out[row * XS + co] = (s >= 0 && s < S) ? v : 0.f;
+            }
     }
 }
 
@@ -183,7 +192,7 @@ __device__ void count_frames(const float* __restrict__ dur, int B, int S, const 
 // (one wave per row, the halo rows redundantly) and stores its own 14
 // normalised rows to enc_out - the encoder output the length regulator
 // expands - in place of a separate layer_norm_kernel launch.
-template <int H, bool LN, bool COUNT>
+template <int H, bool LN, bool COUNT, int RBK>
 __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ enc, int S, const float4* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ a1, const float* __restrict__ c1, const float4* __restrict__ w2,
@@ -191,10 +200,11 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ pw, const float* __restrict__ pb, float* __restrict__ dur,
     const float* __restrict__ lng, const float* __restrict__ lnb, float* __restrict__ enc_out, DurCount dc) {
     constexpr int XS = H + 2, NT = 64 * DUR_WAVES;
-    __shared__ float X[18 * XS];   // positions s0-2 .. s0+15
-    __shared__ float Y1[18 * XS];  // s0-1 .. s0+14 (+2 zero rows read by conv2's unused rows)
-    __shared__ float Y2[16 * XS];  // s0 .. s0+13 (+2 unused)
-    const int b = blockIdx.y, s0 = blockIdx.x * DUR_TS, tid = threadIdx.x;
+    constexpr int TS = 16 * RBK - 2, NX = TS + 4;  // phonemes per tile, input rows with the halo
+    __shared__ float X[NX * XS];        // positions s0-2 .. s0+TS+1
+    __shared__ float Y1[NX * XS];       // s0-1 .. s0+TS (+2 zero rows read by conv2's unused rows)
+    __shared__ float Y2[16 * RBK * XS];  // s0 .. s0+TS-1 (+2 unused)
+    const int b = blockIdx.y, s0 = blockIdx.x * TS, tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const float* e = enc + (size_t)b * S * H;
     DurW<H> W1, W2;
@@ -203,7 +213,7 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     if constexpr (LN) {
         // every row of this wave is loaded before the first is normalised (one
         // memory round trip per wave instead of one per row)
-        constexpr int NR = (18 + DUR_WAVES - 1) / DUR_WAVES, KP = (H + 63) / 64;
+        constexpr int NR = (NX + DUR_WAVES - 1) / DUR_WAVES, KP = (H + 63) / 64;
         float xv[NR][KP];
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
@@ -215,12 +225,12 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
             const int p = wave + j * DUR_WAVES, s = s0 - 2 + p;
-            if (p >= 18) break;
+            if (p >= NX) break;
             float* d = X + p * XS;
             if (s >= 0 && s < S) {
                 float mean, rstd;
                 ln_row_stats_regs<KP>(xv[j], H, lane, mean, rstd);
-                float* yo = (p >= 2 && p < 2 + DUR_TS) ? enc_out + ((size_t)b * S + s) * H : nullptr;
+                float* yo = (p >= 2 && p < 2 + TS) ? enc_out + ((size_t)b * S + s) * H : nullptr;
 #pragma unroll
                 for (int q = 0; q < KP; ++q) {
                     const int k = lane + 64 * q;
@@ -235,7 +245,7 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
             }
         }
     } else {
-        for (int idx = tid; idx < 18 * (H / 4); idx += NT) {
+        for (int idx = tid; idx < NX * (H / 4); idx += NT) {
             const int p = idx / (H / 4), c4 = (idx - p * (H / 4)) * 4, s = s0 - 2 + p;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (s >= 0 && s < S) v = *reinterpret_cast<const float4*>(e + (size_t)s * H + c4);
@@ -243,14 +253,14 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
     }
-    for (int idx = tid; idx < 2 * XS; idx += NT) Y1[16 * XS + idx] = 0.f;
+    for (int idx = tid; idx < 2 * XS; idx += NT) Y1[16 * RBK * XS + idx] = 0.f;
     __syncthreads();
-    dur_conv_mfma<H>(X, W1, b1, a1, c1, Y1, s0 - 1, S);
+    dur_conv_mfma<H, RBK>(X, W1, b1, a1, c1, Y1, s0 - 1, S);
     __syncthreads();
-    dur_conv_mfma<H>(Y1, W2, b2, a2, c2, Y2, s0, S);
+    dur_conv_mfma<H, RBK>(Y1, W2, b2, a2, c2, Y2, s0, S);
     __syncthreads();
     // k=1 projection H -> 1: one wave per phoneme, shuffle reduction.
-    for (int p = wave; p < DUR_TS; p += DUR_WAVES) {
+    for (int p = wave; p < TS; p += DUR_WAVES) {
         const int s = s0 + p;
         float acc = 0.f;
         for (int ci = lane; ci < H; ci += 64) acc = fmaf(pw[ci], Y2[p * XS + ci], acc);
@@ -418,19 +428,31 @@ namespace {
 int32_t duration_launch(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st,
                         const float* ln_g, const float* ln_b, float* enc_out, const DurCount* dc) {
     if (B == 0 || S == 0) return M2_OK;
-    const dim3 grid(cdiv(S, DUR_TS), B), blk(64 * DUR_WAVES);
+    // 14-phoneme tiles (one 16-position row block per wave) while they fit one
+    // round of the CUs; beyond, 30-phoneme tiles (two row blocks sharing each
+    // weight fragment): half the workgroups, each streaming the same weights.
+    // M2_DUR_RB=1|2 forces one (read per call: A/B and tests).
+    int rbk = (long)B * cdiv(S, DUR_TS) > 256 ? 2 : 1;
+    if (const char* e = std::getenv("M2_DUR_RB")) {
+        const int v = std::atoi(e);
+        if (v == 1 || v == 2) rbk = v;
+    }
+    const dim3 grid(cdiv(S, 16 * rbk - 2), B), blk(64 * DUR_WAVES);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
     const DurCount none{};
-#define M2_DUR_L(HH, LL, CC)                                                                                       \
-    hipLaunchKernelGGL((duration_kernel<HH, LL, CC>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], p[3],         \
+#define M2_DUR_L(HH, LL, CC, RR)                                                                                   \
+    hipLaunchKernelGGL((duration_kernel<HH, LL, CC, RR>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], p[3],     \
                        f4(p[4]), p[5], p[6], p[7], p[8], p[9], dur, LL ? ln_g : nullptr, LL ? ln_b : nullptr,        \
                        LL ? enc_out : nullptr, dc ? *dc : none)
+#define M2_DUR_R(HH, LL, CC)                      \
+    if (rbk == 2) M2_DUR_L(HH, LL, CC, 2);        \
+    else M2_DUR_L(HH, LL, CC, 1)
 #define M2_DUR(HH)                                            \
     case HH:                                                  \
-        if (enc_out && dc) M2_DUR_L(HH, true, true);          \
-        else if (enc_out) M2_DUR_L(HH, true, false);          \
-        else if (dc) M2_DUR_L(HH, false, true);               \
-        else M2_DUR_L(HH, false, false);                      \
+        if (enc_out && dc) M2_DUR_R(HH, true, true);          \
+        else if (enc_out) M2_DUR_R(HH, true, false);          \
+        else if (dc) M2_DUR_R(HH, false, true);               \
+        else M2_DUR_R(HH, false, false);                      \
         break;
     switch (H) {
         M2_DUR(32)
@@ -439,6 +461,7 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
         M2_DUR(128)
         default: return fail(M2_E_SHAPE, "duration: hidden_dim must be 32, 64, 96 or 128");
     }
+#undef M2_DUR_R
 #undef M2_DUR
 #undef M2_DUR_L
     M2_LAUNCHED("duration_kernel");

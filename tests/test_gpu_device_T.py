@@ -246,3 +246,28 @@ def test_fused_frame_count_equals_count_kernel(gpu, stage, B, S, scale, monkeypa
     for _ in range(2):
         mel1, audio1 = m.inference(ids, lens, duration_scale=scale)
         assert torch.equal(mel0, mel1) and torch.equal(audio0, audio1)
+
+
+@pytest.mark.parametrize("stage,B,S", [("s2", 64, 100), ("s1", 3, 1), ("s1", 9, 31), ("s2", 5, 61), ("s1", 40, 45)])
+def test_duration_two_row_block_tiles_bit_identical(gpu, stage, B, S, monkeypatch):
+    """30-phoneme duration tiles (two 16-position row blocks per wave sharing
+    each weight fragment; the default once 14-phoneme tiles exceed 256
+    workgroups) give the 14-phoneme tiles' durations, encoder output and
+    inference results bit for bit (the same MFMA chain per output), and both
+    match the oracle (tts_model.py:99-117)."""
+    m = build_model(stage, gpu)
+    g = torch.Generator().manual_seed(B * 100 + S)
+    ids = torch.randint(0, 42, (B, S), generator=g)
+    lens = torch.randint(1, S + 1, (B,), generator=g)
+    out = {}
+    for rb in ("1", "2"):
+        monkeypatch.setenv("M2_DUR_RB", rb)
+        with torch.no_grad():
+            d = m(ids.to(gpu), lens.to(gpu))["duration_pred"]
+        out[rb] = (d.clone(),) + tuple(t.clone() for t in m.inference(ids.to(gpu), lens.to(gpu)))
+    for a, b in zip(out["1"], out["2"]):
+        assert a.shape == b.shape and torch.equal(a, b)
+    sd = golden_state(stage)
+    enc, _ = orc.text_encoder(sd, stage_config(stage), ids, lens)
+    ref = orc.duration_predictor(sd, enc)
+    assert maxabs(out["2"][0], ref) <= 1e-4  # test_gpu_parity.py ENC_TOL
