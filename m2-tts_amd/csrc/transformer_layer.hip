@@ -1506,8 +1506,15 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.npad = tfl_npad(N);
     // rows per workgroup: the layers' choice up to 32 (64-row tiles made this
     // launch 23 % faster but the step 1.4 % slower at stage2 B=64, in-process
-    // A/B, profiles/r03/ab/r03x_ab.txt)
-    const int rb = tfl_rb(B, N) > 1 ? 2 : 1;
+    // A/B, profiles/r03/ab/r03x_ab.txt), 64 for grids of >= 16 rounds of
+    // 16-row tiles (the long-form decoder: a series of latency-bound rounds);
+    // M2_TFL_FIRST_RB=1|2|4 forces one (read per call: A/B and tests)
+    int rb = tfl_rb(B, N) > 1 ? 2 : 1;
+    if ((long)B * (tfl_npad(N) / tfl::TQ) >= 16L * 256) rb = 4;
+    if (const char* e = std::getenv("M2_TFL_FIRST_RB")) {
+        const int v = std::atoi(e);
+        if (v == 1 || v == 2 || v == 4) rb = v;
+    }
     a.ntile = a.npad / (tfl::TQ * rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
@@ -1536,7 +1543,8 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
 #define M2_TFF(HH, SS, MM)                                                                      \
     if (H == HH && f.src == SS && masked == MM) {                                               \
-        if (rb == 2) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 2>), grid, blk, 0, st, a);  \
+        if (rb == 4) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 4>), grid, blk, 0, st, a);  \
+        else if (rb == 2) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 2>), grid, blk, 0, st, a);  \
         else hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 1>), grid, blk, 0, st, a);          \
         M2_LAUNCHED("tfl first_kernel");                                                        \
         return M2_OK;                                                                           \

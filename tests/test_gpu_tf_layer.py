@@ -28,14 +28,17 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
-@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2"])
+@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "f4"])
 def rows_per_tile(request, monkeypatch):
     """16- and 32-row workgroup tiles with key-quarter attention, 64-row tiles
     with query-split attention (K / V staged in LDS) (M2_TFL_RB) - the
     per-head-dim default, one query block and both chunks of each 64-key step
     ("4q1", M2_TFL_QS2=0) or two query blocks and one chunk ("4q2") - and the
-    per-call choice."""
-    if request.param != "auto":
+    per-call choice; "f4": 64-row tiles for the first (LN1 -> QKV) launch
+    (M2_TFL_FIRST_RB, the default for very large grids)."""
+    if request.param == "f4":
+        monkeypatch.setenv("M2_TFL_FIRST_RB", "4")
+    elif request.param != "auto":
         monkeypatch.setenv("M2_TFL_RB", request.param[0])
     if request.param in ("4q1", "4q2"):
         monkeypatch.setenv("M2_TFL_QS2", request.param[-1:] if request.param == "4q2" else "0")
