@@ -884,7 +884,12 @@ struct CI {
     static constexpr int value = V;
 };
 
-template <int H, int HD, bool MASKED>
+// LEAN (M2_TFL_QS2=3): the softmax with fewer VALU instructions per step -
+// unmasked, the QK^T MFMAs start from C = -m (scores arrive relative to the
+// lazy base: no subtraction before exp2), and the row sums come from two more
+// MFMAs on a constant all-ones A fragment (P_hi + P_lo summed by the matrix
+// core, already complete over the chunk's keys) instead of 16 adds per step.
+template <int H, int HD, bool MASKED, bool LEAN = false>
 __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
                                                   const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
                                                   int len, float sl2, unsigned char* A, unsigned char* ring) {
@@ -940,7 +945,7 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
         for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
     };
 
-    f32x4 acc[2][MT];
+    f32x4 acc[2][MT], lacc[2];
     float m[2], lsum[2];
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
@@ -948,7 +953,9 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
         for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         m[qq] = MASKED ? -INFINITY : 0.f;
         lsum[qq] = 0.f;
+        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
     bool fresh = true;  // no chunk processed yet (wave-uniform)
 
     // keys 64 p + 32 j + 16 u + 4 g + r of query li of block qq
@@ -958,6 +965,10 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
         for (int u = 0; u < 2; ++u) {
             const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
             f32x4 st[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            if constexpr (LEAN && !MASKED)
+                if (!fresh)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq) st[qq] = f32x4{-m[qq], -m[qq], -m[qq], -m[qq]};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
@@ -1015,9 +1026,34 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
                 const float mn = vmax(m[qq], grp4_max(cmax[qq]));  // finite: the chunk holds a key < N
                 const float corr = __builtin_amdgcn_exp2f(m[qq] - mn);  // m = -inf on the first chunk -> 0
                 lsum[qq] *= corr;
+                if constexpr (LEAN) lacc[qq] *= corr;
 #pragma unroll
                 for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
                 m[qq] = mn;
+            }
+        } else if constexpr (LEAN) {
+            // scores relative to the base already: move it (and them) only on
+            // the first chunk or when one exceeds it by more than 2^kLazyT
+            bool up = fresh;
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) up = up || cmax[qq] > kLazyT;
+            if (__builtin_amdgcn_ballot_w64(up) != 0) {
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    const float cm = grp4_max(cmax[qq]);  // finite: the chunk holds a key < N
+                    const float d = fresh ? cm : vmax(cm, 0.f);
+                    m[qq] += d;
+                    if (!fresh) {
+                        const float corr = __builtin_amdgcn_exp2f(-d);
+                        lacc[qq] *= corr;
+#pragma unroll
+                        for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
+                }
             }
         } else {
             // lazy base (attention_split_kernel): moved only on the first chunk or
@@ -1048,8 +1084,12 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    s[qq][u][r] = __builtin_amdgcn_exp2f(s[qq][u][r] - m[qq]);
-                    lsum[qq] += s[qq][u][r];
+                    if constexpr (LEAN && !MASKED) {
+                        s[qq][u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+                    } else {
+                        s[qq][u][r] = __builtin_amdgcn_exp2f(s[qq][u][r] - m[qq]);
+                        if constexpr (!LEAN) lsum[qq] += s[qq][u][r];
+                    }
                 }
             // B = P^T: lane (query li) holds keys 4g + e (u = 0) and 16 + 4g + e (u = 1)
             unsigned ph[4], pl[4];
@@ -1060,6 +1100,12 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
             bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
             bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
         }
+        if constexpr (LEAN)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
+                lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
+            }
         const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -1100,7 +1146,7 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
         constexpr int qo = 1 - decltype(J)::value;
         float* w = rec + (size_t)wave * RW * 64 + lane;
         w[0] = m[qo];
-        w[64] = lsum[qo];
+        w[64] = LEAN ? lacc[qo][0] : lsum[qo];
 #pragma unroll
         for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -1112,9 +1158,11 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
         const float mo = o[0];
         const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
         const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
-        float ls = lsum[qq] * fm + o[64] * fo;
-        ls += __shfl_xor(ls, 16);
-        ls += __shfl_xor(ls, 32);
+        float ls = (LEAN ? lacc[qq][0] : lsum[qq]) * fm + o[64] * fo;
+        if constexpr (!LEAN) {  // lane-partial sums (keys 4g + r): add the four groups
+            ls += __shfl_xor(ls, 16);
+            ls += __shfl_xor(ls, 32);
+        }
         const float inv = 1.0f / ls;
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -1199,7 +1247,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
     if constexpr (QS) {
-        if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         if (wave < H / 16) so.load(a.Wo, wave);
         __syncthreads();
@@ -1476,16 +1525,21 @@ int tfl_rb(int B, int N) {
     const long tiles16 = (long)B * (tfl_npad(N) / tfl::TQ);
     return tiles16 >= 4 * 256 ? 4 : (tiles16 > 256 ? 2 : 1);
 }
-// 64-row tiles: two query blocks per wave (attention_qsplit2) at head_dim 48
-// (stage2: B=128 T=2600 decoder layer 1614 -> 1547 us per launch, step
-// -0.7 %; at stage2 B=64 T=500 level), the one-block form at head_dim 32
-// (stage1 B=32 pipeline +0.6 % with two blocks, in-process A/Bs,
-// profiles/r03/r03ab_*, r03ad_ab.txt).  M2_TFL_QS2=0|1 forces either (read per
-// call: A/B and tests switch it).
-bool tfl_qs2(int H) {
+// 64-row tiles: two query blocks per wave with the lean softmax
+// (attention_qsplit2<..., LEAN>) at head_dim 48 (stage2: B=128 T=2600 step
+// -1.5 %, B=16 T=2600 -1.9 %, B=64 T=500 -0.8 % against the plain two-block
+// form, which was itself -0.7 % at B=128 T=2600 against one block), the
+// one-block form at head_dim 32 (stage1 B=32: two blocks +0.6 %, lean +0.3 %;
+// in-process A/Bs, profiles/r03/r03ab_*, r03ad_ab.txt, r03aj_ab.txt).
+// M2_TFL_QS2=0|1|3 forces one block / two / two lean (read per call: A/B and
+// tests switch it).
+int tfl_qs2(int H) {
     const char* e = std::getenv("M2_TFL_QS2");
-    if (e && *e) return std::atoi(e) != 0;
-    return H / tfl::HEADS >= 48;
+    if (e && *e) {
+        const int v = std::atoi(e);
+        return v == 3 ? 3 : (v != 0 ? 2 : 0);
+    }
+    return H / tfl::HEADS >= 48 ? 3 : 0;
 }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
 float tfl_sl2(int H) {
@@ -1604,10 +1658,11 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nv = out.v;
     a.z = z;
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
-    const bool qs2 = tfl_qs2(H);
+    const int qs2 = tfl_qs2(H);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
         else if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
         else if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2>), grid, blk, 0, st, a);  \
         else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 1>), grid, blk, 0, st, a);          \

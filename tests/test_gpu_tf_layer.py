@@ -28,7 +28,7 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
-@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "f4"])
+@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "4q3", "f4"])
 def rows_per_tile(request, monkeypatch):
     """16- and 32-row workgroup tiles with key-quarter attention, 64-row tiles
     with query-split attention (K / V staged in LDS) (M2_TFL_RB) - the
@@ -40,8 +40,8 @@ def rows_per_tile(request, monkeypatch):
         monkeypatch.setenv("M2_TFL_FIRST_RB", "4")
     elif request.param != "auto":
         monkeypatch.setenv("M2_TFL_RB", request.param[0])
-    if request.param in ("4q1", "4q2"):
-        monkeypatch.setenv("M2_TFL_QS2", request.param[-1:] if request.param == "4q2" else "0")
+    if request.param in ("4q1", "4q2", "4q3"):  # "4q3": two blocks, lean softmax (C = -m, MFMA row sums)
+        monkeypatch.setenv("M2_TFL_QS2", "0" if request.param == "4q1" else request.param[-1:])
     return request.param
 
 
