@@ -676,7 +676,9 @@ struct QsGeo {
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int H, int HD, bool MASKED>
+// LEAN (M2_TFL_QS2=4): the lean softmax of attention_qsplit2 (C = -m
+// accumulators when unmasked, row sums by MFMA on an all-ones fragment).
+template <int H, int HD, bool MASKED, bool LEAN = false>
 __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
                                                  const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
                                                  int len, float sl2, unsigned char* A, unsigned char* ring) {
@@ -730,11 +732,12 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
         for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
     };
 
-    f32x4 acc[MT];
+    f32x4 acc[MT], lacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = MASKED ? -INFINITY : 0.f, lsum = 0.f;
     bool fresh = true;
+    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
 
     // keys 64 p + 32 j + 16 u + 4 g + r, j = chunk of the step, u = 16-key block
     auto process = [&](const unsigned char* sb, int p) {
@@ -744,7 +747,8 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
-                f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+                const float c0 = (LEAN && !MASKED && !fresh) ? -m : 0.f;
+                f32x4 st = f32x4{c0, c0, c0, c0};
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks) {
                     const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
@@ -794,9 +798,30 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
             const float mn = vmax(m, grp4_max(cmax));
             const float corr = __builtin_amdgcn_exp2f(m - mn);
             lsum *= corr;
+            if constexpr (LEAN) lacc *= corr;
 #pragma unroll
             for (int t = 0; t < MT; ++t) acc[t] *= corr;
             m = mn;
+        } else if constexpr (LEAN) {
+            // scores relative to the base already (attention_qsplit2's LEAN form)
+            if (__builtin_amdgcn_ballot_w64(fresh || cmax > kLazyT) != 0) {
+                const float cm = grp4_max(cmax);  // finite: the step's first chunk has a live key
+                const float d = fresh ? cm : vmax(cm, 0.f);
+                m += d;
+                if (!fresh) {
+                    const float corr = __builtin_amdgcn_exp2f(-d);
+                    lacc *= corr;
+#pragma unroll
+                    for (int t = 0; t < MT; ++t) acc[t] *= corr;
+                }
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[jj][u][r] -= d;
+            }
+            fresh = false;
         } else {
             // lazy base (attention_split_kernel): move it only on the first step or
             // when a score exceeds it by more than 2^kLazyT (wave-uniform)
@@ -820,8 +845,12 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    s[j][u][r] = __builtin_amdgcn_exp2f(s[j][u][r] - m);
-                    lsum += s[j][u][r];
+                    if constexpr (LEAN && !MASKED) {
+                        s[j][u][r] = __builtin_amdgcn_exp2f(s[j][u][r]);
+                    } else {
+                        s[j][u][r] = __builtin_amdgcn_exp2f(s[j][u][r] - m);
+                        if constexpr (!LEAN) lsum += s[j][u][r];
+                    }
                 }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -831,6 +860,10 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
             split2u(s[j][1][0], s[j][1][1], ph[2], pl[2]);
             split2u(s[j][1][2], s[j][1][3], ph[3], pl[3]);
             const u32x4 bh4 = u32x4{ph[0], ph[1], ph[2], ph[3]}, bl4 = u32x4{pl[0], pl[1], pl[2], pl[3]};
+            if constexpr (LEAN) {
+                lacc = mfma(ones, bh4, lacc);
+                lacc = mfma(ones, bl4, lacc);
+            }
             const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
@@ -860,8 +893,12 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
         lds_barrier();
     }
     TSTAMP(1);
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
+    if constexpr (LEAN) {
+        lsum = lacc[0];  // complete over the keys already
+    } else {
+        lsum += __shfl_xor(lsum, 16);
+        lsum += __shfl_xor(lsum, 32);
+    }
     const float inv = 1.0f / lsum;
 #pragma unroll
     for (int t = 0; t < MT; ++t)
@@ -1249,6 +1286,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     if constexpr (QS) {
         if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        else if constexpr (QV == 4) attention_qsplit<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         if (wave < H / 16) so.load(a.Wo, wave);
         __syncthreads();
@@ -1528,18 +1566,19 @@ int tfl_rb(int B, int N) {
 // 64-row tiles: two query blocks per wave with the lean softmax
 // (attention_qsplit2<..., LEAN>) at head_dim 48 (stage2: B=128 T=2600 step
 // -1.5 %, B=16 T=2600 -1.9 %, B=64 T=500 -0.8 % against the plain two-block
-// form, which was itself -0.7 % at B=128 T=2600 against one block), the
-// one-block form at head_dim 32 (stage1 B=32: two blocks +0.6 %, lean +0.3 %;
-// in-process A/Bs, profiles/r03/r03ab_*, r03ad_ab.txt, r03aj_ab.txt).
-// M2_TFL_QS2=0|1|3 forces one block / two / two lean (read per call: A/B and
-// tests switch it).
+// form, which was itself -0.7 % at B=128 T=2600 against one block; the lean
+// one-block form +2.2 % at B=16 T=2600), the lean one-block form below
+// (stage1 B=32: -0.7 % against the plain one-block form; two blocks +0.3 to
+// +0.6 %; in-process A/Bs, profiles/r03/r03ab_*, r03ad_ab.txt, r03aj_ab.txt,
+// r03al_ab.txt).  M2_TFL_QS2=0|1|3|4 forces one block / two / two lean / one
+// lean (read per call: A/B and tests switch it).
 int tfl_qs2(int H) {
     const char* e = std::getenv("M2_TFL_QS2");
     if (e && *e) {
         const int v = std::atoi(e);
-        return v == 3 ? 3 : (v != 0 ? 2 : 0);
+        return v == 3 || v == 4 ? v : (v != 0 ? 2 : 0);
     }
-    return H / tfl::HEADS >= 48 ? 3 : 0;
+    return H / tfl::HEADS >= 48 ? 3 : 4;
 }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
 float tfl_sl2(int H) {
@@ -1661,7 +1700,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     const int qs2 = tfl_qs2(H);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
         else if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
         else if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2>), grid, blk, 0, st, a);  \
