@@ -1286,7 +1286,10 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     if constexpr (QS) {
         if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
-        else if constexpr (QV == 4) attention_qsplit<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        // (lean one-block form for the unmasked decoder only: masked, its MFMA
+        // row sums moved the stage1 encoder's error at B=128 S=130 from under
+        // to just over the tile tests' 2e-5 bound, for no measured gain)
+        else if constexpr (QV == 4) attention_qsplit<H, HD, MASKED, !MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         if (wave < H / 16) so.load(a.Wo, wave);
         __syncthreads();
