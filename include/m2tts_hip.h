@@ -82,6 +82,13 @@ int64_t m2_weight_numel(const m2_config* cfg, int32_t index);
 int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_t n_weights,
                         void* stream, m2_model** out);
 int32_t m2_model_destroy(m2_model* model);
+
+/* Re-reads the developer switches (M2_* environment variables that force one
+ * code path for A/B comparisons and tests) into the library's switch table.
+ * The table is read when the library loads and at every m2_model_create;
+ * no entry point reads the environment per call.  Not part of the
+ * reference's surface (it has no FFI). */
+void m2_reload_switches(void);
 int32_t m2_model_config(const m2_model* model, m2_config* out);
 
 /* Scratch bytes needed by the stage calls for a batch of B utterances of S
@@ -337,8 +344,8 @@ int32_t m2_add_positional(const float* x, const float* pe, int32_t B, int32_t S,
  *   audio [B, L] fp32; frames T = m2_dsp_frames(L) = 1 + L / hop;
  *   m2_stft -> complex64 [B, T, n_fft/2 + 1]; m2_mel_spectrogram -> out_mel
  *     [B, n_mels, T] normalised dB;
- *   m2_griffin_lim: from mel [B, n_mels, T] (normalised dB; nnls_iters
- *     projected-gradient steps) or, when mag != NULL, from magnitudes
+ *   m2_griffin_lim: from mel [B, n_mels, T] (normalised dB; magnitudes as
+ *     m2_mel_to_magnitude) or, when mag != NULL, from magnitudes
  *     [B, T, n_fft/2+1] (bare griffinlim, no peak normalisation);
  *     init_angles complex64 [B, T, n_fft/2+1] unit phases (librosa's
  *     init='random' draw, made explicit); out_audio [B, hop (T - 1)]. */
@@ -350,9 +357,17 @@ int32_t m2_dsp_frames(const m2_dsp* dsp, int32_t L);
 int32_t m2_stft(const m2_dsp* dsp, const float* audio, int32_t B, int32_t L, void* out_spec, void* stream);
 int32_t m2_mel_spectrogram(const m2_dsp* dsp, const float* audio, int32_t B, int32_t L, float* out_mel,
                            void* stream);
-/* mel_to_stft alone: mel [B, n_mels, T] -> magnitudes out_mag [B, T, n_fft/2+1]. */
+/* mel_to_stft alone (librosa.feature.inverse.mel_to_stft, power 2, as
+ * audio.py:138 reaches it): mel [B, n_mels, T] -> magnitudes out_mag
+ * [B, T, n_fft/2+1] = sqrt(librosa.util.nnls(mel_basis, db_to_power)).
+ * librosa's L-BFGS-B stops at its start X0 = max(0, pinv(W) M) whenever the
+ * block's projected gradient there is <= 1e-5 (every mel in the normalised
+ * range); that test is made exactly and X0 returned; a block that would
+ * iterate gets nnls_iters projected-gradient steps per frame instead.
+ * Scratch: m2_mel_to_magnitude_workspace_bytes. */
+size_t m2_mel_to_magnitude_workspace_bytes(const m2_dsp* dsp, int32_t B, int32_t T);
 int32_t m2_mel_to_magnitude(const m2_dsp* dsp, const float* mel, int32_t B, int32_t T, int32_t nnls_iters,
-                            float* out_mag, void* stream);
+                            float* out_mag, void* workspace, size_t workspace_bytes, void* stream);
 size_t m2_griffin_lim_workspace_bytes(const m2_dsp* dsp, int32_t B, int32_t T);
 int32_t m2_griffin_lim(const m2_dsp* dsp, const float* mel, const float* mag, const void* init_angles,
                        int32_t B, int32_t T, int32_t n_iter, float momentum, int32_t nnls_iters,

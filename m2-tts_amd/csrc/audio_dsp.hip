@@ -140,17 +140,38 @@ __global__ __launch_bounds__(1024) void db_norm_kernel(float* __restrict__ mel, 
     for (int i = threadIdx.x; i < n; i += blockDim.x) x[i] = (x[i] - lo) * sc - 1.f;
 }
 
-// Griffin-Lim magnitudes of one frame: M = 10^(0.1 (x + 1) / 2) for the
-// frame's mel column, X = argmin ||W X - M||^2 s.t. X >= 0 by Nesterov
-// projected gradient (step 1/||W||^2) from X0 = max(0, pinv(W) M), S = sqrt(X).
-__global__ __launch_bounds__(NT) void mel_to_mag_kernel(const float* __restrict__ mel, int n_mels, int frames, int F,
+// Griffin-Lim magnitudes (librosa.feature.inverse.mel_to_stft, power 2):
+// X = librosa.util.nnls(W, M) for M = 10^(0.1 (x + 1) / 2), S = sqrt(X).
+// librosa solves each block of kNnlsBlockBytes / (n_mels * 4) columns with
+// scipy's L-BFGS-B (pgtol 1e-5) on (1 / block size) * 0.5 ||W X - M||^2 from
+// X0 = max(0, pinv(W) M), and L-BFGS-B's first act is its convergence test
+// at X0: the infinity norm of the projected gradient (g if g < 0, else
+// min(x, g)).  For every mel in the reference's normalised range it passes
+// (the scaled gradient at X0 is ~1e-7 or less), so librosa returns X0.  Two
+// launches reproduce that exactly:
+//   nnls_start_kernel  (one workgroup per frame): X0, the residual and the
+//     scaled gradient in double, the frame's projected-gradient maximum;
+//   nnls_finish_kernel (one per frame): the block's maximum; a converged
+//     block stores sqrt(X0) - librosa's result - and a block L-BFGS-B would
+//     iterate (mel far outside the normalised range) runs `iters` Nesterov
+//     projected-gradient steps per frame from X0 instead, which reaches an
+//     NNLS minimiser of the frame but not necessarily L-BFGS-B's (the
+//     system is under-determined).
+constexpr double kNnlsPgtol = 1e-5;            // scipy fmin_l_bfgs_b default
+constexpr int kNnlsBlockBytes = 256 * 1024;    // librosa.util.utils.MAX_MEM_BLOCK
+__host__ __device__ inline int nnls_block_cols(int n_mels) {
+    const int c = kNnlsBlockBytes / (n_mels * 4);
+    return c > 0 ? c : 1;
+}
+
+__global__ __launch_bounds__(NT) void nnls_start_kernel(const float* __restrict__ mel, int n_mels, int frames, int F,
                                                         const float* __restrict__ W, const float* __restrict__ Wp,
-                                                        float step, int iters, float* __restrict__ S) {
+                                                        float* __restrict__ X0, float* __restrict__ pgmax) {
     extern __shared__ float sh[];
-    float* M = sh;              // [n_mels]
-    float* r = M + n_mels;      // [n_mels] residual
-    float* X = r + n_mels;      // [F]
-    float* Yk = X + F;          // [F] extrapolated point
+    float* M = sh;                                      // [n_mels]
+    float* X = M + n_mels;                              // [F]
+    double* r = reinterpret_cast<double*>(X + F + (F & 1));  // [n_mels] residual (8-B aligned)
+    __shared__ double red[NT / 64];
     const int t = blockIdx.x, u = blockIdx.y;
     for (int m = threadIdx.x; m < n_mels; m += NT)
         M[m] = exp10f(0.1f * 0.5f * (mel[((size_t)u * n_mels + m) * frames + t] + 1.f));
@@ -159,6 +180,61 @@ __global__ __launch_bounds__(NT) void mel_to_mag_kernel(const float* __restrict_
         float s = 0.f;
         for (int m = 0; m < n_mels; ++m) s += Wp[(size_t)f * n_mels + m] * M[m];
         X[f] = fmaxf(s, 0.f);
+        X0[((size_t)u * frames + t) * F + f] = X[f];
+    }
+    __syncthreads();
+    for (int m = threadIdx.x; m < n_mels; m += NT) {
+        double s = -(double)M[m];
+        for (int f = 0; f < F; ++f) s += (double)W[(size_t)m * F + f] * (double)X[f];
+        r[m] = s;
+    }
+    __syncthreads();
+    const int bc = nnls_block_cols(n_mels), b0 = t / bc * bc;
+    const double inv = 1.0 / ((double)n_mels * (double)min(bc, frames - b0));
+    double mx = 0.0;
+    for (int f = threadIdx.x; f < F; f += NT) {
+        double g = 0.0;
+        for (int m = 0; m < n_mels; ++m) g += (double)W[(size_t)m * F + f] * r[m];
+        g *= inv;
+        const double pg = g < 0.0 ? g : fmin((double)X[f], g);  // L-BFGS-B projgr, bound x >= 0
+        mx = fmax(mx, fabs(pg));
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < NT / 64; ++w) mx = fmax(mx, red[w]);
+        pgmax[(size_t)u * frames + t] = (float)mx;
+    }
+}
+
+__global__ __launch_bounds__(NT) void nnls_finish_kernel(const float* __restrict__ mel, int n_mels, int frames, int F,
+                                                         const float* __restrict__ W, float step, int iters,
+                                                         const float* __restrict__ pgmax, float* __restrict__ S) {
+    extern __shared__ float sh[];
+    float* M = sh;              // [n_mels]
+    float* r = M + n_mels;      // [n_mels] residual
+    float* X = r + n_mels;      // [F]
+    float* Yk = X + F;          // [F] extrapolated point
+    __shared__ int conv;
+    const int t = blockIdx.x, u = blockIdx.y;
+    const int bc = nnls_block_cols(n_mels), b0 = t / bc * bc, b1 = min(frames, b0 + bc);
+    float mx = 0.f;
+    for (int k = b0 + threadIdx.x; k < b1; k += NT) mx = fmaxf(mx, pgmax[(size_t)u * frames + k]);
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (threadIdx.x == 0) conv = 1;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && !((double)mx <= kNnlsPgtol)) conv = 0;
+    __syncthreads();
+    float* srow = S + ((size_t)u * frames + t) * F;  // holds X0 (nnls_start_kernel)
+    if (conv || iters == 0) {  // librosa's result: X0
+        for (int f = threadIdx.x; f < F; f += NT) srow[f] = sqrtf(srow[f]);
+        return;
+    }
+    for (int m = threadIdx.x; m < n_mels; m += NT)
+        M[m] = exp10f(0.1f * 0.5f * (mel[((size_t)u * n_mels + m) * frames + t] + 1.f));
+    for (int f = threadIdx.x; f < F; f += NT) {
+        X[f] = srow[f];
         Yk[f] = X[f];
     }
     __syncthreads();
@@ -181,7 +257,7 @@ __global__ __launch_bounds__(NT) void mel_to_mag_kernel(const float* __restrict_
         tk = tn;
         __syncthreads();
     }
-    for (int f = threadIdx.x; f < F; f += NT) S[((size_t)u * frames + t) * F + f] = sqrtf(X[f]);
+    for (int f = threadIdx.x; f < F; f += NT) srow[f] = sqrtf(X[f]);
 }
 
 // iSTFT frame t: the spectrum S * angles (Hermitian-completed; the imaginary
@@ -329,6 +405,22 @@ bool pinv_rows(const std::vector<double>& W, int R, int F, std::vector<double>* 
 }
 
 int frames_of(const m2_dsp* d, int L) { return 1 + L / d->hop; }  // 1 + (L + 2 (n_fft/2) - n_fft) / hop
+
+// X = librosa.util.nnls(W, M) -> S = sqrt(X) [B, T, F] (nnls_start_kernel /
+// nnls_finish_kernel); pg: B * T floats of scratch.
+int32_t nnls_magnitudes(const m2_dsp* d, const float* mel, int B, int T, int iters, float* S, float* pg,
+                        hipStream_t st) {
+    const int F = d->n_fft / 2 + 1;
+    const dim3 grid(T, B);
+    const size_t shs = ((size_t)d->n_mels + (size_t)F + 1) * sizeof(float) + (size_t)d->n_mels * sizeof(double) + 8;
+    hipLaunchKernelGGL(dsp::nnls_start_kernel, grid, dim3(dsp::NT), shs, st, mel, d->n_mels, T, F, d->W, d->Wp, S, pg);
+    M2_LAUNCHED("nnls_start_kernel");
+    const size_t shf = (2 * (size_t)d->n_mels + 2 * (size_t)F) * sizeof(float);
+    hipLaunchKernelGGL(dsp::nnls_finish_kernel, grid, dim3(dsp::NT), shf, st, mel, d->n_mels, T, F, d->W, d->step,
+                       iters, pg, S);
+    M2_LAUNCHED("nnls_finish_kernel");
+    return M2_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -473,16 +565,19 @@ int32_t m2_mel_spectrogram(const m2_dsp* d, const float* audio, int32_t B, int32
     return M2_OK;
 }
 
+size_t m2_mel_to_magnitude_workspace_bytes(const m2_dsp* d, int32_t B, int32_t T) {
+    if (!d || B < 0 || T < 0) return 0;
+    return ((size_t)B * T * sizeof(float) + 255) / 256 * 256 + 256;
+}
+
 int32_t m2_mel_to_magnitude(const m2_dsp* d, const float* mel, int32_t B, int32_t T, int32_t nnls_iters,
-                            float* out_mag, void* stream) {
+                            float* out_mag, void* workspace, size_t workspace_bytes, void* stream) {
     M2_CHECK_ARG(d && mel && out_mag && B >= 0 && T >= 0 && nnls_iters >= 0, "m2_mel_to_magnitude: bad argument");
     if (B == 0 || T == 0) return M2_OK;
-    const int F = d->n_fft / 2 + 1;
-    const size_t shm = (2 * (size_t)d->n_mels + 2 * (size_t)F) * sizeof(float);
-    hipLaunchKernelGGL(dsp::mel_to_mag_kernel, dim3(T, B), dim3(dsp::NT), shm, static_cast<hipStream_t>(stream), mel,
-                       d->n_mels, T, F, d->W, d->Wp, d->step, nnls_iters, out_mag);
-    M2_LAUNCHED("mel_to_mag_kernel");
-    return M2_OK;
+    Carve c(workspace, workspace_bytes);
+    float* pg = c.take<float>((size_t)B * T);
+    if (!c.ok) return fail(M2_E_WORKSPACE, "m2_mel_to_magnitude: workspace too small");
+    return nnls_magnitudes(d, mel, B, T, nnls_iters, out_mag, pg, static_cast<hipStream_t>(stream));
 }
 
 size_t m2_griffin_lim_workspace_bytes(const m2_dsp* d, int32_t B, int32_t T) {
@@ -494,6 +589,7 @@ size_t m2_griffin_lim_workspace_bytes(const m2_dsp* d, int32_t B, int32_t T) {
     s.take<float2>((size_t)B * T * F);          // previous rebuilt spectrum
     s.take<float>((size_t)B * T * d->n_fft);    // windowed inverse frames
     s.take<float>((size_t)B * (Lout > 0 ? Lout : 1));  // the signal of each iteration
+    s.take<float>((size_t)B * T);               // NNLS: per-frame projected-gradient maxima
     return s.off + 256;
 }
 
@@ -513,16 +609,15 @@ int32_t m2_griffin_lim(const m2_dsp* d, const float* mel, const float* mag, cons
     float2* prev = c.take<float2>((size_t)B * T * F);
     float* fr = c.take<float>((size_t)B * T * N);
     float* y = c.take<float>((size_t)B * Lout);
+    float* pgw = mag ? nullptr : c.take<float>((size_t)B * T);
     if (!c.ok) return fail(M2_E_WORKSPACE, "m2_griffin_lim: workspace too small");
     hipStream_t st = static_cast<hipStream_t>(stream);
     const dim3 fgrid(T, B);
     if (mag) {
         M2_HIP(hipMemcpyAsync(S, mag, (size_t)B * T * F * sizeof(float), hipMemcpyDeviceToDevice, st));
     } else {
-        const size_t shm = (2 * (size_t)d->n_mels + 2 * (size_t)F) * sizeof(float);
-        hipLaunchKernelGGL(dsp::mel_to_mag_kernel, fgrid, dim3(dsp::NT), shm, st, mel, d->n_mels, T, F, d->W, d->Wp,
-                           d->step, nnls_iters, S);
-        M2_LAUNCHED("mel_to_mag_kernel");
+        int32_t rc;
+        if ((rc = nnls_magnitudes(d, mel, B, T, nnls_iters, S, pgw, st))) return rc;
     }
     M2_HIP(hipMemcpyAsync(ang, init_angles, (size_t)B * T * F * sizeof(float2), hipMemcpyDeviceToDevice, st));
     M2_HIP(hipMemsetAsync(prev, 0, (size_t)B * T * F * sizeof(float2), st));

@@ -283,6 +283,14 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
         // whose add returns the last ticket reads every duration with sc1 loads
         // (no fences: no L2 write-back per workgroup, which made round 1's
         // fused form slower than the separate count kernel)
+        // This hand-off relies on gfx950's cache behaviour, not on the C++
+        // memory model: sc1 stores write through to the device-coherent
+        // level and retire in order before s_waitcnt vmcnt(0) returns, and sc1
+        // loads bypass the non-coherent caches; the relaxed atomics carry no
+        // ordering of their own.  Other targets must use lr_count_kernel.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "duration_kernel<COUNT=true>: the fused frame count's hand-off is written for gfx950 only"
+#endif
         __shared__ int last;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -431,12 +439,9 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
     // 14-phoneme tiles (one 16-position row block per wave) while they fit one
     // round of the CUs; beyond, 30-phoneme tiles (two row blocks sharing each
     // weight fragment): half the workgroups, each streaming the same weights.
-    // M2_DUR_RB=1|2 forces one (read per call: A/B and tests).
+    // M2_DUR_RB=1|2 forces one (switch table, m2_common.h).
     int rbk = (long)B * cdiv(S, DUR_TS) > 256 ? 2 : 1;
-    if (const char* e = std::getenv("M2_DUR_RB")) {
-        const int v = std::atoi(e);
-        if (v == 1 || v == 2) rbk = v;
-    }
+    if (sw().dur_rb) rbk = sw().dur_rb;
     const dim3 grid(cdiv(S, 16 * rbk - 2), B), blk(64 * DUR_WAVES);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
     const DurCount none{};

@@ -18,6 +18,39 @@ enum Act : int { ACT_NONE = 0, ACT_LEAKY = 1, ACT_TANH = 2, ACT_RELU = 3, ACT_SO
 
 void set_error(const std::string& msg);
 
+// Developer switches (M2_* environment variables: A/B comparisons and tests
+// force one code path).  Read into this table when the library loads, again
+// at every m2_model_create and by m2_reload_switches() - never per call.
+// 0 (or -1 where 0 is a valid choice) = the default rule.
+struct Switches {
+    int dur_rb = 0;           // M2_DUR_RB=1|2: duration tiles of one / two row blocks
+    int dur_count = -1;       // M2_DUR_COUNT=0|1: frame count fused into the duration kernel
+    int speculative = 1;      // M2_SPECULATIVE=0: host-side T only
+    bool tf_chain = true;     // M2_TF_CHAIN=0: separate ln_gemm launches
+    bool tf_layer = true;     // M2_TF_LAYER=0: three-launch transformer layers
+    bool tf_unfused = false;  // M2_TF_UNFUSED: five-linear layers (handle creation)
+    int tf_waves = 0;         // M2_TF_WAVES=4|8
+    int tfl_rb = 0;           // M2_TFL_RB=1|2|4
+    int tfl_first_rb = 0;     // M2_TFL_FIRST_RB=1|2|4
+    int tfl_qs2 = -1;         // M2_TFL_QS2=0|1|3|4
+    int att_qt = 0;           // M2_ATT_QT
+    bool att_f32 = false;     // M2_ATT_F32
+    bool voc_perlayer = false;  // M2_VOCODER_PERLAYER (handle creation)
+    bool voc_f32 = false;       // M2_VOC_F32 (handle creation)
+    bool voc_tail_x3 = false;   // M2_VOC_TAIL_X3 (handle creation)
+    bool voc_mid_x3 = false;    // M2_VOC_MID_X3 (handle creation)
+    int voc_plan = -1;          // M2_VOC_PLAN
+    int midp_nch = 16;          // M2_MIDP_NCH=8|16|32
+    int tailp_nch = 0;          // M2_TAILP_NCH=21|32|48
+    bool tailp_seven = false;   // M2_TAILP_SEVEN
+    int tailp2_nch = 0;         // M2_TAILP2_NCH
+    bool tailp2_seven = false;  // M2_TAILP2_SEVEN
+    bool head_inconv = false;   // M2_HEAD_INCONV
+    bool s2_head_tf16 = false;  // M2_S2_HEAD_TF16
+};
+const Switches& sw();
+void reload_switches();
+
 // Status helpers: every C entry point returns through these.
 int32_t fail(int32_t code, const char* what);
 int32_t hip_status(hipError_t e, const char* where);

@@ -17,6 +17,60 @@
 
 namespace m2 {
 
+namespace {
+Switches g_sw;
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atoi(e) : dflt;
+}
+bool env_set(const char* name) { return std::getenv(name) != nullptr; }
+bool env_on(const char* name, bool dflt) {  // unset / empty -> dflt, else != "0"
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atoi(e) != 0 : dflt;
+}
+// reloaded when the library loads
+const bool g_sw_loaded = (reload_switches(), true);
+}  // namespace
+
+const Switches& sw() { return g_sw; }
+
+void reload_switches() {
+    Switches s;
+    const int rb = env_int("M2_DUR_RB", 0);
+    s.dur_rb = (rb == 1 || rb == 2) ? rb : 0;
+    s.dur_count = std::getenv("M2_DUR_COUNT") && *std::getenv("M2_DUR_COUNT") ? (env_int("M2_DUR_COUNT", 0) != 0) : -1;
+    s.speculative = env_on("M2_SPECULATIVE", true) ? 1 : 0;
+    s.tf_chain = env_on("M2_TF_CHAIN", true);
+    s.tf_layer = env_on("M2_TF_LAYER", true);
+    s.tf_unfused = env_set("M2_TF_UNFUSED");
+    const int tw = env_int("M2_TF_WAVES", 0);
+    s.tf_waves = (tw == 4 || tw == 8) ? tw : 0;
+    auto rb124 = [](int v) { return (v == 1 || v == 2 || v == 4) ? v : 0; };
+    s.tfl_rb = rb124(env_int("M2_TFL_RB", 0));
+    s.tfl_first_rb = rb124(env_int("M2_TFL_FIRST_RB", 0));
+    if (const char* e = std::getenv("M2_TFL_QS2"); e && *e) {
+        const int v = std::atoi(e);
+        s.tfl_qs2 = v == 3 || v == 4 ? v : (v != 0 ? 2 : 0);
+    }
+    s.att_qt = env_int("M2_ATT_QT", 0);
+    if (const char* e = std::getenv("M2_ATT_F32")) s.att_f32 = *e && *e != '0';
+    s.voc_perlayer = env_set("M2_VOCODER_PERLAYER");
+    s.voc_f32 = env_set("M2_VOC_F32");
+    s.voc_tail_x3 = env_set("M2_VOC_TAIL_X3");
+    s.voc_mid_x3 = env_set("M2_VOC_MID_X3");
+    s.voc_plan = env_int("M2_VOC_PLAN", -1);
+    const int mn = env_int("M2_MIDP_NCH", 16);
+    s.midp_nch = (mn == 8 || mn == 32) ? mn : 16;
+    const int tn = env_int("M2_TAILP_NCH", 0);
+    s.tailp_nch = (tn == 21 || tn == 32 || tn == 48) ? tn : 0;
+    s.tailp_seven = env_set("M2_TAILP_SEVEN");
+    s.tailp2_nch = env_int("M2_TAILP2_NCH", 0);
+    s.tailp2_seven = env_set("M2_TAILP2_SEVEN");
+    s.head_inconv = env_set("M2_HEAD_INCONV");
+    s.s2_head_tf16 = env_set("M2_S2_HEAD_TF16");
+    g_sw = s;
+}
+
 // ---- launchers defined in the kernel translation units ---------------------
 int32_t launch_embed_pe(const int64_t*, const float*, const float*, int, int, int, int, float*, const int64_t*,
                         uint8_t*, hipStream_t);
@@ -360,12 +414,8 @@ int32_t run_layer(const m2_model* m, const m2_layer_w& L, const float* x_in, flo
 // *fin_done), one launch per layer fewer; results are identical to the
 // separate launches (same fp32 y into the same LayerNorm / GEMM code).
 bool tf_chain(const m2_model* m) {
-    static const bool chain_ok = [] {  // M2_TF_CHAIN=0: separate ln_gemm launches (A/B)
-        const char* e = std::getenv("M2_TF_CHAIN");
-        return !e || std::atoi(e) != 0;
-    }();
-    const int H = m->cfg.hidden_dim;
-    return chain_ok && m->tfused && tf_post_next_supported(H, 3 * H);
+    const int H = m->cfg.hidden_dim;  // M2_TF_CHAIN=0: separate ln_gemm launches (A/B)
+    return sw().tf_chain && m->tfused && tf_post_next_supported(H, 3 * H);
 }
 
 // The first layer's input rows built by its LN1 -> QKV launch (embedding /
@@ -387,9 +437,7 @@ int32_t tfl_reset(const m2_model* m, hipStream_t st, int32_t rc) {
 // heads == 2, H in {32, 64, 96}, the split-f16 transformer path.
 // M2_TF_LAYER=0 keeps the three-launch layers (A/B comparisons, tests).
 bool tfl_use(const m2_model* m, const std::vector<m2_layer_w>& layers) {
-    const char* e = std::getenv("M2_TF_LAYER");  // read per call: a process can switch (tests)
-    const bool on = !e || !*e || std::atoi(e) != 0;
-    return on && m->tfused && !m->att_f32 && !layers.empty() &&
+    return sw().tf_layer && m->tfused && !m->att_f32 && !layers.empty() &&
            tfl_supported(m->cfg.hidden_dim, m->cfg.num_heads);
 }
 
@@ -504,8 +552,11 @@ int64_t m2_weight_numel(const m2_config* cfg, int32_t index) {
     return t[index].numel;
 }
 
+void m2_reload_switches(void) { reload_switches(); }
+
 int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_t n_weights,
                         void* stream, m2_model** out) {
+    reload_switches();  // the developer switches of this handle's creation (m2_common.h)
     M2_CHECK_ARG(config_ok(cfg), "m2_model_create: invalid config");
     M2_CHECK_ARG(weights && out, "m2_model_create: null argument");
     const auto table = weight_table(*cfg);
@@ -610,7 +661,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     // Fused transformer layers: pack qkv / out / ffn / mel-projection weights
     // in B-fragment order (M2_TF_UNFUSED=1 keeps the five-linear layer).
     m->tfused = tf_fused_supported(H, 3 * H) && tf_fused_supported(H, cfg->mel_channels) &&
-                !std::getenv("M2_TF_UNFUSED");
+                !sw().tf_unfused;
     if (m->tfused) {
         size_t o = tf_off;
         auto pack_up = [&](const std::string& n, int N, int K, const float** slot) -> hipError_t {
@@ -723,7 +774,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     m->vout_b = P("vocoder.output_conv.bias");
 
     // Fused vocoder: pack conv / convT weights into MFMA A-fragment order.
-    m->fused = vocoder_fused_supported(cfg->mel_channels, cfg->vocoder_channels) && !std::getenv("M2_VOCODER_PERLAYER");
+    m->fused = vocoder_fused_supported(cfg->mel_channels, cfg->vocoder_channels) && !sw().voc_perlayer;
     if (m->fused) {
         auto fetch = [&](const std::string& n) {
             const int i = idx(n);
@@ -772,7 +823,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
 
         // Split-f16 packs (default path when the shapes are supported and every
         // weight is inside the f16 range; M2_VOC_F32=1 keeps the exact-f32 MFMA).
-        if (vocoder_x3_supported(M, C) && !std::getenv("M2_VOC_F32")) {
+        if (vocoder_x3_supported(M, C) && !sw().voc_f32) {
             bool ok = true;
             std::vector<std::vector<uint16_t>> xp;
             std::vector<const vx_u32x4**> xs;
@@ -846,7 +897,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 // stage1 / stage2: the last two upsampling stages as one
                 // pipelined kernel (M2_VOC_TAIL_X3=1 keeps the x3 tail kernel).
                 const bool s2tail = M == 80 && C == 256;
-                if (((M == 64 && C == 128) || s2tail) && !std::getenv("M2_VOC_TAIL_X3")) {
+                if (((M == 64 && C == 128) || s2tail) && !sw().voc_tail_x3) {
                     const char* names[14] = {
                         "vocoder.upsamples.2.weight",         "vocoder.upsamples.2.bias",
                         "vocoder.resblocks.2.conv1.weight", "vocoder.resblocks.2.conv1.bias",
@@ -892,7 +943,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 }
                 // stage1: the second upsampling stage as one pipelined kernel
                 // (M2_VOC_MID_X3=1 keeps the x3 mid kernel).
-                if (M == 64 && C == 128 && !std::getenv("M2_VOC_MID_X3")) {
+                if (M == 64 && C == 128 && !sw().voc_mid_x3) {
                     const char* names[6] = {"vocoder.upsamples.1.weight",         "vocoder.upsamples.1.bias",
                                             "vocoder.resblocks.1.conv1.weight", "vocoder.resblocks.1.conv1.bias",
                                             "vocoder.resblocks.1.conv2.weight", "vocoder.resblocks.1.conv2.bias"};
@@ -1478,6 +1529,7 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
                                         buf[0], buf[1], out_audio, st, mark)))
                 return rc;
             vw.guard = m->rflag_dev + redo;
+            vw.guard_queue = reinterpret_cast<const unsigned*>(m->rflag_dev + 4);  // words 4-7 (zeroed at creation)
             return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vw,
                                         buf[0], buf[1], out_audio, st, [](int, bool) {});
         }
@@ -1618,8 +1670,7 @@ struct CountFuse {
 // A/B, profiles/r03/r03aa_ab.txt).  M2_DUR_COUNT=1 fuses up to the kernel's
 // limit (8192), =0 never.
 bool fuse_count(int B, int S) {
-    const char* e = std::getenv("M2_DUR_COUNT");  // read per call (tests and A/B switch it)
-    if (e && *e) return std::atoi(e) != 0 && duration_count_fusable(B, S);
+    if (sw().dur_count >= 0) return sw().dur_count != 0 && duration_count_fusable(B, S);
     return (long)B * S <= 2048 && duration_count_fusable(B, S);
 }
 template <typename Count>
@@ -1659,8 +1710,7 @@ int32_t front_run(const m2_model* m, const int64_t* ids, const int64_t* lengths,
 // sized for T_cap frames: the one-launch decoder layers with the mel
 // projection fused into the last one, and the fused (unchunked) vocoder.
 bool dev_back_ok(const m2_model* m, int32_t T_cap) {
-    const char* e = std::getenv("M2_SPECULATIVE");  // 0: host-side T only (A/B, tests; read per call)
-    if (e && *e && std::atoi(e) == 0) return false;
+    if (!sw().speculative) return false;  // M2_SPECULATIVE=0: host-side T only (A/B, tests)
     return T_cap > 0 && tfl_use(m, m->dec) && tfl_proj_supported(m->cfg.hidden_dim, m->cfg.mel_channels) &&
            m->fused && !(m->chunk_frames > 0 && T_cap > m->chunk_frames);
 }

@@ -835,10 +835,7 @@ template <int HD>
 static int32_t launch_att_split(dim3 grid, const float* qkv, const uint8_t* mask, int N, int H, float scale,
                                 float* out, hipStream_t st) {
     const int heads = (int)grid.y, B = (int)grid.z;
-    static const int forced = [] {
-        const char* e = std::getenv("M2_ATT_QT");
-        return e ? std::atoi(e) : 0;
-    }();
+    const int forced = sw().att_qt;
     // head_dim > 32: two tiles' registers spill past the 256-VGPR cap (400-432
     // B/lane of scratch, 6-8x slower), so those instances are not compiled and
     // M2_ATT_QT=2 is refused for them
@@ -967,9 +964,8 @@ int32_t launch_attention(const float* qkv, const uint8_t* mask, int B, int N, in
     const float scale = (float)(1.0 / std::sqrt((double)hd));  // components.py:52 (self.scale), fp32 at the mul
     dim3 grid(cdiv(N, 64), heads, B);
     // split-f16 MFMA by default; M2_ATT_F32=1: the exact-f32 MFMA kernel
-    // (read per launch, so a process can switch: tests/test_gpu_parity.py)
-    const char* env = std::getenv("M2_ATT_F32");
-    const bool f32 = force_f32 || (env && *env && *env != '0');
+    // (switch table, m2_common.h)
+    const bool f32 = force_f32 || sw().att_f32;
     // float4 reads of q/k/v rows in the MFMA kernels: H and the head offsets 16-B aligned
     if (H % 4 != 0 || (hd != 16 && hd != 32 && hd != 48 && hd != 64)) {  // no MFMA instance: the generic kernel
         M2_CHECK_SHAPE(hd <= 256, "attention: head_dim must be at most 256");

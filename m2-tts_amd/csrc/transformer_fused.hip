@@ -430,11 +430,7 @@ bool pack_bfrag_split(const float* W, int N, int K, std::vector<float>* out) {
 // warm-up of the layer's weights at kernel start measured 1 us slower: across
 // steps they stay L2-resident.)
 static int tf_waves(int R) {
-    static const int forced = [] {
-        const char* e = std::getenv("M2_TF_WAVES");
-        const int v = e ? std::atoi(e) : 0;
-        return (v == 4 || v == 8) ? v : 0;
-    }();
+    const int forced = sw().tf_waves;
     if (forced) return forced;
     return cdiv(R, tfx::TR) < 2 * 256 ? 8 : 4;
 }

@@ -1560,9 +1560,7 @@ namespace {
 // one round of the CUs holds the 16-row grid, else 32.  M2_TFL_RB=1|2|4
 // forces one.  The first (LN1 -> QKV) launch has no attention: at most 32.
 int tfl_rb(int B, int N) {
-    const char* e = std::getenv("M2_TFL_RB");  // per call: tests switch it
-    const int forced = e ? std::atoi(e) : 0;
-    if (forced == 1 || forced == 2 || forced == 4) return forced;
+    if (sw().tfl_rb) return sw().tfl_rb;
     const long tiles16 = (long)B * (tfl_npad(N) / tfl::TQ);
     return tiles16 >= 4 * 256 ? 4 : (tiles16 > 256 ? 2 : 1);
 }
@@ -1574,13 +1572,9 @@ int tfl_rb(int B, int N) {
 // (stage1 B=32: -0.7 % against the plain one-block form; two blocks +0.3 to
 // +0.6 %; in-process A/Bs, profiles/r03/r03ab_*, r03ad_ab.txt, r03aj_ab.txt,
 // r03al_ab.txt).  M2_TFL_QS2=0|1|3|4 forces one block / two / two lean / one
-// lean (read per call: A/B and tests switch it).
+// lean (switch table, m2_common.h).
 int tfl_qs2(int H) {
-    const char* e = std::getenv("M2_TFL_QS2");
-    if (e && *e) {
-        const int v = std::atoi(e);
-        return v == 3 || v == 4 ? v : (v != 0 ? 2 : 0);
-    }
+    if (sw().tfl_qs2 >= 0) return sw().tfl_qs2;
     return H / tfl::HEADS >= 48 ? 3 : 4;
 }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
@@ -1595,7 +1589,10 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
                          hipStream_t st) {
     M2_CHECK_SHAPE(tfl_supported(H, heads), "tfl: unsupported (hidden_dim, heads)");
     M2_CHECK_ARG(q.cnt, "tfl: no work-queue counters");
-    if (B == 0 || N == 0) return M2_OK;
+    // every launch must run: its workgroups zero the NEXT launch's work-queue
+    // counter set (TflQueue), so an empty launch that returned M2_OK would
+    // leave that set stale (callers return before an empty batch)
+    if (B == 0 || N == 0) return fail(M2_E_INTERNAL, "tfl: empty launch (no work-queue hand-off)");
     tfl::FArgs a{};
     a.B = B;
     a.N = N;
@@ -1604,13 +1601,10 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     // launch 23 % faster but the step 1.4 % slower at stage2 B=64, in-process
     // A/B, profiles/r03/ab/r03x_ab.txt), 64 for grids of >= 16 rounds of
     // 16-row tiles (the long-form decoder: a series of latency-bound rounds);
-    // M2_TFL_FIRST_RB=1|2|4 forces one (read per call: A/B and tests)
+    // M2_TFL_FIRST_RB=1|2|4 forces one (switch table, m2_common.h)
     int rb = tfl_rb(B, N) > 1 ? 2 : 1;
     if ((long)B * (tfl_npad(N) / tfl::TQ) >= 16L * 256) rb = 4;
-    if (const char* e = std::getenv("M2_TFL_FIRST_RB")) {
-        const int v = std::atoi(e);
-        if (v == 1 || v == 2 || v == 4) rb = v;
-    }
+    if (sw().tfl_first_rb) rb = sw().tfl_first_rb;
     a.ntile = a.npad / (tfl::TQ * rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
@@ -1665,7 +1659,10 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     M2_CHECK_SHAPE(tfl_supported(H, heads), "tfl: unsupported (hidden_dim, heads)");
     M2_CHECK_ARG(!masked || lengths, "tfl: masked attention needs lengths");
     M2_CHECK_ARG(q.cnt, "tfl: no work-queue counters");
-    if (B == 0 || N == 0) return M2_OK;
+    // every launch must run: its workgroups zero the NEXT launch's work-queue
+    // counter set (TflQueue), so an empty launch that returned M2_OK would
+    // leave that set stale (callers return before an empty batch)
+    if (B == 0 || N == 0) return fail(M2_E_INTERNAL, "tfl: empty launch (no work-queue hand-off)");
     auto u4 = [](const float* p) { return reinterpret_cast<const vx_u32x4*>(p); };
     tfl::LArgs a{};
     a.B = B;

@@ -15,10 +15,12 @@ struct VocW {
     const float *wt[4], *bt[4];
     const float *w1[4], *b1[4], *w2[4], *b2[4];
     const float *wo, *bo;
-    // device word; when set, every workgroup returns at once unless it is
-    // non-zero (the range policy's on-device redo of a split-path call whose
-    // audio came out non-finite)
+    // device word; when set, the call is the range policy's on-device redo
+    // of a split-path call whose audio came out non-finite: ONE persistent
+    // launch (voc_redo_kernel) whose workgroups return at once unless it is
+    // non-zero, with guard_queue its 4 zeroed work-queue words
     const int* guard = nullptr;
+    const unsigned* guard_queue = nullptr;
     // device frame count (dev_frames); T of the launch = capacity when set
     const int32_t* dT = nullptr;
 };

@@ -22,6 +22,7 @@
 // are padded to a stride = 16 mod 32 floats so the two 32-lane halves of a
 // ds_read_b32 hit disjoint banks).  K = (tap, channel).  ConvT is r GEMMs,
 // one per output phase, each with K = 2 taps x Cin (the 2-tap polyphase form).
+#include <algorithm>
 #include <cstdlib>
 #include <functional>
 
@@ -381,15 +382,16 @@ __device__ unsigned long long g_stamps[3][4096][16][16];
     } while (0)
 #endif
 
+// The three kernels' bodies are device functions of the window (bx, b), so
+// the guarded redo below can run them from one persistent launch.
 template <class Cfg, bool TRANS>
-__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(const float* __restrict__ mel, int T,
-                                                                             VocW w, float* __restrict__ U1) {
-    if (w.guard && *w.guard == 0) return;  // guarded redo, not needed
+__device__ __forceinline__ void voc_head_body(int bx, int b, const float* __restrict__ mel, int T, const VocW& w,
+                                              float* __restrict__ U1) {
     constexpr int M = Cfg::M, C = Cfg::C, TF = Cfg::TF;
     using Pl = HeadPlan<M, C, TF, Cfg::CP>;
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = blockIdx.y, f0 = blockIdx.x * TF;
+    const int f0 = bx * TF;
     if (w.dT) {  // speculative launch: T was the capacity
         T = dev_frames(w.dT, T);
         if (f0 >= T) return;
@@ -426,14 +428,13 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(co
 }
 
 template <class Cfg>
-__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(const float* __restrict__ U1, int L1,
-                                                                            VocW w, float* __restrict__ U2) {
-    if (w.guard && *w.guard == 0) return;  // guarded redo, not needed
+__device__ __forceinline__ void voc_mid_body(int bx, int b, const float* __restrict__ U1, int L1, const VocW& w,
+                                             float* __restrict__ U2) {
     constexpr int CI = Cfg::C / 2, W = Cfg::W2;
     using Pl = MidPlan<CI, W>;
     constexpr int CO = Pl::CO;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = blockIdx.y, p0 = blockIdx.x * W;
+    const int p0 = bx * W;
     if (w.dT) {  // speculative launch: L1 was the capacity
         L1 = 4 * dev_frames(w.dT, L1 / 4);
         if (p0 >= L1) return;
@@ -466,14 +467,13 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(con
 }
 
 template <class Cfg>
-__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(const float* __restrict__ U2, int L2,
-                                                                             VocW w, float* __restrict__ audio) {
-    if (w.guard && *w.guard == 0) return;  // guarded redo, not needed
+__device__ __forceinline__ void voc_tail_body(int bx, int b, const float* __restrict__ U2, int L2, const VocW& w,
+                                              float* __restrict__ audio) {
     constexpr int CI = Cfg::C / 4, W = Cfg::W3;
     using Pl = TailPlan<CI, W>;
     constexpr int C3 = Pl::C3, C4 = Pl::C4;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = blockIdx.y, p0 = blockIdx.x * W;
+    const int p0 = bx * W;
     if (w.dT) {  // speculative launch: L2 was the capacity
         L2 = 16 * dev_frames(w.dT, L2 / 16);
         if (p0 >= L2) return;
@@ -536,6 +536,76 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(co
     STAMP(2, 14);
 }
 
+template <class Cfg, bool TRANS>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(const float* __restrict__ mel, int T,
+                                                                             VocW w, float* __restrict__ U1) {
+    voc_head_body<Cfg, TRANS>(blockIdx.x, blockIdx.y, mel, T, w, U1);
+}
+template <class Cfg>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(const float* __restrict__ U1, int L1,
+                                                                            VocW w, float* __restrict__ U2) {
+    voc_mid_body<Cfg>(blockIdx.x, blockIdx.y, U1, L1, w, U2);
+}
+template <class Cfg>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(const float* __restrict__ U2, int L2,
+                                                                             VocW w, float* __restrict__ audio) {
+    voc_tail_body<Cfg>(blockIdx.x, blockIdx.y, U2, L2, w, audio);
+}
+
+// The range policy's on-device redo (m2_set_range_policy "fallback"): ONE
+// launch after the split-f16 kernels.  Every workgroup returns at once unless
+// the call's flag word (*w.guard) is raised; then the workgroups claim the
+// exact-f32 head, mid and tail windows from one ordered queue (q[0]) and a
+// mid (tail) window waits until every head (mid) window is published (q[1],
+// q[2]).  A workgroup only ever waits for windows claimed before its own, by
+// workgroups already running, so any number of resident workgroups finishes
+// (no co-residency assumption).  Publication: every wave's stores are written
+// back (agent-scope release fence) before the count; a waiter acquires after
+// it (U1 / U2 cross XCDs, whose L2s are not coherent).  The last workgroup out
+// (q[3]) re-zeroes the four words for the next redo.
+__device__ __forceinline__ void redo_publish(unsigned* c) {
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(c, 1u);
+}
+__device__ __forceinline__ void redo_wait(unsigned* c, unsigned n) {
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+    __threadfence();
+}
+template <class Cfg, bool TRANS>
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_redo_kernel(const float* __restrict__ mel, int B,
+                                                                             int T, VocW w, float* __restrict__ U1,
+                                                                             float* __restrict__ U2,
+                                                                             float* __restrict__ audio,
+                                                                             unsigned* __restrict__ q) {
+    if (*w.guard == 0) return;  // the split-f16 result is finite: nothing to redo
+    const int hx = (T + Cfg::TF - 1) / Cfg::TF, mx = (4 * T + Cfg::W2 - 1) / Cfg::W2, tx = (16 * T + Cfg::W3 - 1) / Cfg::W3;
+    const int nh = hx * B, nm = mx * B, nt = tx * B;
+    __shared__ int item;
+    for (;;) {
+        __syncthreads();  // the previous window is done with LDS and `item`
+        if (threadIdx.x == 0) item = (int)atomicAdd(q, 1u);
+        __syncthreads();
+        const int i = item;
+        if (i >= nh + nm + nt) break;
+        if (i < nh) {
+            voc_head_body<Cfg, TRANS>(i % hx, i / hx, mel, T, w, U1);
+            redo_publish(q + 1);
+        } else if (i < nh + nm) {
+            redo_wait(q + 1, (unsigned)nh);
+            voc_mid_body<Cfg>((i - nh) % mx, (i - nh) / mx, U1, 4 * T, w, U2);
+            redo_publish(q + 2);
+        } else {
+            redo_wait(q + 2, (unsigned)nm);
+            voc_tail_body<Cfg>((i - nh - nm) % tx, (i - nh - nm) / tx, U2, 16 * T, w, audio);
+        }
+    }
+    if (threadIdx.x == 0 && atomicAdd(q + 3, 1u) == gridDim.x - 1)
+        for (int k = 0; k < 4; ++k) __hip_atomic_store(q + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------
 namespace {
 template <typename K>
@@ -547,8 +617,39 @@ int32_t set_lds(K kernel, size_t bytes) {
 }
 
 template <class Cfg>
+int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
+                 hipStream_t st) {
+    using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
+    using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
+    using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
+    constexpr int threads = Cfg::WAVES * 64;
+    constexpr size_t lds = 4 * (size_t)std::max(std::max(HP::LDS_FLOATS, MP::LDS_FLOATS), TP::LDS_FLOATS);
+    static int grid = 0;
+    if (!grid) {
+        int32_t rc;
+        if ((rc = set_lds(voc_redo_kernel<Cfg, false>, lds))) return rc;
+        if ((rc = set_lds(voc_redo_kernel<Cfg, true>, lds))) return rc;
+        int occ = 0, dev = 0, cus = 0;
+        M2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, voc_redo_kernel<Cfg, false>, threads, lds));
+        M2_HIP(hipGetDevice(&dev));
+        M2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        grid = std::max(1, occ) * std::max(1, cus);
+    }
+    unsigned* q = const_cast<unsigned*>(reinterpret_cast<const unsigned*>(w.guard_queue));
+    if (trans)
+        hipLaunchKernelGGL((voc_redo_kernel<Cfg, true>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2, audio,
+                           q);
+    else
+        hipLaunchKernelGGL((voc_redo_kernel<Cfg, false>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2,
+                           audio, q);
+    M2_LAUNCHED("voc_redo_kernel");
+    return M2_OK;
+}
+
+template <class Cfg>
 int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                   hipStream_t st, const std::function<void(int, bool)>& mark) {
+    if (w.guard) return voc_redo<Cfg>(mel, trans, B, T, w, U1, U2, audio, st);
     using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
@@ -593,7 +694,7 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
                              float* U2, float* audio, hipStream_t st,
                              const std::function<void(int, bool)>& mark) {
     if (B == 0 || T == 0) return M2_OK;
-    static const int plan = std::getenv("M2_VOC_PLAN") ? std::atoi(std::getenv("M2_VOC_PLAN")) : -1;
+    const int plan = sw().voc_plan;
     if (M == 64 && C == 128) {
         // Workgroup rounds: one 16-wave WG per CU; 8-wave WGs pair up.  Pick the
         // tiling whose workgroup count wastes the least of its last round.

@@ -299,11 +299,7 @@ const char* const kVocMidpKernelName = "midp_kernel (ConvT2 + ResBlock2, pipelin
 int32_t launch_vocoder_midp(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2,
                             hipStream_t st, const int32_t* dT) {
     if (B == 0 || L1 == 0) return M2_OK;
-    static const int nch = [] {
-        const char* e = std::getenv("M2_MIDP_NCH");
-        const int v = e ? std::atoi(e) : 16;
-        return (v == 8 || v == 32) ? v : 16;
-    }();
+    const int nch = sw().midp_nch;
     if (nch == 8) return mp::launch<8>(U1, L1, B, W, bias, U2, st, dT);
     if (nch == 32) return mp::launch<32>(U1, L1, B, W, bias, U2, st, dT);
     return mp::launch<16>(U1, L1, B, W, bias, U2, st, dT);

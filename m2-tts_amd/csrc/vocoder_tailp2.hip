@@ -538,15 +538,13 @@ int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, 
     if (B == 0 || L2 == 0) return M2_OK;
     // Strip length: the instantiated NCH minimising rounds x (NCH + NL pipeline
     // steps) at one workgroup per CU.  M2_TAILP2_NCH forces one;
-    // M2_TAILP2_SEVEN=1 the seven-layer form (read per call: A/B and tests).
-    const bool seven = std::getenv("M2_TAILP2_SEVEN") != nullptr;
+    // M2_TAILP2_SEVEN=1 the seven-layer form (switch table, m2_common.h).
+    const bool seven = sw().tailp2_seven;
     const int nl = seven ? 7 : 6;
     static constexpr int kN[] = {8, 16, 32, 64, 128, 192};
-    static const int forced = [] {
-        const char* e = std::getenv("M2_TAILP2_NCH");
-        const int v = e ? std::atoi(e) : 0;
+    const int forced = [] {
         for (int n : kN)
-            if (v == n) return v;
+            if (sw().tailp2_nch == n) return n;
         return 0;
     }();
     int nch = forced;

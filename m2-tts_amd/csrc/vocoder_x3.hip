@@ -1327,11 +1327,11 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     mark(0, true);
     // the composed input_conv o ConvT1 head when packed (stage1; 22.1 -> 19.7
     // us, profiles/ab/r02l_head_comp.txt); M2_HEAD_INCONV=1 runs the two
-    // layers (A/B and test switch, read per call)
-    const bool comp = w.hc && !std::getenv("M2_HEAD_INCONV");
+    // layers (A/B and test switch, m2_common.h switch table)
+    const bool comp = w.hc && !sw().head_inconv;
     const dim3 hg(cdiv(T, Cfg::TF), B), hb(Cfg::HW * 64);
     bool wide = false;  // stage2, composed head, large grid: 24-frame windows
-    if constexpr (S2) wide = comp && (long)cdiv(T, Cfg::TF) * B >= kS2WideHeadWGs && !std::getenv("M2_S2_HEAD_TF16");
+    if constexpr (S2) wide = comp && (long)cdiv(T, Cfg::TF) * B >= kS2WideHeadWGs && !sw().s2_head_tf16;
     if (wide) {
         if constexpr (S2) {
             const dim3 hg24(cdiv(T, CfgS2H24::TF), B);

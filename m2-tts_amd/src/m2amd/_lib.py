@@ -36,6 +36,7 @@ _SIGNATURES = {
     "m2_weight_numel": (c_i64, [ctypes.POINTER(M2Config), c_i32]),
     "m2_model_create": (c_i32, [ctypes.POINTER(M2Config), ctypes.POINTER(c_vp), c_i32, c_vp, ctypes.POINTER(c_vp)]),
     "m2_model_destroy": (c_i32, [c_vp]),
+    "m2_reload_switches": (None, []),
     "m2_model_config": (c_i32, [c_vp, ctypes.POINTER(M2Config)]),
     "m2_workspace_bytes": (c_size, [c_vp, c_i32, c_i32, c_i32]),
     "m2_text_encoder": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_size, c_vp]),
@@ -78,7 +79,8 @@ _SIGNATURES = {
     "m2_stft": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "m2_mel_spectrogram": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "m2_griffin_lim_workspace_bytes": (c_size, [c_vp, c_i32, c_i32]),
-    "m2_mel_to_magnitude": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "m2_mel_to_magnitude_workspace_bytes": (c_size, [c_vp, c_i32, c_i32]),
+    "m2_mel_to_magnitude": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_size, c_vp]),
     "m2_griffin_lim": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_i32, c_vp, c_vp, c_size, c_vp]),
     "m2_transformer_path": (c_i32, [c_vp]),
     "m2_front_bytes": (c_size, [c_vp, c_i32, c_i32]),
@@ -127,6 +129,12 @@ def load(path: Path = None):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def reload_switches():
+    """Re-read the M2_* developer switches into the library's table (it reads
+    them at load and at every model-handle creation, never per call)."""
+    load().m2_reload_switches()
 
 
 def exported_symbols():

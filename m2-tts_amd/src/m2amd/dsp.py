@@ -65,14 +65,19 @@ class Dsp:
         return out
 
     def mel_to_magnitude(self, mel: Tensor, nnls_iters: int = 200) -> Tensor:
-        """librosa.feature.inverse.mel_to_stft of (mel + 1) / 2 in dB (audio.py:128-132,
-        NNLS by projected gradient) -> magnitudes [B, F, T]."""
+        """librosa.feature.inverse.mel_to_stft of (mel + 1) / 2 in dB (audio.py:128-132)
+        -> magnitudes [B, F, T]: librosa.util.nnls's result, its L-BFGS-B's
+        start max(0, pinv(W) M) where its convergence test passes there (every
+        mel in the normalised range); ``nnls_iters`` projected-gradient steps
+        per frame for a block that would iterate (m2_mel_to_magnitude)."""
         require_device(mel, what="m2 mel_to_magnitude")
         m = mel.float().reshape(-1, self.n_mels, mel.shape[-1]).contiguous()
         B, T = m.shape[0], m.shape[2]
         out = torch.empty(B, T, self.F, device=m.device, dtype=torch.float32)
+        n = int(_lib.load().m2_mel_to_magnitude_workspace_bytes(self.handle, B, T))
+        ws = torch.empty(max(n, 1), dtype=torch.uint8, device=m.device)
         _lib.call("m2_mel_to_magnitude", self.handle, m.data_ptr(), B, T, int(nnls_iters), out.data_ptr(),
-                  stream_handle(m.device))
+                  ws.data_ptr(), ws.numel(), stream_handle(m.device))
         return out.transpose(1, 2)
 
     def random_angles(self, B: int, T: int, seed: Optional[int] = None) -> Tensor:

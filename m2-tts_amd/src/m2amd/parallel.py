@@ -121,6 +121,18 @@ def hip_stages(model) -> HipStages:
     return HipStages(model)
 
 
+def _stages_device(stages) -> Optional[torch.device]:
+    """The device the stages compute on (the model's parameters for
+    HipStages; None for host stages such as the oracle-backed Stages).  It is
+    the same on every rank, unlike the placement of a rank's input tensors."""
+    model = getattr(stages, "model", None)
+    if model is None:
+        return None
+    for p in model.parameters():
+        return p.device
+    return None
+
+
 def _collective_device(ref: Optional[Tensor], group) -> torch.device:
     """nccl (RCCL) moves device tensors only; gloo host tensors."""
     if dist.is_initialized() and dist.get_backend(group) == "nccl":
@@ -328,15 +340,21 @@ def sharded_inference(stages, phoneme_ids: Optional[Tensor], phoneme_lengths: Op
     docstring); the first step of a (B, S) shape runs the host path."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
+    sdev = _stages_device(stages)
     if src is not None and world > 1:
-        phoneme_ids, phoneme_lengths = broadcast_inputs(phoneme_ids, phoneme_lengths, src, group)
+        phoneme_ids, phoneme_lengths = broadcast_inputs(phoneme_ids, phoneme_lengths, src, group, device=sdev)
+    elif sdev is not None and phoneme_ids.device != sdev:
+        phoneme_ids = phoneme_ids.to(sdev)
+        phoneme_lengths = phoneme_lengths.to(sdev) if phoneme_lengths is not None else None
     B = phoneme_ids.shape[0]
     lo, hi = shard_bounds(B, world, rank)
     ids = phoneme_ids[lo:hi]
     lens = phoneme_lengths[lo:hi] if phoneme_lengths is not None else None
     key = (B, phoneme_ids.shape[1], float(duration_scale))
-    use_dev = device_T and hasattr(stages, "dev_handle") and phoneme_ids.is_cuda and \
-        not (one_call_world1 and world == 1 and hi > lo and hasattr(stages, "both"))
+    # decided from values every rank shares (the stages' type and device, the
+    # world size): the device-T and host paths issue different collectives
+    use_dev = device_T and hasattr(stages, "dev_handle") and sdev is not None and sdev.type == "cuda" and \
+        not (one_call_world1 and world == 1 and hasattr(stages, "both"))
     if use_dev:
         cap = stages.tcap.get(key, 0)
         hm = stages.dev_handle(phoneme_ids.device, cap) if cap > 0 else None
@@ -423,7 +441,11 @@ class ShardedPipeline:
 
     def __init__(self, model, depth: int = 2, group=None, gather_to: Optional[int] = 0):
         tcap: dict = {}
-        self.lanes = [(HipStages(model, lane=i, tcap=tcap), torch.cuda.Stream()) for i in range(depth)]
+        # lanes 1..depth: lane 0 is the model's default handle, which
+        # model.inference() / forward() use on the caller's stream, and a
+        # handle's device state (work-queue counters, frame mailbox, redo
+        # words) is ordered on one stream
+        self.lanes = [(HipStages(model, lane=i + 1, tcap=tcap), torch.cuda.Stream()) for i in range(depth)]
         self.group, self.gather_to = group, gather_to
         self._next = 0
 

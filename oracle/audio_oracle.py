@@ -21,8 +21,9 @@ in /root/reference to check it against).  What it restates:
   mel_to_audio (audio.py:101-151)
     (mel + 1) / 2, librosa.db_to_power, librosa.feature.inverse.mel_to_audio
       (n_iter=32, power=2.0): mel_to_stft = nnls(mel_basis, M) ** (1/power)
-      (librosa.util.nnls: pinv init clipped at 0, scipy fmin_l_bfgs_b with
-      bounds >= 0 and m = n_mels), then griffinlim(momentum=0.99,
+      (librosa.util.nnls: pinv init clipped at 0, then per block of <= 1024
+      columns scipy fmin_l_bfgs_b with bounds >= 0 and m = n_fft // 2 + 1
+      on the objective normalised by the block's size), then griffinlim(momentum=0.99,
       init='random') and istft; finally / max|audio|.
   The random phase init of griffinlim is an input here (init_angles), so a
   run is reproducible and the GPU path can be checked on the same angles.
@@ -133,20 +134,56 @@ def compute_mel_spectrogram(audio, sample_rate=22050, n_fft=1024, hop_length=256
     return (2 * (db - db.min()) / (db.max() - db.min()) - 1).astype(np.float32)
 
 
-def nnls_lbfgs(A: np.ndarray, B: np.ndarray) -> np.ndarray:
-    """librosa.util.nnls for a 2-D B (one block): pinv init clipped at 0,
-    scipy.optimize.fmin_l_bfgs_b on 0.5 ||A X - B||^2 with X >= 0, m = A.shape[1]."""
+MAX_MEM_BLOCK = 2 ** 8 * 2 ** 10  # librosa.util.utils.MAX_MEM_BLOCK (256 KiB)
+
+
+def nnls_block_columns(A: np.ndarray, B: np.ndarray) -> int:
+    """librosa.util.nnls: columns per L-BFGS-B block, MAX_MEM_BLOCK //
+    (prod(B.shape[:-1]) * A.itemsize) (1024 for 64 float32 mel bands)."""
+    return max(1, int(MAX_MEM_BLOCK // (int(np.prod(B.shape[:-1])) * A.itemsize)))
+
+
+def nnls_lbfgs(A: np.ndarray, B: np.ndarray, return_info: bool = False):
+    """librosa.util.nnls (0.10) for a 2-D B: X0 = max(0, pinv(A) B) (float32,
+    as A), then per block of nnls_block_columns columns scipy's
+    fmin_l_bfgs_b(bounds >= 0, m = A.shape[1], default pgtol 1e-5 / factr 1e7)
+    on librosa's _nnls_obj: (1 / B_blk.size) * 0.5 ||A X - B_blk||^2 and its
+    gradient (1 / B_blk.size) A^T (A X - B_blk), from X0's columns.  The
+    normalisation by B.size makes the stopping test scale-free: for every
+    mel in the reference's normalised range the projected gradient at X0 is
+    below pgtol and L-BFGS-B returns X0 itself (nit 0).  return_info adds
+    the per-block scipy (nit, task)."""
     import scipy.optimize
-    x0 = np.clip(np.linalg.pinv(A) @ B, 0, None)
-    shape = x0.shape
+    x_init = np.clip(np.linalg.pinv(A) @ B, 0, None)
+    n_col = nnls_block_columns(A, B)
+    x = x_init.copy()
+    info = []
+    for s0 in range(0, B.shape[-1], n_col):
+        s1 = min(s0 + n_col, B.shape[-1])
+        Bb = B[:, s0:s1]
+        x0 = x_init[:, s0:s1]
+        shape, scale = x0.shape, 1.0 / Bb.size
 
-    def obj(x):
-        x = x.reshape(shape)
-        diff = A @ x - B
-        return 0.5 * np.sum(diff ** 2), (A.T @ diff).ravel()
+        def obj(v, shape=shape, Bb=Bb, scale=scale):
+            v = v.reshape(shape)
+            diff = A @ v - Bb
+            return scale * 0.5 * np.sum(diff ** 2), (scale * (A.T @ diff)).ravel()
 
-    x, _, _ = scipy.optimize.fmin_l_bfgs_b(obj, x0.ravel(), bounds=[(0, None)] * x0.size, m=A.shape[1])
-    return x.reshape(shape).astype(A.dtype)
+        v, _, d = scipy.optimize.fmin_l_bfgs_b(obj, x0.ravel(), bounds=[(0, None)] * x0.size, m=A.shape[1])
+        x[:, s0:s1] = v.reshape(shape)
+        info.append((int(d["nit"]), str(d["task"])))
+    x = x.astype(A.dtype)
+    return (x, info) if return_info else x
+
+
+def nnls_projected_gradient_norm(A: np.ndarray, X: np.ndarray, B: np.ndarray) -> float:
+    """L-BFGS-B's convergence measure (projgr) at X for one block: the
+    infinity norm of the projected gradient of librosa's scaled objective
+    (lower bound 0: g if g < 0 else min(x, g))."""
+    Xd, Ad = X.astype(np.float64), A.astype(np.float64)
+    g = (Ad.T @ (Ad @ Xd - B.astype(np.float64))) / B.size
+    pg = np.where(g < 0, g, np.minimum(Xd, g))
+    return float(np.abs(pg).max()) if pg.size else 0.0
 
 
 def nnls_objective(A, X, B) -> float:

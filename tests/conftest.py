@@ -59,3 +59,33 @@ def gpu():
     from m2amd import _lib
     _lib.load()
     return torch.device("cuda:0")
+
+
+def _reload_switches():
+    from m2amd import _lib
+    if _lib._lib is not None:
+        _lib.reload_switches()
+
+
+@pytest.fixture
+def monkeypatch():
+    """pytest's monkeypatch, plus: setting or deleting an M2_* developer switch
+    re-reads the library's switch table (m2_reload_switches; the library never
+    reads the environment per call), and so does the undo at teardown."""
+    mp = pytest.MonkeyPatch()
+    set0, del0 = mp.setenv, mp.delenv
+
+    def setenv(name, value, prepend=None):
+        set0(name, value, prepend)
+        if name.startswith("M2_"):
+            _reload_switches()
+
+    def delenv(name, raising=True):
+        del0(name, raising)
+        if name.startswith("M2_"):
+            _reload_switches()
+
+    mp.setenv, mp.delenv = setenv, delenv
+    yield mp
+    mp.undo()
+    _reload_switches()

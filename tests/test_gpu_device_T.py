@@ -162,6 +162,12 @@ def _dev_worker(rank, world, port, outfile):
         for i in range(2):  # B = 1 < world: rank 1's shard is empty
             mel, audio = sharded_inference(st, ids[:1].to(dev), lens[:1].to(dev))
             outs[f"one{i}"] = mel.cpu().numpy()
+        # only rank 0 holds the inputs, as host tensors: broadcast to the
+        # model's device on every rank, so both ranks take the same (device-T
+        # from the second step) path and issue the same collectives
+        for i in range(3):
+            mel, audio = sharded_inference(st, ids if rank == 0 else None, lens if rank == 0 else None, src=0)
+            outs[f"src{i}"], outs[f"srca{i}"] = mel.cpu().numpy(), audio.cpu().numpy()
         if rank == 0:
             np.savez(outfile, ids=ids.numpy(), lens=lens.numpy(), **outs)
     finally:
@@ -182,6 +188,9 @@ def test_sharded_device_T_two_ranks_gloo(gpu, tmp_path):
     mel1, _ = m.inference(ids[:1], lens[:1])
     for i in range(2):
         assert torch.equal(torch.from_numpy(z[f"one{i}"]), mel1.cpu())
+    for i in range(3):
+        assert torch.equal(torch.from_numpy(z[f"src{i}"]), torch.from_numpy(z["mel0"])), i
+        assert torch.equal(torch.from_numpy(z[f"srca{i}"]), torch.from_numpy(z["audio0"])), i
 
 
 @pytest.mark.parametrize("depth", [2, 3])
@@ -210,6 +219,33 @@ def test_sharded_pipeline_world1(gpu, depth):
     for r, k in pend:
         mel, audio = r.wait()
         assert torch.equal(mel, batches[k][2][0]) and torch.equal(audio, batches[k][2][1])
+
+
+def test_sharded_pipeline_interleaved_with_inference(gpu):
+    """Pipeline lanes use handles of their own: model.inference() on the
+    caller's stream, between submits whose steps are still in flight, shares
+    no device state (work-queue counters, frame mailbox) with them."""
+    from m2amd.parallel import ShardedPipeline
+    m = build_model("s2", gpu)
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, 42, (8, 100), generator=g).to(gpu)
+    lens = torch.randint(30, 101, (8,), generator=g).to(gpu)
+    ids2 = torch.randint(0, 42, (6, 64), generator=g).to(gpu)
+    lens2 = torch.randint(10, 65, (6,), generator=g).to(gpu)
+    ref = m.inference(ids, lens)
+    ref2 = m.inference(ids2, lens2)
+    pipe = ShardedPipeline(m, depth=2)
+    pend = []
+    for i in range(6):
+        pend.append(pipe.submit(ids, lens))
+        mel2, audio2 = m.inference(ids2, lens2)
+        assert torch.equal(mel2, ref2[0]) and torch.equal(audio2, ref2[1]), i
+        if len(pend) > 2:
+            mel, audio = pend.pop(0).wait()
+            assert torch.equal(mel, ref[0]) and torch.equal(audio, ref[1]), i
+    for r in pend:
+        mel, audio = r.wait()
+        assert torch.equal(mel, ref[0]) and torch.equal(audio, ref[1])
 
 
 @pytest.mark.parametrize("stage,B,S,scale", [("s2", 8, 100, 1.0), ("s1", 64, 128, 1.0), ("s1", 65, 128, 1.0),
@@ -246,6 +282,37 @@ def test_fused_frame_count_equals_count_kernel(gpu, stage, B, S, scale, monkeypa
     for _ in range(2):
         mel1, audio1 = m.inference(ids, lens, duration_scale=scale)
         assert torch.equal(mel0, mel1) and torch.equal(audio0, audio1)
+
+
+def test_fused_frame_count_stress(gpu, monkeypatch):
+    """The fused count's hand-off (write-through duration stores, a relaxed
+    ticket, sc1 loads by the last workgroup; duration.hip) at the kernel's
+    limit B*S = 8192 (hundreds of workgroups over all eight XCDs), 60 calls
+    back to back with new lengths every call, each equal to the separate
+    count kernel's front buffer and T_max."""
+    m = build_model("s1", gpu)
+    hm = m._hip(gpu)
+    B, S = 64, 128
+    g = torch.Generator().manual_seed(77)
+    ids = torch.randint(0, 42, (B, S), generator=g).to(gpu)
+    lens_all = [torch.randint(1, S + 1, (B,), generator=g).to(gpu) for _ in range(6)]
+    ref = []
+    monkeypatch.setenv("M2_DUR_COUNT", "0")
+    for lens in lens_all:
+        tw = torch.full((1,), -7, dtype=torch.int32, device=gpu)
+        st = hm.inference_front_dev(ids, lens, 1.0, tw)
+        torch.cuda.synchronize(gpu)
+        ref.append((st[2].clone(), int(tw.item())))
+    monkeypatch.setenv("M2_DUR_COUNT", "1")
+    words = [torch.full((1,), -7, dtype=torch.int32, device=gpu) for _ in range(60)]
+    for i in range(60):
+        st = hm.inference_front_dev(ids, lens_all[i % 6], 1.0, words[i])
+        if i % 6 == 5 or i == 59:
+            torch.cuda.synchronize(gpu)
+            assert torch.equal(st[2], ref[i % 6][0]), i
+    torch.cuda.synchronize(gpu)
+    for i in range(60):
+        assert int(words[i].item()) == ref[i % 6][1], i
 
 
 @pytest.mark.parametrize("stage,B,S", [("s2", 64, 100), ("s1", 3, 1), ("s1", 9, 31), ("s2", 5, 61), ("s1", 40, 45)])
