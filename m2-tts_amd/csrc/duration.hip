@@ -122,6 +122,89 @@ __device__ __forceinline__ void dur_conv_mfma(const float* in, const DurW<H>& W,
     }
 }
 
+// Split-f16 form of the convs (the inference path's fused-LayerNorm
+// launches when the model's static range bound allows, m2_model_create):
+// every fp32 operand as f16 hi + lo, three v_mfma_f32_16x16x32_f16 per 32-deep
+// K step (hi.hi + lo.hi + hi.lo, fp32 accumulate) - 48 cycles of matrix core
+// per K step where the exact-f32 MFMA needs 8 x 32.  Activation rows in LDS
+// as [hi: H f16 | lo: H f16 | 32 B pad] (stride dur_rs(H): conflict-free
+// ds_read_b128 of 16 rows); the weights (pack_bfrag_split of [co][tap*H + ci])
+// are the B operand: lane (output channel co, k-group g) holds 8 K elements.
+typedef unsigned dur_u32x4 __attribute__((ext_vector_type(4)));
+constexpr int dur_rs(int H) { return 4 * H + 32; }
+template <int H>
+struct DurWS {
+    dur_u32x4 w[3 * H / 32][2];
+};
+template <int H>
+__device__ __forceinline__ void dur_wload_split(const float* __restrict__ Wp, DurWS<H>& r) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave < H / 16) {
+        const dur_u32x4* p = reinterpret_cast<const dur_u32x4*>(Wp) + (size_t)wave * (3 * H / 32) * 128 + lane;
+#pragma unroll
+        for (int ks = 0; ks < 3 * H / 32; ++ks) {
+            r.w[ks][0] = p[ks * 128];
+            r.w[ks][1] = p[ks * 128 + 64];
+        }
+    }
+}
+__device__ __forceinline__ dur_f32x4 dur_mfma16(dur_u32x4 a, dur_u32x4 b, dur_f32x4 c) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+// One value as f16 hi / lo halves at row p, column k of a split row buffer.
+template <int H>
+__device__ __forceinline__ void dur_put_split(unsigned char* rows, int p, int k, float v) {
+    const _Float16 hi = (_Float16)v, lo = (_Float16)(v - (float)hi);
+    *reinterpret_cast<_Float16*>(rows + p * dur_rs(H) + 2 * k) = hi;
+    *reinterpret_cast<_Float16*>(rows + p * dur_rs(H) + 2 * H + 2 * k) = lo;
+}
+// The conv of dur_conv_mfma on split rows `in`; out: split rows (SPLIT_OUT,
+// conv1 -> conv2's input) or fp32 rows of stride H + 2 (conv2 -> projection).
+template <int H, int RBK, bool SPLIT_OUT>
+__device__ __forceinline__ void dur_conv_split(const unsigned char* in, const DurWS<H>& W, const float* __restrict__ b,
+                                               const float* __restrict__ a, const float* __restrict__ c, void* out,
+                                               int pos0, int S) {
+    constexpr int KS = 3 * H / 32, KPT = H / 32;  // K steps, K steps per tap
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    if (wave < H / 16) {
+        const int nb = wave;
+        dur_f32x4 acc[RBK];
+#pragma unroll
+        for (int rb = 0; rb < RBK; ++rb) acc[rb] = dur_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int tap = ks / KPT, ci0 = 32 * (ks - tap * KPT);
+            dur_u32x4 xh[RBK], xl[RBK];
+#pragma unroll
+            for (int rb = 0; rb < RBK; ++rb) {
+                const unsigned char* p = in + (16 * rb + i + tap) * dur_rs(H) + 2 * (ci0 + 8 * g);
+                xh[rb] = *reinterpret_cast<const dur_u32x4*>(p);
+                xl[rb] = *reinterpret_cast<const dur_u32x4*>(p + 2 * H);
+            }
+#pragma unroll
+            for (int rb = 0; rb < RBK; ++rb) acc[rb] = dur_mfma16(xh[rb], W.w[ks][0], acc[rb]);
+#pragma unroll
+            for (int rb = 0; rb < RBK; ++rb) acc[rb] = dur_mfma16(xl[rb], W.w[ks][0], acc[rb]);
+#pragma unroll
+            for (int rb = 0; rb < RBK; ++rb) acc[rb] = dur_mfma16(xh[rb], W.w[ks][1], acc[rb]);
+        }
+        const int co = nb * 16 + i;
+        const float bb = b[co], aa = a[co], cc = c[co];
+#pragma unroll
+        for (int rb = 0; rb < RBK; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * rb + 4 * g + r, s = pos0 + row;
+                float v = (acc[rb][r] + bb) * aa + cc;
+                v = v > 0.f ? v : 0.f;
+                v = (s >= 0 && s < S) ? v : 0.f;
+                if constexpr (SPLIT_OUT) dur_put_split<H>(static_cast<unsigned char*>(out), row, co, v);
+                else static_cast<float*>(out)[row * (H + 2) + co] = v;
+            }
+    }
+}
+
 __device__ __forceinline__ int32_t sat32(long long v) { return (int32_t)min(v, (long long)INT32_MAX); }
 
 // The length regulator's frame count run by the duration kernel's last
@@ -192,7 +275,7 @@ __device__ void count_frames(const float* __restrict__ dur, int B, int S, const 
 // (one wave per row, the halo rows redundantly) and stores its own 14
 // normalised rows to enc_out - the encoder output the length regulator
 // expands - in place of a separate layer_norm_kernel launch.
-template <int H, bool LN, bool COUNT, int RBK>
+template <int H, bool LN, bool COUNT, int RBK, bool SPL = false>
 __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ enc, int S, const float4* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ a1, const float* __restrict__ c1, const float4* __restrict__ w2,
@@ -201,15 +284,24 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ lng, const float* __restrict__ lnb, float* __restrict__ enc_out, DurCount dc) {
     constexpr int XS = H + 2, NT = 64 * DUR_WAVES;
     constexpr int TS = 16 * RBK - 2, NX = TS + 4;  // phonemes per tile, input rows with the halo
-    __shared__ float X[NX * XS];        // positions s0-2 .. s0+TS+1
-    __shared__ float Y1[NX * XS];       // s0-1 .. s0+TS (+2 zero rows read by conv2's unused rows)
+    static_assert(!SPL || LN, "the split convs take the fused LayerNorm's bounded rows");
+    // SPL: X and Y1 as split rows (stride dur_rs(H) bytes) in the same arrays
+    constexpr int XF = SPL ? (dur_rs(H) + 3) / 4 : XS;  // floats per row of X / Y1
+    __shared__ __attribute__((aligned(16))) float X[NX * XF];   // positions s0-2 .. s0+TS+1
+    __shared__ __attribute__((aligned(16))) float Y1[NX * XF];  // s0-1 .. s0+TS (+2 zero rows read by conv2's unused rows)
     __shared__ float Y2[16 * RBK * XS];  // s0 .. s0+TS-1 (+2 unused)
     const int b = blockIdx.y, s0 = blockIdx.x * TS, tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const float* e = enc + (size_t)b * S * H;
     DurW<H> W1, W2;
-    dur_wload<H>(w1, W1);
-    dur_wload<H>(w2, W2);
+    DurWS<H> V1, V2;
+    if constexpr (SPL) {
+        dur_wload_split<H>(reinterpret_cast<const float*>(w1), V1);
+        dur_wload_split<H>(reinterpret_cast<const float*>(w2), V2);
+    } else {
+        dur_wload<H>(w1, W1);
+        dur_wload<H>(w2, W2);
+    }
     if constexpr (LN) {
         // every row of this wave is loaded before the first is normalised (one
         // memory round trip per wave instead of one per row)
@@ -226,7 +318,7 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
         for (int j = 0; j < NR; ++j) {
             const int p = wave + j * DUR_WAVES, s = s0 - 2 + p;
             if (p >= NX) break;
-            float* d = X + p * XS;
+            float* d = X + p * XF;
             if (s >= 0 && s < S) {
                 float mean, rstd;
                 ln_row_stats_regs<KP>(xv[j], H, lane, mean, rstd);
@@ -236,12 +328,16 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
                     const int k = lane + 64 * q;
                     if (k < H) {
                         const float y = ln_apply(xv[j][q], mean, rstd, lng[k], lnb[k]);
-                        d[k] = y;
+                        if constexpr (SPL) dur_put_split<H>(reinterpret_cast<unsigned char*>(X), p, k, y);
+                        else d[k] = y;
                         if (yo) yo[k] = y;
                     }
                 }
             } else {
-                for (int k = lane; k < H; k += 64) d[k] = 0.f;
+                for (int k = lane; k < H; k += 64) {
+                    if constexpr (SPL) dur_put_split<H>(reinterpret_cast<unsigned char*>(X), p, k, 0.f);
+                    else d[k] = 0.f;
+                }
             }
         }
     } else {
@@ -253,11 +349,17 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
     }
-    for (int idx = tid; idx < 2 * XS; idx += NT) Y1[16 * RBK * XS + idx] = 0.f;
+    for (int idx = tid; idx < 2 * XF; idx += NT) Y1[16 * RBK * XF + idx] = 0.f;
     __syncthreads();
-    dur_conv_mfma<H, RBK>(X, W1, b1, a1, c1, Y1, s0 - 1, S);
-    __syncthreads();
-    dur_conv_mfma<H, RBK>(Y1, W2, b2, a2, c2, Y2, s0, S);
+    if constexpr (SPL) {
+        dur_conv_split<H, RBK, true>(reinterpret_cast<const unsigned char*>(X), V1, b1, a1, c1, Y1, s0 - 1, S);
+        __syncthreads();
+        dur_conv_split<H, RBK, false>(reinterpret_cast<const unsigned char*>(Y1), V2, b2, a2, c2, Y2, s0, S);
+    } else {
+        dur_conv_mfma<H, RBK>(X, W1, b1, a1, c1, Y1, s0 - 1, S);
+        __syncthreads();
+        dur_conv_mfma<H, RBK>(Y1, W2, b2, a2, c2, Y2, s0, S);
+    }
     __syncthreads();
     // k=1 projection H -> 1: one wave per phoneme, shuffle reduction.
     for (int p = wave; p < TS; p += DUR_WAVES) {
@@ -434,7 +536,8 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict_
 // p: w1 (packed), b1, alpha1, beta1, w2 (packed), b2, alpha2, beta2, proj_w, proj_b
 namespace {
 int32_t duration_launch(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st,
-                        const float* ln_g, const float* ln_b, float* enc_out, const DurCount* dc) {
+                        const float* ln_g, const float* ln_b, float* enc_out, const DurCount* dc,
+                        const float* const* wsplit) {
     if (B == 0 || S == 0) return M2_OK;
     // 14-phoneme tiles (one 16-position row block per wave) while they fit one
     // round of the CUs; beyond, 30-phoneme tiles (two row blocks sharing each
@@ -445,19 +548,27 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
     const dim3 grid(cdiv(S, 16 * rbk - 2), B), blk(64 * DUR_WAVES);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
     const DurCount none{};
-#define M2_DUR_L(HH, LL, CC, RR)                                                                                   \
-    hipLaunchKernelGGL((duration_kernel<HH, LL, CC, RR>), grid, blk, 0, st, enc, S, f4(p[0]), p[1], p[2], p[3],     \
-                       f4(p[4]), p[5], p[6], p[7], p[8], p[9], dur, LL ? ln_g : nullptr, LL ? ln_b : nullptr,        \
-                       LL ? enc_out : nullptr, dc ? *dc : none)
-#define M2_DUR_R(HH, LL, CC)                      \
-    if (rbk == 2) M2_DUR_L(HH, LL, CC, 2);        \
-    else M2_DUR_L(HH, LL, CC, 1)
-#define M2_DUR(HH)                                            \
-    case HH:                                                  \
-        if (enc_out && dc) M2_DUR_R(HH, true, true);          \
-        else if (enc_out) M2_DUR_R(HH, true, false);          \
-        else if (dc) M2_DUR_R(HH, false, true);               \
-        else M2_DUR_R(HH, false, false);                      \
+    // split-f16 convs: the fused-LayerNorm (inference) launches of a model
+    // whose static bound allows them (wsplit = its split weight packs)
+    const bool spl = wsplit && enc_out;
+#define M2_DUR_L(HH, LL, CC, RR, SP)                                                                                \
+    hipLaunchKernelGGL((duration_kernel<HH, LL, CC, RR, SP>), grid, blk, 0, st, enc, S,                          \
+                       f4(SP ? wsplit[0] : p[0]), p[1], p[2], p[3], f4(SP ? wsplit[1] : p[4]), p[5], p[6], p[7],    \
+                       p[8], p[9], dur, LL ? ln_g : nullptr, LL ? ln_b : nullptr, LL ? enc_out : nullptr,           \
+                       dc ? *dc : none)
+#define M2_DUR_R(HH, LL, CC, SP)                      \
+    if (rbk == 2) M2_DUR_L(HH, LL, CC, 2, SP);        \
+    else M2_DUR_L(HH, LL, CC, 1, SP)
+#define M2_DUR(HH)                                                      \
+    case HH:                                                            \
+        if (enc_out && dc) {                                            \
+            if (spl) M2_DUR_R(HH, true, true, true);                    \
+            else M2_DUR_R(HH, true, true, false);                       \
+        } else if (enc_out) {                                           \
+            if (spl) M2_DUR_R(HH, true, false, true);                   \
+            else M2_DUR_R(HH, true, false, false);                      \
+        } else if (dc) M2_DUR_R(HH, false, true, false);                \
+        else M2_DUR_R(HH, false, false, false);                         \
         break;
     switch (H) {
         M2_DUR(32)
@@ -476,8 +587,8 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
 
 // p: w1 (packed), b1, alpha1, beta1, w2 (packed), b2, alpha2, beta2, proj_w, proj_b
 int32_t launch_duration(const float* enc, int B, int S, int H, const float* const* p, float* dur, hipStream_t st,
-                        const float* ln_g, const float* ln_b, float* enc_out) {
-    return duration_launch(enc, B, S, H, p, dur, st, ln_g, ln_b, enc_out, nullptr);
+                        const float* ln_g, const float* ln_b, float* enc_out, const float* const* wsplit) {
+    return duration_launch(enc, B, S, H, p, dur, st, ln_g, ln_b, enc_out, nullptr, wsplit);
 }
 
 // The same launch with the length regulator's count (lr_count_kernel<true>'s
@@ -487,10 +598,11 @@ bool duration_count_fusable(int B, int S) { return B > 0 && S > 0 && (long)B * S
 
 int32_t launch_duration_count(const float* enc, int B, int S, int H, const float* const* p, float* dur,
                               hipStream_t st, const float* ln_g, const float* ln_b, float* enc_out, float scale,
-                              int32_t* cum, int32_t* T, int32_t* Tmax, unsigned* ticket, int32_t* mbox, int32_t seq) {
+                              int32_t* cum, int32_t* T, int32_t* Tmax, unsigned* ticket, int32_t* mbox, int32_t seq,
+                              const float* const* wsplit) {
     M2_CHECK_ARG(B > 0 && S > 0 && (long)B * S <= kDurCountMax, "duration + count: batch too large to fuse");
     const DurCount dc{scale, cum, T, Tmax, ticket, mbox, seq};
-    return duration_launch(enc, B, S, H, p, dur, st, ln_g, ln_b, enc_out, &dc);
+    return duration_launch(enc, B, S, H, p, dur, st, ln_g, ln_b, enc_out, &dc, wsplit);
 }
 
 int32_t launch_lr_count(const void* dur, int is_int, float scale, int B, int S, int32_t* cum,

@@ -47,6 +47,8 @@ struct Switches {
     bool tailp2_seven = false;  // M2_TAILP2_SEVEN
     bool head_inconv = false;   // M2_HEAD_INCONV
     bool s2_head_tf16 = false;  // M2_S2_HEAD_TF16
+    int redo_grid = -1;         // M2_REDO_GRID: workgroups of the guarded redo launch (-1: one per CU)
+    bool dur_split = true;      // M2_DUR_SPLIT=0: the duration convs on the exact-f32 MFMA always
 };
 const Switches& sw();
 void reload_switches();

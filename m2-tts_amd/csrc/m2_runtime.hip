@@ -68,6 +68,8 @@ void reload_switches() {
     s.tailp2_seven = env_set("M2_TAILP2_SEVEN");
     s.head_inconv = env_set("M2_HEAD_INCONV");
     s.s2_head_tf16 = env_set("M2_S2_HEAD_TF16");
+    s.redo_grid = env_int("M2_REDO_GRID", -1);
+    s.dur_split = env_on("M2_DUR_SPLIT", true);
     g_sw = s;
 }
 
@@ -80,9 +82,11 @@ int32_t launch_linear(const float*, const float*, const float*, const float*, co
 // force_f32: the exact-f32 MFMA attention (a model whose q/k/v bound is outside the split-f16 range)
 int32_t launch_attention(const float*, const uint8_t*, int, int, int, int, float*, hipStream_t, bool force_f32 = false);
 int32_t launch_duration(const float*, int, int, int, const float* const*, float*, hipStream_t,
-                        const float* ln_g = nullptr, const float* ln_b = nullptr, float* enc_out = nullptr);
+                        const float* ln_g = nullptr, const float* ln_b = nullptr, float* enc_out = nullptr,
+                        const float* const* wsplit = nullptr);
 int32_t launch_duration_count(const float*, int, int, int, const float* const*, float*, hipStream_t, const float*,
-                              const float*, float*, float, int32_t*, int32_t*, int32_t*, unsigned*, int32_t*, int32_t);
+                              const float*, float*, float, int32_t*, int32_t*, int32_t*, unsigned*, int32_t*, int32_t,
+                              const float* const* wsplit = nullptr);
 bool duration_count_fusable(int, int);
 int32_t launch_lr_count(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int32_t launch_lr_count_sync(const void*, int, float, int, int, int32_t*, int32_t*, int32_t*, unsigned*, int32_t*,
@@ -218,6 +222,10 @@ struct m2_model {
     std::vector<m2_layer_w> enc, dec;
     const float *emb = nullptr, *pe = nullptr, *enc_nw = nullptr, *enc_nb = nullptr;
     const float* dur[10] = {};  // w1,b1,alpha1,beta1, w2,b2,alpha2,beta2, proj_w, proj_b
+    // the duration convs' split-f16 fragments, used on the inference path
+    // (fused final LayerNorm) when the static range bound allows (dur_split)
+    const float* dur_split_w[2] = {};
+    bool dur_split = false;
     const float *dec_nw = nullptr, *dec_nb = nullptr, *mel_w = nullptr, *mel_b = nullptr;
     const float* mel_p = nullptr;  // packed mel projection (fused path)
     bool tfused = false;           // transformer layers on ln_gemm + attention + post_attn
@@ -582,6 +590,9 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     const size_t dw_off = total;  // duration conv weights, B-fragment order, 2 layers
     total += 2 * 3 * (size_t)H * H;
     total = align_up(total, 64);
+    const size_t dws_off = total;  // the same as split-f16 hi/lo fragments (pack_bfrag_split)
+    total += 2 * 3 * (size_t)H * H;
+    total = align_up(total, 64);
     const size_t tf_off = total;  // fused-layer B-fragment packs: 8H^2 per layer + mel projection
     const int n_layers = cfg->text_encoder_layers + cfg->decoder_layers;
     total += (size_t)n_layers * 8 * H * H + (size_t)cfg->mel_channels * H;
@@ -627,8 +638,12 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             host[(2 * j + 1) * H + c] = bnb[c] - bnm[c] * a;
         }
     }
-    // Duration convs: W[co][ci][tap] -> GEMM B matrix [co][tap*H + ci] -> B-fragment order.
-    std::vector<float> dpack(2 * 3 * (size_t)H * H);
+    // Duration convs: W[co][ci][tap] -> GEMM B matrix [co][tap*H + ci] -> B-fragment order
+    // (exact-f32 MFMA) and split-f16 hi/lo fragments (v_mfma_f32_16x16x32_f16).
+    std::vector<float> dpack(2 * 3 * (size_t)H * H), dspack(2 * 3 * (size_t)H * H);
+    bool dsplit = true;
+    double dconv_rows[2] = {0.0, 0.0};  // max over co of sum_{ci, tap} |W[co][ci][tap]|
+    std::vector<float> dconv_bias[2];
     for (int j = 0; j < 2; ++j) {
         const std::string n = "duration_predictor.predictor.conv_layers." + std::to_string(j) + ".conv.weight";
         std::vector<float> w((size_t)3 * H * H), wt((size_t)3 * H * H);
@@ -640,9 +655,49 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 for (int k = 0; k < 3; ++k) wt[(size_t)co * 3 * H + k * H + ci] = w[((size_t)co * H + ci) * 3 + k];
         const std::vector<float> pk = pack_bfrag(wt.data(), H, 3 * H);
         std::copy(pk.begin(), pk.end(), dpack.begin() + (size_t)j * 3 * H * H);
+        std::vector<float> pks;
+        if (pack_bfrag_split(wt.data(), H, 3 * H, &pks)) std::copy(pks.begin(), pks.end(), dspack.begin() + (size_t)j * 3 * H * H);
+        else dsplit = false;
+        for (int co = 0; co < H; ++co) {
+            double r = 0.0;
+            for (int k = 0; k < 3 * H; ++k) r += std::fabs((double)wt[(size_t)co * 3 * H + k]);
+            dconv_rows[j] = std::max(dconv_rows[j], r);
+        }
+        dconv_bias[j].resize(H);
+        const std::string nb = "duration_predictor.predictor.conv_layers." + std::to_string(j) + ".conv.bias";
+        e = hipMemcpyAsync(dconv_bias[j].data(), weights[idx(nb)], H * sizeof(float), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return bail(e, "hipMemcpyAsync(duration conv bias)");
     }
     e = hipMemcpyAsync(m->buf + dw_off, dpack.data(), dpack.size() * sizeof(float), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return bail(e, "hipMemcpyAsync(duration pack)");
+    e = hipMemcpyAsync(m->buf + dws_off, dspack.data(), dspack.size() * sizeof(float), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return bail(e, "hipMemcpyAsync(duration split pack)");
+    // Split-f16 range of the duration convs on the inference path, where their
+    // input is the encoder's final LayerNorm (|LN| <= sqrt(H-1) max|gamma| +
+    // max|beta|) and conv2's input is BN(conv1) after ReLU (<= max|alpha| (row
+    // sum |W1| x that + max|b1|) + max|beta'|): checked once here against half
+    // the f16 range, as the transformer's bound below; outside it (or with a
+    // weight outside the f16 range) the exact-f32 MFMA convs stay.
+    {
+        std::vector<float> g(H), bb(H);
+        e = hipMemcpyAsync(g.data(), weights[idx("text_encoder.norm.weight")], H * sizeof(float), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(bb.data(), weights[idx("text_encoder.norm.bias")], H * sizeof(float), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return bail(e, "hipMemcpyAsync(encoder norm)");
+        double ga = 0.0, ba = 0.0, b1a = 0.0, a1a = 0.0, c1a = 0.0;
+        for (int c = 0; c < H; ++c) {
+            ga = std::max(ga, (double)std::fabs(g[c]));
+            ba = std::max(ba, (double)std::fabs(bb[c]));
+            b1a = std::max(b1a, (double)std::fabs(dconv_bias[0][c]));
+            a1a = std::max(a1a, (double)std::fabs(host[c]));
+            c1a = std::max(c1a, (double)std::fabs(host[H + c]));
+        }
+        const double x0 = std::sqrt((double)std::max(H - 1, 1)) * ga + ba;
+        const double x1 = a1a * (dconv_rows[0] * x0 + b1a) + c1a;
+        m->dur_split = dsplit && x0 < 32768.0 && x1 < 32768.0;
+    }
     e = hipMemcpyAsync(m->buf + bn_off, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return bail(e, "hipMemcpyAsync(bn up)");
     e = hipStreamSynchronize(st);
@@ -752,6 +807,8 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
         m->dur[4 * j + 2] = m->buf + bn_off + (2 * j) * H;
         m->dur[4 * j + 3] = m->buf + bn_off + (2 * j + 1) * H;
     }
+    m->dur_split_w[0] = m->buf + dws_off;
+    m->dur_split_w[1] = m->buf + dws_off + (size_t)3 * H * H;
     m->dur[8] = P("duration_predictor.predictor.projection.weight");
     m->dur[9] = P("duration_predictor.predictor.projection.bias");
     m->dec_nw = P("decoder.norm.weight");
@@ -1692,11 +1749,13 @@ int32_t front_run(const m2_model* m, const int64_t* ids, const int64_t* lengths,
             return rc;
         // the encoder's final LayerNorm runs inside the duration kernel, which
         // also stores the normalised encoder output (f.enc)
+        // (split-f16 convs when the static range bound allows: dur_split)
+        const float* const* ws = m->dur_split && sw().dur_split ? m->dur_split_w : nullptr;
         if (fuse && fuse_count(B, S))
             return launch_duration_count(x, B, S, m->cfg.hidden_dim, m->dur, f->dur, st, m->enc_nw, m->enc_nb, f->enc,
                                          fuse->scale, f->cum, f->tot, fuse->Tmax ? fuse->Tmax : f->tmax,
-                                         fuse->ticket, fuse->mbox, fuse->seq);
-        if ((rc = launch_duration(x, B, S, m->cfg.hidden_dim, m->dur, f->dur, st, m->enc_nw, m->enc_nb, f->enc)))
+                                         fuse->ticket, fuse->mbox, fuse->seq, ws);
+        if ((rc = launch_duration(x, B, S, m->cfg.hidden_dim, m->dur, f->dur, st, m->enc_nw, m->enc_nb, f->enc, ws)))
             return rc;
     }
     // Round 1's fused count (per-utterance tickets behind release fences: one

@@ -676,6 +676,26 @@ struct QsGeo {
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// A raw buffer descriptor of a wave-uniform base address (the staging loads
+// of the query-split attention: per-lane offset in a VGPR, step in an SGPR).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const unsigned char* base) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)base >> 32));
+    void* p = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7ffffff0, 0x00020000);
+}
+// Lean unmasked softmax: true when a weight of the step exceeds 2^kLazyT,
+// read from the f16 hi halves of P (8 packed words, packed maxima).
+__device__ __forceinline__ bool p_hi_exceeds(u32x4 a, u32x4 b) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    h2 mx = __builtin_elementwise_max(__builtin_bit_cast(h2, a[0]), __builtin_bit_cast(h2, a[1]));
+    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_bit_cast(h2, a[2]), __builtin_bit_cast(h2, a[3])));
+    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_bit_cast(h2, b[0]), __builtin_bit_cast(h2, b[1])));
+    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_bit_cast(h2, b[2]), __builtin_bit_cast(h2, b[3])));
+    constexpr float lim = (float)(1 << (int)kLazyT);
+    return (float)mx.x > lim || (float)mx.y > lim;
+}
+
 // LEAN (M2_TFL_QS2=4): the lean softmax of attention_qsplit2 (C = -m
 // accumulators when unmasked, row sums by MFMA on an all-ones fragment).
 template <int H, int HD, bool MASKED, bool LEAN = false>
@@ -707,25 +727,26 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
             qxl = lane < 32 ? *reinterpret_cast<const u32x4*>(qp + G::TAIL + 512) : z;
         }
     }
-    // the global source of piece i (16 B) of 64-key step 0: [chunk][head][K blocks | V^T chunk]
-    const unsigned char* src[PPT];
-    int step[PPT];  // bytes from one 64-key step to the next for that piece
+    // the global source of piece i (16 B) of 64-key step 0: [chunk][head][K blocks | V^T chunk],
+    // through a buffer descriptor of its region (a wave's 1-KB piece lies in
+    // one K or V^T region): per-lane offset fixed, the step's advance scalar
+    __amdgpu_buffer_rsrc_t rsrc[PPT];
+    int sstep[PPT];  // bytes from one 64-key step to the next for that piece
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
         const int o = 16 * (tid + NW * 64 * i), j = o / CB, oc = o - j * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
         const size_t bh = (size_t)b * HEADS + hh;
-        if (r < Q::KB) {
-            src[i] = kb + (bh * (npad / 16) + 2 * j) * QKBLK + r;
-            step[i] = 4 * QKBLK;
-        } else {
-            src[i] = vb + (bh * nch + j) * G::VCH + (r - Q::KB);
-            step[i] = 2 * G::VCH;
-        }
+        const bool isk = r < Q::KB;
+        const unsigned char* base = isk ? kb + (bh * (npad / 16) + 2 * j) * QKBLK + (r & ~1023)
+                                        : vb + (bh * nch + j) * G::VCH + ((r - Q::KB) & ~1023);
+        rsrc[i] = wave_rsrc(base);
+        sstep[i] = __builtin_amdgcn_readfirstlane(isk ? 4 * QKBLK : 2 * G::VCH);
     }
     u32x4 pre[PPT];
     auto gload = [&](int p) {
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * step[i]);
+        for (int i = 0; i < PPT; ++i)
+            pre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc[i], 16 * lane, p * sstep[i], 0));
     };
     auto lstore = [&](int buf) {
 #pragma unroll
@@ -787,13 +808,81 @@ __device__ __forceinline__ void attention_qsplit(const unsigned char* __restrict
                     for (int r = 0; r < 4; ++r)
                         s[j][u][r] = k0 + 32 * j + 16 * u + 4 * g + r < N ? s[j][u][r] : -INFINITY;
         }
-        float cmax = s[0][0][0];
+        auto step_max = [&]() {
+            float c = s[0][0][0];
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+                for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) cmax = fmaxf(cmax, s[j][u][r]);
+                    for (int r = 0; r < 4; ++r) c = fmaxf(c, s[j][u][r]);
+            return c;
+        };
+        if constexpr (LEAN && !MASKED) {
+            // as attention_qsplit2's lean form: the base from the first step's
+            // maximum, later moves detected on the f16 hi halves of P
+            if (fresh) {  // wave-uniform
+                const float cm = grp4_max(step_max());  // finite: the step's first chunk has a live key
+                m = cm;
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[j][u][r] -= cm;
+                fresh = false;
+            }
+            u32x4 bh4[2], bl4[2];
+            auto exp_split = [&]() {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    float e[2][4];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[j][u][r]);
+                    unsigned ph[4], pl[4];
+                    split2u(e[0][0], e[0][1], ph[0], pl[0]);
+                    split2u(e[0][2], e[0][3], ph[1], pl[1]);
+                    split2u(e[1][0], e[1][1], ph[2], pl[2]);
+                    split2u(e[1][2], e[1][3], ph[3], pl[3]);
+                    bh4[j] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+                    bl4[j] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+                }
+            };
+            exp_split();
+            if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // wave-uniform: move the base
+                const float d = vmax(grp4_max(step_max()), 0.f);
+                m += d;
+                const float corr = __builtin_amdgcn_exp2f(-d);
+                lacc *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[t] *= corr;
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[j][u][r] -= d;
+                exp_split();
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                lacc = mfma(ones, bh4[j], lacc);
+                lacc = mfma(ones, bl4[j], lacc);
+                const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+                    const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+                    acc[t] = mfma(vh, bh4[j], acc[t]);
+                    acc[t] = mfma(vh, bl4[j], acc[t]);
+                    acc[t] = mfma(vl, bh4[j], acc[t]);
+                }
+            }
+            return;
+        }
+        const float cmax = step_max();
         if constexpr (MASKED) {
             const float mn = vmax(m, grp4_max(cmax));
             const float corr = __builtin_amdgcn_exp2f(m - mn);
@@ -957,25 +1046,29 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
             qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
         }
     }
-    // the staging of a 64-key step into LDS: as attention_qsplit
-    const unsigned char* src[PPT];
-    int step[PPT];
+    // the staging of a 64-key step into LDS: as attention_qsplit, but every
+    // piece through a buffer descriptor of its region (a wave's 1-KB piece
+    // lies in one K or V^T region: the region bytes are multiples of 1 KB),
+    // so a step's loads take the per-lane offset from a fixed VGPR and the
+    // step's advance from an SGPR - no 64-bit address arithmetic per step
+    __amdgpu_buffer_rsrc_t rsrc[PPT];
+    int voff[PPT], sstep[PPT];
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
         const int o = 16 * (tid + NW * 64 * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
         const size_t bh = (size_t)b * HEADS + hh;
-        if (r < Q::KB) {
-            src[i] = kb + (bh * (npad / 16) + 2 * jj) * QKBLK + r;
-            step[i] = 4 * QKBLK;
-        } else {
-            src[i] = vb + (bh * nch + jj) * G::VCH + (r - Q::KB);
-            step[i] = 2 * G::VCH;
-        }
+        const bool isk = r < Q::KB;
+        const unsigned char* base = isk ? kb + (bh * (npad / 16) + 2 * jj) * QKBLK + (r & ~1023)
+                                        : vb + (bh * nch + jj) * G::VCH + ((r - Q::KB) & ~1023);
+        rsrc[i] = wave_rsrc(base);
+        voff[i] = 16 * lane;
+        sstep[i] = __builtin_amdgcn_readfirstlane(isk ? 4 * QKBLK : 2 * G::VCH);
     }
     u32x4 pre[PPT];
     auto gload = [&](int p) {
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * step[i]);
+        for (int i = 0; i < PPT; ++i)
+            pre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc[i], voff[i], p * sstep[i], 0));
     };
     auto lstore = [&](int buf) {
 #pragma unroll
@@ -1052,11 +1145,88 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
                     for (int qq = 0; qq < 2; ++qq)
                         s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
         }
+        auto chunk_max = [&](int qq) {
+            return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
+                         fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+        };
+        if constexpr (LEAN && !MASKED) {
+            // the scores arrive relative to the base.  First chunk: the base is
+            // the chunk's maximum.  Later: the base moves only when some weight
+            // exceeds 2^kLazyT, detected AFTER the exponentials on the f16 hi
+            // halves of P (packed maxima: ~10 VALU in place of the ~23 of a
+            // per-score maximum before them); then, rarely, the exponentials
+            // are recomputed from the kept scores.
+            if (fresh) {  // wave-uniform
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
+                    m[qq] = cm;
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
+                }
+                fresh = false;
+            }
+            u32x4 bh4[2], bl4[2];
+            auto exp_split = [&]() {
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    float e[2][4];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+                    unsigned ph[4], pl[4];
+                    split2u(e[0][0], e[0][1], ph[0], pl[0]);
+                    split2u(e[0][2], e[0][3], ph[1], pl[1]);
+                    split2u(e[1][0], e[1][1], ph[2], pl[2]);
+                    split2u(e[1][2], e[1][3], ph[3], pl[3]);
+                    bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+                    bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+                }
+            };
+            exp_split();
+            {
+                if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // wave-uniform: move the base
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq) {
+                        const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
+                        m[qq] += d;
+                        const float corr = __builtin_amdgcn_exp2f(-d);
+                        lacc[qq] *= corr;
+#pragma unroll
+                        for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+#pragma unroll
+                        for (int u = 0; u < 2; ++u)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
+                    }
+                    exp_split();
+                }
+            }
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
+                lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
+            }
+            const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+                const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
+                    acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
+                    acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
+                }
+            }
+            return;
+        }
         float cmax[2];
 #pragma unroll
-        for (int qq = 0; qq < 2; ++qq)
-            cmax[qq] = fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
-                             fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+        for (int qq = 0; qq < 2; ++qq) cmax[qq] = chunk_max(qq);
         if constexpr (MASKED) {
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {

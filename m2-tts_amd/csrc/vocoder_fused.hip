@@ -624,17 +624,22 @@ int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, floa
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
     constexpr int threads = Cfg::WAVES * 64;
     constexpr size_t lds = 4 * (size_t)std::max(std::max(HP::LDS_FLOATS, MP::LDS_FLOATS), TP::LDS_FLOATS);
-    static int grid = 0;
-    if (!grid) {
+    static int full = 0, cus = 0;
+    if (!full) {
         int32_t rc;
         if ((rc = set_lds(voc_redo_kernel<Cfg, false>, lds))) return rc;
         if ((rc = set_lds(voc_redo_kernel<Cfg, true>, lds))) return rc;
-        int occ = 0, dev = 0, cus = 0;
+        int occ = 0, dev = 0;
         M2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, voc_redo_kernel<Cfg, false>, threads, lds));
         M2_HIP(hipGetDevice(&dev));
         M2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        grid = std::max(1, occ) * std::max(1, cus);
+        cus = std::max(1, cus);
+        full = std::max(1, occ) * cus;
     }
+    // workgroups of the (usually empty) launch: one per CU by default; the
+    // ordered queue needs no co-residency, so any count is correct
+    // (M2_REDO_GRID=n forces n, 0 = every resident slot)
+    const int grid = sw().redo_grid < 0 ? cus : (sw().redo_grid == 0 ? full : sw().redo_grid);
     unsigned* q = const_cast<unsigned*>(reinterpret_cast<const unsigned*>(w.guard_queue));
     if (trans)
         hipLaunchKernelGGL((voc_redo_kernel<Cfg, true>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2, audio,

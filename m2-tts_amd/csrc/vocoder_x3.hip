@@ -95,17 +95,18 @@ constexpr int nkb_of() { return (NTAP * (CIN / 8) + 3) / 4; }
 // already issued the loads of k-blocks 0 .. PD-1 (the previous layer's item
 // did, before its epilogue and the barrier); wp_next (PD == 4, NMB == 1): once
 // this item's last MFMA is issued, start the next item's first PD k-blocks.
-template <int CIN, int NTAP, int NMB>
+template <int CIN, int NTAP, int NMB, int PDM = 4>
 constexpr int pd_of() {
     constexpr int NKB = (NTAP * (CIN / 8) + 3) / 4;
-    return NKB < 4 / NMB ? NKB : 4 / NMB;
+    return NKB < PDM / NMB ? NKB : PDM / NMB;
 }
 // TB: tap k's rows start at tb[k] (this lane's row, before the lane-group
 // offset) instead of bp + k*STEP*RSI - the phase-planar layouts of the head.
-template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE, bool TB = false>
+template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE, bool TB = false,
+          int PDM = 4>
 __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
                                        const unsigned char* xr, f32x4 (&acc)[NMB][NT],
-                                       u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2], const u32x4* wp_next,
+                                       u32x4 (&a)[pd_of<CIN, NTAP, NMB, PDM>()][NMB][2], const u32x4* wp_next,
                                        const unsigned char* const* tb = nullptr) {
     constexpr int NOCT = CIN / 8, NK = NTAP * NOCT, NKB = (NK + 3) / 4;
     static_assert(CIN % 8 == 0 && (NOCT <= 2 || NOCT % 4 == 0), "channel count must be 8, 16 or a multiple of 32");
@@ -125,10 +126,11 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
     const unsigned char* b_last = o_last < NK ? bl + koff(NKB - 1)
                                               : (XR ? xr + (o_last - NK) * 16 : bp + koff(NKB - 1));
     // Weight fragments stream PD k-blocks ahead (PD = all of them up to
-    // 4 / NMB): one L2 round trip per item rather than one per k-block (a
-    // k-block is only 3*NT*NMB MFMAs, shorter than an L2 hit), at most 32
-    // VGPRs in flight.
-    constexpr int PD = pd_of<CIN, NTAP, NMB>();
+    // PDM / NMB): one L2 round trip per item rather than one per k-block (a
+    // k-block is only 3*NT*NMB MFMAs, shorter than an L2 hit), at most
+    // 8 * PDM VGPRs in flight (PDM = 4 where the register budget is 128 per
+    // wave, the config's PDM where it is 256: the stage2 kernels).
+    constexpr int PD = pd_of<CIN, NTAP, NMB, PDM>();
     if (!PRE)
 #pragma unroll
     for (int kb = 0; kb < PD; ++kb)
@@ -243,10 +245,10 @@ constexpr bool kFold = res_fold_channels(C);
 // corr (the composed stage2 head): per-(phase, channel) terms subtracted from
 // the outputs of input column qe (an utterance edge), before the activation.
 template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int ACT, bool RES, bool XR, int RR,
-          int JMAX, int NMB, bool PRE, bool GO = false>
+          int JMAX, int NMB, bool PRE, bool GO = false, int PDM = 4>
 __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
                                          const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
-                                         int ph, int tile0, int L, u32x4 (&a)[pd_of<CIN, NTAP, NMB>()][NMB][2],
+                                         int ph, int tile0, int L, u32x4 (&a)[pd_of<CIN, NTAP, NMB, PDM>()][NMB][2],
                                          const u32x4* wp_next, unsigned char* gout = nullptr,
                                          const unsigned char* corr = nullptr, int qe = 0) {
     constexpr int WS = nkb_of<CIN, NTAP>() * 128;  // u32x4 between consecutive m-blocks' weights
@@ -259,7 +261,7 @@ __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const flo
 #pragma unroll
         for (int n = 0; n < NTT; ++n) acc[m][n] = bv;
     }
-    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR, NMB, WS, PRE>(wp, bp, xr, acc, a, wp_next);
+    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR, NMB, WS, PRE, false, PDM>(wp, bp, xr, acc, a, wp_next);
     const bool edge = (p0 + tile0 * 16) * RR < 0 || (p0 + (tile0 + NTT) * 16) * RR > L;
     const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
     if (corr) {  // wave-uniform
@@ -337,7 +339,7 @@ struct ConvTItems {
 // 8/16 channels, read back in the epilogue otherwise.
 // GO: store the output tiles to global rows (gout) instead of `out`.
 template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS, int NMB = 1, int ONE = 0,
-          bool GO = false>
+          bool GO = false, int PDM = 4>
 __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
                                        int a0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr,
                                        unsigned char* gout = nullptr) {
@@ -357,16 +359,16 @@ __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float
         const u32x4* wp = IT::wp(Wp, item);
         const unsigned char* bp = in.p + (p - 1 - in.start) * RSI;
         const unsigned char* xr = out.p + (p - out.start) * RSO;
-        u32x4 al[pd_of<CIN, 3, NMB>()][NMB][2];
+        u32x4 al[pd_of<CIN, 3, NMB, PDM>()][NMB][2];
         auto& a = [&]() -> auto& {
             if constexpr (PRE) return *ap;
             else return al;
         }();
         if (nt == CH::QHI)
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO>(
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO, PDM>(
                 wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next, gout);
         else
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO>(
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO, PDM>(
                 wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next, gout);
     };
     if constexpr (ONE) {
@@ -381,7 +383,7 @@ __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float
 // leaky(ConvTranspose1d(k=2R, stride R, pad R/2)): inputs q in [q0, q0+NQ)
 // give outputs t = q*R + ph.  Phase ph reads taps (q, q-1) if ph + R/2 < R,
 // else (q+1, q): B base row q + d0, tap k at row q + d0 - k.
-template <int CIN, int COUT, int R, int NT, int RSI, int RSO, int NQ, int NMB = 1, int ONE = 0>
+template <int CIN, int COUT, int R, int NT, int RSI, int RSO, int NQ, int NMB = 1, int ONE = 0, int PDM = 4>
 __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
                                        int q0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr) {
     using IT = ConvTItems<CIN, COUT, R, NT, NQ, NMB>;
@@ -398,16 +400,16 @@ __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float
         const int co0 = mb * 16 + 4 * g;
         const u32x4* wp = IT::wp(Wp, item);
         const unsigned char* bp = in.p + (q0 + tile0 * 16 + li + d0 - in.start) * RSI;
-        u32x4 al[pd_of<CIN, 2, NMB>()][NMB][2];
+        u32x4 al[pd_of<CIN, 2, NMB, PDM>()][NMB][2];
         auto& a = [&]() -> auto& {
             if constexpr (PRE) return *ap;
             else return al;
         }();
         if (nt == CH::QHI)
-            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, NMB, PRE>(
+            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, NMB, PRE, false, PDM>(
                 wp, bias, bp, nullptr, out, co0, q0, ph, tile0, L, a, wp_next);
         else
-            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, NMB, PRE>(
+            run_item<CIN, COUT, 2, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, NMB, PRE, false, PDM>(
                 wp, bias, bp, nullptr, out, co0, q0, ph, tile0, L, a, wp_next);
     };
     if constexpr (ONE) {
@@ -422,7 +424,7 @@ __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float
 // The composed input_conv o ConvT1 on the generic item path (the stage2
 // head): head_convT1c_planar's layer over (phase, m-block, chunk) items, 4
 // mel taps (frames q + d0 + 1 - k), per-phase bias, edge terms from `corr`.
-template <int MP, int COUT, int NT, int RSI, int RSO, int NQ>
+template <int MP, int COUT, int NT, int RSI, int RSO, int NQ, int PDM = 4>
 __device__ __forceinline__ void xconvT1c(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
                                          const unsigned char* corr, XW mel, XW out, int q0, int T) {
     constexpr int R = 4, MB = (COUT + 15) / 16, NKB = nkb_of<MP, 4>();
@@ -436,12 +438,12 @@ __device__ __forceinline__ void xconvT1c(const u32x4* __restrict__ Wp, const flo
         const u32x4* wp = Wp + (size_t)(ph * MB + mb) * NKB * 128 + lane;
         const unsigned char* bp = mel.p + (q0 + tile0 * 16 + li + d0 + 1 - mel.start) * RSI;
         const int qe = ph < 2 ? 0 : T - 1;
-        u32x4 al[pd_of<MP, 4, 1>()][1][2];
+        u32x4 al[pd_of<MP, 4, 1, PDM>()][1][2];
         if (nt == CH::QHI)
-            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, 1, false>(
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM>(
                 wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
         else
-            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, 1, false>(
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM>(
                 wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
     }
 }
@@ -838,6 +840,7 @@ struct TailPlan {  // A: in | h3 | u4   B: u3 | h4
 #define X3_PLANAR 1
 #endif
 struct CfgS1 {
+    static constexpr int PDM = 4;
     static constexpr int M = 64, MP = 64, C = 128;
     static constexpr int TF = X3_HEAD_TF, HW = X3_HEAD_HW, HMIN = 4;
     static constexpr int W2 = 125, MW = 16, MMIN = 4;
@@ -863,6 +866,9 @@ struct CfgS1 {
 #ifndef X3S2_HW  // stage2 head waves per workgroup (tiling experiments)
 #define X3S2_HW 8
 #endif
+#ifndef X3S2_PDM  // stage2 weight-fragment k-blocks in flight per item (mma_x3)
+#define X3S2_PDM 8
+#endif
 struct CfgS2 {
     static constexpr int M = 80, MP = 96, C = 256;
     static constexpr int TF = X3S2_TF, HW = X3S2_HW, HMIN = 2;
@@ -871,6 +877,10 @@ struct CfgS2 {
     static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = X3S2_NT_R1, NT_T2 = 4, NT_R2 = X3S2_NT_R2, NT_T3 = X3S2_NT_T3,
                          NT_R3 = X3S2_NT_R3, NT_T4 = 4, NT_R4 = 4;
     static constexpr int G_T1 = 1, G_R1 = 1;
+    // weight k-blocks in flight per item: 8 waves per workgroup at one
+    // workgroup per CU leave 256 VGPRs per wave, so an item's weight stream
+    // runs PDM k-blocks (8 VGPRs each) ahead instead of stage1's 4
+    static constexpr int PDM = X3S2_PDM;
 };
 // Stage2 mid / tail tilings for small grids (run<CfgS2> picks per call): at
 // B=8, T=500 the default windows make 576 mid workgroups (1.1 rounds of 512
@@ -893,6 +903,7 @@ constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
 // 16-frame, 8-wave head stays, tools/probe/s2_tiles.sh with X3S2_HW=16).
 struct CfgS2H24 : CfgS2 {
     static constexpr int TF = 24, HW = 16;
+    static constexpr int PDM = 4;  // 16 waves: 128 VGPRs per wave
 };
 constexpr long kS2WideHeadWGs = 1024;
 
@@ -991,17 +1002,17 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         XSTAMP(0, 2);
         XSTAMP(0, 3);
         XSTAMP(0, 4);
-        xconvT1c<MP, C1, Cfg::NT_T1, Pl::RS_M, Pl::RS_1, Pl::NQ>(w.hc, w.hcb, (left || right) ? corr : nullptr, melA,
+        xconvT1c<MP, C1, Cfg::NT_T1, Pl::RS_M, Pl::RS_1, Pl::NQ, Cfg::PDM>(w.hc, w.hcb, (left || right) ? corr : nullptr, melA,
                                                               uw, f0 - 1, T);
         XSTAMP(0, 5);
         __syncthreads();
         XSTAMP(0, 6);
-        xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1,
+        xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N, 1, 0, false, Cfg::PDM>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1,
                                                                                  4 * T);
         XSTAMP(0, 7);
         __syncthreads();
         XSTAMP(0, 8);
-        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, 0, true>(
+        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, 0, true, Cfg::PDM>(
             w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T, nullptr, nullptr, U1 + (size_t)b * 4 * T * 4 * C1);
         XSTAMP(0, 9);
         return;
@@ -1171,15 +1182,15 @@ __global__ __launch_bounds__(Cfg::MW * 64, Cfg::MMIN) void x3_mid_kernel(const u
     XSTAMP(1, 1);
     __syncthreads();
     XSTAMP(1, 2);
-    xconvT<CI, CO, 4, Cfg::NT_T2, Pl::RS_I, Pl::RS_O, Pl::NQ>(w.wt[1], w.bt[1], inw, uw, p0 - 1, L2);
+    xconvT<CI, CO, 4, Cfg::NT_T2, Pl::RS_I, Pl::RS_O, Pl::NQ, 1, 0, Cfg::PDM>(w.wt[1], w.bt[1], inw, uw, p0 - 1, L2);
     XSTAMP(1, 3);
     __syncthreads();
     XSTAMP(1, 4);
-    xconv3<CO, CO, Cfg::NT_R2, ACT_LEAKY, false, Pl::RS_O, Pl::RS_O, Pl::H_N>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, L2);
+    xconv3<CO, CO, Cfg::NT_R2, ACT_LEAKY, false, Pl::RS_O, Pl::RS_O, Pl::H_N, 1, 0, false, Cfg::PDM>(w.w1[1], w.b1[1], uw, hw, 4 * p0 - 1, L2);
     XSTAMP(1, 5);
     __syncthreads();
     XSTAMP(1, 6);
-    xconv3<CO, CO, Cfg::NT_R2, ACT_NONE, true, Pl::RS_O, Pl::RS_O, Pl::O_N>(w.w2[1], w.b2[1], hw, uw, 4 * p0, L2);
+    xconv3<CO, CO, Cfg::NT_R2, ACT_NONE, true, Pl::RS_O, Pl::RS_O, Pl::O_N, 1, 0, false, Cfg::PDM>(w.w2[1], w.b2[1], hw, uw, 4 * p0, L2);
     XSTAMP(1, 7);
     __syncthreads();
     XSTAMP(1, 8);
@@ -1213,27 +1224,27 @@ __global__ __launch_bounds__(Cfg::TW * 64, Cfg::TMIN) void x3_tail_kernel(const 
     XSTAMP(2, 1);
     __syncthreads();
     XSTAMP(2, 2);
-    xconvT<CI, C3, 2, Cfg::NT_T3, Pl::RS_I, Pl::RS_3, Pl::NQ3>(w.wt[2], w.bt[2], inw, u3, p0 - 3, L3);
+    xconvT<CI, C3, 2, Cfg::NT_T3, Pl::RS_I, Pl::RS_3, Pl::NQ3, 1, 0, Cfg::PDM>(w.wt[2], w.bt[2], inw, u3, p0 - 3, L3);
     XSTAMP(2, 3);
     __syncthreads();
     XSTAMP(2, 4);
-    xconv3<C3, C3, Cfg::NT_R3, ACT_LEAKY, false, Pl::RS_3, Pl::RS_3, Pl::H3_N>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, L3);
+    xconv3<C3, C3, Cfg::NT_R3, ACT_LEAKY, false, Pl::RS_3, Pl::RS_3, Pl::H3_N, 1, 0, false, Cfg::PDM>(w.w1[2], w.b1[2], u3, h3, 2 * p0 - 4, L3);
     XSTAMP(2, 5);
     __syncthreads();
     XSTAMP(2, 6);
-    xconv3<C3, C3, Cfg::NT_R3, ACT_NONE, true, Pl::RS_3, Pl::RS_3, Pl::O3_N>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, L3);
+    xconv3<C3, C3, Cfg::NT_R3, ACT_NONE, true, Pl::RS_3, Pl::RS_3, Pl::O3_N, 1, 0, false, Cfg::PDM>(w.w2[2], w.b2[2], h3, u3, 2 * p0 - 3, L3);
     XSTAMP(2, 7);
     __syncthreads();
     XSTAMP(2, 8);
-    xconvT<C3, C4, 2, Cfg::NT_T4, Pl::RS_3, Pl::RS_4, Pl::NQ4>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, L4);
+    xconvT<C3, C4, 2, Cfg::NT_T4, Pl::RS_3, Pl::RS_4, Pl::NQ4, 1, 0, Cfg::PDM>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, L4);
     XSTAMP(2, 9);
     __syncthreads();
     XSTAMP(2, 10);
-    xconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::RS_4, Pl::RS_4, Pl::H4_N>(w.w1[3], w.b1[3], u4, h4w, 4 * p0 - 2, L4);
+    xconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::RS_4, Pl::RS_4, Pl::H4_N, 1, 0, false, Cfg::PDM>(w.w1[3], w.b1[3], u4, h4w, 4 * p0 - 2, L4);
     XSTAMP(2, 11);
     __syncthreads();
     XSTAMP(2, 12);
-    xconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::RS_4, Pl::RS_4, Pl::O4_N>(w.w2[3], w.b2[3], h4w, u4, 4 * p0 - 1, L4);
+    xconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::RS_4, Pl::RS_4, Pl::O4_N, 1, 0, false, Cfg::PDM>(w.w2[3], w.b2[3], h4w, u4, 4 * p0 - 1, L4);
     XSTAMP(2, 13);
     __syncthreads();
     XSTAMP(2, 14);

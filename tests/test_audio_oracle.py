@@ -52,3 +52,26 @@ def test_tone_lands_in_its_band_and_db_floor():
         assert edges[band] <= f <= edges[band + 2]
     db = ao.power_to_db(np.array([[1.0, 1e-12, 1e-3]], dtype=np.float32))
     assert db.max() == 0.0 and db.min() == -80.0 and abs(db[0, 2] + 30.0) < 1e-4
+
+
+def test_nnls_restatement_blocks_and_start():
+    """librosa.util.nnls restated: 1024-column blocks for 64 float32 bands,
+    each an L-BFGS-B problem on the block-normalised objective; in the
+    normalised mel range its convergence test passes at the clipped-pinv
+    start, so the result IS that start (what the GPU reproduces)."""
+    A = ao.mel_filterbank(22050, 1024, 64, 0, 11025.0)
+    rng = np.random.default_rng(2)
+    mel = rng.uniform(-1, 1, (64, 1100)).astype(np.float32)
+    M = np.power(10.0, 0.1 * (mel + 1) / 2).astype(np.float32)
+    assert ao.nnls_block_columns(A, M) == 1024
+    X, info = ao.nnls_lbfgs(A, M, return_info=True)
+    assert len(info) == 2 and all(nit == 0 for nit, _ in info)
+    X0 = np.clip(np.linalg.pinv(A) @ M, 0, None)
+    assert np.array_equal(X, X0.astype(np.float32))
+    assert ao.nnls_projected_gradient_norm(A, X0[:, :1024], M[:, :1024]) <= 1e-5
+    # far outside the range the start is not stationary and L-BFGS-B iterates
+    big = (rng.standard_normal((64, 40)) * 20).astype(np.float32)
+    Mb = np.power(10.0, 0.1 * (big + 1) / 2).astype(np.float32)
+    Xb, ib = ao.nnls_lbfgs(A, Mb, return_info=True)
+    assert ib[0][0] > 0
+    assert ao.nnls_objective(A, Xb, Mb) < ao.nnls_objective(A, np.clip(np.linalg.pinv(A) @ Mb, 0, None), Mb)

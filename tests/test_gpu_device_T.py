@@ -338,3 +338,44 @@ def test_duration_two_row_block_tiles_bit_identical(gpu, stage, B, S, monkeypatc
     enc, _ = orc.text_encoder(sd, stage_config(stage), ids, lens)
     ref = orc.duration_predictor(sd, enc)
     assert maxabs(out["2"][0], ref) <= 1e-4  # test_gpu_parity.py ENC_TOL
+
+
+@pytest.mark.parametrize("stage,B,S", [("s2", 8, 100), ("s1", 32, 100), ("s2", 64, 100), ("s1", 3, 17), ("s2", 40, 61)])
+def test_duration_split_convs(gpu, stage, B, S, monkeypatch):
+    """The duration convs of the inference path on split-f16 MFMA
+    (hi.hi + lo.hi + hi.lo, fp32 accumulate; the model's static bound allows
+    it) against the exact-f32 MFMA convs (M2_DUR_SPLIT=0): durations within
+    2e-6 relative, the frame counts, prefix sums and T_max identical, and the
+    oracle's durations within the fixture tolerance (tts_model.py:99-117)."""
+    m = build_model(stage, gpu)
+    hm = m._hip(gpu)
+    g = torch.Generator().manual_seed(B * 7 + S)
+    ids = torch.randint(0, 42, (B, S), generator=g).to(gpu)
+    lens = torch.randint(1, S + 1, (B,), generator=g).to(gpu)
+    H = stage_config(stage).hidden_dim
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("M2_DUR_SPLIT", v)
+        tw = torch.full((1,), -7, dtype=torch.int32, device=gpu)
+        st = hm.inference_front_dev(ids, lens, 1.0, tw)
+        torch.cuda.synchronize(gpu)
+        front = st[2]
+        # front buffer: encoder output [B,S,H] f32 then durations [B,S] f32, then int32 counts
+        out[v] = (front.clone(), int(tw.item()))
+    f1, f0 = out["1"][0], out["0"][0]
+    nb = B * S * H * 4
+    do = (nb + 255) // 256 * 256  # carve_front: 256-B aligned pieces
+    enc1, enc0 = f1[:nb].view(torch.float32), f0[:nb].view(torch.float32)
+    assert torch.equal(enc1, enc0)  # the fused LayerNorm is the same code
+    d1 = f1[do:do + B * S * 4].view(torch.float32).view(B, S)
+    d0 = f0[do:do + B * S * 4].view(torch.float32).view(B, S)
+    rel = float(((d1 - d0).abs() / d0.abs().clamp(min=1e-6)).max())
+    assert rel <= 2e-6, rel
+    assert out["1"][1] == out["0"][1]
+    assert torch.equal(torch.trunc(d1), torch.trunc(d0))
+    sd = golden_state(stage)
+    cfg = stage_config(stage)
+    with torch.no_grad():
+        enc, _ = orc.text_encoder(sd, cfg, ids.cpu(), lens.cpu())
+        dref = orc.duration_predictor(sd, enc)
+    assert maxabs(d1, dref) <= 1e-4

@@ -17,6 +17,7 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     import bench
+    from m2amd import _lib
     var, vals, stage, B, S = sys.argv[1], sys.argv[2].split(","), sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
     rounds = int(sys.argv[6]) if len(sys.argv) > 6 else 8
     steps = int(sys.argv[7]) if len(sys.argv) > 7 else 30
@@ -36,6 +37,7 @@ def main():
                     os.environ.pop(var, None)
                 else:
                     os.environ[var] = v
+                _lib.reload_switches()  # the library reads the M2_* switches once, not per call
                 m.inference(ids, lens)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
