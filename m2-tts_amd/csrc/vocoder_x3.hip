@@ -867,7 +867,7 @@ struct CfgS1 {
 #define X3S2_HW 8
 #endif
 #ifndef X3S2_PDM  // stage2 weight-fragment k-blocks in flight per item (mma_x3)
-#define X3S2_PDM 8
+#define X3S2_PDM 4
 #endif
 struct CfgS2 {
     static constexpr int M = 80, MP = 96, C = 256;
@@ -877,9 +877,12 @@ struct CfgS2 {
     static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = X3S2_NT_R1, NT_T2 = 4, NT_R2 = X3S2_NT_R2, NT_T3 = X3S2_NT_T3,
                          NT_R3 = X3S2_NT_R3, NT_T4 = 4, NT_R4 = 4;
     static constexpr int G_T1 = 1, G_R1 = 1;
-    // weight k-blocks in flight per item: 8 waves per workgroup at one
-    // workgroup per CU leave 256 VGPRs per wave, so an item's weight stream
-    // runs PDM k-blocks (8 VGPRs each) ahead instead of stage1's 4
+    // weight k-blocks in flight per item (8 VGPRs each).  4, as stage1: 8 and
+    // 12 (the 256-VGPR budget of 8 waves at one workgroup per CU allows them)
+    // measured level or slower - head 25.8 / 26.3 / 27.0 us at 8x500, mid
+    // 184.2 / 184.4 / 185.2 us at 16x2600 (profiles/r04/r04b_pdm_pipeline_ab.txt):
+    // the stage2 head and mid are not bound by the latency of their weight
+    // stream
     static constexpr int PDM = X3S2_PDM;
 };
 // Stage2 mid / tail tilings for small grids (run<CfgS2> picks per call): at
