@@ -1387,6 +1387,308 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
     else fin(CI<0>{});
 }
 
+// Software-pipelined form of attention_qsplit2's lean unmasked path (the
+// long-form decoder; M2_TFL_QS2=5): iteration p issues the QK^T MFMAs of step
+// p + 1 beside the softmax VALU of step p (its scores were computed one
+// iteration earlier and stay in registers), then the PV MFMAs of step p - so a
+// wave's matrix and vector work of consecutive steps overlap instead of
+// alternating behind one barrier.  K runs one step ahead of V in the LDS
+// rings: at the top of iteration p the rings hold K(p + 1) and V(p); the
+// iteration stores K(p + 2) and V(p + 1) (requested from L2 one iteration
+// earlier) into the halves iteration p - 1 finished reading, and requests
+// K(p + 3) and V(p + 2).  One barrier per iteration, as before.  The QK^T
+// MFMAs of step p + 1 start from C = -m at the top of the iteration; a base
+// move in the softmax of step p (the first step, or a weight past 2^kLazyT)
+// shifts those scores too.  Same arithmetic per score as the lean two-block
+// form (results within rounding of it: the base moves are the same).
+template <int H, int HD>
+__device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restrict__ qb,
+                                                   const unsigned char* __restrict__ kb,
+                                                   const unsigned char* __restrict__ vb, int b, int t0, int N,
+                                                   int npad, unsigned char* A, unsigned char* ring) {
+    using G = Geo<HD>;
+    using Q = QsGeo<HD>;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK;
+    constexpr int KB = Q::KB, VB = G::VCH;                                // one head's K / V^T of a chunk
+    constexpr int KST = 2 * HEADS * KB, VST = 2 * HEADS * VB;             // K / V^T bytes of a 64-key step
+    constexpr int NT = NW * 64, KP = KST / (16 * NT), VP = VST / (16 * NT);  // 16-B pieces per thread
+    constexpr int RW = 2 + 4 * MT;
+    static_assert(KST % (16 * NT) == 0 && VST % (16 * NT) == 0 && KB % 1024 == 0 && VB % 1024 == 0,
+                  "1-KB wave pieces of one region");
+    static_assert(2 * KST + 2 * VST <= 2 * Q::SB, "K and V^T rings in the attention scratch");
+    static_assert(NW * RW * 64 * 4 <= 2 * Q::SB, "merge records fit the ring");
+    unsigned char* const kring = ring;
+    unsigned char* const vring = ring + 2 * KST;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, g = lane >> 4;
+    const int h = wave >> 2, qp = (wave >> 1) & 1, j = wave & 1;
+    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
+    auto live = [&](int p) { return 2 * KC * p + KC * j < N; };  // this wave's chunk of step p holds keys
+
+    u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+        const unsigned char* qp8 =
+            qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + 2 * qp + qq) * QKBLK + 16 * lane;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            qh[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks);
+            ql[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024);
+        }
+        if constexpr (KT) {
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            qxh[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
+            qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
+        }
+    }
+    // staging: piece i of a step's K (V^T) region [chunk][head][bytes] - a
+    // wave's 1-KB piece lies in one (chunk, head) region
+    __amdgpu_buffer_rsrc_t krs[KP], vrs[VP];
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+        const int o = 16 * (tid + NT * i), jj = o / (HEADS * KB), r1 = o - jj * HEADS * KB, hh = r1 / KB,
+                  r = r1 - hh * KB;
+        krs[i] = wave_rsrc(kb + ((size_t)(b * HEADS + hh) * (npad / 16) + 2 * jj) * QKBLK + (r & ~1023));
+    }
+#pragma unroll
+    for (int i = 0; i < VP; ++i) {
+        const int o = 16 * (tid + NT * i), jj = o / (HEADS * VB), r1 = o - jj * HEADS * VB, hh = r1 / VB,
+                  r = r1 - hh * VB;
+        vrs[i] = wave_rsrc(vb + ((size_t)(b * HEADS + hh) * nch + jj) * VB + (r & ~1023));
+    }
+    u32x4 kpre[KP], vpre[VP];
+    auto gload_k = [&](int p) {
+#pragma unroll
+        for (int i = 0; i < KP; ++i)
+            kpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs[i], 16 * lane, p * 4 * QKBLK, 0));
+    };
+    auto gload_v = [&](int p) {
+#pragma unroll
+        for (int i = 0; i < VP; ++i)
+            vpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs[i], 16 * lane, p * 2 * VB, 0));
+    };
+    auto lstore_k = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < KP; ++i) *reinterpret_cast<u32x4*>(kring + buf * KST + 16 * (tid + NT * i)) = kpre[i];
+    };
+    auto lstore_v = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < VP; ++i) *reinterpret_cast<u32x4*>(vring + buf * VST + 16 * (tid + NT * i)) = vpre[i];
+    };
+
+    f32x4 acc[2][MT], lacc[2];
+    float m[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        m[qq] = 0.f;
+        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
+
+    // S(p) of this wave's chunk from K ring half kbuf, relative to -c0
+    // (keys past N -inf).  s[qq][u][r]: key 64 p + 32 j + 16 u + 4 g + r.
+    auto qk = [&](const unsigned char* kbuf, int p, const float (&c0)[2], float (&s)[2][2][4]) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const unsigned char* kp = kbuf + j * (HEADS * KB) + h * KB + u * QKBLK + 16 * lane;
+            f32x4 st[2] = {f32x4{c0[0], c0[0], c0[0], c0[0]}, f32x4{c0[1], c0[1], c0[1], c0[1]}};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
+                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kh, qh[qq][ks], st[qq]);
+                    st[qq] = mfma(kh, ql[qq][ks], st[qq]);
+                    st[qq] = mfma(kl, qh[qq][ks], st[qq]);
+                }
+            }
+            if constexpr (KT) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
+                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
+                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kxh, qxh[qq], st[qq]);
+                    st[qq] = mfma(kxh, qxl[qq], st[qq]);
+                    st[qq] = mfma(kxl, qxh[qq], st[qq]);
+                }
+            }
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
+        }
+        const int k0 = p * 2 * KC + j * KC;
+        if (N - k0 < KC) {  // the chunk straddles N (wave-uniform)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq)
+                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
+        }
+    };
+    auto chunk_max = [](const float (&s)[2][2][4], int qq) {
+        return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
+                     fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+    };
+    auto exp_split = [](const float (&s)[2][2][4], u32x4 (&bh4)[2], u32x4 (&bl4)[2]) {
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            float e[2][4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+            unsigned ph[4], pl[4];
+            split2u(e[0][0], e[0][1], ph[0], pl[0]);
+            split2u(e[0][2], e[0][3], ph[1], pl[1]);
+            split2u(e[1][0], e[1][1], ph[2], pl[2]);
+            split2u(e[1][2], e[1][3], ph[3], pl[3]);
+            bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+            bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+        }
+    };
+    // iteration p: (K(p + 2), V(p + 1)) to LDS, (K(p + 3), V(p + 2)) requested,
+    // S(p + 1) = QK(p + 1) beside softmax(p) on sc, PV(p); sn: S(p + 1)
+    auto iterate = [&](int p, float (&sc)[2][2][4], float (&sn)[2][2][4]) {
+        if (p + 2 < nsc) lstore_k(p & 1);
+        if (p + 1 < nsc) lstore_v((p + 1) & 1);
+        if (p + 3 < nsc) gload_k(p + 3);
+        if (p + 2 < nsc) gload_v(p + 2);
+        const bool nxt = p + 1 < nsc && live(p + 1);  // wave-uniform
+        const float c0[2] = {-m[0], -m[1]};
+        if (nxt) qk(kring + ((p + 1) & 1) * KST, p + 1, c0, sn);
+        if (live(p)) {
+            u32x4 bh4[2], bl4[2];
+            float d[2] = {0.f, 0.f};
+            bool moved = false;
+            if (p == 0) {  // the first step: the base is the chunk's maximum (wave-uniform)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    d[qq] = grp4_max(chunk_max(sc, qq));  // finite: the chunk holds a key < N
+                    m[qq] = d[qq];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
+                }
+                moved = true;
+            }
+            exp_split(sc, bh4, bl4);
+            if (p > 0 && __builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    d[qq] = vmax(grp4_max(chunk_max(sc, qq)), 0.f);
+                    m[qq] += d[qq];
+                    const float corr = __builtin_amdgcn_exp2f(-d[qq]);
+                    lacc[qq] *= corr;
+#pragma unroll
+                    for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
+                }
+                exp_split(sc, bh4, bl4);
+                moved = true;
+            }
+            if (moved && nxt)  // S(p + 1) was computed against the old base
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) sn[qq][u][r] -= d[qq];
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
+                lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
+            }
+            const unsigned char* vp = vring + (p & 1) * VST + j * (HEADS * VB) + h * VB + 16 * lane;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+                const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
+                    acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
+                    acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
+                }
+            }
+        }
+        lds_barrier();
+    };
+
+    // prologue: K(0), V(0), K(1) in LDS, S(0) computed, K(2) and V(1) requested
+    float sa[2][2][4], sb[2][2][4];
+    gload_k(0);
+    gload_v(0);
+    lstore_k(0);
+    lstore_v(0);
+    if (1 < nsc) {
+        gload_k(1);
+        lstore_k(1);
+    }
+    lds_barrier();
+    {
+        const float z[2] = {0.f, 0.f};
+        if (live(0)) qk(kring, 0, z, sa);
+    }
+    if (2 < nsc) gload_k(2);
+    if (1 < nsc) gload_v(1);
+    lds_barrier();  // every wave has read K(0) before iteration 0 overwrites it
+#pragma unroll 1
+    for (int p = 0; p < nsc; p += 2) {
+        iterate(p, sa, sb);
+        if (p + 1 < nsc) iterate(p + 1, sb, sa);  // wave-uniform
+    }
+    TSTAMP(1);
+    const bool saw = live(0);
+    if (!saw) {  // this wave saw no key
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) m[qq] = -INFINITY;
+    }
+    // merge the two chunk waves of (h, qp) as attention_qsplit2 does
+    float* rec = reinterpret_cast<float*>(ring);
+    auto put = [&](auto J) {
+        constexpr int qo = 1 - decltype(J)::value;
+        float* w = rec + (size_t)wave * RW * 64 + lane;
+        w[0] = m[qo];
+        w[64] = lacc[qo][0];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qo][t][r];
+    };
+    auto fin = [&](auto J) {
+        constexpr int qq = decltype(J)::value;
+        const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
+        const float mo = o[0];
+        const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
+        const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
+        const float ls = lacc[qq][0] * fm + o[64] * fo;
+        const float inv = 1.0f / ls;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (acc[qq][t][r] * fm + o[(2 + 4 * t + r) * 64] * fo) * inv;
+            put_split4<H>(A + (16 * (2 * qp + qq) + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2],
+                          v[3]);
+        }
+    };
+    if (j) put(CI<1>{});
+    else put(CI<0>{});
+    __syncthreads();
+    if (j) fin(CI<1>{});
+    else fin(CI<0>{});
+}
+
 // ---------------------------------------------------------------------------
 struct LArgs {
     int B, N, npad, ntile;
@@ -1454,7 +1756,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
     if constexpr (QS) {
-        if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        if constexpr (QV == 5 && !MASKED) attention_qsplit2p<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 3 || QV == 5) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
         // row sums moved the stage1 encoder's error at B=128 S=130 from under
@@ -1870,7 +2173,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     const int qs2 = tfl_qs2(H);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
         else if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
