@@ -1423,7 +1423,6 @@ __device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restri
     const int li = lane & 15, g = lane >> 4;
     const int h = wave >> 2, qp = (wave >> 1) & 1, j = wave & 1;
     const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
-    auto live = [&](int p) { return 2 * KC * p + KC * j < N; };  // this wave's chunk of step p holds keys
 
     u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
 #pragma unroll
@@ -1489,7 +1488,7 @@ __device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restri
 
     // S(p) of this wave's chunk from K ring half kbuf, relative to -c0
     // (keys past N -inf).  s[qq][u][r]: key 64 p + 32 j + 16 u + 4 g + r.
-    auto qk = [&](const unsigned char* kbuf, int p, const float (&c0)[2], float (&s)[2][2][4]) {
+    auto qk = [&](auto MK, const unsigned char* kbuf, int p, const float (&c0)[2], float (&s)[2][2][4]) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const unsigned char* kp = kbuf + j * (HEADS * KB) + h * KB + u * QKBLK + 16 * lane;
@@ -1520,8 +1519,8 @@ __device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restri
 #pragma unroll
                 for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
         }
-        const int k0 = p * 2 * KC + j * KC;
-        if (N - k0 < KC) {  // the chunk straddles N (wave-uniform)
+        if constexpr (decltype(MK)::value) {  // this wave's last chunk: keys past N score -inf
+            const int k0 = p * 2 * KC + j * KC;
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -1552,51 +1551,57 @@ __device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restri
             bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
         }
     };
-    // iteration p: (K(p + 2), V(p + 1)) to LDS, (K(p + 3), V(p + 2)) requested,
-    // S(p + 1) = QK(p + 1) beside softmax(p) on sc, PV(p); sn: S(p + 1)
-    auto iterate = [&](int p, float (&sc)[2][2][4], float (&sn)[2][2][4]) {
+    // the staging of iteration p: (K(p + 2), V(p + 1)) to LDS, (K(p + 3),
+    // V(p + 2)) requested (scalar branches ahead of the compute block)
+    auto stage = [&](int p) {
         if (p + 2 < nsc) lstore_k(p & 1);
         if (p + 1 < nsc) lstore_v((p + 1) & 1);
         if (p + 3 < nsc) gload_k(p + 3);
         if (p + 2 < nsc) gload_v(p + 2);
-        const bool nxt = p + 1 < nsc && live(p + 1);  // wave-uniform
+    };
+    // iteration p of a live step: S(p + 1) = QK(p + 1) (QN; MN: masked, this
+    // wave's last chunk) beside softmax(p) on sc, PV(p).  Compile-time flags
+    // only: in the steady state the QK^T MFMAs of p + 1 and the exponentials
+    // of p are one basic block the scheduler can interleave.
+    auto iterate = [&](auto FIRST, auto QN, auto MN, int p, float (&sc)[2][2][4], float (&sn)[2][2][4]) {
+        constexpr bool F = decltype(FIRST)::value, QK = decltype(QN)::value;
+        stage(p);
         const float c0[2] = {-m[0], -m[1]};
-        if (nxt) qk(kring + ((p + 1) & 1) * KST, p + 1, c0, sn);
-        if (live(p)) {
-            u32x4 bh4[2], bl4[2];
-            float d[2] = {0.f, 0.f};
-            bool moved = false;
-            if (p == 0) {  // the first step: the base is the chunk's maximum (wave-uniform)
+        if constexpr (QK) qk(MN, kring + ((p + 1) & 1) * KST, p + 1, c0, sn);
+        u32x4 bh4[2], bl4[2];
+        float d[2] = {0.f, 0.f};
+        if constexpr (F) {  // the first step: the base is the chunk's maximum
 #pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    d[qq] = grp4_max(chunk_max(sc, qq));  // finite: the chunk holds a key < N
-                    m[qq] = d[qq];
+            for (int qq = 0; qq < 2; ++qq) {
+                d[qq] = grp4_max(chunk_max(sc, qq));  // finite: the chunk holds a key < N
+                m[qq] = d[qq];
 #pragma unroll
-                    for (int u = 0; u < 2; ++u)
+                for (int u = 0; u < 2; ++u)
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
-                }
-                moved = true;
+                    for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
+            }
+        }
+        exp_split(sc, bh4, bl4);
+        bool moved = F;
+        if (!F && __builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                d[qq] = vmax(grp4_max(chunk_max(sc, qq)), 0.f);
+                m[qq] += d[qq];
+                const float corr = __builtin_amdgcn_exp2f(-d[qq]);
+                lacc[qq] *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
             }
             exp_split(sc, bh4, bl4);
-            if (p > 0 && __builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    d[qq] = vmax(grp4_max(chunk_max(sc, qq)), 0.f);
-                    m[qq] += d[qq];
-                    const float corr = __builtin_amdgcn_exp2f(-d[qq]);
-                    lacc[qq] *= corr;
-#pragma unroll
-                    for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
-#pragma unroll
-                    for (int u = 0; u < 2; ++u)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
-                }
-                exp_split(sc, bh4, bl4);
-                moved = true;
-            }
-            if (moved && nxt)  // S(p + 1) was computed against the old base
+            moved = true;
+        }
+        if constexpr (QK)
+            if (moved)  // S(p + 1) was computed against the old base
 #pragma unroll
                 for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
@@ -1604,27 +1609,29 @@ __device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restri
 #pragma unroll
                         for (int r = 0; r < 4; ++r) sn[qq][u][r] -= d[qq];
 #pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
+            lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
+        }
+        const unsigned char* vp = vring + (p & 1) * VST + j * (HEADS * VB) + h * VB + 16 * lane;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+            const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+#pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
-                lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
-                lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
-            }
-            const unsigned char* vp = vring + (p & 1) * VST + j * (HEADS * VB) + h * VB + 16 * lane;
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
-                const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
-                    acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
-                    acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
-                }
+                acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
             }
         }
         lds_barrier();
     };
+    const CI<0> n0{};
+    const CI<1> n1{};
 
     // prologue: K(0), V(0), K(1) in LDS, S(0) computed, K(2) and V(1) requested
+    const int nl = N > KC * j ? (N - KC * j + 2 * KC - 1) / (2 * KC) : 0;  // steps with keys for this wave
     float sa[2][2][4], sb[2][2][4];
     gload_k(0);
     gload_v(0);
@@ -1637,19 +1644,55 @@ __device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restri
     lds_barrier();
     {
         const float z[2] = {0.f, 0.f};
-        if (live(0)) qk(kring, 0, z, sa);
+        if (nl == 1) qk(n1, kring, 0, z, sa);
+        else if (nl > 1) qk(n0, kring, 0, z, sa);
     }
     if (2 < nsc) gload_k(2);
     if (1 < nsc) gload_v(1);
     lds_barrier();  // every wave has read K(0) before iteration 0 overwrites it
+    // this wave's steps: 0 (first), 1 .. nl - 3 (steady), nl - 2 (QK of the
+    // masked last chunk), nl - 1 (no QK); then staging-only steps up to nsc
+    auto finish = [&](int p, float (&x)[2][2][4], float (&y)[2][2][4]) {  // x holds S(p)
+        if (p == nl - 2) {
+            iterate(n0, n1, n1, p, x, y);
+            iterate(n0, n0, n0, p + 1, y, x);
+            p += 2;
+        } else if (p == nl - 1) {
+            iterate(n0, n0, n0, p, x, y);
+            ++p;
+        }
 #pragma unroll 1
-    for (int p = 0; p < nsc; p += 2) {
-        iterate(p, sa, sb);
-        if (p + 1 < nsc) iterate(p + 1, sb, sa);  // wave-uniform
+        for (; p < nsc; ++p) {
+            stage(p);
+            lds_barrier();
+        }
+    };
+    if (nl >= 3) {
+        iterate(n1, n1, n0, 0, sa, sb);
+        int p = 1;
+#pragma unroll 1
+        for (; p + 2 <= nl - 2; p += 2) {
+            iterate(n0, n1, n0, p, sb, sa);
+            iterate(n0, n1, n0, p + 1, sa, sb);
+        }
+        if (p < nl - 2) {
+            iterate(n0, n1, n0, p, sb, sa);
+            finish(p + 1, sa, sb);
+        } else {
+            finish(p, sb, sa);
+        }
+    } else if (nl == 2) {
+        iterate(n1, n1, n1, 0, sa, sb);
+        iterate(n0, n0, n0, 1, sb, sa);
+        finish(2, sa, sb);
+    } else if (nl == 1) {
+        iterate(n1, n0, n0, 0, sa, sb);
+        finish(1, sb, sa);
+    } else {
+        finish(0, sa, sb);
     }
     TSTAMP(1);
-    const bool saw = live(0);
-    if (!saw) {  // this wave saw no key
+    if (nl == 0) {  // this wave saw no key
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq) m[qq] = -INFINITY;
     }
