@@ -100,8 +100,9 @@ constexpr int pd_of() {
     constexpr int NKB = (NTAP * (CIN / 8) + 3) / 4;
     return NKB < PDM / NMB ? NKB : PDM / NMB;
 }
-// TB: tap k's rows start at tb[k] (this lane's row, before the lane-group
-// offset) instead of bp + k*STEP*RSI - the phase-planar layouts of the head.
+// TB: tap k's rows start at tb[k] (this lane's row and lane-group chunk, the
+// plane swizzle applied) instead of bp + k*STEP*RSI - the phase-planar
+// layouts of the head.
 template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE, bool TB = false,
           int PDM = 4>
 __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
@@ -144,7 +145,7 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
         const unsigned char* b0;
         if constexpr (TB) {
             static_assert(NOCT >= 4 && !XR, "tap bases: whole octet rows only");
-            b0 = tb[kb / (NOCT / 4)] + g * 16 + (kb % (NOCT / 4)) * 64;
+            b0 = tb[kb / (NOCT / 4)] + (kb % (NOCT / 4)) * 64;  // tb: the lane group's chunk included
         } else {
             b0 = kb == NKB - 1 ? b_last : bl + koff(kb);
         }
@@ -484,21 +485,31 @@ __device__ __forceinline__ void head_edge_terms_s2(const float* __restrict__ hce
 // fewer ConvT1 MFMAs) and conflict-free epilogue stores (consecutive lanes,
 // consecutive rows); the ResBlock1 convs become per-phase GEMMs whose three
 // taps read rows of the neighbouring planes (mma_x3 with tap bases).
+// Plane rows are swizzled: row r's 16-B chunks c and c ^ 1 trade places when
+// bit 2 of r is set (plane_sw).  A tile's epilogue writes rows li of one
+// chunk per lane group, 8 consecutive lanes per ds_write_b128 pass; at a row
+// stride of 18 chunks rows r and r + 4 met in the same banks (2-way); the
+// swizzle moves rows 4-7 by 4 banks.  The B-fragment reads (4 lane groups
+// of 16, chunks c0 + g) stay conflict-free: the bit only permutes the chunk
+// pairs of one k-block, per lane, and folds into the tap bases.
+__device__ __forceinline__ int plane_sw(int r) { return (r >> 2) & 1; }
 __device__ __forceinline__ int qs_u(int p, int f0) { return f0 - (p >= 2 ? 1 : 0); }
 __device__ __forceinline__ int qs_h(int p, int f0) { return f0 - (p == 3 ? 1 : 0); }
 constexpr int kPlane = 64;
 
-// Epilogue of one tile into an explicit LDS row (rowp) or straight to global
-// (GO); the residual, if any, is read from xrow.
+// Epilogue of one tile into an explicit plane row (rowp, swizzle bit rsw) or
+// straight to global (GO); the residual, if any, is read from plane row xrow
+// (swizzle bit xsw).
 template <int COUT, int ACT, bool RES, bool GO>
 __device__ __forceinline__ void store_row(const f32x4& acc, unsigned char* rowp, const unsigned char* xrow, int co0,
-                                          bool zero, bool store, unsigned char* gout, int t) {
+                                          bool zero, bool store, unsigned char* gout, int t, int rsw, int xsw = 0) {
+    const int g = (threadIdx.x & 63) >> 4;
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = acc[r];
     if constexpr (ACT == ACT_LEAKY) leaky4(v);
-    if constexpr (RES) {
-        const unsigned char* row = xrow + co0 * 2;
+    if constexpr (RES) {  // channels co0 .. co0 + 3: chunk co0 / 8, half g & 1
+        const unsigned char* row = xrow + 2 * (co0 - 4 * g) + 16 * ((g >> 1) ^ xsw) + 8 * (g & 1);
         const h4 hi = *reinterpret_cast<const h4*>(row), lo = *reinterpret_cast<const h4*>(row + 2 * COUT);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += (float)hi[r] + (float)lo[r];
@@ -512,13 +523,13 @@ __device__ __forceinline__ void store_row(const f32x4& acc, unsigned char* rowp,
     split2u(v[2], v[3], h1, l1);
     const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
-    const int g = (threadIdx.x & 63) >> 4;
-    const int off = 2 * (co0 - 4 * g + 8 * (g >> 1)) + (g & 1) * 2 * COUT;
+    const int off = 2 * (co0 - 4 * g) + (g & 1) * 2 * COUT;
     if (store) {
         if constexpr (GO)
-            *reinterpret_cast<u32x4*>(gout + (size_t)t * 4 * COUT + off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+            *reinterpret_cast<u32x4*>(gout + (size_t)t * 4 * COUT + off + 16 * (g >> 1)) =
+                u32x4{s0[0], s1[0], s0[1], s1[1]};
         else
-            *reinterpret_cast<u32x4*>(rowp + off) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+            *reinterpret_cast<u32x4*>(rowp + off + 16 * ((g >> 1) ^ rsw)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
     }
 }
 
@@ -546,7 +557,7 @@ __device__ __forceinline__ void head_convT1_planar(const u32x4* __restrict__ Wp,
     for (int n = 0; n < NT; ++n) {
         const int t = 4 * (qs + 16 * n + li) + ph;
         store_row<COUT, ACT_LEAKY, false, false>(acc[0][n], u + (ph * kPlane + 16 * n + li) * RSO, nullptr, co0,
-                                                 t < 0 || t >= L, true, nullptr, t);
+                                                 t < 0 || t >= L, true, nullptr, t, plane_sw(li));
     }
 }
 
@@ -633,7 +644,7 @@ __device__ __forceinline__ void head_convT1c_planar(const u32x4* __restrict__ Wp
             }
         }
         store_row<COUT, ACT_LEAKY, false, false>(acc[0][n], u + (ph * kPlane + 16 * n + li) * RSO, nullptr, co0,
-                                                 t < 0 || t >= L, true, nullptr, t);
+                                                 t < 0 || t >= L, true, nullptr, t, plane_sw(li));
     }
 }
 
@@ -656,7 +667,8 @@ __device__ __forceinline__ void head_rb1_planar(const u32x4* __restrict__ Wp, co
     for (int d = 0; d < 3; ++d) {
         const int pd = p + d - 1, dq = pd < 0 ? -1 : (pd > 3 ? 1 : 0), pi = pd - 4 * dq;
         const int qsi = CONV2 ? qs_h(pi, f0) : qs_u(pi, f0);
-        tb[d] = in + (pi * kPlane + qo + dq - qsi + li) * RS;
+        const int r = qo + dq - qsi + li;  // row in plane pi (>= 0)
+        tb[d] = in + (pi * kPlane + r) * RS + 16 * (g ^ plane_sw(r));
     }
     const u32x4* wp = Wp + (size_t)mb * NKB * 128 + lane;
     f32x4 acc[1][NT];
@@ -670,11 +682,12 @@ __device__ __forceinline__ void head_rb1_planar(const u32x4* __restrict__ Wp, co
     for (int n = 0; n < NT; ++n) {
         const int q = qo + 16 * n + li, t = 4 * q + p;
         if constexpr (CONV2) {
-            const unsigned char* xrow = x + (p * kPlane + q - qs_u(p, f0)) * RS;
-            store_row<C, ACT_NONE, true, true>(acc[0][n], nullptr, xrow, co0, false, q < f0 + tf && t < L, gout, t);
+            const int xr = q - qs_u(p, f0);
+            store_row<C, ACT_NONE, true, true>(acc[0][n], nullptr, x + (p * kPlane + xr) * RS, co0, false,
+                                               q < f0 + tf && t < L, gout, t, 0, plane_sw(xr));
         } else {
             store_row<C, ACT_LEAKY, false, false>(acc[0][n], out + (p * kPlane + 16 * n + li) * RS, nullptr, co0,
-                                                  t < 0 || t >= L, true, nullptr, t);
+                                                  t < 0 || t >= L, true, nullptr, t, plane_sw(li));
         }
     }
 }

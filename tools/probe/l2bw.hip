@@ -13,7 +13,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // ROWS = 0: a wave-instruction reads 1 KB contiguous (lane i: element base + i);
 // ROWS = 1: 16 rows of 64 B, rows 256 B apart (lane (i, g): row i, 16 g) -
 // the one-launch layer's K-fragment pattern; a wave covers 4 such blocks
-// (the row's 4 x 64 B) before moving on.
+// (the row's 4 x 64 B) before moving on.  ROWS = 2: that pattern, each
+// workgroup of an XCD starting k/32 of the way into the slice; ROWS = 3:
+// contiguous 1 KB with that rotated start (time-skewed readers of one
+// shared buffer: the query-split attention's K / V stream).
 template <int INF, int ROWS>
 __global__ __launch_bounds__(512) void rd(const u32x4* __restrict__ buf, size_t slice_elems, int per_wg_elems,
                                           unsigned* __restrict__ out) {
@@ -26,12 +29,12 @@ __global__ __launch_bounds__(512) void rd(const u32x4* __restrict__ buf, size_t 
 #pragma unroll
         for (int i = 0; i < INF; ++i) {
             int e = base + i * blockDim.x;
-            if (ROWS) {
+            if (ROWS == 1 || ROWS == 2) {
                 const int ins = (base - threadIdx.x) / 64 + w + i * (blockDim.x / 64);  // wave-instruction index
                 const int blk = ins >> 2, part = ins & 3;                               // 16-row block, 64-B column
                 e = blk * 256 + (lane & 15) * 16 + part * 4 + (lane >> 4);              // 16-B elements
             }
-            if (ROWS == 2) {  // rotated start: workgroup k of an XCD begins k/32 of the way in
+            if (ROWS >= 2) {  // rotated start: workgroup k of an XCD begins k/32 of the way in
                 const int rot = (int)(((long long)(blockIdx.x >> 3) * per_wg_elems / 32) & ~63);
                 e = e < per_wg_elems ? (e + rot) % per_wg_elems : e;
             }
@@ -56,7 +59,7 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int inf : {4, 8, 16, -4, -8, 104, 108, 116}) {
+    for (int inf : {4, 8, 16, -4, -8, 104, 108, 116, 204, 208, 216}) {
         auto launch = [&] {
             if (inf == 4) hipLaunchKernelGGL((rd<4, 0>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
             if (inf == 8) hipLaunchKernelGGL((rd<8, 0>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
@@ -67,6 +70,9 @@ int main(int argc, char** argv) {
             if (inf == 104) hipLaunchKernelGGL((rd<4, 2>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
             if (inf == 108) hipLaunchKernelGGL((rd<8, 2>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
             if (inf == 116) hipLaunchKernelGGL((rd<16, 2>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 204) hipLaunchKernelGGL((rd<4, 3>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 208) hipLaunchKernelGGL((rd<8, 3>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
+            if (inf == 216) hipLaunchKernelGGL((rd<16, 3>), dim3(grid), dim3(threads), 0, 0, buf, slice, (int)slice, out);
         };
         for (int i = 0; i < 50; ++i) launch();
         hipDeviceSynchronize();
@@ -80,8 +86,9 @@ int main(int argc, char** argv) {
         const double us = ms * 1e3 / n;
         const double per_cu = (double)per_wg / (us * 1e-6) / 1e9;
         printf("per_wg %d B, grid %d x %d threads, %s, %2d loads/lane in flight: %.2f us/launch, %.1f GB/s per WG, %.2f TB/s chip\n",
-               per_wg, grid, threads, inf > 100 ? "rotated 1 KB" : inf > 0 ? "contiguous 1 KB" : "16 rows x 64 B",
-               inf > 100 ? inf - 100 : inf > 0 ? inf : -inf, us, per_cu,
+               per_wg, grid, threads,
+               inf > 200 ? "rotated contiguous 1 KB" : inf > 100 ? "rotated 16 rows x 64 B" : inf > 0 ? "contiguous 1 KB" : "16 rows x 64 B",
+               inf > 200 ? inf - 200 : inf > 100 ? inf - 100 : inf > 0 ? inf : -inf, us, per_cu,
                per_cu * grid / 1e3);
     }
     return 0;
