@@ -30,7 +30,7 @@ struct Switches {
     bool tf_layer = true;     // M2_TF_LAYER=0: three-launch transformer layers
     bool tf_unfused = false;  // M2_TF_UNFUSED: five-linear layers (handle creation)
     int tf_waves = 0;         // M2_TF_WAVES=4|8
-    int tfl_rb = 0;           // M2_TFL_RB=1|2|4
+    int tfl_rb = 0;           // M2_TFL_RB=1|2|4|8
     int tfl_first_rb = 0;     // M2_TFL_FIRST_RB=1|2|4
     int tfl_qs2 = -1;         // M2_TFL_QS2=0|1|3|4
     int att_qt = 0;           // M2_ATT_QT

@@ -46,7 +46,8 @@ void reload_switches() {
     const int tw = env_int("M2_TF_WAVES", 0);
     s.tf_waves = (tw == 4 || tw == 8) ? tw : 0;
     auto rb124 = [](int v) { return (v == 1 || v == 2 || v == 4) ? v : 0; };
-    s.tfl_rb = rb124(env_int("M2_TFL_RB", 0));
+    const int trb = env_int("M2_TFL_RB", 0);
+    s.tfl_rb = trb == 8 ? 8 : rb124(trb);  // 8: 128-row tiles for the unmasked layers (masked ones run 4)
     s.tfl_first_rb = rb124(env_int("M2_TFL_FIRST_RB", 0));
     if (const char* e = std::getenv("M2_TFL_QS2"); e && *e) {
         const int v = std::atoi(e);

@@ -1732,6 +1732,222 @@ __device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restri
     else fin(CI<0>{});
 }
 
+// 128-query tiles (the long-form decoder, unmasked; layer_kernel RB = 8):
+// wave w = (head w / 4, query pair w % 4) owns query blocks 2 (w % 4) and
+// 2 (w % 4) + 1 of its head over ALL keys - both 32-key chunks of every
+// 64-key step, one after the other, through the lean online softmax of
+// attention_qsplit2 (C = -m accumulators, MFMA row sums, base moves on an
+// f16 weight past 2^kLazyT).  The workgroup stages each step's K / V^T once
+// for twice the queries of the 64-row tile: the 64-row form streams 48 KB of
+// K / V^T per step and CU from L2 at ~36 GB/s per CU (B=128 T=2600: 10.5 GB
+// per launch, ~8 TB/s chip-wide), the attention's bound; here the same
+// stream feeds 128 queries, and the MFMA work per step and wave doubles over
+// the same barrier.  No partner merge (every wave sees every key).  Query
+// blocks past npad (the tile's second half when npad is not a multiple of
+// 128) load zero queries; their rows are never used.  Leaves the normalised
+// rows 0 .. 127 in A (split, stride srs(H)).
+template <int H, int HD>
+__device__ __forceinline__ void attention_q128(const unsigned char* __restrict__ qb,
+                                               const unsigned char* __restrict__ kb,
+                                               const unsigned char* __restrict__ vb, int b, int t0, int N,
+                                               int npad, unsigned char* A, unsigned char* ring) {
+    using G = Geo<HD>;
+    using Q = QsGeo<HD>;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
+    constexpr int PPT = Q::PPT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, g = lane >> 4;
+    const int h = wave >> 2, qp = wave & 3;
+    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
+
+    u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+        const int blk = t0 / 16 + 2 * qp + qq;
+        const bool have = 16 * blk < npad;  // wave-uniform
+        const unsigned char* qp8 = qb + ((size_t)(b * HEADS + h) * (npad / 16) + blk) * QKBLK + 16 * lane;
+        const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            qh[qq][ks] = have ? *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks) : z;
+            ql[qq][ks] = have ? *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024) : z;
+        }
+        if constexpr (KT) {
+            qxh[qq] = have && lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
+            qxl[qq] = have && lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
+        }
+    }
+    // staging of a 64-key step: as attention_qsplit2
+    __amdgpu_buffer_rsrc_t rsrc[PPT];
+    int sstep[PPT];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int o = 16 * (tid + NW * 64 * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
+        const size_t bh = (size_t)b * HEADS + hh;
+        const bool isk = r < Q::KB;
+        const unsigned char* base = isk ? kb + (bh * (npad / 16) + 2 * jj) * QKBLK + (r & ~1023)
+                                        : vb + (bh * nch + jj) * G::VCH + ((r - Q::KB) & ~1023);
+        rsrc[i] = wave_rsrc(base);
+        sstep[i] = __builtin_amdgcn_readfirstlane(isk ? 4 * QKBLK : 2 * G::VCH);
+    }
+    u32x4 pre[PPT];
+    auto gload = [&](int p) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i)
+            pre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc[i], 16 * lane, p * sstep[i], 0));
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
+    };
+
+    f32x4 acc[2][MT], lacc[2];
+    float m[2] = {0.f, 0.f};
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
+
+    // keys 64 p + 32 j + 16 u + 4 g + r of queries li of blocks 2 qp + qq
+    auto process = [&](const unsigned char* sb, int p, int j, bool fresh) {
+        float s[2][2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
+            f32x4 st[2] = {f32x4{-m[0], -m[0], -m[0], -m[0]}, f32x4{-m[1], -m[1], -m[1], -m[1]}};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
+                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kh, qh[qq][ks], st[qq]);
+                    st[qq] = mfma(kh, ql[qq][ks], st[qq]);
+                    st[qq] = mfma(kl, qh[qq][ks], st[qq]);
+                }
+            }
+            if constexpr (KT) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
+                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
+                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kxh, qxh[qq], st[qq]);
+                    st[qq] = mfma(kxh, qxl[qq], st[qq]);
+                    st[qq] = mfma(kxl, qxh[qq], st[qq]);
+                }
+            }
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
+        }
+        const int k0 = p * 2 * KC + j * KC;
+        if (N - k0 < KC) {  // the chunk straddles N: keys past N score -inf (wave-uniform)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq)
+                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
+        }
+        auto chunk_max = [&](int qq) {
+            return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
+                         fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+        };
+        if (fresh) {  // the first chunk (m = 0 above): the base is its maximum (wave-uniform)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
+                m[qq] = cm;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
+            }
+        }
+        u32x4 bh4[2], bl4[2];
+        auto exp_split = [&]() {
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                float e[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+                unsigned ph[4], pl[4];
+                split2u(e[0][0], e[0][1], ph[0], pl[0]);
+                split2u(e[0][2], e[0][3], ph[1], pl[1]);
+                split2u(e[1][0], e[1][1], ph[2], pl[2]);
+                split2u(e[1][2], e[1][3], ph[3], pl[3]);
+                bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+                bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+            }
+        };
+        exp_split();
+        if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
+                m[qq] += d;
+                const float corr = __builtin_amdgcn_exp2f(-d);
+                lacc[qq] *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
+            }
+            exp_split();
+        }
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
+            lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
+        }
+        const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+            const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
+            }
+        }
+    };
+
+    gload(0);
+    lstore(0);
+    if (1 < nsc) gload(1);
+    lds_barrier();
+#pragma unroll 1
+    for (int p = 0; p < nsc; ++p) {
+        // step p from buffer p & 1; p + 1 goes to the other buffer, p + 2 is requested
+        if (p + 1 < nsc) lstore((p + 1) & 1);
+        if (p + 2 < nsc) gload(p + 2);
+        unsigned char* sb = ring + (p & 1) * SB;
+        process(sb, p, 0, p == 0);                       // chunk 0 of step p holds key 64 p < N
+        if (2 * KC * p + KC < N) process(sb, p, 1, false);  // wave-uniform
+        lds_barrier();
+    }
+    TSTAMP(1);
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+        const float inv = 1.0f / lacc[qq][0];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+            put_split4<H>(A + (16 * (2 * qp + qq) + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), acc[qq][t][0] * inv,
+                          acc[qq][t][1] * inv, acc[qq][t][2] * inv, acc[qq][t][3] * inv);
+    }
+}
+
 // ---------------------------------------------------------------------------
 struct LArgs {
     int B, N, npad, ntile;
@@ -1751,15 +1967,19 @@ struct LArgs {
 
 // RB = 1 (16-row tiles) while the grid fits one round of the CUs, else 2
 // (32-row tiles: every K / V and weight fragment a workgroup reads serves
-// twice the rows).
+// twice the rows), 4 (64-row query-split tiles), 8 (unmasked only: 128-row
+// tiles whose attention runs over all 128 queries, attention_q128, and whose
+// row-local phases run as two 64-row halves in the same LDS).
 template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
+    static_assert(RB != 8 || !MASKED, "128-row tiles: unmasked attention only");
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
-    constexpr bool QS = RB == 4;  // 64-row tiles: attention_qsplit
+    constexpr bool QS = RB >= 4;                  // 64- / 128-row tiles: K / V staged in LDS
+    constexpr int RBH = RB == 8 ? 4 : RB, TRH = 16 * RBH, NHALF = RB == 8 ? 2 : 1;  // row-local phases
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att, then LN2(o), LN(y) (split)
     // the attention's scratch (key-quarter merge records / the K-V chunk ring)
     // and, after it, o / y (fp32, O) and relu(FFN1) (split, Hd)
-    constexpr int OB = TR * frs(H) * 4, HB = TR * srs(F);
+    constexpr int OB = TRH * frs(H) * 4, HB = TRH * srs(F);
     constexpr int XB = QS ? 2 * QsGeo<HD>::SB : NW * RB * 64 * Geo<HD>::XW * 4;
     __shared__ __attribute__((aligned(16))) unsigned char U[OB + HB > XB ? OB + HB : XB];
     float* const O = reinterpret_cast<float*>(U);
@@ -1777,7 +1997,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     const QkvOut qo{a.nq, a.nk, a.nv, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
     if (t0 >= N) {
-        if constexpr (NEXT == 1) zero_tile<H, HD, RB>(qo, b, t0);
+        if constexpr (NEXT == 1)
+            for (int hf = 0; hf < NHALF && t0 + TRH * hf < a.npad; ++hf) zero_tile<H, HD, RBH>(qo, b, t0 + TRH * hf);
         return;
     }
     for (int e = threadIdx.x; e < H; e += NW * 64) {
@@ -1798,7 +2019,11 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     int len = N;
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
-    if constexpr (QS) {
+    if constexpr (RB == 8) {
+        attention_q128<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        __syncthreads();
+        TSTAMP(2);
+    } else if constexpr (QS) {
         if constexpr (QV == 5 && !MASKED) attention_qsplit2p<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 3 || QV == 5) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
@@ -1815,107 +2040,129 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
             if (wave < H / 16) so.load(a.Wo, wave);
         });
     }
-    const size_t row0 = (size_t)b * N + t0;
-    // o = x + att . Wo^T + bo
-    if (wave < H / 16) {
-        const int col = wave * 16 + 4 * gq;
-        f32x4 acc[RB];
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VO + col);
-        gemm_t<H, RB>(A, so, acc);
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-            const int rr = rb * 16 + i;
-            f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (t0 + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
-            *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = x + acc[rb];
-        }
-    }
-    Strip<H> s1;
-    if (wave < F / 16) s1.load(a.W1, wave);
-    __syncthreads();
-    TSTAMP(3);
-    ln_rows<H, TR>(O, A, vec + VG2, vec + VB2N);
-    __syncthreads();
-    TSTAMP(4);
-    // h = relu(LN2(o) . W1^T + b1)
 #pragma unroll 1
-    for (int nb = wave; nb < F / 16; nb += NW) {
-        Strip<H> nxt;
-        if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
-        const int col = nb * 16 + 4 * gq;
-        f32x4 acc[RB];
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
-        gemm_t<H, RB>(A, s1, acc);
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-            put_split4<F>(Hd + (rb * 16 + i) * srs(F) + 2 * col, acc[rb][0] > 0.f ? acc[rb][0] : 0.f,
-                          acc[rb][1] > 0.f ? acc[rb][1] : 0.f, acc[rb][2] > 0.f ? acc[rb][2] : 0.f,
-                          acc[rb][3] > 0.f ? acc[rb][3] : 0.f);
-        if (nb + NW < F / 16) s1 = nxt;
-    }
-    Strip<F> s2;
-    if (wave < H / 16) s2.load(a.W2, wave);
-    __syncthreads();
-    TSTAMP(5);
-    // y = o + h . W2^T + b2
-    if (wave < H / 16) {
-        const int col = wave * 16 + 4 * gq;
-        f32x4 acc[RB];
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB2 + col);
-        gemm_t<F, RB>(Hd, s2, acc);
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-            const int rr = rb * 16 + i;
-            const f32x4 y = *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
-            if (t0 + rr < N) *reinterpret_cast<f32x4*>(a.x_out + (row0 + rr) * H + col) = y;
-            if constexpr (NEXT != 0) *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = y;
-        }
-    }
-    if constexpr (NEXT == 1) {
-        Strip<H> sn;
-        if (wave < 3 * H / 16) sn.load(a.Wn, wave);
-        __syncthreads();
-        TSTAMP(6);
-        ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
-        __syncthreads();
-        TSTAMP(7);
-        qkv_phase<H, HD, RB>(A, a.Wn, sn, qo, b, t0, N);
-        TSTAMP(8);
-        TSTAMP_RT(15);
-    } else if constexpr (NEXT == 2) {
-        Strip<H> sn;
-        if (wave < NN / 16) sn.load(a.Wn, wave);
-        __syncthreads();
-        TSTAMP(6);
-        ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
-        __syncthreads();
-        TSTAMP(7);
-#pragma unroll 1
-        for (int nb = wave; nb < NN / 16; nb += NW) {
-            Strip<H> nxt;
-            if (nb + NW < NN / 16) nxt.load(a.Wn, nb + NW);
-            const int col = nb * 16 + 4 * gq;
-            f32x4 acc[RB];
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VBN2 + col);
-            gemm_t<H, RB>(A, sn, acc);
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) {
-                const int rr = rb * 16 + i;
-                if (t0 + rr < N) *reinterpret_cast<f32x4*>(a.z + (row0 + rr) * NN + col) = acc[rb];
+    for (int hf = 0; hf < NHALF; ++hf) {
+        // rows t0h .. t0h + TRH - 1: their attention rows at Ah
+        const int t0h = t0 + TRH * hf;
+        unsigned char* const Ah = A + TRH * hf * srs(H);
+        if (hf > 0) {
+            if (t0h >= a.npad) break;  // workgroup-uniform
+            if (t0h >= N) {
+                if constexpr (NEXT == 1) zero_tile<H, HD, RBH>(qo, b, t0h);
+                break;
             }
-            if (nb + NW < NN / 16) sn = nxt;
+            __syncthreads();  // the first half's last readers of O / Hd / Ah are done
         }
-        TSTAMP(8);
-        TSTAMP_RT(15);
-    } else {
-        TSTAMP(6);
-        TSTAMP(7);
-        TSTAMP(8);
-        TSTAMP_RT(15);
+        // Wo's strip: per half with 128-row tiles (a strip held across the
+        // loop would stay live through both halves' FFN and spill)
+        Strip<H> soh;
+        if constexpr (NHALF == 2) {
+            if (wave < H / 16) soh.load(a.Wo, wave);
+        } else {
+            soh = so;
+        }
+        const size_t row0 = (size_t)b * N + t0h;
+        // o = x + att . Wo^T + bo
+        if (wave < H / 16) {
+            const int col = wave * 16 + 4 * gq;
+            f32x4 acc[RBH];
+#pragma unroll
+            for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VO + col);
+            gemm_t<H, RBH>(Ah, soh, acc);
+#pragma unroll
+            for (int rb = 0; rb < RBH; ++rb) {
+                const int rr = rb * 16 + i;
+                f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (t0h + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
+                *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = x + acc[rb];
+            }
+        }
+        Strip<H> s1;
+        if (wave < F / 16) s1.load(a.W1, wave);
+        __syncthreads();
+        TSTAMP(3);
+        ln_rows<H, TRH>(O, Ah, vec + VG2, vec + VB2N);
+        __syncthreads();
+        TSTAMP(4);
+        // h = relu(LN2(o) . W1^T + b1)
+#pragma unroll 1
+        for (int nb = wave; nb < F / 16; nb += NW) {
+            Strip<H> nxt;
+            if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
+            const int col = nb * 16 + 4 * gq;
+            f32x4 acc[RBH];
+#pragma unroll
+            for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
+            gemm_t<H, RBH>(Ah, s1, acc);
+#pragma unroll
+            for (int rb = 0; rb < RBH; ++rb)
+                put_split4<F>(Hd + (rb * 16 + i) * srs(F) + 2 * col, acc[rb][0] > 0.f ? acc[rb][0] : 0.f,
+                              acc[rb][1] > 0.f ? acc[rb][1] : 0.f, acc[rb][2] > 0.f ? acc[rb][2] : 0.f,
+                              acc[rb][3] > 0.f ? acc[rb][3] : 0.f);
+            if (nb + NW < F / 16) s1 = nxt;
+        }
+        Strip<F> s2;
+        if (wave < H / 16) s2.load(a.W2, wave);
+        __syncthreads();
+        TSTAMP(5);
+        // y = o + h . W2^T + b2
+        if (wave < H / 16) {
+            const int col = wave * 16 + 4 * gq;
+            f32x4 acc[RBH];
+#pragma unroll
+            for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB2 + col);
+            gemm_t<F, RBH>(Hd, s2, acc);
+#pragma unroll
+            for (int rb = 0; rb < RBH; ++rb) {
+                const int rr = rb * 16 + i;
+                const f32x4 y = *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
+                if (t0h + rr < N) *reinterpret_cast<f32x4*>(a.x_out + (row0 + rr) * H + col) = y;
+                if constexpr (NEXT != 0) *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = y;
+            }
+        }
+        if constexpr (NEXT == 1) {
+            Strip<H> sn;
+            if (wave < 3 * H / 16) sn.load(a.Wn, wave);
+            __syncthreads();
+            TSTAMP(6);
+            ln_rows<H, TRH>(O, Ah, vec + VGN, vec + VBN);
+            __syncthreads();
+            TSTAMP(7);
+            qkv_phase<H, HD, RBH>(Ah, a.Wn, sn, qo, b, t0h, N);
+            TSTAMP(8);
+            TSTAMP_RT(15);
+        } else if constexpr (NEXT == 2) {
+            Strip<H> sn;
+            if (wave < NN / 16) sn.load(a.Wn, wave);
+            __syncthreads();
+            TSTAMP(6);
+            ln_rows<H, TRH>(O, Ah, vec + VGN, vec + VBN);
+            __syncthreads();
+            TSTAMP(7);
+#pragma unroll 1
+            for (int nb = wave; nb < NN / 16; nb += NW) {
+                Strip<H> nxt;
+                if (nb + NW < NN / 16) nxt.load(a.Wn, nb + NW);
+                const int col = nb * 16 + 4 * gq;
+                f32x4 acc[RBH];
+#pragma unroll
+                for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VBN2 + col);
+                gemm_t<H, RBH>(Ah, sn, acc);
+#pragma unroll
+                for (int rb = 0; rb < RBH; ++rb) {
+                    const int rr = rb * 16 + i;
+                    if (t0h + rr < N) *reinterpret_cast<f32x4*>(a.z + (row0 + rr) * NN + col) = acc[rb];
+                }
+                if (nb + NW < NN / 16) sn = nxt;
+            }
+            TSTAMP(8);
+            TSTAMP_RT(15);
+        } else {
+            TSTAMP(6);
+            TSTAMP(7);
+            TSTAMP(8);
+            TSTAMP_RT(15);
+        }
     }
 }
 
@@ -2080,6 +2327,13 @@ int tfl_rb(int B, int N) {
     const long tiles16 = (long)B * (tfl_npad(N) / tfl::TQ);
     return tiles16 >= 4 * 256 ? 4 : (tiles16 > 256 ? 2 : 1);
 }
+// 128-row tiles (unmasked layers; M2_TFL_RB=8 forces them there): the
+// attention's K / V stream from L2 serves twice the queries of a 64-row tile
+// (attention_q128).  Default: off until measured.
+int tfl_rb_layer(int B, int N, bool masked) {
+    const int rb = tfl_rb(B, N);
+    return rb == 8 && masked ? 4 : rb;
+}
 // 64-row tiles: two query blocks per wave with the lean softmax
 // (attention_qsplit2<..., LEAN>) at head_dim 48 (stage2: B=128 T=2600 step
 // -1.5 %, B=16 T=2600 -1.9 %, B=64 T=500 -0.8 % against the plain two-block
@@ -2093,7 +2347,8 @@ int tfl_qs2(int H) {
     if (sw().tfl_qs2 >= 0) return sw().tfl_qs2;
     return H / tfl::HEADS >= 48 ? 3 : 4;
 }
-dim3 tfl_grid(int B, int N, int rb) { return dim3(B * (tfl_npad(N) / (tfl::TQ * rb))); }
+int tfl_ntile(int N, int rb) { return (tfl_npad(N) + tfl::TQ * rb - 1) / (tfl::TQ * rb); }
+dim3 tfl_grid(int B, int N, int rb) { return dim3(B * tfl_ntile(N, rb)); }
 float tfl_sl2(int H) {
     const float scale = (float)(1.0 / std::sqrt((double)(H / tfl::HEADS)));  // components.py:52, fp32 at the mul
     return scale * tfl::kLog2e;
@@ -2121,7 +2376,7 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     int rb = tfl_rb(B, N) > 1 ? 2 : 1;
     if ((long)B * (tfl_npad(N) / tfl::TQ) >= 16L * 256) rb = 4;
     if (sw().tfl_first_rb) rb = sw().tfl_first_rb;
-    a.ntile = a.npad / (tfl::TQ * rb);
+    a.ntile = tfl_ntile(N, rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
     a.sl2 = tfl_sl2(H);
@@ -2185,8 +2440,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.N = N;
     a.dN = dN;
     a.npad = tfl_npad(N);
-    const int rb = tfl_rb(B, N);
-    a.ntile = a.npad / (tfl::TQ * rb);
+    const int rb = tfl_rb_layer(B, N, masked);
+    a.ntile = tfl_ntile(N, rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
     a.sl2 = tfl_sl2(H);
@@ -2216,6 +2471,12 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     const int qs2 = tfl_qs2(H);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
+        if constexpr (!MM)                                                                      \
+            if (rb == 8) {                                                                      \
+                hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 8, 3>), grid, blk, 0, st, a); \
+                M2_LAUNCHED("tfl layer_kernel");                                                \
+                return M2_OK;                                                                   \
+            }                                                                                   \
         if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \

@@ -28,14 +28,15 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
-@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "4q3", "4q4", "4q5", "f4"])
+@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "4q3", "4q4", "4q5", "8", "f4"])
 def rows_per_tile(request, monkeypatch):
     """16- and 32-row workgroup tiles with key-quarter attention, 64-row tiles
     with query-split attention (K / V staged in LDS) (M2_TFL_RB) - the
     per-head-dim default, one query block and both chunks of each 64-key step
     ("4q1", M2_TFL_QS2=0) or two query blocks and one chunk ("4q2") - and the
     per-call choice; "f4": 64-row tiles for the first (LN1 -> QKV) launch
-    (M2_TFL_FIRST_RB, the default for very large grids)."""
+    (M2_TFL_FIRST_RB, the default for very large grids); "8": 128-row tiles
+    for the unmasked layers (attention_q128 over two 64-row halves)."""
     if request.param == "f4":
         monkeypatch.setenv("M2_TFL_FIRST_RB", "4")
     elif request.param != "auto":
