@@ -94,6 +94,13 @@ __device__ unsigned long long g_tfl_stamps[4096][8][16];
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef vx_u32x4 u32x4;
 
+// Diagnostic builds only (-DTFL_DIAG=bits, tools/runs): attention_qsplit2's
+// lean path without 1 its global K / V loads after step 2, 2 its softmax
+// VALU, 4 its LDS stores, 8 its QK^T MFMAs, 16 its PV MFMAs - the per-step
+// time each piece holds (results are garbage; never the product).
+#ifndef TFL_DIAG
+#define TFL_DIAG 0
+#endif
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLazyT = 8.f;  // unmasked lazy rescale: weights stay <= 2^kLazyT
 constexpr int TQ = 16;         // rows (queries) per workgroup
@@ -1100,7 +1107,7 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
 #pragma unroll
                     for (int qq = 0; qq < 2; ++qq) st[qq] = f32x4{-m[qq], -m[qq], -m[qq], -m[qq]};
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
+            for (int ks = 0; ks < KS * !(TFL_DIAG & 8); ++ks) {
                 const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
                 const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
 #pragma unroll
@@ -1110,7 +1117,7 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
                     st[qq] = mfma(kl, qh[qq][ks], st[qq]);
                 }
             }
-            if constexpr (KT) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
+            if constexpr (KT && !(TFL_DIAG & 8)) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
                 const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
                 const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
 #pragma unroll
@@ -1186,8 +1193,17 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
                     bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
                 }
             };
-            exp_split();
-            {
+            if constexpr (TFL_DIAG & 2) {  // diagnostic: no softmax VALU (P = the scores' bits)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    bh4[qq] = u32x4{__float_as_uint(s[qq][0][0]), __float_as_uint(s[qq][0][1]),
+                                    __float_as_uint(s[qq][0][2]), __float_as_uint(s[qq][0][3])};
+                    bl4[qq] = u32x4{__float_as_uint(s[qq][1][0]), __float_as_uint(s[qq][1][1]),
+                                    __float_as_uint(s[qq][1][2]), __float_as_uint(s[qq][1][3])};
+                }
+            } else
+                exp_split();
+            if constexpr (!(TFL_DIAG & 2)) {
                 if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // wave-uniform: move the base
 #pragma unroll
                     for (int qq = 0; qq < 2; ++qq) {
@@ -1212,7 +1228,7 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
             }
             const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
 #pragma unroll
-            for (int t = 0; t < MT; ++t) {
+            for (int t = 0; t < MT * !(TFL_DIAG & 16); ++t) {
                 const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
                 const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
 #pragma unroll
@@ -1222,6 +1238,9 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
                     acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
                 }
             }
+            if constexpr ((TFL_DIAG & 16) != 0)  // keep P live
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) asm volatile("" ::"v"(bh4[qq]), "v"(bl4[qq]));
             return;
         }
         float cmax[2];
@@ -1334,8 +1353,13 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
 #pragma unroll 1
     for (int p = 0; p < nsc; ++p) {
         // step p from buffer p & 1; p + 1 goes to the other buffer, p + 2 is requested
-        if (p + 1 < nsc) lstore((p + 1) & 1);
-        if (p + 2 < nsc) gload(p + 2);
+        if (p + 1 < nsc) {
+            if constexpr (!(TFL_DIAG & 4)) lstore((p + 1) & 1);
+            else
+#pragma unroll
+                for (int i = 0; i < PPT; ++i) asm volatile("" ::"v"(pre[i]));  // diagnostic: loads kept, no LDS stores
+        }
+        if (p + 2 < nsc && (!(TFL_DIAG & 1) || p < 2)) gload(p + 2);
         if (2 * KC * p + KC * j < N) process(ring + (p & 1) * SB, p);  // wave-uniform
         lds_barrier();
     }

@@ -956,6 +956,27 @@ __device__ unsigned long long g_x3_stamps[3][4096][16][16];
     } while (0)
 #endif
 
+// Window x and utterance y of a head workgroup, XCD-aware: workgroups go to
+// the 8 XCDs round-robin by linear id, and with x fastest the 8 windows of an
+// utterance land on 8 different XCDs, each of which fetches the mel lines
+// its window shares with its neighbours ([M][T] rows: a 69-frame window of a
+// channel row spans 3-4 lines of 128 B): FETCH_SIZE grew 0.22 MB per
+// utterance against 0.13 MB of mel at T = 500 (profiles/r04/r04c_head_fetch_*).
+// With B a multiple of 8 XCD k takes every window of utterances b = k mod 8,
+// so shared lines are fetched once per utterance.  Otherwise the plain order.
+#ifndef X3_HEAD_XCD  // A/B builds: 0 = plain order
+#define X3_HEAD_XCD 1
+#endif
+__device__ __forceinline__ void head_tile(int& x, int& y) {
+    x = blockIdx.x;
+    y = blockIdx.y;
+    if (X3_HEAD_XCD && (gridDim.y & 7) == 0) {
+        const int L = blockIdx.y * gridDim.x + blockIdx.x, k = L & 7, s = L >> 3, nx = gridDim.x;
+        y = 8 * (s / nx) + k;
+        x = s - (s / nx) * nx;
+    }
+}
+
 // The stage1 head runs ConvT1 / ResBlock1 phase-planar when one item per wave
 // covers them: planes of 64 rows hold TF + 2 <= 65 input columns and the
 // (phase, m-block) items of the C/2-channel layers number exactly HW.
@@ -972,14 +993,16 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     if (w.rclear && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         *reinterpret_cast<volatile int*>(w.rclear) = 0;
     constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
+    int wx, wy;
+    head_tile(wx, wy);
     if (w.dT) {  // speculative launch: T was the capacity
         T = dev_frames(w.dT, T);
-        if ((int)blockIdx.x * TF >= T) return;
+        if (wx * TF >= T) return;
     }
     using Pl = HeadPlan<MP, C, TF, head_planar<Cfg>()>;
     constexpr int C1 = Pl::C1;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int b = blockIdx.y, f0 = blockIdx.x * TF;
+    const int b = wy, f0 = wx * TF;
     XW a0w{lds, f0 - 2};
     XW hw{lds, 4 * f0 - 1};
     XW melw{lds + Pl::RA, f0 - 3};
