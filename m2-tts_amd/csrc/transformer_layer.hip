@@ -101,6 +101,9 @@ typedef vx_u32x4 u32x4;
 #ifndef TFL_DIAG
 #define TFL_DIAG 0
 #endif
+#ifndef TFL_STAGE_FIRST  // A/B builds: 1 = a step's staging before its K fragment reads
+#define TFL_STAGE_FIRST 0
+#endif
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLazyT = 8.f;  // unmasked lazy rescale: weights stay <= 2^kLazyT
 constexpr int TQ = 16;         // rows (queries) per workgroup
@@ -1096,11 +1099,29 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
     bool fresh = true;  // no chunk processed yet (wave-uniform)
 
     // keys 64 p + 32 j + 16 u + 4 g + r of query li of block qq
-    auto process = [&](const unsigned char* sb, int p) {
+    // stage: the next steps' staging (LDS stores, global loads), issued after
+    // this chunk's K fragment reads - LDS serves its queue in order, so K
+    // reads behind a step's 48 KB of stores would wait for all of them
+    // (TFL_STAGE_FIRST: the previous order, for A/B builds)
+    auto process = [&](const unsigned char* sb, int p, auto&& stage) {
         float s[2][2][4];
+        u32x4 kf[2][KSA][2], kx[2][2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
+#pragma unroll
+            for (int ks = 0; ks < KS * !(TFL_DIAG & 8); ++ks) {
+                kf[u][ks][0] = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
+                kf[u][ks][1] = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
+            }
+            if constexpr (KT && !(TFL_DIAG & 8)) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
+                kx[u][0] = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
+                kx[u][1] = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
+            }
+        }
+        if constexpr (!TFL_STAGE_FIRST) stage();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
             f32x4 st[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
             if constexpr (LEAN && !MASKED)
                 if (!fresh)
@@ -1108,23 +1129,19 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
                     for (int qq = 0; qq < 2; ++qq) st[qq] = f32x4{-m[qq], -m[qq], -m[qq], -m[qq]};
 #pragma unroll
             for (int ks = 0; ks < KS * !(TFL_DIAG & 8); ++ks) {
-                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
-                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
 #pragma unroll
                 for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kh, qh[qq][ks], st[qq]);
-                    st[qq] = mfma(kh, ql[qq][ks], st[qq]);
-                    st[qq] = mfma(kl, qh[qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][0], qh[qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][0], ql[qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][1], qh[qq][ks], st[qq]);
                 }
             }
-            if constexpr (KT && !(TFL_DIAG & 8)) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
-                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
-                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
+            if constexpr (KT && !(TFL_DIAG & 8)) {
 #pragma unroll
                 for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kxh, qxh[qq], st[qq]);
-                    st[qq] = mfma(kxh, qxl[qq], st[qq]);
-                    st[qq] = mfma(kxl, qxh[qq], st[qq]);
+                    st[qq] = mfma(kx[u][0], qxh[qq], st[qq]);
+                    st[qq] = mfma(kx[u][0], qxl[qq], st[qq]);
+                    st[qq] = mfma(kx[u][1], qxh[qq], st[qq]);
                 }
             }
 #pragma unroll
@@ -1353,14 +1370,18 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
 #pragma unroll 1
     for (int p = 0; p < nsc; ++p) {
         // step p from buffer p & 1; p + 1 goes to the other buffer, p + 2 is requested
-        if (p + 1 < nsc) {
-            if constexpr (!(TFL_DIAG & 4)) lstore((p + 1) & 1);
-            else
+        auto stage = [&] {
+            if (p + 1 < nsc) {
+                if constexpr (!(TFL_DIAG & 4)) lstore((p + 1) & 1);
+                else
 #pragma unroll
-                for (int i = 0; i < PPT; ++i) asm volatile("" ::"v"(pre[i]));  // diagnostic: loads kept, no LDS stores
-        }
-        if (p + 2 < nsc && (!(TFL_DIAG & 1) || p < 2)) gload(p + 2);
-        if (2 * KC * p + KC * j < N) process(ring + (p & 1) * SB, p);  // wave-uniform
+                    for (int i = 0; i < PPT; ++i) asm volatile("" ::"v"(pre[i]));  // diagnostic: loads kept, no LDS stores
+            }
+            if (p + 2 < nsc && (!(TFL_DIAG & 1) || p < 2)) gload(p + 2);
+        };
+        const bool live = 2 * KC * p + KC * j < N;  // wave-uniform
+        if (TFL_STAGE_FIRST || !live) stage();
+        if (live) process(ring + (p & 1) * SB, p, stage);
         lds_barrier();
     }
     TSTAMP(1);
