@@ -101,8 +101,8 @@ typedef vx_u32x4 u32x4;
 #ifndef TFL_DIAG
 #define TFL_DIAG 0
 #endif
-#ifndef TFL_STAGE_FIRST  // A/B builds: 1 = a step's staging before its K fragment reads
-#define TFL_STAGE_FIRST 0
+#ifndef TFL_STAGE_FIRST  // A/B builds: 0 = a step's staging after its K fragment reads
+#define TFL_STAGE_FIRST 1  // (0: decoder layers +4.5 % at B=128 T=2600, profiles/r04/r04i_stage_order.txt)
 #endif
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLazyT = 8.f;  // unmasked lazy rescale: weights stay <= 2^kLazyT
@@ -1099,10 +1099,9 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
     bool fresh = true;  // no chunk processed yet (wave-uniform)
 
     // keys 64 p + 32 j + 16 u + 4 g + r of query li of block qq
-    // stage: the next steps' staging (LDS stores, global loads), issued after
-    // this chunk's K fragment reads - LDS serves its queue in order, so K
-    // reads behind a step's 48 KB of stores would wait for all of them
-    // (TFL_STAGE_FIRST: the previous order, for A/B builds)
+    // stage: the next steps' staging (LDS stores, global loads), issued
+    // before this chunk's K fragment reads (TFL_STAGE_FIRST, the default) or
+    // after them (measured slower)
     auto process = [&](const unsigned char* sb, int p, auto&& stage) {
         float s[2][2][4];
         u32x4 kf[2][KSA][2], kx[2][2];
@@ -1415,6 +1414,287 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
             ls += __shfl_xor(ls, 16);
             ls += __shfl_xor(ls, 32);
         }
+        const float inv = 1.0f / ls;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (acc[qq][t][r] * fm + o[(2 + 4 * t + r) * 64] * fo) * inv;
+            put_split4<H>(A + (16 * (2 * qp + qq) + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2],
+                          v[3]);
+        }
+    };
+    if (j) put(CI<1>{});
+    else put(CI<0>{});
+    __syncthreads();
+    if (j) fin(CI<1>{});
+    else fin(CI<0>{});
+}
+
+// Ping-pong form of attention_qsplit2's lean unmasked path (M2_TFL_QS2=6).
+// Waves w and w + 4 share a SIMD (the workgroup's waves go to SIMDs
+// c[(w + r) mod 4]: tools/probe/simd_map.hip) and, in lockstep between the
+// per-step barriers, issue the same kind of work at the same time: both
+// waves' QK^T MFMAs, then both softmaxes (VALU), then both PV MFMAs - the
+// SIMD's matrix and vector pipes take turns.  Here the head-1 waves (w >= 4)
+// run one phase late: at step p they first issue the PV MFMAs of step p - 1
+// (P and V^T of step p - 1 held in registers across the barrier), then QK^T
+// of step p, then its softmax, and read step p's V^T fragments into
+// registers before the barrier.  So while the head-0 wave of a SIMD runs its
+// softmax the head-1 wave issues QK^T MFMAs, and while the head-0 wave
+// issues PV the head-1 wave runs its softmax.  Same arithmetic per score as
+// attention_qsplit2<..., LEAN> (the row sums by MFMA right after each
+// softmax, so a later base move scales them in the same order).
+template <int H, int HD>
+__device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restrict__ qb,
+                                                    const unsigned char* __restrict__ kb,
+                                                    const unsigned char* __restrict__ vb, int b, int t0, int N,
+                                                    int npad, unsigned char* A, unsigned char* ring) {
+    using G = Geo<HD>;
+    using Q = QsGeo<HD>;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
+    constexpr int PPT = Q::PPT, RW = 2 + 4 * MT;
+    static_assert(NW * RW * 64 * 4 <= 2 * SB, "merge records fit the ring");
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, g = lane >> 4;
+    const int h = wave >> 2, qp = (wave >> 1) & 1, j = wave & 1;
+    const bool late = h == 1;  // wave-uniform
+    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
+
+    u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+        const unsigned char* qp8 =
+            qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + 2 * qp + qq) * QKBLK + 16 * lane;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            qh[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks);
+            ql[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024);
+        }
+        if constexpr (KT) {
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            qxh[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
+            qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
+        }
+    }
+    __amdgpu_buffer_rsrc_t rsrc[PPT];
+    int sstep[PPT];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int o = 16 * (tid + NW * 64 * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
+        const size_t bh = (size_t)b * HEADS + hh;
+        const bool isk = r < Q::KB;
+        const unsigned char* base = isk ? kb + (bh * (npad / 16) + 2 * jj) * QKBLK + (r & ~1023)
+                                        : vb + (bh * nch + jj) * G::VCH + ((r - Q::KB) & ~1023);
+        rsrc[i] = wave_rsrc(base);
+        sstep[i] = __builtin_amdgcn_readfirstlane(isk ? 4 * QKBLK : 2 * G::VCH);
+    }
+    u32x4 pre[PPT];
+    auto gload = [&](int p) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i)
+            pre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc[i], 16 * lane, p * sstep[i], 0));
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
+    };
+
+    f32x4 acc[2][MT], lacc[2];
+    float m[2] = {0.f, 0.f};
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
+    bool fresh = true;
+    u32x4 bh4[2], bl4[2];  // P of the last softmax (split)
+    u32x4 vf[MT][2];       // the late waves' V^T fragments of that step
+    bool pend = false;     // late waves: PV of the previous step still to issue (wave-uniform)
+
+    auto pv = [&](const u32x4 (&v)[MT][2]) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                acc[qq][t] = mfma(v[t][0], bh4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(v[t][0], bl4[qq], acc[qq][t]);
+                acc[qq][t] = mfma(v[t][1], bh4[qq], acc[qq][t]);
+            }
+    };
+    auto vread = [&](const unsigned char* sb, u32x4 (&v)[MT][2]) {
+        const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            v[t][0] = *reinterpret_cast<const u32x4*>(vp + t * 2048);
+            v[t][1] = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
+        }
+    };
+    // QK^T and the softmax of this wave's chunk of step p (scores relative to
+    // the base; the first chunk sets it), P into bh4 / bl4, row sums by MFMA
+    auto qk_softmax = [&](const unsigned char* sb, int p, auto&& stage) {
+        u32x4 kf[2][KSA][2], kx[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                kf[u][ks][0] = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
+                kf[u][ks][1] = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
+            }
+            if constexpr (KT) {
+                kx[u][0] = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
+                kx[u][1] = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
+            }
+        }
+        if constexpr (!TFL_STAGE_FIRST) stage();
+        float s[2][2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 st[2] = {f32x4{-m[0], -m[0], -m[0], -m[0]}, f32x4{-m[1], -m[1], -m[1], -m[1]}};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kf[u][ks][0], qh[qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][0], ql[qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][1], qh[qq][ks], st[qq]);
+                }
+            if constexpr (KT)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kx[u][0], qxh[qq], st[qq]);
+                    st[qq] = mfma(kx[u][0], qxl[qq], st[qq]);
+                    st[qq] = mfma(kx[u][1], qxh[qq], st[qq]);
+                }
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
+        }
+        const int k0 = p * 2 * KC + j * KC;
+        if (N - k0 < KC) {  // the chunk straddles N (wave-uniform)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq)
+                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
+        }
+        auto chunk_max = [&](int qq) {
+            return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
+                         fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+        };
+        if (fresh) {
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
+                m[qq] = cm;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
+            }
+            fresh = false;
+        }
+        auto exp_split = [&]() {
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                float e[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+                unsigned ph[4], pl[4];
+                split2u(e[0][0], e[0][1], ph[0], pl[0]);
+                split2u(e[0][2], e[0][3], ph[1], pl[1]);
+                split2u(e[1][0], e[1][1], ph[2], pl[2]);
+                split2u(e[1][2], e[1][3], ph[3], pl[3]);
+                bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+                bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+            }
+        };
+        exp_split();
+        if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
+                m[qq] += d;
+                const float corr = __builtin_amdgcn_exp2f(-d);
+                lacc[qq] *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
+            }
+            exp_split();
+        }
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
+            lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
+        }
+    };
+
+    gload(0);
+    lstore(0);
+    if (1 < nsc) gload(1);
+    lds_barrier();
+#pragma unroll 1
+    for (int p = 0; p < nsc; ++p) {
+        auto stage = [&] {
+            if (p + 1 < nsc) lstore((p + 1) & 1);
+            if (p + 2 < nsc) gload(p + 2);
+        };
+        const bool live = 2 * KC * p + KC * j < N;  // wave-uniform
+        const unsigned char* sb = ring + (p & 1) * SB;
+        if (late) {
+            if (pend) pv(vf);  // step p - 1's PV (its P and V^T in registers)
+            pend = false;
+        }
+        if (TFL_STAGE_FIRST || !live) stage();
+        if (live) {
+            qk_softmax(sb, p, stage);
+            if (late) {
+                vread(sb, vf);
+                pend = true;
+            } else {
+                u32x4 v[MT][2];
+                vread(sb, v);
+                pv(v);
+            }
+        }
+        lds_barrier();
+    }
+    if (pend) pv(vf);
+    TSTAMP(1);
+    if (fresh) {  // this wave saw no key
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) m[qq] = -INFINITY;
+    }
+    float* rec = reinterpret_cast<float*>(ring);
+    auto put = [&](auto J) {
+        constexpr int qo = 1 - decltype(J)::value;
+        float* w = rec + (size_t)wave * RW * 64 + lane;
+        w[0] = m[qo];
+        w[64] = lacc[qo][0];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qo][t][r];
+    };
+    auto fin = [&](auto J) {
+        constexpr int qq = decltype(J)::value;
+        const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
+        const float mo = o[0];
+        const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
+        const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
+        const float ls = lacc[qq][0] * fm + o[64] * fo;
         const float inv = 1.0f / ls;
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -2070,7 +2350,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         TSTAMP(2);
     } else if constexpr (QS) {
         if constexpr (QV == 5 && !MASKED) attention_qsplit2p<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 3 || QV == 5) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        else if constexpr (QV == 6 && !MASKED) attention_qsplit2pp<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 3 || QV == 5 || QV == 6) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
         // row sums moved the stage1 encoder's error at B=128 S=130 from under
@@ -2522,7 +2803,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
                 M2_LAUNCHED("tfl layer_kernel");                                                \
                 return M2_OK;                                                                   \
             }                                                                                   \
-        if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
