@@ -2667,11 +2667,16 @@ int tfl_rb_layer(int B, int N, bool masked) {
 // one-block form +2.2 % at B=16 T=2600), the lean one-block form below
 // (stage1 B=32: -0.7 % against the plain one-block form; two blocks +0.3 to
 // +0.6 %; in-process A/Bs, profiles/r03/r03ab_*, r03ad_ab.txt, r03aj_ab.txt,
-// r03al_ab.txt).  M2_TFL_QS2=0|1|3|4 forces one block / two / two lean / one
-// lean (switch table, m2_common.h).
+// r03al_ab.txt).  Round 4: at head_dim 48 the ping-pong form of the lean
+// two-block attention (attention_qsplit2pp; masked launches keep the lean
+// two-block form): long-form step -0.9 %, decoder layer 1,575 -> 1,558 us,
+// B=16 T=2600 -0.6 %, B=64 T=500 -0.6 % (in-process A/Bs,
+// profiles/r04/r04j_*); the software-pipelined form (5) measured level or
+// slower (r04d / r04e).  M2_TFL_QS2=0|1|3|4|5|6 forces one block / two / two
+// lean / one lean / pipelined / ping-pong (switch table, m2_common.h).
 int tfl_qs2(int H) {
     if (sw().tfl_qs2 >= 0) return sw().tfl_qs2;
-    return H / tfl::HEADS >= 48 ? 3 : 4;
+    return H / tfl::HEADS >= 48 ? 6 : 4;
 }
 int tfl_ntile(int N, int rb) { return (tfl_npad(N) + tfl::TQ * rb - 1) / (tfl::TQ * rb); }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * tfl_ntile(N, rb)); }
