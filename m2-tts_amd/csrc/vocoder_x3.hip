@@ -962,10 +962,17 @@ __device__ unsigned long long g_x3_stamps[3][4096][16][16];
 // its window shares with its neighbours ([M][T] rows: a 69-frame window of a
 // channel row spans 3-4 lines of 128 B): FETCH_SIZE grew 0.22 MB per
 // utterance against 0.13 MB of mel at T = 500 (profiles/r04/r04c_head_fetch_*).
-// With B a multiple of 8 XCD k takes every window of utterances b = k mod 8,
-// so shared lines are fetched once per utterance.  Otherwise the plain order.
-#ifndef X3_HEAD_XCD  // A/B builds: 0 = plain order
-#define X3_HEAD_XCD 1
+// With B a multiple of 8 XCD k could take every window of utterances
+// b = k mod 8, so shared lines are fetched once per utterance: FETCH 9.66 ->
+// 7.71 MB per launch at B=32 ((FETCH - the 2.7 MB of weights per 8 XCDs) /
+// mel 1.7 -> 1.22), but the headline step +0.3 % (0.07158 / 0.07148 /
+// 0.07172 vs 0.07145 / 0.07138 / 0.07123 ms alternated,
+// profiles/r04/r04h_head_*, r04k_headline_xcd_ab.txt): the over-read lines
+// are served by the Infinity Cache, and the plain order spreads an
+// utterance's edge windows over the XCDs.  Kept as a build option
+// (-DX3_HEAD_XCD=1); the plain order is the default.
+#ifndef X3_HEAD_XCD
+#define X3_HEAD_XCD 0
 #endif
 __device__ __forceinline__ void head_tile(int& x, int& y) {
     x = blockIdx.x;
