@@ -1712,6 +1712,286 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
     else fin(CI<0>{});
 }
 
+// Wave-specialised query-split attention (M2_TFL_QS2=7, unmasked): the
+// diagnostic builds of the lean two-block form (profiles/r04/r04h_attention_diag.txt)
+// show its 64-key step as the serial sum of staging (~600 cycles of LDS
+// stores), softmax (~600) and the MFMAs, every wave doing each in turn.
+// Here waves 0-3 compute and waves 4-7 stage: consumer wave w = (head w / 2,
+// chunk w % 2) owns all four 16-query blocks of its head over its 32-key
+// chunk of every step (each K / V^T fragment it reads from LDS feeds four
+// blocks: half the LDS reads of the two-block form), producer wave 4 + c
+// shares a SIMD with consumer c (waves w and w + 4 do: tools/probe/simd_map.hip)
+// and moves steps p + 1 (registers -> LDS) and p + 2 (L2 -> registers) while
+// its consumer runs step p - so the stores and the loads' waits sit on the
+// producers' issue path, beside the consumers' MFMAs.  One barrier per step,
+// as before.  Consumers take their four blocks as two pairs (the two-block
+// lean softmax per pair: scores from C = -m, base moves on an f16 weight past
+// 2^kLazyT, row sums by MFMA); chunk waves (h, 0) and (h, 1) merge at the end
+// as in attention_qsplit2, wave (h, j) finalising blocks 2j, 2j + 1.
+template <int H, int HD>
+__device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restrict__ qb,
+                                                    const unsigned char* __restrict__ kb,
+                                                    const unsigned char* __restrict__ vb, int b, int t0, int N,
+                                                    int npad, unsigned char* A, unsigned char* ring) {
+    using G = Geo<HD>;
+    using Q = QsGeo<HD>;
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
+    constexpr int NP = NW / 2, PT = NP * 64;           // producer waves / threads
+    constexpr int PPT = SB / (16 * PT);                // 16-B pieces per producer thread per step
+    constexpr int RW = 2 * (2 + 4 * MT);               // merge record floats per lane: two blocks
+    static_assert(SB % (16 * PT) == 0, "a step is whole producer rounds");
+    static_assert((NW / 2) * RW * 64 * 4 <= 2 * SB, "merge records fit the ring");
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, g = lane >> 4;
+    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
+    const bool producer = wave >= NP;  // wave-uniform
+
+    if (producer) {
+        const int pt = tid - PT;  // 0 .. PT - 1
+        const unsigned char* src[PPT];
+        int sstep[PPT];
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int o = 16 * (pt + PT * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
+            const size_t bh = (size_t)b * HEADS + hh;
+            const bool isk = r < Q::KB;
+            src[i] = isk ? kb + (bh * (npad / 16) + 2 * jj) * QKBLK + r
+                         : vb + (bh * nch + jj) * G::VCH + (r - Q::KB);
+            sstep[i] = isk ? 4 * QKBLK : 2 * G::VCH;
+        }
+        u32x4 pre[PPT];
+        auto gload = [&](int p) {
+#pragma unroll
+            for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * sstep[i]);
+        };
+        auto lstore = [&](int buf) {
+#pragma unroll
+            for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (pt + PT * i)) = pre[i];
+        };
+        gload(0);
+        lstore(0);
+        if (1 < nsc) gload(1);
+        lds_barrier();
+#pragma unroll 1
+        for (int p = 0; p < nsc; ++p) {
+            if (p + 1 < nsc) lstore((p + 1) & 1);
+            if (p + 2 < nsc) gload(p + 2);
+            lds_barrier();
+        }
+        TSTAMP(1);
+        __syncthreads();  // the consumers' merge records
+        return;
+    }
+
+    const int h = wave >> 1, j = wave & 1;
+    u32x4 qh[4][KSA], ql[4][KSA], qxh[4], qxl[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+        const unsigned char* qp8 = qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + qq) * QKBLK + 16 * lane;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            qh[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks);
+            ql[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024);
+        }
+        if constexpr (KT) {
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            qxh[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
+            qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
+        }
+    }
+    f32x4 acc[4][MT], lacc[4];
+    float m[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
+    bool fresh = true;
+
+    // blocks Q0, Q0 + 1 of this wave's chunk of step p, K / V^T fragments in registers
+    auto pair = [&](auto Q0c, int p, const u32x4 (&kf)[2][KSA][2], const u32x4 (&kx)[2][2],
+                    const u32x4 (&vf)[MT][2], bool first) {
+        constexpr int Q0 = decltype(Q0c)::value;
+        float s[2][2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kf[u][ks][0], qh[Q0 + qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][0], ql[Q0 + qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][1], qh[Q0 + qq][ks], st[qq]);
+                }
+            if constexpr (KT)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kx[u][0], qxh[Q0 + qq], st[qq]);
+                    st[qq] = mfma(kx[u][0], qxl[Q0 + qq], st[qq]);
+                    st[qq] = mfma(kx[u][1], qxh[Q0 + qq], st[qq]);
+                }
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
+        }
+        const int k0 = p * 2 * KC + j * KC;
+        if (N - k0 < KC) {  // the chunk straddles N (wave-uniform)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq)
+                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
+        }
+        auto chunk_max = [&](int qq) {
+            return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
+                         fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+        };
+        if (first) {  // the wave's first chunk: the base is its maximum (wave-uniform)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
+                m[Q0 + qq] = cm;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
+            }
+        }
+        u32x4 bh4[2], bl4[2];
+        auto exp_split = [&]() {
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                float e[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+                unsigned ph[4], pl[4];
+                split2u(e[0][0], e[0][1], ph[0], pl[0]);
+                split2u(e[0][2], e[0][3], ph[1], pl[1]);
+                split2u(e[1][0], e[1][1], ph[2], pl[2]);
+                split2u(e[1][2], e[1][3], ph[3], pl[3]);
+                bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+                bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+            }
+        };
+        exp_split();
+        if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
+                m[Q0 + qq] += d;
+                const float corr = __builtin_amdgcn_exp2f(-d);
+                lacc[Q0 + qq] *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[Q0 + qq][t] *= corr;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
+            }
+            exp_split();
+        }
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            lacc[Q0 + qq] = mfma(ones, bh4[qq], lacc[Q0 + qq]);
+            lacc[Q0 + qq] = mfma(ones, bl4[qq], lacc[Q0 + qq]);
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                acc[Q0 + qq][t] = mfma(vf[t][0], bh4[qq], acc[Q0 + qq][t]);
+                acc[Q0 + qq][t] = mfma(vf[t][0], bl4[qq], acc[Q0 + qq][t]);
+                acc[Q0 + qq][t] = mfma(vf[t][1], bh4[qq], acc[Q0 + qq][t]);
+            }
+    };
+
+    lds_barrier();  // step 0 staged
+#pragma unroll 1
+    for (int p = 0; p < nsc; ++p) {
+        if (2 * KC * p + KC * j < N) {  // wave-uniform
+            const unsigned char* sb = ring + (p & 1) * SB + j * CB + h * Q::HB + 16 * lane;
+            u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    kf[u][ks][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks);
+                    kf[u][ks][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks + 1024);
+                }
+                if constexpr (KT) {
+                    kx[u][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL);
+                    kx[u][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                vf[t][0] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048);
+                vf[t][1] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048 + 1024);
+            }
+            pair(CI<0>{}, p, kf, kx, vf, fresh);
+            pair(CI<2>{}, p, kf, kx, vf, fresh);
+            fresh = false;
+        }
+        lds_barrier();
+    }
+    TSTAMP(1);
+    if (fresh) {  // this wave saw no key
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) m[qq] = -INFINITY;
+    }
+    // merge the chunk waves (h, 0), (h, 1): wave (h, j) finalises blocks
+    // 2j, 2j + 1 and hands its state of the other two to its partner
+    float* rec = reinterpret_cast<float*>(ring);
+    auto put = [&](auto J) {
+        constexpr int q0 = 2 * (1 - decltype(J)::value);
+        float* w = rec + (size_t)wave * RW * 64 + lane;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            float* we = w + e * (2 + 4 * MT) * 64;
+            we[0] = m[q0 + e];
+            we[64] = lacc[q0 + e][0];
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) we[(2 + 4 * t + r) * 64] = acc[q0 + e][t][r];
+        }
+    };
+    auto fin = [&](auto J) {
+        constexpr int q0 = 2 * decltype(J)::value;
+        const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float* oe = o + e * (2 + 4 * MT) * 64;
+            const int qq = q0 + e;
+            const float mo = oe[0];
+            const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
+            const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
+            const float ls = lacc[qq][0] * fm + oe[64] * fo;
+            const float inv = 1.0f / ls;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = (acc[qq][t][r] * fm + oe[(2 + 4 * t + r) * 64] * fo) * inv;
+                put_split4<H>(A + (16 * qq + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2], v[3]);
+            }
+        }
+    };
+    if (j) put(CI<1>{});
+    else put(CI<0>{});
+    __syncthreads();
+    if (j) fin(CI<1>{});
+    else fin(CI<0>{});
+}
+
 // Software-pipelined form of attention_qsplit2's lean unmasked path (the
 // long-form decoder; M2_TFL_QS2=5): iteration p issues the QK^T MFMAs of step
 // p + 1 beside the softmax VALU of step p (its scores were computed one
@@ -2351,7 +2631,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     } else if constexpr (QS) {
         if constexpr (QV == 5 && !MASKED) attention_qsplit2p<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 6 && !MASKED) attention_qsplit2pp<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 3 || QV == 5 || QV == 6) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        else if constexpr (QV == 7 && !MASKED) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 3 || QV == 5 || QV == 6 || QV == 7) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
         // row sums moved the stage1 encoder's error at B=128 S=130 from under
@@ -2808,7 +3089,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
                 M2_LAUNCHED("tfl layer_kernel");                                                \
                 return M2_OK;                                                                   \
             }                                                                                   \
-        if (rb == 4 && qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2 == 7) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 7>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
