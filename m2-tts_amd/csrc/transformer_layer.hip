@@ -1728,7 +1728,15 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
 // lean softmax per pair: scores from C = -m, base moves on an f16 weight past
 // 2^kLazyT, row sums by MFMA); chunk waves (h, 0) and (h, 1) merge at the end
 // as in attention_qsplit2, wave (h, j) finalising blocks 2j, 2j + 1.
-template <int H, int HD>
+// IL (M2_TFL_QS2=8): the consumers' steps that need neither the first-chunk
+// base nor the N mask run as three scheduling regions, each a matrix phase
+// with a vector phase laid into its MFMA gaps (__builtin_amdgcn_sched_group_barrier):
+// QK^T of pair 1 with the softmax of pair 0, then PV of pair 0 with the
+// softmax of pair 1 (V^T fragments read there, after K's are dead), then PV
+// of pair 1; the rare base moves branch between the regions, before the PV
+// that uses them.  One wave per SIMD computes, so the vector work only
+// overlaps the matrix work when one instruction stream carries both.
+template <int H, int HD, bool IL = false>
 __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restrict__ qb,
                                                     const unsigned char* __restrict__ kb,
                                                     const unsigned char* __restrict__ vb, int b, int t0, int N,
@@ -1914,9 +1922,142 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
     };
 
     lds_barrier();  // step 0 staged
+    // the interleaved step (IL): scores of a pair, their exponentials and split
+    auto qk2 = [&](auto Q0c, const u32x4 (&kf)[2][KSA][2], const u32x4 (&kx)[2][2], float (&s)[2][2][4]) {
+        constexpr int Q0 = decltype(Q0c)::value;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kf[u][ks][0], qh[Q0 + qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][0], ql[Q0 + qq][ks], st[qq]);
+                    st[qq] = mfma(kf[u][ks][1], qh[Q0 + qq][ks], st[qq]);
+                }
+            if constexpr (KT)
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq) {
+                    st[qq] = mfma(kx[u][0], qxh[Q0 + qq], st[qq]);
+                    st[qq] = mfma(kx[u][0], qxl[Q0 + qq], st[qq]);
+                    st[qq] = mfma(kx[u][1], qxh[Q0 + qq], st[qq]);
+                }
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
+        }
+    };
+    auto esplit = [](const float (&s)[2][2][4], u32x4 (&bh)[2], u32x4 (&bl)[2]) {
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            float e[2][4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+            unsigned ph[4], pl[4];
+            split2u(e[0][0], e[0][1], ph[0], pl[0]);
+            split2u(e[0][2], e[0][3], ph[1], pl[1]);
+            split2u(e[1][0], e[1][1], ph[2], pl[2]);
+            split2u(e[1][2], e[1][3], ph[3], pl[3]);
+            bh[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
+            bl[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
+        }
+    };
+    // a base move of a pair (rare; between the regions, before its PV)
+    auto rare = [&](auto Q0c, float (&s)[2][2][4], u32x4 (&bh)[2], u32x4 (&bl)[2]) {
+        constexpr int Q0 = decltype(Q0c)::value;
+        if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh[0], bh[1])) != 0) {
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const float cm = fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
+                                       fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
+                const float d = vmax(grp4_max(cm), 0.f);
+                m[Q0 + qq] += d;
+                const float corr = __builtin_amdgcn_exp2f(-d);
+                lacc[Q0 + qq] *= corr;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) acc[Q0 + qq][t] *= corr;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
+            }
+            esplit(s, bh, bl);
+        }
+    };
+    auto pv2 = [&](auto Q0c, const u32x4 (&bh)[2], const u32x4 (&bl)[2], const u32x4 (&vf)[MT][2]) {
+        constexpr int Q0 = decltype(Q0c)::value;
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            lacc[Q0 + qq] = mfma(ones, bh[qq], lacc[Q0 + qq]);
+            lacc[Q0 + qq] = mfma(ones, bl[qq], lacc[Q0 + qq]);
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                acc[Q0 + qq][t] = mfma(vf[t][0], bh[qq], acc[Q0 + qq][t]);
+                acc[Q0 + qq][t] = mfma(vf[t][0], bl[qq], acc[Q0 + qq][t]);
+                acc[Q0 + qq][t] = mfma(vf[t][1], bh[qq], acc[Q0 + qq][t]);
+            }
+    };
+    constexpr int NQK = 2 * 2 * 3 * (KS + KT), NPV = 4 + 6 * MT;  // MFMAs of a pair's QK^T / row sums + PV
+
 #pragma unroll 1
     for (int p = 0; p < nsc; ++p) {
-        if (2 * KC * p + KC * j < N) {  // wave-uniform
+        const int k0 = p * 2 * KC + j * KC;
+        if (IL && !fresh && N - k0 >= KC) {  // wave-uniform: a whole chunk after the first
+            const unsigned char* sb = ring + (p & 1) * SB + j * CB + h * Q::HB + 16 * lane;
+            u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    kf[u][ks][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks);
+                    kf[u][ks][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks + 1024);
+                }
+                if constexpr (KT) {
+                    kx[u][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL);
+                    kx[u][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
+                }
+            }
+            float s0[2][2][4], s1[2][2][4];
+            u32x4 bh0[2], bl0[2], bh1[2], bl1[2];
+            qk2(CI<0>{}, kf, kx, s0);
+            __builtin_amdgcn_sched_barrier(0);
+            // region 1: QK^T of pair 1 | softmax of pair 0 | V^T reads
+            qk2(CI<2>{}, kf, kx, s1);
+            esplit(s0, bh0, bl0);
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                vf[t][0] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048);
+                vf[t][1] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048 + 1024);
+            }
+#pragma unroll
+            for (int i = 0; i < NQK; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+                if (i < 2 * MT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            rare(CI<0>{}, s0, bh0, bl0);
+            __builtin_amdgcn_sched_barrier(0);
+            // region 2: PV of pair 0 | softmax of pair 1
+            pv2(CI<0>{}, bh0, bl0, vf);
+            esplit(s1, bh1, bl1);
+#pragma unroll
+            for (int i = 0; i < NPV; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            rare(CI<2>{}, s1, bh1, bl1);
+            __builtin_amdgcn_sched_barrier(0);
+            pv2(CI<2>{}, bh1, bl1, vf);
+        } else if (2 * KC * p + KC * j < N) {  // wave-uniform
             const unsigned char* sb = ring + (p & 1) * SB + j * CB + h * Q::HB + 16 * lane;
             u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
 #pragma unroll
@@ -2632,7 +2773,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         if constexpr (QV == 5 && !MASKED) attention_qsplit2p<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 6 && !MASKED) attention_qsplit2pp<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 7 && !MASKED) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 3 || QV == 5 || QV == 6 || QV == 7) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+        else if constexpr (QV == 8 && !MASKED) attention_qsplit_ws<H, HD, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 3 || QV >= 5) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
         // row sums moved the stage1 encoder's error at B=128 S=130 from under
@@ -3089,7 +3231,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
                 M2_LAUNCHED("tfl layer_kernel");                                                \
                 return M2_OK;                                                                   \
             }                                                                                   \
-        if (rb == 4 && qs2 == 7) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 7>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2 == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 8>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 7) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 7>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
