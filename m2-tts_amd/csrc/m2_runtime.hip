@@ -51,7 +51,7 @@ void reload_switches() {
     s.tfl_first_rb = rb124(env_int("M2_TFL_FIRST_RB", 0));
     if (const char* e = std::getenv("M2_TFL_QS2"); e && *e) {
         const int v = std::atoi(e);
-        s.tfl_qs2 = v >= 3 && v <= 8 ? v : (v != 0 ? 2 : 0);
+        s.tfl_qs2 = v >= 3 && v <= 10 ? v : (v != 0 ? 2 : 0);
     }
     s.att_qt = env_int("M2_ATT_QT", 0);
     if (const char* e = std::getenv("M2_ATT_F32")) s.att_f32 = *e && *e != '0';

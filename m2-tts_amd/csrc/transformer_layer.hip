@@ -1736,7 +1736,11 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
 // of pair 1; the rare base moves branch between the regions, before the PV
 // that uses them.  One wave per SIMD computes, so the vector work only
 // overlaps the matrix work when one instruction stream carries both.
-template <int H, int HD, bool IL = false>
+// DMA (M2_TFL_QS2=9, 10 with IL): the producers stage by LDS-DMA
+// (global_load_lds_dwordx4: L2 -> LDS, no VGPRs, no ds_write): step p + 1's
+// 12 pieces per producer lane are issued at the top of step p into the free
+// half of the ring and retired (vmcnt(0)) before the step's barrier.
+template <int H, int HD, bool IL = false, bool DMA = false>
 __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restrict__ qb,
                                                     const unsigned char* __restrict__ kb,
                                                     const unsigned char* __restrict__ vb, int b, int t0, int N,
@@ -1767,24 +1771,44 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
                          : vb + (bh * nch + jj) * G::VCH + (r - Q::KB);
             sstep[i] = isk ? 4 * QKBLK : 2 * G::VCH;
         }
-        u32x4 pre[PPT];
-        auto gload = [&](int p) {
+        if constexpr (DMA) {
+            const int pw = __builtin_amdgcn_readfirstlane(pt >> 6);
+            auto dma = [&](int p, int buf) {  // LDS destination: the wave's 1 KB (M0) + 16 x lane
 #pragma unroll
-            for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * sstep[i]);
-        };
-        auto lstore = [&](int buf) {
-#pragma unroll
-            for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (pt + PT * i)) = pre[i];
-        };
-        gload(0);
-        lstore(0);
-        if (1 < nsc) gload(1);
-        lds_barrier();
-#pragma unroll 1
-        for (int p = 0; p < nsc; ++p) {
-            if (p + 1 < nsc) lstore((p + 1) & 1);
-            if (p + 2 < nsc) gload(p + 2);
+                for (int i = 0; i < PPT; ++i)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(src[i] + (size_t)p * sstep[i]),
+                        (__attribute__((address_space(3))) void*)(ring + buf * SB + 16 * PT * i + 1024 * pw), 16, 0, 0);
+            };
+            dma(0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_barrier();
+#pragma unroll 1
+            for (int p = 0; p < nsc; ++p) {
+                if (p + 1 < nsc) dma(p + 1, (p + 1) & 1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                lds_barrier();
+            }
+        } else {
+            u32x4 pre[PPT];
+            auto gload = [&](int p) {
+#pragma unroll
+                for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * sstep[i]);
+            };
+            auto lstore = [&](int buf) {
+#pragma unroll
+                for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (pt + PT * i)) = pre[i];
+            };
+            gload(0);
+            lstore(0);
+            if (1 < nsc) gload(1);
+            lds_barrier();
+#pragma unroll 1
+            for (int p = 0; p < nsc; ++p) {
+                if (p + 1 < nsc) lstore((p + 1) & 1);
+                if (p + 2 < nsc) gload(p + 2);
+                lds_barrier();
+            }
         }
         TSTAMP(1);
         __syncthreads();  // the consumers' merge records
@@ -2774,6 +2798,8 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         else if constexpr (QV == 6 && !MASKED) attention_qsplit2pp<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 7 && !MASKED) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 8 && !MASKED) attention_qsplit_ws<H, HD, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 9 && !MASKED) attention_qsplit_ws<H, HD, false, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 10 && !MASKED) attention_qsplit_ws<H, HD, true, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 3 || QV >= 5) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
@@ -3231,7 +3257,9 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
                 M2_LAUNCHED("tfl layer_kernel");                                                \
                 return M2_OK;                                                                   \
             }                                                                                   \
-        if (rb == 4 && qs2 == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 8>), grid, blk, 0, st, a);  \
+        if (rb == 4 && qs2 == 10) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 10>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 9) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 9>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 8>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 7) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 7>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \

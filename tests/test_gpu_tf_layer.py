@@ -28,7 +28,7 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
-@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "4q3", "4q4", "4q5", "4q6", "4q7", "4q8", "8", "f4"])
+@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "4q3", "4q4", "4q5", "4q6", "4q7", "4q8", "4q9", "4q10", "8", "f4"])
 def rows_per_tile(request, monkeypatch):
     """16- and 32-row workgroup tiles with key-quarter attention, 64-row tiles
     with query-split attention (K / V staged in LDS) (M2_TFL_RB) - the
@@ -44,10 +44,10 @@ def rows_per_tile(request, monkeypatch):
     # "4q3" / "4q4": two / one block, lean softmax; "4q5": two blocks, lean,
     # software-pipelined, "4q6": two blocks, lean, ping-pong, "4q7": four
     # blocks per computing wave, staging waves, "4q8": that with the
-    # interleaved matrix / vector regions (unmasked launches; masked ones run
-    # "4q3")
-    if request.param in ("4q1", "4q2", "4q3", "4q4", "4q5", "4q6", "4q7", "4q8"):
-        monkeypatch.setenv("M2_TFL_QS2", "0" if request.param == "4q1" else request.param[-1:])
+    # interleaved matrix / vector regions, "4q9" / "4q10": "4q7" / "4q8" with
+    # LDS-DMA staging (unmasked launches; masked ones run "4q3")
+    if request.param.startswith("4q"):
+        monkeypatch.setenv("M2_TFL_QS2", "0" if request.param == "4q1" else request.param[2:])
     return request.param
 
 
