@@ -1736,11 +1736,13 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
 // of pair 1; the rare base moves branch between the regions, before the PV
 // that uses them.  One wave per SIMD computes, so the vector work only
 // overlaps the matrix work when one instruction stream carries both.
-// DMA (M2_TFL_QS2=9, 10 with IL): the producers stage by LDS-DMA
+// DMA (M2_TFL_QS2=9, 10 with IL = 2): the producers stage by LDS-DMA
 // (global_load_lds_dwordx4: L2 -> LDS, no VGPRs, no ds_write): step p + 1's
 // 12 pieces per producer lane are issued at the top of step p into the free
 // half of the ring and retired (vmcnt(0)) before the step's barrier.
-template <int H, int HD, bool IL = false, bool DMA = false>
+// IL = 2: the same regions without the group barriers (the compiler's own
+// order inside each region).
+template <int H, int HD, int IL = 0, bool DMA = false>
 __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restrict__ qb,
                                                     const unsigned char* __restrict__ kb,
                                                     const unsigned char* __restrict__ vb, int b, int t0, int N,
@@ -2033,7 +2035,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
 #pragma unroll 1
     for (int p = 0; p < nsc; ++p) {
         const int k0 = p * 2 * KC + j * KC;
-        if (IL && !fresh && N - k0 >= KC) {  // wave-uniform: a whole chunk after the first
+        if (IL != 0 && !fresh && N - k0 >= KC) {  // wave-uniform: a whole chunk after the first
             const unsigned char* sb = ring + (p & 1) * SB + j * CB + h * Q::HB + 16 * lane;
             u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
 #pragma unroll
@@ -2060,23 +2062,25 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
                 vf[t][0] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048);
                 vf[t][1] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048 + 1024);
             }
+            if constexpr (IL == 1)
 #pragma unroll
-            for (int i = 0; i < NQK; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-                if (i < 2 * MT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            }
+                for (int i = 0; i < NQK; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+                    if (i < 2 * MT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                }
             __builtin_amdgcn_sched_barrier(0);
             rare(CI<0>{}, s0, bh0, bl0);
             __builtin_amdgcn_sched_barrier(0);
             // region 2: PV of pair 0 | softmax of pair 1
             pv2(CI<0>{}, bh0, bl0, vf);
             esplit(s1, bh1, bl1);
+            if constexpr (IL == 1)
 #pragma unroll
-            for (int i = 0; i < NPV; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-            }
+                for (int i = 0; i < NPV; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                }
             __builtin_amdgcn_sched_barrier(0);
             rare(CI<2>{}, s1, bh1, bl1);
             __builtin_amdgcn_sched_barrier(0);
@@ -2797,9 +2801,9 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         if constexpr (QV == 5 && !MASKED) attention_qsplit2p<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 6 && !MASKED) attention_qsplit2pp<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 7 && !MASKED) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 8 && !MASKED) attention_qsplit_ws<H, HD, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 9 && !MASKED) attention_qsplit_ws<H, HD, false, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 10 && !MASKED) attention_qsplit_ws<H, HD, true, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 8 && !MASKED) attention_qsplit_ws<H, HD, 1>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 9 && !MASKED) attention_qsplit_ws<H, HD, 0, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 10 && !MASKED) attention_qsplit_ws<H, HD, 2, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 3 || QV >= 5) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
@@ -3116,16 +3120,20 @@ int tfl_rb_layer(int B, int N, bool masked) {
 // one-block form +2.2 % at B=16 T=2600), the lean one-block form below
 // (stage1 B=32: -0.7 % against the plain one-block form; two blocks +0.3 to
 // +0.6 %; in-process A/Bs, profiles/r03/r03ab_*, r03ad_ab.txt, r03aj_ab.txt,
-// r03al_ab.txt).  Round 4: at head_dim 48 the ping-pong form of the lean
-// two-block attention (attention_qsplit2pp; masked launches keep the lean
-// two-block form): long-form step -0.9 %, decoder layer 1,575 -> 1,558 us,
-// B=16 T=2600 -0.6 %, B=64 T=500 -0.6 % (in-process A/Bs,
-// profiles/r04/r04j_*); the software-pipelined form (5) measured level or
-// slower (r04d / r04e).  M2_TFL_QS2=0|1|3|4|5|6 forces one block / two / two
-// lean / one lean / pipelined / ping-pong (switch table, m2_common.h).
+// r03al_ab.txt).  Round 4: at head_dim 48 the wave-specialised form with
+// LDS-DMA staging (attention_qsplit_ws<..., DMA>; masked launches keep the
+// lean two-block form): against the ping-pong form (6), itself -0.9 % on the
+// long-form step against the lean two-block form (3): long-form step -1.5 %,
+// B=16 T=2600 -1.1 %, B=64 T=500 level (in-process A/Bs,
+// profiles/r04/r04j_*, r04l_*, r04m_*, r04n_*); at head_dim 32 it is slower
+// than the lean one-block form (stage1 B=32 +0.5 %, B=128 +1.4 %).  Measured
+// and not kept: the software-pipelined form (5, level or slower, r04d / r04e),
+// the wave-specialised form with register staging (7, between 6 and 9) and
+// with its regions interleaved by group barriers (8, +3 %).
+// M2_TFL_QS2=0|1|3..10 forces a form (switch table, m2_common.h).
 int tfl_qs2(int H) {
     if (sw().tfl_qs2 >= 0) return sw().tfl_qs2;
-    return H / tfl::HEADS >= 48 ? 6 : 4;
+    return H / tfl::HEADS >= 48 ? 9 : 4;
 }
 int tfl_ntile(int N, int rb) { return (tfl_npad(N) + tfl::TQ * rb - 1) / (tfl::TQ * rb); }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * tfl_ntile(N, rb)); }
