@@ -96,7 +96,9 @@ typedef vx_u32x4 u32x4;
 
 // Diagnostic builds only (-DTFL_DIAG=bits, tools/runs): attention_qsplit2's
 // lean path without 1 its global K / V loads after step 2, 2 its softmax
-// VALU, 4 its LDS stores, 8 its QK^T MFMAs, 16 its PV MFMAs - the per-step
+// VALU, 4 its LDS stores, 8 its QK^T MFMAs, 16 its PV MFMAs; the
+// wave-specialised DMA form's producers without 32 the wait for their
+// DMAs before the step barrier, 64 the DMAs after step 0 - the per-step
 // time each piece holds (results are garbage; never the product).
 #ifndef TFL_DIAG
 #define TFL_DIAG 0
@@ -1787,8 +1789,8 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             lds_barrier();
 #pragma unroll 1
             for (int p = 0; p < nsc; ++p) {
-                if (p + 1 < nsc) dma(p + 1, (p + 1) & 1);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (p + 1 < nsc && !(TFL_DIAG & 64)) dma(p + 1, (p + 1) & 1);
+                if constexpr (!(TFL_DIAG & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 lds_barrier();
             }
         } else {
