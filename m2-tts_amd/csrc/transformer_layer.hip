@@ -1776,13 +1776,25 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             sstep[i] = isk ? 4 * QKBLK : 2 * G::VCH;
         }
         if constexpr (DMA) {
-            const int pw = __builtin_amdgcn_readfirstlane(pt >> 6);
+            // buffer_load ... lds through a descriptor of each piece's 1-KB
+            // region: the lane offset in a fixed VGPR, the step's advance in
+            // an SGPR - no per-step address VALU
+            [[maybe_unused]] const int pw = __builtin_amdgcn_readfirstlane(pt >> 6);
+            __amdgpu_buffer_rsrc_t rs[PPT];
+            int ss[PPT];
+#pragma unroll
+            for (int i = 0; i < PPT; ++i) {
+                rs[i] = wave_rsrc(src[i] - 16 * lane);
+                ss[i] = __builtin_amdgcn_readfirstlane(sstep[i]);
+            }
             auto dma = [&](int p, int buf) {  // LDS destination: the wave's 1 KB (M0) + 16 x lane
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc does not know this builtin)
 #pragma unroll
                 for (int i = 0; i < PPT; ++i)
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void*)(src[i] + (size_t)p * sstep[i]),
-                        (__attribute__((address_space(3))) void*)(ring + buf * SB + 16 * PT * i + 1024 * pw), 16, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rs[i], (__attribute__((address_space(3))) void*)(ring + buf * SB + 16 * PT * i + 1024 * pw), 16,
+                        16 * lane, p * ss[i], 0, 0);
+#endif
             };
             dma(0, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1837,6 +1849,11 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
     }
     f32x4 acc[4][MT], lacc[4];
     float m[4] = {0.f, 0.f, 0.f, 0.f};
+    // -m as an accumulator (the QK^T chains start from it: the C operand of
+    // the first MFMA, no per-step vector build), refreshed when m moves
+    f32x4 nm[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) nm[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
 #pragma unroll
@@ -1853,7 +1870,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         float s[2][2][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
+            f32x4 st[2] = {nm[Q0], nm[Q0 + 1]};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -1893,6 +1910,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             for (int qq = 0; qq < 2; ++qq) {
                 const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
                 m[Q0 + qq] = cm;
+                nm[Q0 + qq] = f32x4{-cm, -cm, -cm, -cm};
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -1923,6 +1941,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             for (int qq = 0; qq < 2; ++qq) {
                 const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
                 m[Q0 + qq] += d;
+                nm[Q0 + qq] = f32x4{-m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq]};
                 const float corr = __builtin_amdgcn_exp2f(-d);
                 lacc[Q0 + qq] *= corr;
 #pragma unroll
@@ -1955,7 +1974,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         constexpr int Q0 = decltype(Q0c)::value;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
+            f32x4 st[2] = {nm[Q0], nm[Q0 + 1]};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -2004,6 +2023,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
                                        fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
                 const float d = vmax(grp4_max(cm), 0.f);
                 m[Q0 + qq] += d;
+                nm[Q0 + qq] = f32x4{-m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq]};
                 const float corr = __builtin_amdgcn_exp2f(-d);
                 lacc[Q0 + qq] *= corr;
 #pragma unroll
