@@ -1849,11 +1849,6 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
     }
     f32x4 acc[4][MT], lacc[4];
     float m[4] = {0.f, 0.f, 0.f, 0.f};
-    // -m as an accumulator (the QK^T chains start from it: the C operand of
-    // the first MFMA, no per-step vector build), refreshed when m moves
-    f32x4 nm[4];
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) nm[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
 #pragma unroll
@@ -1870,7 +1865,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         float s[2][2][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {nm[Q0], nm[Q0 + 1]};
+            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -1910,7 +1905,6 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             for (int qq = 0; qq < 2; ++qq) {
                 const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
                 m[Q0 + qq] = cm;
-                nm[Q0 + qq] = f32x4{-cm, -cm, -cm, -cm};
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -1941,7 +1935,6 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             for (int qq = 0; qq < 2; ++qq) {
                 const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
                 m[Q0 + qq] += d;
-                nm[Q0 + qq] = f32x4{-m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq]};
                 const float corr = __builtin_amdgcn_exp2f(-d);
                 lacc[Q0 + qq] *= corr;
 #pragma unroll
@@ -1974,7 +1967,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         constexpr int Q0 = decltype(Q0c)::value;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {nm[Q0], nm[Q0 + 1]};
+            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -2023,7 +2016,6 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
                                        fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
                 const float d = vmax(grp4_max(cm), 0.f);
                 m[Q0 + qq] += d;
-                nm[Q0 + qq] = f32x4{-m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq], -m[Q0 + qq]};
                 const float corr = __builtin_amdgcn_exp2f(-d);
                 lacc[Q0 + qq] *= corr;
 #pragma unroll
