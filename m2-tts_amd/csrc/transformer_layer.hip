@@ -1857,6 +1857,36 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
     }
     const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
     bool fresh = true;
+    // QT (head_dim 48): the base rides in the tail k-step.  Its MFMA sums 32
+    // k-elements of which only 16 are head dims (lane groups 2, 3 carry zero
+    // Q).  Lane group 2's first two elements become A = (1, 1) (every key)
+    // and B = (hi, lo) of -m (its query): the QK^T chain then delivers
+    // q.k - m itself, from C = 0 - no per-step -m vector build (16 VALU per
+    // query pair).  The base is kept as the value those two f16 halves
+    // represent (hi + lo, exact in f32), so every use of m stays consistent.
+    constexpr bool QT = KT == 1 && KS >= 1;
+    const bool g2 = (lane >> 4) == 2;
+    auto set_base = [&](int qq, float mnew) {  // m[qq] := mnew (as the tail's halves hold it)
+        if constexpr (QT) {
+            const _Float16 hi = (_Float16)(-mnew);
+            const _Float16 lo = (_Float16)(-mnew - (float)hi);
+            m[qq] = -((float)hi + (float)lo);
+            const unsigned w = (unsigned)__builtin_bit_cast(unsigned short, hi) |
+                               ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+            if (g2) qxh[qq][0] = w;
+        } else {
+            m[qq] = mnew;
+        }
+    };
+    auto fix_tail = [&](u32x4 (&kx)[2][2]) {  // lane group 2: A = (1, 1) for kxh, 0 for kxl
+        if constexpr (QT)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                kx[u][0][0] = g2 ? 0x3C003C00u : kx[u][0][0];
+                kx[u][1][0] = g2 ? 0u : kx[u][1][0];
+            }
+    };
+    auto c0 = [&](int qq) { return QT ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{-m[qq], -m[qq], -m[qq], -m[qq]}; };
 
     // blocks Q0, Q0 + 1 of this wave's chunk of step p, K / V^T fragments in registers
     auto pair = [&](auto Q0c, int p, const u32x4 (&kf)[2][KSA][2], const u32x4 (&kx)[2][2],
@@ -1865,7 +1895,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         float s[2][2][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
+            f32x4 st[2] = {c0(Q0), c0(Q0 + 1)};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -1903,12 +1933,11 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         if (first) {  // the wave's first chunk: the base is its maximum (wave-uniform)
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
-                const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
-                m[Q0 + qq] = cm;
+                set_base(Q0 + qq, grp4_max(chunk_max(qq)));  // finite: the chunk holds a key < N
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= m[Q0 + qq];
             }
         }
         u32x4 bh4[2], bl4[2];
@@ -1933,8 +1962,9 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
-                const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
-                m[Q0 + qq] += d;
+                const float mold = m[Q0 + qq];
+                set_base(Q0 + qq, mold + vmax(grp4_max(chunk_max(qq)), 0.f));
+                const float d = m[Q0 + qq] - mold;
                 const float corr = __builtin_amdgcn_exp2f(-d);
                 lacc[Q0 + qq] *= corr;
 #pragma unroll
@@ -1967,7 +1997,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
         constexpr int Q0 = decltype(Q0c)::value;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {f32x4{-m[Q0], -m[Q0], -m[Q0], -m[Q0]}, f32x4{-m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1], -m[Q0 + 1]}};
+            f32x4 st[2] = {c0(Q0), c0(Q0 + 1)};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -2014,8 +2044,9 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             for (int qq = 0; qq < 2; ++qq) {
                 const float cm = fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
                                        fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
-                const float d = vmax(grp4_max(cm), 0.f);
-                m[Q0 + qq] += d;
+                const float mold = m[Q0 + qq];
+                set_base(Q0 + qq, mold + vmax(grp4_max(cm), 0.f));
+                const float d = m[Q0 + qq] - mold;
                 const float corr = __builtin_amdgcn_exp2f(-d);
                 lacc[Q0 + qq] *= corr;
 #pragma unroll
@@ -2064,6 +2095,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
                     kx[u][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
                 }
             }
+            fix_tail(kx);
             float s0[2][2][4], s1[2][2][4];
             u32x4 bh0[2], bl0[2], bh1[2], bl1[2];
             qk2(CI<0>{}, kf, kx, s0);
@@ -2114,6 +2146,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
                     kx[u][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
                 }
             }
+            fix_tail(kx);
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
                 vf[t][0] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048);
