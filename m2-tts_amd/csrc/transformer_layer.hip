@@ -3303,22 +3303,25 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nv = out.v;
     a.z = z;
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
-    const int qs2 = tfl_qs2(H);
+    // forms 5-10 are unmasked-only (masked launches of those forms run 3):
+    // no masked instantiations of them
+    const int qs2 = masked && tfl_qs2(H) >= 5 ? 3 : tfl_qs2(H);
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        if constexpr (!MM)                                                                      \
-            if (rb == 8) {                                                                      \
-                hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 8, 3>), grid, blk, 0, st, a); \
+        if constexpr (!MM) {                                                                    \
+            if (rb == 8 || (rb == 4 && qs2 >= 5)) {                                             \
+                if (rb == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 8, 3>), grid, blk, 0, st, a); \
+                else if (qs2 == 10) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 10>), grid, blk, 0, st, a); \
+                else if (qs2 == 9) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 9>), grid, blk, 0, st, a); \
+                else if (qs2 == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 8>), grid, blk, 0, st, a); \
+                else if (qs2 == 7) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 7>), grid, blk, 0, st, a); \
+                else if (qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a); \
+                else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a); \
                 M2_LAUNCHED("tfl layer_kernel");                                                \
                 return M2_OK;                                                                   \
             }                                                                                   \
-        if (rb == 4 && qs2 == 10) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 10>), grid, blk, 0, st, a);  \
-        else if (rb == 4 && qs2 == 9) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 9>), grid, blk, 0, st, a);  \
-        else if (rb == 4 && qs2 == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 8>), grid, blk, 0, st, a);  \
-        else if (rb == 4 && qs2 == 7) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 7>), grid, blk, 0, st, a);  \
-        else if (rb == 4 && qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a);  \
-        else if (rb == 4 && qs2 == 5) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a);  \
-        else if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
+        }                                                                                       \
+        if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
         else if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
