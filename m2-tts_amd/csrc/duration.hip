@@ -275,13 +275,20 @@ __device__ void count_frames(const float* __restrict__ dur, int B, int S, const 
 // (one wave per row, the halo rows redundantly) and stores its own 14
 // normalised rows to enc_out - the encoder output the length regulator
 // expands - in place of a separate layer_norm_kernel launch.
-template <int H, bool LN, bool COUNT, int RBK, bool SPL = false>
+// PERS (large grids, no fused count): a grid of at most one workgroup per CU
+// walks the tiles (tile t: utterance t / ntx, phonemes (t % ntx) * TS ..),
+// loading both convs' weight fragments once instead of once per tile - at
+// B=128 S=520 the 2,304 30-phoneme tiles streamed 0.44 MB of split weights
+// each (1 GB per launch from L2).
+template <int H, bool LN, bool COUNT, int RBK, bool SPL = false, bool PERS = false>
 __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     const float* __restrict__ enc, int S, const float4* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ a1, const float* __restrict__ c1, const float4* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ a2, const float* __restrict__ c2,
     const float* __restrict__ pw, const float* __restrict__ pb, float* __restrict__ dur,
-    const float* __restrict__ lng, const float* __restrict__ lnb, float* __restrict__ enc_out, DurCount dc) {
+    const float* __restrict__ lng, const float* __restrict__ lnb, float* __restrict__ enc_out, DurCount dc,
+    int ntiles) {
+    static_assert(!(PERS && COUNT), "the fused count's ticket counts workgroups of a one-tile-each grid");
     constexpr int XS = H + 2, NT = 64 * DUR_WAVES;
     constexpr int TS = 16 * RBK - 2, NX = TS + 4;  // phonemes per tile, input rows with the halo
     static_assert(!SPL || LN, "the split convs take the fused LayerNorm's bounded rows");
@@ -290,9 +297,8 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
     __shared__ __attribute__((aligned(16))) float X[NX * XF];   // positions s0-2 .. s0+TS+1
     __shared__ __attribute__((aligned(16))) float Y1[NX * XF];  // s0-1 .. s0+TS (+2 zero rows read by conv2's unused rows)
     __shared__ float Y2[16 * RBK * XS];  // s0 .. s0+TS-1 (+2 unused)
-    const int b = blockIdx.y, s0 = blockIdx.x * TS, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const float* e = enc + (size_t)b * S * H;
     DurW<H> W1, W2;
     DurWS<H> V1, V2;
     if constexpr (SPL) {
@@ -302,6 +308,8 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
         dur_wload<H>(w1, W1);
         dur_wload<H>(w2, W2);
     }
+    auto tile = [&](const int b, const int s0) {
+    const float* e = enc + (size_t)b * S * H;
     if constexpr (LN) {
         // every row of this wave is loaded before the first is normalised (one
         // memory round trip per wave instead of one per row)
@@ -377,6 +385,17 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
             else
                 dur[(size_t)b * S + s] = d;
         }
+    }
+    };
+    if constexpr (PERS) {
+        const int ntx = (S + TS - 1) / TS;
+#pragma unroll 1
+        for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+            tile(t / ntx, (t % ntx) * TS);
+            __syncthreads();  // the next tile's rows overwrite X / Y1 / Y2
+        }
+    } else {
+        tile(blockIdx.y, blockIdx.x * TS);
     }
     if constexpr (COUNT) {
         // hand-off to the last workgroup (MI355X_MICROARCH.md, inter-workgroup
@@ -545,17 +564,37 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
     // M2_DUR_RB=1|2 forces one (switch table, m2_common.h).
     int rbk = (long)B * cdiv(S, DUR_TS) > 256 ? 2 : 1;
     if (sw().dur_rb) rbk = sw().dur_rb;
-    const dim3 grid(cdiv(S, 16 * rbk - 2), B), blk(64 * DUR_WAVES);
+    dim3 grid(cdiv(S, 16 * rbk - 2), B);
+    const dim3 blk(64 * DUR_WAVES);
+    // persistent tiles (PERS) past two rounds of the CUs, without the fused
+    // count (M2_DUR_PERS=0 never)
+    const int ntiles = (int)grid.x * B;
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    }
+    const bool pers = !dc && sw().dur_pers && ntiles > 2 * ncu;
+    if (pers) grid = dim3(ncu, 1);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
     const DurCount none{};
     // split-f16 convs: the fused-LayerNorm (inference) launches of a model
     // whose static bound allows them (wsplit = its split weight packs)
     const bool spl = wsplit && enc_out;
-#define M2_DUR_L(HH, LL, CC, RR, SP)                                                                                \
-    hipLaunchKernelGGL((duration_kernel<HH, LL, CC, RR, SP>), grid, blk, 0, st, enc, S,                          \
+#define M2_DUR_K(HH, LL, CC, RR, SP, PP)                                                                            \
+    hipLaunchKernelGGL((duration_kernel<HH, LL, CC, RR, SP, PP>), grid, blk, 0, st, enc, S,                      \
                        f4(SP ? wsplit[0] : p[0]), p[1], p[2], p[3], f4(SP ? wsplit[1] : p[4]), p[5], p[6], p[7],    \
                        p[8], p[9], dur, LL ? ln_g : nullptr, LL ? ln_b : nullptr, LL ? enc_out : nullptr,           \
-                       dc ? *dc : none)
+                       dc ? *dc : none, ntiles)
+#define M2_DUR_L(HH, LL, CC, RR, SP)                      \
+    do {                                                  \
+        if constexpr (!CC) {                              \
+            if (pers) M2_DUR_K(HH, LL, CC, RR, SP, true); \
+            else M2_DUR_K(HH, LL, CC, RR, SP, false);     \
+        } else {                                          \
+            M2_DUR_K(HH, LL, CC, RR, SP, false);          \
+        }                                                 \
+    } while (0)
 #define M2_DUR_R(HH, LL, CC, SP)                      \
     if (rbk == 2) M2_DUR_L(HH, LL, CC, 2, SP);        \
     else M2_DUR_L(HH, LL, CC, 1, SP)
@@ -580,6 +619,7 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
 #undef M2_DUR_R
 #undef M2_DUR
 #undef M2_DUR_L
+#undef M2_DUR_K
     M2_LAUNCHED("duration_kernel");
     return M2_OK;
 }

@@ -49,6 +49,7 @@ struct Switches {
     bool s2_head_tf16 = false;  // M2_S2_HEAD_TF16
     int redo_grid = -1;         // M2_REDO_GRID: workgroups of the guarded redo launch (-1: one per CU)
     bool dur_split = true;      // M2_DUR_SPLIT=0: the duration convs on the exact-f32 MFMA always
+    bool dur_pers = true;       // M2_DUR_PERS=0: one duration tile per workgroup at every grid size
 };
 const Switches& sw();
 void reload_switches();

@@ -71,6 +71,7 @@ void reload_switches() {
     s.s2_head_tf16 = env_set("M2_S2_HEAD_TF16");
     s.redo_grid = env_int("M2_REDO_GRID", -1);
     s.dur_split = env_on("M2_DUR_SPLIT", true);
+    s.dur_pers = env_on("M2_DUR_PERS", true);
     g_sw = s;
 }
 

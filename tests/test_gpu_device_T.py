@@ -379,3 +379,36 @@ def test_duration_split_convs(gpu, stage, B, S, monkeypatch):
         enc, _ = orc.text_encoder(sd, cfg, ids.cpu(), lens.cpu())
         dref = orc.duration_predictor(sd, enc)
     assert maxabs(d1, dref) <= 1e-4
+
+
+@pytest.mark.parametrize("stage,B,S", [("s2", 64, 300), ("s1", 128, 130), ("s2", 37, 517)])
+def test_duration_persistent_tiles(gpu, stage, B, S, monkeypatch):
+    """Grids past two rounds of the CUs run the duration kernel persistent
+    (one workgroup per CU walking the tiles, weights loaded once): the same
+    per-tile arithmetic as one tile per workgroup (M2_DUR_PERS=0), so the
+    front buffer (encoder output, durations, counts) and T_max are bit for bit
+    equal, and the durations match the oracle (tts_model.py:99-117)."""
+    m = build_model(stage, gpu)
+    hm = m._hip(gpu)
+    g = torch.Generator().manual_seed(B * 11 + S)
+    ids = torch.randint(0, 42, (B, S), generator=g).to(gpu)
+    lens = torch.randint(1, S + 1, (B,), generator=g).to(gpu)
+    H = stage_config(stage).hidden_dim
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("M2_DUR_PERS", v)
+        tw = torch.full((1,), -7, dtype=torch.int32, device=gpu)
+        st = hm.inference_front_dev(ids, lens, 1.0, tw)
+        torch.cuda.synchronize(gpu)
+        out[v] = (st[2].clone(), int(tw.item()))
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out["0"][1]
+    nb = B * S * H * 4
+    do = (nb + 255) // 256 * 256
+    d = out["1"][0][do:do + B * S * 4].view(torch.float32).view(B, S)
+    sd = golden_state(stage)
+    cfg = stage_config(stage)
+    with torch.no_grad():
+        enc, _ = orc.text_encoder(sd, cfg, ids.cpu(), lens.cpu())
+        dref = orc.duration_predictor(sd, enc)
+    assert maxabs(d, dref) <= 1e-4
