@@ -1515,23 +1515,6 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
     u32x4 bh4[2], bl4[2];  // P of the last softmax (split)
     u32x4 vf[MT][2];       // the late waves' V^T fragments of that step
     bool pend = false;     // late waves: PV of the previous step still to issue (wave-uniform)
-    // QT (head_dim 48): the base rides in the tail k-step's spare lane group
-    // (as attention_qsplit_ws does)
-    constexpr bool QT = KT == 1 && KS >= 1;
-    const bool g2 = (lane >> 4) == 2;
-    auto set_base = [&](int qq, float mnew) {
-        if constexpr (QT) {
-            const _Float16 hi = (_Float16)(-mnew);
-            const _Float16 lo = (_Float16)(-mnew - (float)hi);
-            m[qq] = -((float)hi + (float)lo);
-            const unsigned w = (unsigned)__builtin_bit_cast(unsigned short, hi) |
-                               ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
-            if (g2) qxh[qq][0] = w;
-        } else {
-            m[qq] = mnew;
-        }
-    };
-    auto c0 = [&](int qq) { return QT ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{-m[qq], -m[qq], -m[qq], -m[qq]}; };
 
     auto pv = [&](const u32x4 (&v)[MT][2]) {
 #pragma unroll
@@ -1566,17 +1549,13 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
             if constexpr (KT) {
                 kx[u][0] = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
                 kx[u][1] = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
-                if constexpr (QT) {
-                    kx[u][0][0] = g2 ? 0x3C003C00u : kx[u][0][0];
-                    kx[u][1][0] = g2 ? 0u : kx[u][1][0];
-                }
             }
         }
         if constexpr (!TFL_STAGE_FIRST) stage();
         float s[2][2][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {c0(0), c0(1)};
+            f32x4 st[2] = {f32x4{-m[0], -m[0], -m[0], -m[0]}, f32x4{-m[1], -m[1], -m[1], -m[1]}};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -1614,11 +1593,12 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
         if (fresh) {
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
-                set_base(qq, grp4_max(chunk_max(qq)));  // finite: the chunk holds a key < N
+                const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
+                m[qq] = cm;
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= m[qq];
+                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
             }
             fresh = false;
         }
@@ -1643,9 +1623,8 @@ __device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restr
         if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
-                const float mold = m[qq];
-                set_base(qq, mold + vmax(grp4_max(chunk_max(qq)), 0.f));
-                const float d = m[qq] - mold;
+                const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
+                m[qq] += d;
                 const float corr = __builtin_amdgcn_exp2f(-d);
                 lacc[qq] *= corr;
 #pragma unroll
