@@ -3018,8 +3018,11 @@ struct FArgs {
     unsigned char *q, *k, *v;
 };
 
+#ifndef FK_MINW  // A/B builds: waves per SIMD the first launch is compiled for
+#define FK_MINW 2
+#endif
 template <int H, int SRC, bool MASKED, int RB>
-__global__ __launch_bounds__(512, 2) void first_kernel(FArgs a) {
+__global__ __launch_bounds__(512, FK_MINW) void first_kernel(FArgs a) {
     constexpr int HD = H / HEADS, H4 = H / 4, TR = 16 * RB;
     __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];
