@@ -212,49 +212,51 @@ __device__ __forceinline__ void put_split4(unsigned char* p, float a, float b, f
 
 // LayerNorm (eps 1e-5, biased variance, affine) of R fp32 LDS rows src into
 // split rows dst: 8 lanes per row, two-pass as nn.LayerNorm; g, b in LDS.
-template <int H, int R>
+template <int H, int R, int NT = NW * 64>
 __device__ __forceinline__ void ln_rows(const float* src, unsigned char* dst, const float* g, const float* b) {
     constexpr int PER = H / 8;
     static_assert(PER % 4 == 0, "H multiple of 32");
-    if (threadIdx.x >= 8 * R) return;
-    const int row = threadIdx.x >> 3, part = threadIdx.x & 7;
-    const float* xr = src + row * frs(H) + part * PER;
-    float v[PER];
+#pragma unroll 1
+    for (int x = threadIdx.x; x < 8 * R; x += NT) {
+        const int row = x >> 3, part = x & 7;
+        const float* xr = src + row * frs(H) + part * PER;
+        float v[PER];
 #pragma unroll
-    for (int q = 0; q < PER / 4; ++q) {
-        const float4 t = *reinterpret_cast<const float4*>(xr + 4 * q);
-        v[4 * q] = t.x;
-        v[4 * q + 1] = t.y;
-        v[4 * q + 2] = t.z;
-        v[4 * q + 3] = t.w;
-    }
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) s += v[k];
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 4);
-    const float mean = s / (float)H;
-    float var = 0.f;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const float d = v[k] - mean;
-        var += d * d;
-    }
-    var += __shfl_xor(var, 1);
-    var += __shfl_xor(var, 2);
-    var += __shfl_xor(var, 4);
-    const float rstd = 1.0f / sqrtf(var / (float)H + kLnEps);
-    unsigned char* yr = dst + row * srs(H) + 2 * part * PER;
-#pragma unroll
-    for (int q = 0; q < PER / 4; ++q) {
-        float y[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int k = part * PER + 4 * q + e;
-            y[e] = (v[4 * q + e] - mean) * rstd * g[k] + b[k];
+        for (int q = 0; q < PER / 4; ++q) {
+            const float4 t = *reinterpret_cast<const float4*>(xr + 4 * q);
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
         }
-        put_split4<H>(yr + 8 * q, y[0], y[1], y[2], y[3]);
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) s += v[k];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        const float mean = s / (float)H;
+        float var = 0.f;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const float d = v[k] - mean;
+            var += d * d;
+        }
+        var += __shfl_xor(var, 1);
+        var += __shfl_xor(var, 2);
+        var += __shfl_xor(var, 4);
+        const float rstd = 1.0f / sqrtf(var / (float)H + kLnEps);
+        unsigned char* yr = dst + row * srs(H) + 2 * part * PER;
+#pragma unroll
+        for (int q = 0; q < PER / 4; ++q) {
+            float y[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = part * PER + 4 * q + e;
+                y[e] = (v[4 * q + e] - mean) * rstd * g[k] + b[k];
+            }
+            put_split4<H>(yr + 8 * q, y[0], y[1], y[2], y[3]);
+        }
     }
 }
 
@@ -319,15 +321,15 @@ __device__ __forceinline__ void store_v(const QkvOut& o, int b, int t0, int N, i
 
 // The QKV projection of the tile's LN rows Xn (16 RB rows from t0) into the
 // attention layouts.
-template <int H, int HD, int RB>
+template <int H, int HD, int RB, int NWV = NW>
 __device__ __forceinline__ void qkv_phase(const unsigned char* Xn, const u32x4* __restrict__ W, Strip<H>& cur,
                                           const QkvOut& o, int b, int t0, int N) {
     constexpr int NB = 3 * H / 16, NQK = 2 * H / 16;
     const int wave = threadIdx.x >> 6;
 #pragma unroll 1
-    for (int nb = wave; nb < NB; nb += NW) {
+    for (int nb = wave; nb < NB; nb += NWV) {
         Strip<H> nxt;
-        if (nb + NW < NB) nxt.load(W, nb + NW);
+        if (nb + NWV < NB) nxt.load(W, nb + NWV);
         f32x4 acc[RB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -340,17 +342,17 @@ __device__ __forceinline__ void qkv_phase(const unsigned char* Xn, const u32x4* 
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) store_v<H, HD>(o, b, t0 + 16 * rb, N, nb, acc[rb]);
         }
-        if (nb + NW < NB) cur = nxt;
+        if (nb + NWV < NB) cur = nxt;
     }
 }
 
 // A tile wholly past the utterance's end: its rows of the next attention
 // buffers are zeros (no GEMM).
-template <int H, int HD, int RB>
+template <int H, int HD, int RB, int NWV = NW>
 __device__ __forceinline__ void zero_tile(const QkvOut& o, int b, int t0) {
     constexpr int NB = 3 * H / 16, NQK = 2 * H / 16;
     const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int nb = threadIdx.x >> 6; nb < NB; nb += NW)
+    for (int nb = threadIdx.x >> 6; nb < NB; nb += NWV)
         for (int rb = 0; rb < RB; ++rb) {
             if (nb < NQK) store_qk<H, HD>(o, b, t0 + 16 * rb, 0, nb, z4);
             else store_v<H, HD>(o, b, t0 + 16 * rb, 0, nb, z4);
@@ -3021,8 +3023,12 @@ struct FArgs {
 #ifndef FK_MINW  // A/B builds: waves per SIMD the first launch is compiled for
 #define FK_MINW 2
 #endif
+#ifndef FK_NW  // A/B builds: waves per first-launch workgroup (4: two workgroups per CU)
+#define FK_NW 8
+#endif
+constexpr int FNW = FK_NW;
 template <int H, int SRC, bool MASKED, int RB>
-__global__ __launch_bounds__(512, FK_MINW) void first_kernel(FArgs a) {
+__global__ __launch_bounds__(FNW * 64, FK_MINW) void first_kernel(FArgs a) {
     constexpr int HD = H / HEADS, H4 = H / 4, TR = 16 * RB;
     __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];
@@ -3039,12 +3045,12 @@ __global__ __launch_bounds__(512, FK_MINW) void first_kernel(FArgs a) {
     const int wave = threadIdx.x >> 6;
     const QkvOut qo{a.q, a.k, a.v, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
     if (t0 >= N) {
-        zero_tile<H, HD, RB>(qo, b, t0);
+        zero_tile<H, HD, RB, FNW>(qo, b, t0);
         return;
     }
     Strip<H> sq;
     if (wave < 3 * H / 16) sq.load(a.W, wave);
-    for (int e = threadIdx.x; e < H; e += NW * 64) {
+    for (int e = threadIdx.x; e < H; e += FNW * 64) {
         vec[e] = a.g[e];
         vec[H + e] = a.bln[e];
     }
@@ -3057,7 +3063,7 @@ __global__ __launch_bounds__(512, FK_MINW) void first_kernel(FArgs a) {
         const int32_t* cg = a.cum + (size_t)b * (a.S + 1);
         const bool in_lds = a.S + 1 <= CS;
         if (in_lds)
-            for (int k = threadIdx.x; k <= a.S; k += NW * 64) cs[k] = cg[k];
+            for (int k = threadIdx.x; k <= a.S; k += FNW * 64) cs[k] = cg[k];
         __syncthreads();
         if (threadIdx.x < TR) {
             const int32_t* c = in_lds ? cs : cg;
@@ -3076,7 +3082,7 @@ __global__ __launch_bounds__(512, FK_MINW) void first_kernel(FArgs a) {
         }
         __syncthreads();
     }
-    for (int idx = threadIdx.x; idx < TR * H4; idx += NW * 64) {
+    for (int idx = threadIdx.x; idx < TR * H4; idx += FNW * 64) {
         const int r = idx / H4, c = (idx - r * H4) * 4, t = t0 + r;
         const size_t row = (size_t)b * N + t;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -3101,9 +3107,9 @@ __global__ __launch_bounds__(512, FK_MINW) void first_kernel(FArgs a) {
         *reinterpret_cast<float4*>(O + r * frs(H) + c) = v;
     }
     __syncthreads();
-    ln_rows<H, TR>(O, A, vec, vec + H);
+    ln_rows<H, TR, FNW * 64>(O, A, vec, vec + H);
     __syncthreads();
-    qkv_phase<H, HD, RB>(A, a.W, sq, qo, b, t0, N);
+    qkv_phase<H, HD, RB, FNW>(A, a.W, sq, qo, b, t0, N);
 }
 
 }  // namespace tfl
@@ -3239,7 +3245,7 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.q = out.q;
     a.k = out.k;
     a.v = out.v;
-    const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
+    const dim3 grid = tfl_grid(B, N, rb), blk(tfl::FNW * 64);
 #define M2_TFF(HH, SS, MM)                                                                      \
     if (H == HH && f.src == SS && masked == MM) {                                               \
         if (rb == 4) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 4>), grid, blk, 0, st, a);  \
