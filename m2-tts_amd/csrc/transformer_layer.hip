@@ -3023,13 +3023,19 @@ struct FArgs {
 #ifndef FK_MINW  // A/B builds: waves per SIMD the first launch is compiled for
 #define FK_MINW 2
 #endif
-#ifndef FK_NW  // A/B builds: waves per first-launch workgroup (4: two workgroups per CU)
-#define FK_NW 8
+// Waves per first-launch workgroup: 64-row tiles (the very large grids) run
+// 4 waves, so two workgroups share a CU at 189 VGPRs and one tile's latency
+// chain (prefix sums -> search -> gather -> LN -> QKV -> stores) overlaps the
+// other's: configs[4]'s frame-expansion launch 210 -> 192 us; the small grids'
+// 16- and 32-row tiles keep 8 (4 there: B=8 6.3 -> 7.5 us,
+// profiles/r04/r04af_*).
+#ifndef FK_NW4  // A/B builds: waves of the 64-row-tile workgroups
+#define FK_NW4 4
 #endif
-constexpr int FNW = FK_NW;
+constexpr int fk_nw(int rb) { return rb == 4 ? FK_NW4 : NW; }
 template <int H, int SRC, bool MASKED, int RB>
-__global__ __launch_bounds__(FNW * 64, FK_MINW) void first_kernel(FArgs a) {
-    constexpr int HD = H / HEADS, H4 = H / 4, TR = 16 * RB;
+__global__ __launch_bounds__(fk_nw(RB) * 64, FK_MINW) void first_kernel(FArgs a) {
+    constexpr int HD = H / HEADS, H4 = H / 4, TR = 16 * RB, FNW = fk_nw(RB);
     __shared__ __attribute__((aligned(16))) float O[TR * frs(H)];
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];
     __shared__ __attribute__((aligned(16))) float vec[2 * H];
@@ -3245,7 +3251,7 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.q = out.q;
     a.k = out.k;
     a.v = out.v;
-    const dim3 grid = tfl_grid(B, N, rb), blk(tfl::FNW * 64);
+    const dim3 grid = tfl_grid(B, N, rb), blk(tfl::fk_nw(rb) * 64);
 #define M2_TFF(HH, SS, MM)                                                                      \
     if (H == HH && f.src == SS && masked == MM) {                                               \
         if (rb == 4) hipLaunchKernelGGL((tfl::first_kernel<HH, SS, MM, 4>), grid, blk, 0, st, a);  \
