@@ -3218,13 +3218,13 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     a.B = B;
     a.N = N;
     a.npad = tfl_npad(N);
-    // rows per workgroup: the layers' choice up to 32 (64-row tiles made this
-    // launch 23 % faster but the step 1.4 % slower at stage2 B=64, in-process
-    // A/B, profiles/r03/ab/r03x_ab.txt), 64 for grids of >= 16 rounds of
-    // 16-row tiles (the long-form decoder: a series of latency-bound rounds);
+    // rows per workgroup: the layers' choice up to 32, 64 for grids of >= 8
+    // rounds of 16-row tiles (latency-bound rounds; with 8-wave workgroups
+    // 64-row tiles made stage2 B=64 1.4 % slower, profiles/r03/ab/r03x_ab.txt,
+    // with the 4-wave ones (fk_nw) 0.5-1.7 % faster, r04ag_s2_b64_first_rb);
     // M2_TFL_FIRST_RB=1|2|4 forces one (switch table, m2_common.h)
     int rb = tfl_rb(B, N) > 1 ? 2 : 1;
-    if ((long)B * (tfl_npad(N) / tfl::TQ) >= 16L * 256) rb = 4;
+    if ((long)B * (tfl_npad(N) / tfl::TQ) >= 8L * 256) rb = 4;
     if (sw().tfl_first_rb) rb = sw().tfl_first_rb;
     a.ntile = tfl_ntile(N, rb);
     a.qcnt = q.cnt;
