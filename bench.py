@@ -188,23 +188,71 @@ def cpu_quota():
         return None
 
 
-def cpu_measure(run, runs: int, min_s: float):
-    """Median / min / max over `runs` measurements of run()'s rate (calls/s),
-    each measurement timing whole calls for at least min_s seconds."""
-    rates = []
+def _cg_throttled_s():
+    """Seconds this cgroup has been throttled by its CPU quota so far (cgroup
+    v2 cpu.stat throttled_usec, v1 throttled_time), or None."""
+    for path, key, scale in (("/sys/fs/cgroup/cpu.stat", "throttled_usec", 1e-6),
+                             ("/sys/fs/cgroup/cpu/cpu.stat", "throttled_time", 1e-9)):
+        try:
+            for line in open(path):
+                k, v = line.split()[:2]
+                if k == key:
+                    return int(v) * scale
+        except (OSError, ValueError):
+            pass
+    return None
+
+
+def _steal_s():
+    """Steal time so far, summed over this process's CPUs (the cpuN lines of
+    /proc/stat, USER_HZ ticks) and divided by their number: wall seconds the
+    hypervisor took from a thread pinned there, on average."""
+    try:
+        mine = {f"cpu{c}" for c in os.sched_getaffinity(0)}
+        tot = 0
+        for line in open("/proc/stat"):
+            f = line.split()
+            if f and f[0] in mine and len(f) > 8:
+                tot += int(f[8])
+        return tot / os.sysconf("SC_CLK_TCK") / max(1, len(mine))
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def cpu_measure(run, runs: int, min_s: float, threads: int):
+    """`runs` measurements of run()'s rate (calls/s), each timing whole calls
+    for at least min_s seconds, with what each run got of the CPUs: busy =
+    this process's CPU seconds / (wall seconds x threads), and the cgroup
+    throttle / host steal seconds that fell inside it.  A run that another
+    tenant's load slowed down shows a busy fraction well under the best run's
+    (its threads were descheduled) or throttle / steal time: it is dropped
+    (kept: busy >= 0.85 x the best run's, throttle + steal <= 5 % of the wall
+    time), and the statistics are over the kept runs."""
+    recs = []
     with torch.no_grad():
         run()  # warm-up
         for _ in range(runs):
-            n, t0 = 0, time.perf_counter()
+            n, th0, st0 = 0, _cg_throttled_s(), _steal_s()
+            c0, t0 = time.process_time(), time.perf_counter()
             while True:
                 run()
                 n += 1
                 el = time.perf_counter() - t0
                 if el >= min_s:
                     break
-            rates.append(n / el)
-    rates.sort()
-    return rates[len(rates) // 2], rates[0], rates[-1], rates
+            cpu = time.process_time() - c0
+            th1, st1 = _cg_throttled_s(), _steal_s()
+            thr = th1 - th0 if th0 is not None and th1 is not None else 0.0
+            stl = st1 - st0 if st0 is not None and st1 is not None else 0.0
+            recs.append({"rate": n / el, "busy": round(cpu / (el * max(1, threads)), 3), "throttled_s": round(thr, 3),
+                         "steal_s": round(stl, 3), "wall_s": round(el, 3)})
+    best_busy = max(r["busy"] for r in recs)
+    kept = [r for r in recs
+            if r["busy"] >= 0.85 * best_busy and r["throttled_s"] + r["steal_s"] <= 0.05 * r["wall_s"]]
+    if len(kept) < 3:  # too few clean runs: keep them all and say so
+        kept = recs
+    rates = sorted(r["rate"] for r in kept)
+    return rates[len(rates) // 2], rates[0], rates[-1], recs, len(kept)
 
 
 def cpu_child_main(spec):
@@ -234,18 +282,20 @@ def cpu_child_main(spec):
                          "min_duration_dist_to_int": float((dur - dur.round()).abs().min())}
     for name, run in (("vocoder", lambda: orc.vocoder(sd, mel)),
                       ("inference_as_written", lambda: orc.inference(sd, cfg, ids, lens, as_written=True))):
-        med, lo, hi, rates = cpu_measure(run, spec["runs"], spec["min_s"])
+        med, lo, hi, recs, nkept = cpu_measure(run, spec["runs"], spec["min_s"], len(spec["cpus"]))
         out[name] = {"median": med * B * 64 * T, "min": lo * B * 64 * T, "max": hi * B * 64 * T,
-                     "calls_per_s": [round(r, 3) for r in rates]}
+                     "calls_per_s": [round(r["rate"], 3) for r in recs], "runs": recs, "kept": nkept}
     print(json.dumps(out), flush=True)
 
 
-def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_seed=None):
+def cpu_baseline(B: int, S: int, T: int, runs: int = 7, min_s: float = 1.5, ids_seed=None):
     """Time the CPU oracle (the reference's op sequence) on the
     node's host cores: a child process pinned to one logical CPU per physical
     core of this process's affinity mask, one OpenMP thread per core
-    (torch.set_num_threads(physical cores)), median of `runs` measurements
-    with the spread (value = the median run).  Two figures for the headline configuration: the
+    (torch.set_num_threads(physical cores)), median of the clean runs among
+    `runs` measurements (cpu_measure drops runs another tenant's load slowed
+    down), with their spread; `unstable` when the kept runs still spread by
+    20 % or more (value = the median run).  Two figures for the headline configuration: the
     vocoder single pass (configs[1], the `value`) and M2TTSModel.inference as
     written (2 vocoder passes, Python length-regulator loop)."""
     phys, sockets = physical_cores()
@@ -266,6 +316,7 @@ def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_
     cpu_model, ncpu, aff = host_info()
     voc, inf = res["vocoder"], res["inference_as_written"]
     spread = lambda d: round((d["max"] - d["min"]) / d["median"], 3)  # noqa: E731
+    unstable = lambda d: spread(d) >= 0.2  # noqa: E731
     # value = the median of the runs; the best run (other tenants' load on the
     # shared host only slows a run down) and the spread are reported beside it
     return {"value": voc["median"], "best": voc["max"], "unit": "audio samples/s", "cores": len(cpus),
@@ -274,15 +325,18 @@ def cpu_baseline(B: int, S: int, T: int, runs: int = 5, min_s: float = 1.5, ids_
             "physical_cores_in_affinity": len(phys), "cgroup_cpu_quota": quota,
             "torch_threads": res["torch_threads"], "pinned": "one OpenMP thread per physical core "
             "(OMP_PROC_BIND=close on one logical CPU per core)", "cpu_model": cpu_model,
-            "stat": f"median of {runs} runs of >= {min_s} s (best, min, max beside it)", "min": voc["min"],
+            "stat": f"median of the {voc['kept']} clean runs of {runs} of >= {min_s} s (best, min, max "
+                    f"beside it; a run is dropped when its threads got < 0.85 x the best run's CPU time or the "
+                    f"cgroup throttle / host steal took > 5 % of it)", "min": voc["min"],
             "max": voc["max"],
-            "spread": spread(voc),
+            "spread": spread(voc), "unstable": unstable(voc), "runs": voc["runs"],
             "sample": f"oracle SimpleVocoder single pass (the reference's ATen op sequence), B={B} mel [{B},64,{T}] "
                       f"(configs[1]); torch {torch.__version__} CPU ops on {len(cpus)} physical cores "
                       f"(of {len(phys)} on {sockets} sockets; job CPU quota {quota}) of {cpu_model}",
             "inference_as_written": {"value": inf["median"], "best": inf["max"], "min": inf["min"],
                                      "max": inf["max"],
-                                     "spread": spread(inf), "unit": "audio samples/s",
+                                     "spread": spread(inf), "unstable": unstable(inf),
+                                     "kept": inf["kept"], "unit": "audio samples/s",
                                      "sample": f"oracle M2TTSModel.inference as written (2 vocoder passes, "
                                                f"Python length-regulator loop), B={B} S={S} -> T={T}"},
             "frames": res.get("frames"), "wall_s": round(time.perf_counter() - t0, 1)}
@@ -326,7 +380,7 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=32, help="utterances per GPU (vocoder / pipeline)")
     ap.add_argument("--phonemes", type=int, default=100)
     ap.add_argument("--s2-shape", default="8x500", help="BxT of the s2_vocoder workload")
-    ap.add_argument("--cpu-runs", type=int, default=5, help="CPU baseline: measurements per workload (median)")
+    ap.add_argument("--cpu-runs", type=int, default=7, help="CPU baseline: measurements per workload (median of the clean ones)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline line only")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -844,6 +898,8 @@ def run(args):
                           ids_seed=pipe["frames"]["ids_seed"] if isinstance(pipe, dict) and "frames" in pipe else None)
         if "value" in cb:
             cb["gpu_over_cpu"] = round(out["value"] / cb["value"], 1)
+            # the ratio moves with the CPU figure: its range over the kept runs
+            cb["gpu_over_cpu_range"] = [round(out["value"] / cb["max"], 1), round(out["value"] / cb["min"], 1)]
             if isinstance(pipe, dict):
                 cb["inference_as_written"]["gpu_pipeline_over_cpu"] = round(
                     pipe["value"] / cb["inference_as_written"]["value"], 1)

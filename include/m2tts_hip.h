@@ -400,8 +400,10 @@ const char* m2_profile_kernel_name_for(const m2_model* model, int32_t index);
  * f16 hi/lo pairs, 3 products per fp32 product, fp32 accumulation). */
 int32_t m2_vocoder_path(const m2_model* model);
 /* Transformer arithmetic of this model: 1 = fused split-f16 layers and
- * attention, 0 = fp32 linears and the exact-f32 attention (weights whose
- * activation bound leaves the f16 range, or M2_TF_UNFUSED / M2_ATT_F32). */
+ * attention, 2 = the same with at least one layer whose attention-score bound
+ * reaches the f16 maximum (that layer keeps its softmax base in fp32 in every
+ * attention form), 0 = fp32 linears and the exact-f32 attention (weights
+ * whose activation bound leaves the f16 range, or M2_TF_UNFUSED / M2_ATT_F32). */
 int32_t m2_transformer_path(const m2_model* model);
 
 #ifdef __cplusplus

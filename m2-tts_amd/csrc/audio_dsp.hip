@@ -170,7 +170,8 @@ __global__ __launch_bounds__(NT) void nnls_start_kernel(const float* __restrict_
     extern __shared__ float sh[];
     float* M = sh;                                      // [n_mels]
     float* X = M + n_mels;                              // [F]
-    double* r = reinterpret_cast<double*>(X + F + (F & 1));  // [n_mels] residual (8-B aligned)
+    // [n_mels] residual: at float offset n_mels + F rounded up to even (8-B aligned)
+    double* r = reinterpret_cast<double*>(sh + ((n_mels + F + 1) & ~1));
     __shared__ double red[NT / 64];
     const int t = blockIdx.x, u = blockIdx.y;
     for (int m = threadIdx.x; m < n_mels; m += NT)
@@ -412,7 +413,8 @@ int32_t nnls_magnitudes(const m2_dsp* d, const float* mel, int B, int T, int ite
                         hipStream_t st) {
     const int F = d->n_fft / 2 + 1;
     const dim3 grid(T, B);
-    const size_t shs = ((size_t)d->n_mels + (size_t)F + 1) * sizeof(float) + (size_t)d->n_mels * sizeof(double) + 8;
+    // M [n_mels] | X [F] floats, rounded up to an even count, then r [n_mels] doubles
+    const size_t shs = (((size_t)d->n_mels + (size_t)F + 1) & ~(size_t)1) * sizeof(float) + (size_t)d->n_mels * sizeof(double);
     hipLaunchKernelGGL(dsp::nnls_start_kernel, grid, dim3(dsp::NT), shs, st, mel, d->n_mels, T, F, d->W, d->Wp, S, pg);
     M2_LAUNCHED("nnls_start_kernel");
     const size_t shf = (2 * (size_t)d->n_mels + 2 * (size_t)F) * sizeof(float);

@@ -574,7 +574,9 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     }
-    const bool pers = !dc && sw().dur_pers && ntiles > 2 * ncu;
+    // (not at H = 128: both convs' weight fragments held for the whole walk
+    // spill there; its tiles keep one tile per workgroup)
+    const bool pers = !dc && sw().dur_pers && ntiles > 2 * ncu && H <= 96;
     if (pers) grid = dim3(ncu, 1);
     auto f4 = [](const float* q) { return reinterpret_cast<const float4*>(q); };
     const DurCount none{};
@@ -588,7 +590,7 @@ int32_t duration_launch(const float* enc, int B, int S, int H, const float* cons
                        dc ? *dc : none, ntiles)
 #define M2_DUR_L(HH, LL, CC, RR, SP)                      \
     do {                                                  \
-        if constexpr (!CC) {                              \
+        if constexpr (!CC && HH <= 96) {                  \
             if (pers) M2_DUR_K(HH, LL, CC, RR, SP, true); \
             else M2_DUR_K(HH, LL, CC, RR, SP, false);     \
         } else {                                          \

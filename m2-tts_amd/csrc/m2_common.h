@@ -30,9 +30,9 @@ struct Switches {
     bool tf_layer = true;     // M2_TF_LAYER=0: three-launch transformer layers
     bool tf_unfused = false;  // M2_TF_UNFUSED: five-linear layers (handle creation)
     int tf_waves = 0;         // M2_TF_WAVES=4|8
-    int tfl_rb = 0;           // M2_TFL_RB=1|2|4|8
+    int tfl_rb = 0;           // M2_TFL_RB=1|2|4
     int tfl_first_rb = 0;     // M2_TFL_FIRST_RB=1|2|4
-    int tfl_qs2 = -1;         // M2_TFL_QS2=0|1|3..10
+    int tfl_qs2 = -1;         // M2_TFL_QS2=0|2|3|4|9
     int att_qt = 0;           // M2_ATT_QT
     bool att_f32 = false;     // M2_ATT_F32
     bool voc_perlayer = false;  // M2_VOCODER_PERLAYER (handle creation)
@@ -47,7 +47,9 @@ struct Switches {
     bool tailp2_seven = false;  // M2_TAILP2_SEVEN
     bool head_inconv = false;   // M2_HEAD_INCONV
     bool s2_head_tf16 = false;  // M2_S2_HEAD_TF16
+    int s2_head_split = 0;      // M2_S2_HEAD_SPLIT=0|1: the stage2 head as two launches (vocoder_x3.hip)
     int redo_grid = -1;         // M2_REDO_GRID: workgroups of the guarded redo launch (-1: one per CU)
+    bool redo_launch = false;   // M2_REDO_LAUNCH: the guarded exact-f32 launch also where the tail redoes locally
     bool dur_split = true;      // M2_DUR_SPLIT=0: the duration convs on the exact-f32 MFMA always
     bool dur_pers = true;       // M2_DUR_PERS=0: one duration tile per workgroup at every grid size
 };

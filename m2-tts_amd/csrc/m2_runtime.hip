@@ -2,11 +2,13 @@
 // See include/m2tts_hip.h for the contract of every entry point.
 #include <immintrin.h>
 
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -18,7 +20,16 @@
 namespace m2 {
 
 namespace {
-Switches g_sw;
+// The published switch table: an immutable snapshot behind an atomic
+// pointer.  reload_switches() (library load, every m2_model_create,
+// m2_reload_switches) builds a new one and publishes it only when the
+// environment changed; a reader sees one whole snapshot, never a table half
+// rewritten by a concurrent creation.  Superseded snapshots are kept (a few
+// hundred bytes per environment change), so a reference taken by sw() stays
+// valid.  The table is process-wide: creating a handle under a changed
+// environment changes the switches of every handle from its next call on.
+std::atomic<const Switches*> g_swp{nullptr};
+std::mutex g_sw_mu;
 int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return (e && *e) ? std::atoi(e) : dflt;
@@ -32,10 +43,13 @@ bool env_on(const char* name, bool dflt) {  // unset / empty -> dflt, else != "0
 const bool g_sw_loaded = (reload_switches(), true);
 }  // namespace
 
-const Switches& sw() { return g_sw; }
+const Switches& sw() { return *g_swp.load(std::memory_order_acquire); }
 
 void reload_switches() {
-    Switches s;
+    // zeroed storage, so the padding compares equal between snapshots
+    void* raw = std::calloc(1, sizeof(Switches));
+    if (!raw) return;  // keep the current table
+    Switches& s = *new (raw) Switches();
     const int rb = env_int("M2_DUR_RB", 0);
     s.dur_rb = (rb == 1 || rb == 2) ? rb : 0;
     s.dur_count = std::getenv("M2_DUR_COUNT") && *std::getenv("M2_DUR_COUNT") ? (env_int("M2_DUR_COUNT", 0) != 0) : -1;
@@ -47,11 +61,11 @@ void reload_switches() {
     s.tf_waves = (tw == 4 || tw == 8) ? tw : 0;
     auto rb124 = [](int v) { return (v == 1 || v == 2 || v == 4) ? v : 0; };
     const int trb = env_int("M2_TFL_RB", 0);
-    s.tfl_rb = trb == 8 ? 8 : rb124(trb);  // 8: 128-row tiles for the unmasked layers (masked ones run 4)
+    s.tfl_rb = rb124(trb);
     s.tfl_first_rb = rb124(env_int("M2_TFL_FIRST_RB", 0));
     if (const char* e = std::getenv("M2_TFL_QS2"); e && *e) {
         const int v = std::atoi(e);
-        s.tfl_qs2 = v >= 3 && v <= 10 ? v : (v != 0 ? 2 : 0);
+        s.tfl_qs2 = (v == 2 || v == 3 || v == 4 || v == 9) ? v : 0;
     }
     s.att_qt = env_int("M2_ATT_QT", 0);
     if (const char* e = std::getenv("M2_ATT_F32")) s.att_f32 = *e && *e != '0';
@@ -69,10 +83,18 @@ void reload_switches() {
     s.tailp2_seven = env_set("M2_TAILP2_SEVEN");
     s.head_inconv = env_set("M2_HEAD_INCONV");
     s.s2_head_tf16 = env_set("M2_S2_HEAD_TF16");
+    s.s2_head_split = env_int("M2_S2_HEAD_SPLIT", 0) ? 1 : 0;
     s.redo_grid = env_int("M2_REDO_GRID", -1);
+    s.redo_launch = env_set("M2_REDO_LAUNCH");
     s.dur_split = env_on("M2_DUR_SPLIT", true);
     s.dur_pers = env_on("M2_DUR_PERS", true);
-    g_sw = s;
+    std::lock_guard<std::mutex> lk(g_sw_mu);
+    const Switches* cur = g_swp.load(std::memory_order_relaxed);
+    if (cur && std::memcmp(cur, &s, sizeof(Switches)) == 0) {
+        std::free(raw);  // unchanged
+        return;
+    }
+    g_swp.store(&s, std::memory_order_release);  // (never freed: see g_swp)
 }
 
 // ---- launchers defined in the kernel translation units ---------------------
@@ -215,6 +237,9 @@ struct m2_layer_w {
     const float *qkv_w, *out_w, *out_b, *ff1_w, *ff1_b, *ff2_w, *ff2_b, *n1_w, *n1_b, *n2_w, *n2_b;
     // B-fragment packs for the fused layer kernels (transformer_fused.hip)
     const float *qkv_p = nullptr, *out_p = nullptr, *ff1_p = nullptr, *ff2_p = nullptr;
+    // the layer's attention scores (log2 units, scale folded) may leave the
+    // f16 range: its one-launch form keeps the softmax base in f32 (TflLayer)
+    bool wide_scores = false;
 };
 
 struct m2_model {
@@ -260,6 +285,9 @@ struct m2_model {
     // call's head kernel zeroes it
     int* rflag_dev = nullptr;
     mutable unsigned rseq = 0;
+    // policy 1 on the pipelined tails: the tail's in-launch local redo
+    // instead of the guarded exact-f32 launch (vocoder_redo.h); device copy
+    const m2::VocRedoW* redo_w = nullptr;
     int range_policy = 0;
     // one-launch transformer layers: work-queue counters and the launch
     // sequence whose parity picks their set (one stream per model)
@@ -465,6 +493,7 @@ int32_t run_tfl(const m2_model* m, const std::vector<m2_layer_w>& layers, const 
     for (int l = 0; l < n; ++l) {
         const m2_layer_w& L = layers[l];
         TflLayer w{L.out_p, L.out_b, L.n2_w, L.n2_b, L.ff1_p, L.ff1_b, L.ff2_p, L.ff2_b};
+        w.wide_scores = L.wide_scores;
         int next = 0, NN = 0;
         float* z = nullptr;
         if (l + 1 < n) {
@@ -785,12 +814,38 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             }
             return best;
         };
+        // scores in log2 units, |q.k| scale log2(e) <= sum over a head's dims of
+        // |q_d| |k_d| (each bounded by its row sum of |W_qkv| x the LN1 bound)
+        // x scale log2(e): the head_dim-48 wave-specialised attention holds its
+        // softmax base m (<= the largest score) as an f16 hi / lo pair, finite
+        // while |m| < 65520, so a layer whose bound reaches the f16 maximum
+        // runs the f32-base form (m2_layer_w::wide_scores; the seeded stage2
+        // weights bound at ~3.5e4)
+        const int heads = cfg->num_heads, hd = H / std::max(heads, 1);
+        const double sl2 = 1.0 / std::sqrt((double)hd) * 1.4426950408889634;
         for (int i = 0; i < n_layers; ++i) {
-            const std::string p = i < cfg->text_encoder_layers
-                                      ? "text_encoder.layers." + std::to_string(i)
-                                      : "decoder.layers." + std::to_string(i - cfg->text_encoder_layers);
+            const bool is_enc = i < cfg->text_encoder_layers;
+            const std::string p = is_enc ? "text_encoder.layers." + std::to_string(i)
+                                         : "decoder.layers." + std::to_string(i - cfg->text_encoder_layers);
             const double b1 = ln_bound(p + ".norm1"), b2 = ln_bound(p + ".norm2");
             const double qkv = row_sum(p + ".self_attn.qkv.weight", 3 * H, H) * b1;
+            {
+                // rows of W_qkv: the reference's reshape (3, heads, head_dim)
+                const std::vector<float> w = host(p + ".self_attn.qkv.weight");
+                auto rs = [&](int r) {
+                    double a = 0.0;
+                    for (int k = 0; k < H; ++k) a += std::fabs(w[(size_t)r * H + k]);
+                    return a * b1;
+                };
+                double sb = 0.0;
+                for (int h = 0; h < heads; ++h) {
+                    double acc = 0.0;
+                    for (int d = 0; d < hd; ++d) acc += rs(h * hd + d) * rs(H + h * hd + d);
+                    sb = std::max(sb, acc * sl2);
+                }
+                m2_layer_w& L = is_enc ? m->enc[i] : m->dec[i - cfg->text_encoder_layers];
+                L.wide_scores = !(sb < 65504.0);
+            }
             const double hid = row_sum(p + ".ffn.linear1.weight", 2 * H, H) * b2 + amax(host(p + ".ffn.linear1.bias"));
             worst = std::max(worst, std::max(std::max(b1, b2), std::max(qkv, hid)));
         }
@@ -1061,6 +1116,35 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
         }
         m->rflag_dev = static_cast<int*>(dv);
     }
+    // the local redo's weight table (range policy "fallback" on the pipelined
+    // tails, vocoder_redo.h): the raw fp32 vocoder weights, one device copy
+    if (m->vx.tp || m->vx.tp2) {
+        VocRedoW rw;
+        rw.M = cfg->mel_channels;
+        rw.C = cfg->vocoder_channels;
+        rw.wi = m->vin_w;
+        rw.bi = m->vin_b;
+        for (int k = 0; k < 4; ++k) {
+            rw.wt[k] = m->up_w[k];
+            rw.bt[k] = m->up_b[k];
+            rw.w1[k] = m->rb_w1[k];
+            rw.b1[k] = m->rb_b1[k];
+            rw.w2[k] = m->rb_w2[k];
+            rw.b2[k] = m->rb_b2[k];
+        }
+        rw.wo = m->vout_w;
+        rw.bo = m->vout_b;
+        void* dv = nullptr;
+        e = hipMalloc(&dv, sizeof(VocRedoW));
+        if (e == hipSuccess) e = hipMemcpyAsync(dv, &rw, sizeof(VocRedoW), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            if (dv) (void)hipFree(dv);
+            m2_model_destroy(m);
+            return hip_status(e, "hipMalloc(redo weights)");
+        }
+        m->redo_w = static_cast<const VocRedoW*>(dv);
+    }
     // work-queue counters of the one-launch transformer layers (TflQueue)
     // (+ 16 words: the count kernel's ticket of the device-T front half)
     e = hipMalloc(&m->tflq, (kTflQueueWords + 16) * sizeof(unsigned));
@@ -1099,6 +1183,7 @@ int32_t m2_model_destroy(m2_model* model) {
     if (model->rflag_dev) (void)hipFree(model->rflag_dev);
     if (model->tflq) (void)hipFree(model->tflq);
     if (model->fpost_host) (void)hipHostFree(model->fpost_host);
+    if (model->redo_w) (void)hipFree(const_cast<VocRedoW*>(model->redo_w));
     hipError_t e = hipFree(model->buf);
     delete model;
     if (e != hipSuccess) return hip_status(e, "hipFree(model)");
@@ -1581,14 +1666,23 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
         VocX vx = m->vx;
         VocW vw = m->vw;
         vx.dT = vw.dT = dT;
+        vx.scratch = buf[2];
         if (x3 && redo >= 0) {
             vx.rflag = m->rflag_dev + redo;
             vx.rclear = m->rflag_dev + (redo ^ 1);
+            vx.rqueue = reinterpret_cast<unsigned*>(m->rflag_dev + 4);
+            if (m->redo_w && !sw().redo_launch) {
+                // the pipelined tail redoes its own non-finite strips
+                // in fp32 inside the launch: no guarded launch behind it
+                vx.redo_w = m->redo_w;
+                return launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T,
+                                         vx, buf[0], buf[1], out_audio, st, mark);
+            }
             if ((rc = launch_vocoder_x3(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vx,
                                         buf[0], buf[1], out_audio, st, mark)))
                 return rc;
             vw.guard = m->rflag_dev + redo;
-            vw.guard_queue = reinterpret_cast<const unsigned*>(m->rflag_dev + 4);  // words 4-7 (zeroed at creation)
+            vw.guard_queue = reinterpret_cast<const unsigned*>(m->rflag_dev + 4);  // words 4-7 (zeroed by the head)
             return launch_vocoder_fused(mel, mel_layout == 1, m->cfg.mel_channels, m->cfg.vocoder_channels, B, T, vw,
                                         buf[0], buf[1], out_audio, st, [](int, bool) {});
         }
@@ -1956,7 +2050,11 @@ int32_t m2_vocoder_path(const m2_model* m) {
 
 int32_t m2_transformer_path(const m2_model* m) {
     if (!m) return -1;
-    return (m->tfused && !m->att_f32) ? 1 : 0;
+    if (!(m->tfused && !m->att_f32)) return 0;
+    for (const auto* st : {&m->enc, &m->dec})
+        for (const m2_layer_w& L : *st)
+            if (L.wide_scores) return 2;
+    return 1;
 }
 
 int32_t m2_profile_enable(m2_model* m, int32_t capacity) {

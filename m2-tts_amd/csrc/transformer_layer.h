@@ -71,6 +71,9 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
 struct TflLayer {
     const float *Wo, *bo, *g2, *b2n, *W1, *b1, *W2, *b2;  // packed (pack_bfrag_split) / fp32
     const float *gn = nullptr, *bn = nullptr, *Wn = nullptr, *bn2 = nullptr;
+    // the layer's scores (log2 units) may leave the f16 range: the unmasked
+    // head_dim-48 default form (f16 softmax base) gives way to the f32-base one
+    bool wide_scores = false;
 };
 int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool masked, const int64_t* lengths,
                          const float* x_in, float* x_out, const TflBufs& in, int next, const TflBufs& out,

@@ -699,15 +699,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const unsigned char*
     return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7ffffff0, 0x00020000);
 }
 // Lean unmasked softmax: true when a weight of the step exceeds 2^kLazyT,
-// read from the f16 hi halves of P (8 packed words, packed maxima).
+// read from the f16 hi halves of P (8 packed words).  The weights are >= 0,
+// so an f16 hi half orders as its bit pattern: packed u16 maxima compared with
+// the bits of 2^kLazyT, which also catches +inf (0x7C00) and NaN (0x7Exx).
+// (The earlier f16 form - packed f16 maxima converted to f32 and compared -
+// missed a +inf hi half on gfx950: a weight past 65504, i.e. a later chunk's
+// score more than 16 above the base, went unmoved and the output became NaN;
+// tests/test_gpu_range.py::test_attention_scores_past_f16_range.)
 __device__ __forceinline__ bool p_hi_exceeds(u32x4 a, u32x4 b) {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    h2 mx = __builtin_elementwise_max(__builtin_bit_cast(h2, a[0]), __builtin_bit_cast(h2, a[1]));
-    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_bit_cast(h2, a[2]), __builtin_bit_cast(h2, a[3])));
-    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_bit_cast(h2, b[0]), __builtin_bit_cast(h2, b[1])));
-    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_bit_cast(h2, b[2]), __builtin_bit_cast(h2, b[3])));
-    constexpr float lim = (float)(1 << (int)kLazyT);
-    return (float)mx.x > lim || (float)mx.y > lim;
+    typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+    auto h = [](unsigned w) { return __builtin_bit_cast(u2, w); };
+    u2 mx = __builtin_elementwise_max(h(a[0]), h(a[1]));
+    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(h(a[2]), h(a[3])));
+    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(h(b[0]), h(b[1])));
+    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(h(b[2]), h(b[3])));
+    static_assert(kLazyT == 8.f, "the bit pattern below is f16 2^8");
+    constexpr unsigned short lim = 0x5C00;  // f16 256.0
+    return mx.x > lim || mx.y > lim;
 }
 
 // LEAN (M2_TFL_QS2=4): the lean softmax of attention_qsplit2 (C = -m
@@ -1435,318 +1443,32 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
     else fin(CI<0>{});
 }
 
-// Ping-pong form of attention_qsplit2's lean unmasked path (M2_TFL_QS2=6).
-// Waves w and w + 4 share a SIMD (the workgroup's waves go to SIMDs
-// c[(w + r) mod 4]: tools/probe/simd_map.hip) and, in lockstep between the
-// per-step barriers, issue the same kind of work at the same time: both
-// waves' QK^T MFMAs, then both softmaxes (VALU), then both PV MFMAs - the
-// SIMD's matrix and vector pipes take turns.  Here the head-1 waves (w >= 4)
-// run one phase late: at step p they first issue the PV MFMAs of step p - 1
-// (P and V^T of step p - 1 held in registers across the barrier), then QK^T
-// of step p, then its softmax, and read step p's V^T fragments into
-// registers before the barrier.  So while the head-0 wave of a SIMD runs its
-// softmax the head-1 wave issues QK^T MFMAs, and while the head-0 wave
-// issues PV the head-1 wave runs its softmax.  Same arithmetic per score as
-// attention_qsplit2<..., LEAN> (the row sums by MFMA right after each
-// softmax, so a later base move scales them in the same order).
+// Wave-specialised query-split attention (M2_TFL_QS2=9, unmasked; the
+// default at head_dim 48): the diagnostic builds of the lean two-block form
+// (profiles/r04/r04h_attention_diag.txt) show its 64-key step as the serial
+// sum of staging (~600 cycles of LDS stores), softmax (~600) and the MFMAs,
+// every wave doing each in turn.  Here waves 0-3 compute and waves 4-7 stage:
+// consumer wave w = (head w / 2, chunk w % 2) owns all four 16-query blocks
+// of its head over its 32-key chunk of every step (each K / V^T fragment it
+// reads from LDS feeds four blocks: half the LDS reads of the two-block
+// form), producer wave 4 + c shares a SIMD with consumer c (waves w and w + 4
+// do: tools/probe/simd_map.hip) and stages by LDS-DMA (global_load_lds_dwordx4:
+// L2 -> LDS, no VGPRs, no ds_write): step p + 1's 12 pieces per producer lane
+// are issued at the top of step p into the free half of the ring and retired
+// (vmcnt(0)) before the step's barrier.  One barrier per step, as before.
+// Consumers take their four blocks as two pairs (the two-block lean softmax
+// per pair: scores from C = -m, base moves on an f16 weight past 2^kLazyT,
+// row sums by MFMA); chunk waves (h, 0) and (h, 1) merge at the end as in
+// attention_qsplit2, wave (h, j) finalising blocks 2j, 2j + 1.  The base m
+// rides in the tail k-step as an f16 hi + lo pair (QT below), so the layer's
+// scores must stay inside the f16 range: launch_tfl_layer runs the lean
+// two-block form (f32 base) for a layer whose score bound does not
+// (TflLayer::wide_scores, set at model creation).
+// Measured and removed in round 5 (history keeps them): register staging by
+// the producer waves (7), the consumers' interleaved matrix / vector regions
+// (8, 10), a software-pipelined two-block form (5), a ping-pong two-block
+// form (6) and 128-row tiles (M2_TFL_RB=8) - DESIGN.md section 4.
 template <int H, int HD>
-__device__ __forceinline__ void attention_qsplit2pp(const unsigned char* __restrict__ qb,
-                                                    const unsigned char* __restrict__ kb,
-                                                    const unsigned char* __restrict__ vb, int b, int t0, int N,
-                                                    int npad, unsigned char* A, unsigned char* ring) {
-    using G = Geo<HD>;
-    using Q = QsGeo<HD>;
-    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
-    constexpr int PPT = Q::PPT, RW = 2 + 4 * MT;
-    static_assert(NW * RW * 64 * 4 <= 2 * SB, "merge records fit the ring");
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = lane & 15, g = lane >> 4;
-    const int h = wave >> 2, qp = (wave >> 1) & 1, j = wave & 1;
-    const bool late = h == 1;  // wave-uniform
-    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
-
-    u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-        const unsigned char* qp8 =
-            qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + 2 * qp + qq) * QKBLK + 16 * lane;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            qh[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks);
-            ql[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024);
-        }
-        if constexpr (KT) {
-            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-            qxh[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
-            qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
-        }
-    }
-    __amdgpu_buffer_rsrc_t rsrc[PPT];
-    int sstep[PPT];
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-        const int o = 16 * (tid + NW * 64 * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
-        const size_t bh = (size_t)b * HEADS + hh;
-        const bool isk = r < Q::KB;
-        const unsigned char* base = isk ? kb + (bh * (npad / 16) + 2 * jj) * QKBLK + (r & ~1023)
-                                        : vb + (bh * nch + jj) * G::VCH + ((r - Q::KB) & ~1023);
-        rsrc[i] = wave_rsrc(base);
-        sstep[i] = __builtin_amdgcn_readfirstlane(isk ? 4 * QKBLK : 2 * G::VCH);
-    }
-    u32x4 pre[PPT];
-    auto gload = [&](int p) {
-#pragma unroll
-        for (int i = 0; i < PPT; ++i)
-            pre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc[i], 16 * lane, p * sstep[i], 0));
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
-    };
-
-    f32x4 acc[2][MT], lacc[2];
-    float m[2] = {0.f, 0.f};
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
-    bool fresh = true;
-    u32x4 bh4[2], bl4[2];  // P of the last softmax (split)
-    u32x4 vf[MT][2];       // the late waves' V^T fragments of that step
-    bool pend = false;     // late waves: PV of the previous step still to issue (wave-uniform)
-
-    auto pv = [&](const u32x4 (&v)[MT][2]) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                acc[qq][t] = mfma(v[t][0], bh4[qq], acc[qq][t]);
-                acc[qq][t] = mfma(v[t][0], bl4[qq], acc[qq][t]);
-                acc[qq][t] = mfma(v[t][1], bh4[qq], acc[qq][t]);
-            }
-    };
-    auto vread = [&](const unsigned char* sb, u32x4 (&v)[MT][2]) {
-        const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            v[t][0] = *reinterpret_cast<const u32x4*>(vp + t * 2048);
-            v[t][1] = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
-        }
-    };
-    // QK^T and the softmax of this wave's chunk of step p (scores relative to
-    // the base; the first chunk sets it), P into bh4 / bl4, row sums by MFMA
-    auto qk_softmax = [&](const unsigned char* sb, int p, auto&& stage) {
-        u32x4 kf[2][KSA][2], kx[2][2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                kf[u][ks][0] = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
-                kf[u][ks][1] = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
-            }
-            if constexpr (KT) {
-                kx[u][0] = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
-                kx[u][1] = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
-            }
-        }
-        if constexpr (!TFL_STAGE_FIRST) stage();
-        float s[2][2][4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {f32x4{-m[0], -m[0], -m[0], -m[0]}, f32x4{-m[1], -m[1], -m[1], -m[1]}};
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kf[u][ks][0], qh[qq][ks], st[qq]);
-                    st[qq] = mfma(kf[u][ks][0], ql[qq][ks], st[qq]);
-                    st[qq] = mfma(kf[u][ks][1], qh[qq][ks], st[qq]);
-                }
-            if constexpr (KT)
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kx[u][0], qxh[qq], st[qq]);
-                    st[qq] = mfma(kx[u][0], qxl[qq], st[qq]);
-                    st[qq] = mfma(kx[u][1], qxh[qq], st[qq]);
-                }
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
-        }
-        const int k0 = p * 2 * KC + j * KC;
-        if (N - k0 < KC) {  // the chunk straddles N (wave-uniform)
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int qq = 0; qq < 2; ++qq)
-                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
-        }
-        auto chunk_max = [&](int qq) {
-            return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
-                         fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
-        };
-        if (fresh) {
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
-                m[qq] = cm;
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
-            }
-            fresh = false;
-        }
-        auto exp_split = [&]() {
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                float e[2][4];
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
-                unsigned ph[4], pl[4];
-                split2u(e[0][0], e[0][1], ph[0], pl[0]);
-                split2u(e[0][2], e[0][3], ph[1], pl[1]);
-                split2u(e[1][0], e[1][1], ph[2], pl[2]);
-                split2u(e[1][2], e[1][3], ph[3], pl[3]);
-                bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
-                bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
-            }
-        };
-        exp_split();
-        if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
-                m[qq] += d;
-                const float corr = __builtin_amdgcn_exp2f(-d);
-                lacc[qq] *= corr;
-#pragma unroll
-                for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
-            }
-            exp_split();
-        }
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
-            lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
-        }
-    };
-
-    gload(0);
-    lstore(0);
-    if (1 < nsc) gload(1);
-    lds_barrier();
-#pragma unroll 1
-    for (int p = 0; p < nsc; ++p) {
-        auto stage = [&] {
-            if (p + 1 < nsc) lstore((p + 1) & 1);
-            if (p + 2 < nsc) gload(p + 2);
-        };
-        const bool live = 2 * KC * p + KC * j < N;  // wave-uniform
-        const unsigned char* sb = ring + (p & 1) * SB;
-        if (late) {
-            if (pend) pv(vf);  // step p - 1's PV (its P and V^T in registers)
-            pend = false;
-        }
-        if (TFL_STAGE_FIRST || !live) stage();
-        if (live) {
-            qk_softmax(sb, p, stage);
-            if (late) {
-                vread(sb, vf);
-                pend = true;
-            } else {
-                u32x4 v[MT][2];
-                vread(sb, v);
-                pv(v);
-            }
-        }
-        lds_barrier();
-    }
-    if (pend) pv(vf);
-    TSTAMP(1);
-    if (fresh) {  // this wave saw no key
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) m[qq] = -INFINITY;
-    }
-    float* rec = reinterpret_cast<float*>(ring);
-    auto put = [&](auto J) {
-        constexpr int qo = 1 - decltype(J)::value;
-        float* w = rec + (size_t)wave * RW * 64 + lane;
-        w[0] = m[qo];
-        w[64] = lacc[qo][0];
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qo][t][r];
-    };
-    auto fin = [&](auto J) {
-        constexpr int qq = decltype(J)::value;
-        const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
-        const float mo = o[0];
-        const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
-        const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
-        const float ls = lacc[qq][0] * fm + o[64] * fo;
-        const float inv = 1.0f / ls;
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = (acc[qq][t][r] * fm + o[(2 + 4 * t + r) * 64] * fo) * inv;
-            put_split4<H>(A + (16 * (2 * qp + qq) + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2],
-                          v[3]);
-        }
-    };
-    if (j) put(CI<1>{});
-    else put(CI<0>{});
-    __syncthreads();
-    if (j) fin(CI<1>{});
-    else fin(CI<0>{});
-}
-
-// Wave-specialised query-split attention (M2_TFL_QS2=7, unmasked): the
-// diagnostic builds of the lean two-block form (profiles/r04/r04h_attention_diag.txt)
-// show its 64-key step as the serial sum of staging (~600 cycles of LDS
-// stores), softmax (~600) and the MFMAs, every wave doing each in turn.
-// Here waves 0-3 compute and waves 4-7 stage: consumer wave w = (head w / 2,
-// chunk w % 2) owns all four 16-query blocks of its head over its 32-key
-// chunk of every step (each K / V^T fragment it reads from LDS feeds four
-// blocks: half the LDS reads of the two-block form), producer wave 4 + c
-// shares a SIMD with consumer c (waves w and w + 4 do: tools/probe/simd_map.hip)
-// and moves steps p + 1 (registers -> LDS) and p + 2 (L2 -> registers) while
-// its consumer runs step p - so the stores and the loads' waits sit on the
-// producers' issue path, beside the consumers' MFMAs.  One barrier per step,
-// as before.  Consumers take their four blocks as two pairs (the two-block
-// lean softmax per pair: scores from C = -m, base moves on an f16 weight past
-// 2^kLazyT, row sums by MFMA); chunk waves (h, 0) and (h, 1) merge at the end
-// as in attention_qsplit2, wave (h, j) finalising blocks 2j, 2j + 1.
-// IL (M2_TFL_QS2=8): the consumers' steps that need neither the first-chunk
-// base nor the N mask run as three scheduling regions, each a matrix phase
-// with a vector phase laid into its MFMA gaps (__builtin_amdgcn_sched_group_barrier):
-// QK^T of pair 1 with the softmax of pair 0, then PV of pair 0 with the
-// softmax of pair 1 (V^T fragments read there, after K's are dead), then PV
-// of pair 1; the rare base moves branch between the regions, before the PV
-// that uses them.  One wave per SIMD computes, so the vector work only
-// overlaps the matrix work when one instruction stream carries both.
-// DMA (M2_TFL_QS2=9, 10 with IL = 2): the producers stage by LDS-DMA
-// (global_load_lds_dwordx4: L2 -> LDS, no VGPRs, no ds_write): step p + 1's
-// 12 pieces per producer lane are issued at the top of step p into the free
-// half of the ring and retired (vmcnt(0)) before the step's barrier.
-// IL = 2: the same regions without the group barriers (the compiler's own
-// order inside each region).
-template <int H, int HD, int IL = 0, bool DMA = false>
 __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restrict__ qb,
                                                     const unsigned char* __restrict__ kb,
                                                     const unsigned char* __restrict__ vb, int b, int t0, int N,
@@ -1777,7 +1499,7 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
                          : vb + (bh * nch + jj) * G::VCH + (r - Q::KB);
             sstep[i] = isk ? 4 * QKBLK : 2 * G::VCH;
         }
-        if constexpr (DMA) {
+        {
             // buffer_load ... lds through a descriptor of each piece's 1-KB
             // region: the lane offset in a fixed VGPR, the step's advance in
             // an SGPR - no per-step address VALU
@@ -1805,26 +1527,6 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             for (int p = 0; p < nsc; ++p) {
                 if (p + 1 < nsc && !(TFL_DIAG & 64)) dma(p + 1, (p + 1) & 1);
                 if constexpr (!(TFL_DIAG & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                lds_barrier();
-            }
-        } else {
-            u32x4 pre[PPT];
-            auto gload = [&](int p) {
-#pragma unroll
-                for (int i = 0; i < PPT; ++i) pre[i] = *reinterpret_cast<const u32x4*>(src[i] + (size_t)p * sstep[i]);
-            };
-            auto lstore = [&](int buf) {
-#pragma unroll
-                for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (pt + PT * i)) = pre[i];
-            };
-            gload(0);
-            lstore(0);
-            if (1 < nsc) gload(1);
-            lds_barrier();
-#pragma unroll 1
-            for (int p = 0; p < nsc; ++p) {
-                if (p + 1 < nsc) lstore((p + 1) & 1);
-                if (p + 2 < nsc) gload(p + 2);
                 lds_barrier();
             }
         }
@@ -1994,146 +1696,10 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
     };
 
     lds_barrier();  // step 0 staged
-    // the interleaved step (IL): scores of a pair, their exponentials and split
-    auto qk2 = [&](auto Q0c, const u32x4 (&kf)[2][KSA][2], const u32x4 (&kx)[2][2], float (&s)[2][2][4]) {
-        constexpr int Q0 = decltype(Q0c)::value;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            f32x4 st[2] = {c0(Q0), c0(Q0 + 1)};
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kf[u][ks][0], qh[Q0 + qq][ks], st[qq]);
-                    st[qq] = mfma(kf[u][ks][0], ql[Q0 + qq][ks], st[qq]);
-                    st[qq] = mfma(kf[u][ks][1], qh[Q0 + qq][ks], st[qq]);
-                }
-            if constexpr (KT)
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kx[u][0], qxh[Q0 + qq], st[qq]);
-                    st[qq] = mfma(kx[u][0], qxl[Q0 + qq], st[qq]);
-                    st[qq] = mfma(kx[u][1], qxh[Q0 + qq], st[qq]);
-                }
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
-        }
-    };
-    auto esplit = [](const float (&s)[2][2][4], u32x4 (&bh)[2], u32x4 (&bl)[2]) {
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            float e[2][4];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
-            unsigned ph[4], pl[4];
-            split2u(e[0][0], e[0][1], ph[0], pl[0]);
-            split2u(e[0][2], e[0][3], ph[1], pl[1]);
-            split2u(e[1][0], e[1][1], ph[2], pl[2]);
-            split2u(e[1][2], e[1][3], ph[3], pl[3]);
-            bh[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
-            bl[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
-        }
-    };
-    // a base move of a pair (rare; between the regions, before its PV)
-    auto rare = [&](auto Q0c, float (&s)[2][2][4], u32x4 (&bh)[2], u32x4 (&bl)[2]) {
-        constexpr int Q0 = decltype(Q0c)::value;
-        if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh[0], bh[1])) != 0) {
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                const float cm = fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
-                                       fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
-                const float mold = m[Q0 + qq];
-                set_base(Q0 + qq, mold + vmax(grp4_max(cm), 0.f));
-                const float d = m[Q0 + qq] - mold;
-                const float corr = __builtin_amdgcn_exp2f(-d);
-                lacc[Q0 + qq] *= corr;
-#pragma unroll
-                for (int t = 0; t < MT; ++t) acc[Q0 + qq][t] *= corr;
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
-            }
-            esplit(s, bh, bl);
-        }
-    };
-    auto pv2 = [&](auto Q0c, const u32x4 (&bh)[2], const u32x4 (&bl)[2], const u32x4 (&vf)[MT][2]) {
-        constexpr int Q0 = decltype(Q0c)::value;
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            lacc[Q0 + qq] = mfma(ones, bh[qq], lacc[Q0 + qq]);
-            lacc[Q0 + qq] = mfma(ones, bl[qq], lacc[Q0 + qq]);
-        }
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                acc[Q0 + qq][t] = mfma(vf[t][0], bh[qq], acc[Q0 + qq][t]);
-                acc[Q0 + qq][t] = mfma(vf[t][0], bl[qq], acc[Q0 + qq][t]);
-                acc[Q0 + qq][t] = mfma(vf[t][1], bh[qq], acc[Q0 + qq][t]);
-            }
-    };
-    constexpr int NQK = 2 * 2 * 3 * (KS + KT), NPV = 4 + 6 * MT;  // MFMAs of a pair's QK^T / row sums + PV
 
 #pragma unroll 1
     for (int p = 0; p < nsc; ++p) {
-        const int k0 = p * 2 * KC + j * KC;
-        if (IL != 0 && !fresh && N - k0 >= KC) {  // wave-uniform: a whole chunk after the first
-            const unsigned char* sb = ring + (p & 1) * SB + j * CB + h * Q::HB + 16 * lane;
-            u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    kf[u][ks][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks);
-                    kf[u][ks][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks + 1024);
-                }
-                if constexpr (KT) {
-                    kx[u][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL);
-                    kx[u][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
-                }
-            }
-            fix_tail(kx);
-            float s0[2][2][4], s1[2][2][4];
-            u32x4 bh0[2], bl0[2], bh1[2], bl1[2];
-            qk2(CI<0>{}, kf, kx, s0);
-            __builtin_amdgcn_sched_barrier(0);
-            // region 1: QK^T of pair 1 | softmax of pair 0 | V^T reads
-            qk2(CI<2>{}, kf, kx, s1);
-            esplit(s0, bh0, bl0);
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                vf[t][0] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048);
-                vf[t][1] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048 + 1024);
-            }
-            if constexpr (IL == 1)
-#pragma unroll
-                for (int i = 0; i < NQK; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-                    if (i < 2 * MT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-                }
-            __builtin_amdgcn_sched_barrier(0);
-            rare(CI<0>{}, s0, bh0, bl0);
-            __builtin_amdgcn_sched_barrier(0);
-            // region 2: PV of pair 0 | softmax of pair 1
-            pv2(CI<0>{}, bh0, bl0, vf);
-            esplit(s1, bh1, bl1);
-            if constexpr (IL == 1)
-#pragma unroll
-                for (int i = 0; i < NPV; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                }
-            __builtin_amdgcn_sched_barrier(0);
-            rare(CI<2>{}, s1, bh1, bl1);
-            __builtin_amdgcn_sched_barrier(0);
-            pv2(CI<2>{}, bh1, bl1, vf);
-        } else if (2 * KC * p + KC * j < N) {  // wave-uniform
+        if (2 * KC * p + KC * j < N) {  // wave-uniform
             const unsigned char* sb = ring + (p & 1) * SB + j * CB + h * Q::HB + 16 * lane;
             u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
 #pragma unroll
@@ -2210,567 +1776,6 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
     else fin(CI<0>{});
 }
 
-// Software-pipelined form of attention_qsplit2's lean unmasked path (the
-// long-form decoder; M2_TFL_QS2=5): iteration p issues the QK^T MFMAs of step
-// p + 1 beside the softmax VALU of step p (its scores were computed one
-// iteration earlier and stay in registers), then the PV MFMAs of step p - so a
-// wave's matrix and vector work of consecutive steps overlap instead of
-// alternating behind one barrier.  K runs one step ahead of V in the LDS
-// rings: at the top of iteration p the rings hold K(p + 1) and V(p); the
-// iteration stores K(p + 2) and V(p + 1) (requested from L2 one iteration
-// earlier) into the halves iteration p - 1 finished reading, and requests
-// K(p + 3) and V(p + 2).  One barrier per iteration, as before.  The QK^T
-// MFMAs of step p + 1 start from C = -m at the top of the iteration; a base
-// move in the softmax of step p (the first step, or a weight past 2^kLazyT)
-// shifts those scores too.  Same arithmetic per score as the lean two-block
-// form (results within rounding of it: the base moves are the same).
-template <int H, int HD>
-__device__ __forceinline__ void attention_qsplit2p(const unsigned char* __restrict__ qb,
-                                                   const unsigned char* __restrict__ kb,
-                                                   const unsigned char* __restrict__ vb, int b, int t0, int N,
-                                                   int npad, unsigned char* A, unsigned char* ring) {
-    using G = Geo<HD>;
-    using Q = QsGeo<HD>;
-    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK;
-    constexpr int KB = Q::KB, VB = G::VCH;                                // one head's K / V^T of a chunk
-    constexpr int KST = 2 * HEADS * KB, VST = 2 * HEADS * VB;             // K / V^T bytes of a 64-key step
-    constexpr int NT = NW * 64, KP = KST / (16 * NT), VP = VST / (16 * NT);  // 16-B pieces per thread
-    constexpr int RW = 2 + 4 * MT;
-    static_assert(KST % (16 * NT) == 0 && VST % (16 * NT) == 0 && KB % 1024 == 0 && VB % 1024 == 0,
-                  "1-KB wave pieces of one region");
-    static_assert(2 * KST + 2 * VST <= 2 * Q::SB, "K and V^T rings in the attention scratch");
-    static_assert(NW * RW * 64 * 4 <= 2 * Q::SB, "merge records fit the ring");
-    unsigned char* const kring = ring;
-    unsigned char* const vring = ring + 2 * KST;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = lane & 15, g = lane >> 4;
-    const int h = wave >> 2, qp = (wave >> 1) & 1, j = wave & 1;
-    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
-
-    u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-        const unsigned char* qp8 =
-            qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + 2 * qp + qq) * QKBLK + 16 * lane;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            qh[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks);
-            ql[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024);
-        }
-        if constexpr (KT) {
-            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-            qxh[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
-            qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
-        }
-    }
-    // staging: piece i of a step's K (V^T) region [chunk][head][bytes] - a
-    // wave's 1-KB piece lies in one (chunk, head) region
-    __amdgpu_buffer_rsrc_t krs[KP], vrs[VP];
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-        const int o = 16 * (tid + NT * i), jj = o / (HEADS * KB), r1 = o - jj * HEADS * KB, hh = r1 / KB,
-                  r = r1 - hh * KB;
-        krs[i] = wave_rsrc(kb + ((size_t)(b * HEADS + hh) * (npad / 16) + 2 * jj) * QKBLK + (r & ~1023));
-    }
-#pragma unroll
-    for (int i = 0; i < VP; ++i) {
-        const int o = 16 * (tid + NT * i), jj = o / (HEADS * VB), r1 = o - jj * HEADS * VB, hh = r1 / VB,
-                  r = r1 - hh * VB;
-        vrs[i] = wave_rsrc(vb + ((size_t)(b * HEADS + hh) * nch + jj) * VB + (r & ~1023));
-    }
-    u32x4 kpre[KP], vpre[VP];
-    auto gload_k = [&](int p) {
-#pragma unroll
-        for (int i = 0; i < KP; ++i)
-            kpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs[i], 16 * lane, p * 4 * QKBLK, 0));
-    };
-    auto gload_v = [&](int p) {
-#pragma unroll
-        for (int i = 0; i < VP; ++i)
-            vpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs[i], 16 * lane, p * 2 * VB, 0));
-    };
-    auto lstore_k = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < KP; ++i) *reinterpret_cast<u32x4*>(kring + buf * KST + 16 * (tid + NT * i)) = kpre[i];
-    };
-    auto lstore_v = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < VP; ++i) *reinterpret_cast<u32x4*>(vring + buf * VST + 16 * (tid + NT * i)) = vpre[i];
-    };
-
-    f32x4 acc[2][MT], lacc[2];
-    float m[2];
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        m[qq] = 0.f;
-        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
-
-    // S(p) of this wave's chunk from K ring half kbuf, relative to -c0
-    // (keys past N -inf).  s[qq][u][r]: key 64 p + 32 j + 16 u + 4 g + r.
-    auto qk = [&](auto MK, const unsigned char* kbuf, int p, const float (&c0)[2], float (&s)[2][2][4]) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const unsigned char* kp = kbuf + j * (HEADS * KB) + h * KB + u * QKBLK + 16 * lane;
-            f32x4 st[2] = {f32x4{c0[0], c0[0], c0[0], c0[0]}, f32x4{c0[1], c0[1], c0[1], c0[1]}};
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
-                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kh, qh[qq][ks], st[qq]);
-                    st[qq] = mfma(kh, ql[qq][ks], st[qq]);
-                    st[qq] = mfma(kl, qh[qq][ks], st[qq]);
-                }
-            }
-            if constexpr (KT) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
-                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
-                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kxh, qxh[qq], st[qq]);
-                    st[qq] = mfma(kxh, qxl[qq], st[qq]);
-                    st[qq] = mfma(kxl, qxh[qq], st[qq]);
-                }
-            }
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
-        }
-        if constexpr (decltype(MK)::value) {  // this wave's last chunk: keys past N score -inf
-            const int k0 = p * 2 * KC + j * KC;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int qq = 0; qq < 2; ++qq)
-                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
-        }
-    };
-    auto chunk_max = [](const float (&s)[2][2][4], int qq) {
-        return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
-                     fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
-    };
-    auto exp_split = [](const float (&s)[2][2][4], u32x4 (&bh4)[2], u32x4 (&bl4)[2]) {
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            float e[2][4];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
-            unsigned ph[4], pl[4];
-            split2u(e[0][0], e[0][1], ph[0], pl[0]);
-            split2u(e[0][2], e[0][3], ph[1], pl[1]);
-            split2u(e[1][0], e[1][1], ph[2], pl[2]);
-            split2u(e[1][2], e[1][3], ph[3], pl[3]);
-            bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
-            bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
-        }
-    };
-    // the staging of iteration p: (K(p + 2), V(p + 1)) to LDS, (K(p + 3),
-    // V(p + 2)) requested (scalar branches ahead of the compute block)
-    auto stage = [&](int p) {
-        if (p + 2 < nsc) lstore_k(p & 1);
-        if (p + 1 < nsc) lstore_v((p + 1) & 1);
-        if (p + 3 < nsc) gload_k(p + 3);
-        if (p + 2 < nsc) gload_v(p + 2);
-    };
-    // iteration p of a live step: S(p + 1) = QK(p + 1) (QN; MN: masked, this
-    // wave's last chunk) beside softmax(p) on sc, PV(p).  Compile-time flags
-    // only: in the steady state the QK^T MFMAs of p + 1 and the exponentials
-    // of p are one basic block the scheduler can interleave.
-    auto iterate = [&](auto FIRST, auto QN, auto MN, int p, float (&sc)[2][2][4], float (&sn)[2][2][4]) {
-        constexpr bool F = decltype(FIRST)::value, QK = decltype(QN)::value;
-        stage(p);
-        const float c0[2] = {-m[0], -m[1]};
-        if constexpr (QK) qk(MN, kring + ((p + 1) & 1) * KST, p + 1, c0, sn);
-        u32x4 bh4[2], bl4[2];
-        float d[2] = {0.f, 0.f};
-        if constexpr (F) {  // the first step: the base is the chunk's maximum
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                d[qq] = grp4_max(chunk_max(sc, qq));  // finite: the chunk holds a key < N
-                m[qq] = d[qq];
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
-            }
-        }
-        exp_split(sc, bh4, bl4);
-        bool moved = F;
-        if (!F && __builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                d[qq] = vmax(grp4_max(chunk_max(sc, qq)), 0.f);
-                m[qq] += d[qq];
-                const float corr = __builtin_amdgcn_exp2f(-d[qq]);
-                lacc[qq] *= corr;
-#pragma unroll
-                for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) sc[qq][u][r] -= d[qq];
-            }
-            exp_split(sc, bh4, bl4);
-            moved = true;
-        }
-        if constexpr (QK)
-            if (moved)  // S(p + 1) was computed against the old base
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq)
-#pragma unroll
-                    for (int u = 0; u < 2; ++u)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) sn[qq][u][r] -= d[qq];
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
-            lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
-        }
-        const unsigned char* vp = vring + (p & 1) * VST + j * (HEADS * VB) + h * VB + 16 * lane;
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
-            const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
-                acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
-                acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
-            }
-        }
-        lds_barrier();
-    };
-    const CI<0> n0{};
-    const CI<1> n1{};
-
-    // prologue: K(0), V(0), K(1) in LDS, S(0) computed, K(2) and V(1) requested
-    const int nl = N > KC * j ? (N - KC * j + 2 * KC - 1) / (2 * KC) : 0;  // steps with keys for this wave
-    float sa[2][2][4], sb[2][2][4];
-    gload_k(0);
-    gload_v(0);
-    lstore_k(0);
-    lstore_v(0);
-    if (1 < nsc) {
-        gload_k(1);
-        lstore_k(1);
-    }
-    lds_barrier();
-    {
-        const float z[2] = {0.f, 0.f};
-        if (nl == 1) qk(n1, kring, 0, z, sa);
-        else if (nl > 1) qk(n0, kring, 0, z, sa);
-    }
-    if (2 < nsc) gload_k(2);
-    if (1 < nsc) gload_v(1);
-    lds_barrier();  // every wave has read K(0) before iteration 0 overwrites it
-    // this wave's steps: 0 (first), 1 .. nl - 3 (steady), nl - 2 (QK of the
-    // masked last chunk), nl - 1 (no QK); then staging-only steps up to nsc
-    auto finish = [&](int p, float (&x)[2][2][4], float (&y)[2][2][4]) {  // x holds S(p)
-        if (p == nl - 2) {
-            iterate(n0, n1, n1, p, x, y);
-            iterate(n0, n0, n0, p + 1, y, x);
-            p += 2;
-        } else if (p == nl - 1) {
-            iterate(n0, n0, n0, p, x, y);
-            ++p;
-        }
-#pragma unroll 1
-        for (; p < nsc; ++p) {
-            stage(p);
-            lds_barrier();
-        }
-    };
-    if (nl >= 3) {
-        iterate(n1, n1, n0, 0, sa, sb);
-        int p = 1;
-#pragma unroll 1
-        for (; p + 2 <= nl - 2; p += 2) {
-            iterate(n0, n1, n0, p, sb, sa);
-            iterate(n0, n1, n0, p + 1, sa, sb);
-        }
-        if (p < nl - 2) {
-            iterate(n0, n1, n0, p, sb, sa);
-            finish(p + 1, sa, sb);
-        } else {
-            finish(p, sb, sa);
-        }
-    } else if (nl == 2) {
-        iterate(n1, n1, n1, 0, sa, sb);
-        iterate(n0, n0, n0, 1, sb, sa);
-        finish(2, sa, sb);
-    } else if (nl == 1) {
-        iterate(n1, n0, n0, 0, sa, sb);
-        finish(1, sb, sa);
-    } else {
-        finish(0, sa, sb);
-    }
-    TSTAMP(1);
-    if (nl == 0) {  // this wave saw no key
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) m[qq] = -INFINITY;
-    }
-    // merge the two chunk waves of (h, qp) as attention_qsplit2 does
-    float* rec = reinterpret_cast<float*>(ring);
-    auto put = [&](auto J) {
-        constexpr int qo = 1 - decltype(J)::value;
-        float* w = rec + (size_t)wave * RW * 64 + lane;
-        w[0] = m[qo];
-        w[64] = lacc[qo][0];
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qo][t][r];
-    };
-    auto fin = [&](auto J) {
-        constexpr int qq = decltype(J)::value;
-        const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
-        const float mo = o[0];
-        const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
-        const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
-        const float ls = lacc[qq][0] * fm + o[64] * fo;
-        const float inv = 1.0f / ls;
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = (acc[qq][t][r] * fm + o[(2 + 4 * t + r) * 64] * fo) * inv;
-            put_split4<H>(A + (16 * (2 * qp + qq) + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2],
-                          v[3]);
-        }
-    };
-    if (j) put(CI<1>{});
-    else put(CI<0>{});
-    __syncthreads();
-    if (j) fin(CI<1>{});
-    else fin(CI<0>{});
-}
-
-// 128-query tiles (the long-form decoder, unmasked; layer_kernel RB = 8):
-// wave w = (head w / 4, query pair w % 4) owns query blocks 2 (w % 4) and
-// 2 (w % 4) + 1 of its head over ALL keys - both 32-key chunks of every
-// 64-key step, one after the other, through the lean online softmax of
-// attention_qsplit2 (C = -m accumulators, MFMA row sums, base moves on an
-// f16 weight past 2^kLazyT).  The workgroup stages each step's K / V^T once
-// for twice the queries of the 64-row tile: the 64-row form streams 48 KB of
-// K / V^T per step and CU from L2 at ~36 GB/s per CU (B=128 T=2600: 10.5 GB
-// per launch, ~8 TB/s chip-wide), the attention's bound; here the same
-// stream feeds 128 queries, and the MFMA work per step and wave doubles over
-// the same barrier.  No partner merge (every wave sees every key).  Query
-// blocks past npad (the tile's second half when npad is not a multiple of
-// 128) load zero queries; their rows are never used.  Leaves the normalised
-// rows 0 .. 127 in A (split, stride srs(H)).
-template <int H, int HD>
-__device__ __forceinline__ void attention_q128(const unsigned char* __restrict__ qb,
-                                               const unsigned char* __restrict__ kb,
-                                               const unsigned char* __restrict__ vb, int b, int t0, int N,
-                                               int npad, unsigned char* A, unsigned char* ring) {
-    using G = Geo<HD>;
-    using Q = QsGeo<HD>;
-    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
-    constexpr int PPT = Q::PPT;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = lane & 15, g = lane >> 4;
-    const int h = wave >> 2, qp = wave & 3;
-    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
-
-    u32x4 qh[2][KSA], ql[2][KSA], qxh[2], qxl[2];
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-        const int blk = t0 / 16 + 2 * qp + qq;
-        const bool have = 16 * blk < npad;  // wave-uniform
-        const unsigned char* qp8 = qb + ((size_t)(b * HEADS + h) * (npad / 16) + blk) * QKBLK + 16 * lane;
-        const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            qh[qq][ks] = have ? *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks) : z;
-            ql[qq][ks] = have ? *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks + 1024) : z;
-        }
-        if constexpr (KT) {
-            qxh[qq] = have && lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
-            qxl[qq] = have && lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
-        }
-    }
-    // staging of a 64-key step: as attention_qsplit2
-    __amdgpu_buffer_rsrc_t rsrc[PPT];
-    int sstep[PPT];
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-        const int o = 16 * (tid + NW * 64 * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
-        const size_t bh = (size_t)b * HEADS + hh;
-        const bool isk = r < Q::KB;
-        const unsigned char* base = isk ? kb + (bh * (npad / 16) + 2 * jj) * QKBLK + (r & ~1023)
-                                        : vb + (bh * nch + jj) * G::VCH + ((r - Q::KB) & ~1023);
-        rsrc[i] = wave_rsrc(base);
-        sstep[i] = __builtin_amdgcn_readfirstlane(isk ? 4 * QKBLK : 2 * G::VCH);
-    }
-    u32x4 pre[PPT];
-    auto gload = [&](int p) {
-#pragma unroll
-        for (int i = 0; i < PPT; ++i)
-            pre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc[i], 16 * lane, p * sstep[i], 0));
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) *reinterpret_cast<u32x4*>(ring + buf * SB + 16 * (tid + NW * 64 * i)) = pre[i];
-    };
-
-    f32x4 acc[2][MT], lacc[2];
-    float m[2] = {0.f, 0.f};
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-#pragma unroll
-        for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
-
-    // keys 64 p + 32 j + 16 u + 4 g + r of queries li of blocks 2 qp + qq
-    auto process = [&](const unsigned char* sb, int p, int j, bool fresh) {
-        float s[2][2][4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const unsigned char* kp = sb + j * CB + h * Q::HB + u * QKBLK + 16 * lane;
-            f32x4 st[2] = {f32x4{-m[0], -m[0], -m[0], -m[0]}, f32x4{-m[1], -m[1], -m[1], -m[1]}};
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const u32x4 kh = *reinterpret_cast<const u32x4*>(kp + 2048 * ks);
-                const u32x4 kl = *reinterpret_cast<const u32x4*>(kp + 2048 * ks + 1024);
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kh, qh[qq][ks], st[qq]);
-                    st[qq] = mfma(kh, ql[qq][ks], st[qq]);
-                    st[qq] = mfma(kl, qh[qq][ks], st[qq]);
-                }
-            }
-            if constexpr (KT) {  // lanes of groups 2, 3 read other tail bytes: their Q operand is zero
-                const u32x4 kxh = *reinterpret_cast<const u32x4*>(kp + G::TAIL);
-                const u32x4 kxl = *reinterpret_cast<const u32x4*>(kp + G::TAIL + 512 - 512 * (lane >> 5));
-#pragma unroll
-                for (int qq = 0; qq < 2; ++qq) {
-                    st[qq] = mfma(kxh, qxh[qq], st[qq]);
-                    st[qq] = mfma(kxh, qxl[qq], st[qq]);
-                    st[qq] = mfma(kxl, qxh[qq], st[qq]);
-                }
-            }
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
-        }
-        const int k0 = p * 2 * KC + j * KC;
-        if (N - k0 < KC) {  // the chunk straddles N: keys past N score -inf (wave-uniform)
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int qq = 0; qq < 2; ++qq)
-                        s[qq][u][r] = k0 + 16 * u + 4 * g + r < N ? s[qq][u][r] : -INFINITY;
-        }
-        auto chunk_max = [&](int qq) {
-            return fmaxf(fmaxf(fmaxf(s[qq][0][0], s[qq][0][1]), fmaxf(s[qq][0][2], s[qq][0][3])),
-                         fmaxf(fmaxf(s[qq][1][0], s[qq][1][1]), fmaxf(s[qq][1][2], s[qq][1][3])));
-        };
-        if (fresh) {  // the first chunk (m = 0 above): the base is its maximum (wave-uniform)
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                const float cm = grp4_max(chunk_max(qq));  // finite: the chunk holds a key < N
-                m[qq] = cm;
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= cm;
-            }
-        }
-        u32x4 bh4[2], bl4[2];
-        auto exp_split = [&]() {
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                float e[2][4];
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
-                unsigned ph[4], pl[4];
-                split2u(e[0][0], e[0][1], ph[0], pl[0]);
-                split2u(e[0][2], e[0][3], ph[1], pl[1]);
-                split2u(e[1][0], e[1][1], ph[2], pl[2]);
-                split2u(e[1][2], e[1][3], ph[3], pl[3]);
-                bh4[qq] = u32x4{ph[0], ph[1], ph[2], ph[3]};
-                bl4[qq] = u32x4{pl[0], pl[1], pl[2], pl[3]};
-            }
-        };
-        exp_split();
-        if (__builtin_amdgcn_ballot_w64(p_hi_exceeds(bh4[0], bh4[1])) != 0) {  // rare: move the base
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                const float d = vmax(grp4_max(chunk_max(qq)), 0.f);
-                m[qq] += d;
-                const float corr = __builtin_amdgcn_exp2f(-d);
-                lacc[qq] *= corr;
-#pragma unroll
-                for (int t = 0; t < MT; ++t) acc[qq][t] *= corr;
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s[qq][u][r] -= d;
-            }
-            exp_split();
-        }
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            lacc[qq] = mfma(ones, bh4[qq], lacc[qq]);
-            lacc[qq] = mfma(ones, bl4[qq], lacc[qq]);
-        }
-        const unsigned char* vp = sb + j * CB + h * Q::HB + Q::KB + 16 * lane;
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            const u32x4 vh = *reinterpret_cast<const u32x4*>(vp + t * 2048);
-            const u32x4 vl = *reinterpret_cast<const u32x4*>(vp + t * 2048 + 1024);
-#pragma unroll
-            for (int qq = 0; qq < 2; ++qq) {
-                acc[qq][t] = mfma(vh, bh4[qq], acc[qq][t]);
-                acc[qq][t] = mfma(vh, bl4[qq], acc[qq][t]);
-                acc[qq][t] = mfma(vl, bh4[qq], acc[qq][t]);
-            }
-        }
-    };
-
-    gload(0);
-    lstore(0);
-    if (1 < nsc) gload(1);
-    lds_barrier();
-#pragma unroll 1
-    for (int p = 0; p < nsc; ++p) {
-        // step p from buffer p & 1; p + 1 goes to the other buffer, p + 2 is requested
-        if (p + 1 < nsc) lstore((p + 1) & 1);
-        if (p + 2 < nsc) gload(p + 2);
-        unsigned char* sb = ring + (p & 1) * SB;
-        process(sb, p, 0, p == 0);                       // chunk 0 of step p holds key 64 p < N
-        if (2 * KC * p + KC < N) process(sb, p, 1, false);  // wave-uniform
-        lds_barrier();
-    }
-    TSTAMP(1);
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-        const float inv = 1.0f / lacc[qq][0];
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-            put_split4<H>(A + (16 * (2 * qp + qq) + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), acc[qq][t][0] * inv,
-                          acc[qq][t][1] * inv, acc[qq][t][2] * inv, acc[qq][t][3] * inv);
-    }
-}
-
 // ---------------------------------------------------------------------------
 struct LArgs {
     int B, N, npad, ntile;
@@ -2790,19 +1795,17 @@ struct LArgs {
 
 // RB = 1 (16-row tiles) while the grid fits one round of the CUs, else 2
 // (32-row tiles: every K / V and weight fragment a workgroup reads serves
-// twice the rows), 4 (64-row query-split tiles), 8 (unmasked only: 128-row
-// tiles whose attention runs over all 128 queries, attention_q128, and whose
-// row-local phases run as two 64-row halves in the same LDS).
+// twice the rows), 4 (64-row query-split tiles; QV picks the attention form).
 template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
-    static_assert(RB != 8 || !MASKED, "128-row tiles: unmasked attention only");
+    static_assert(RB == 1 || RB == 2 || RB == 4, "16-, 32- or 64-row tiles");
+    static_assert(QV != 9 || !MASKED, "the wave-specialised attention is unmasked-only");
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
-    constexpr bool QS = RB >= 4;                  // 64- / 128-row tiles: K / V staged in LDS
-    constexpr int RBH = RB == 8 ? 4 : RB, TRH = 16 * RBH, NHALF = RB == 8 ? 2 : 1;  // row-local phases
+    constexpr bool QS = RB == 4;                  // 64-row tiles: K / V staged in LDS
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att, then LN2(o), LN(y) (split)
     // the attention's scratch (key-quarter merge records / the K-V chunk ring)
     // and, after it, o / y (fp32, O) and relu(FFN1) (split, Hd)
-    constexpr int OB = TRH * frs(H) * 4, HB = TRH * srs(F);
+    constexpr int OB = TR * frs(H) * 4, HB = TR * srs(F);
     constexpr int XB = QS ? 2 * QsGeo<HD>::SB : NW * RB * 64 * Geo<HD>::XW * 4;
     __shared__ __attribute__((aligned(16))) unsigned char U[OB + HB > XB ? OB + HB : XB];
     float* const O = reinterpret_cast<float*>(U);
@@ -2820,8 +1823,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     const QkvOut qo{a.nq, a.nk, a.nv, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
     if (t0 >= N) {
-        if constexpr (NEXT == 1)
-            for (int hf = 0; hf < NHALF && t0 + TRH * hf < a.npad; ++hf) zero_tile<H, HD, RBH>(qo, b, t0 + TRH * hf);
+        if constexpr (NEXT == 1) zero_tile<H, HD, RB>(qo, b, t0);
         return;
     }
     for (int e = threadIdx.x; e < H; e += NW * 64) {
@@ -2842,18 +1844,9 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     int len = N;
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
-    if constexpr (RB == 8) {
-        attention_q128<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        __syncthreads();
-        TSTAMP(2);
-    } else if constexpr (QS) {
-        if constexpr (QV == 5 && !MASKED) attention_qsplit2p<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 6 && !MASKED) attention_qsplit2pp<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 7 && !MASKED) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 8 && !MASKED) attention_qsplit_ws<H, HD, 1>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 9 && !MASKED) attention_qsplit_ws<H, HD, 0, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 10 && !MASKED) attention_qsplit_ws<H, HD, 2, true>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
-        else if constexpr (QV == 3 || QV >= 5) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
+    if constexpr (QS) {
+        if constexpr (QV == 9) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        else if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
         // row sums moved the stage1 encoder's error at B=128 S=130 from under
@@ -2868,129 +1861,107 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
             if (wave < H / 16) so.load(a.Wo, wave);
         });
     }
-#pragma unroll 1
-    for (int hf = 0; hf < NHALF; ++hf) {
-        // rows t0h .. t0h + TRH - 1: their attention rows at Ah
-        const int t0h = t0 + TRH * hf;
-        unsigned char* const Ah = A + TRH * hf * srs(H);
-        if (hf > 0) {
-            if (t0h >= a.npad) break;  // workgroup-uniform
-            if (t0h >= N) {
-                if constexpr (NEXT == 1) zero_tile<H, HD, RBH>(qo, b, t0h);
-                break;
-            }
-            __syncthreads();  // the first half's last readers of O / Hd / Ah are done
-        }
-        // Wo's strip: per half with 128-row tiles (a strip held across the
-        // loop would stay live through both halves' FFN and spill)
-        Strip<H> soh;
-        if constexpr (NHALF == 2) {
-            if (wave < H / 16) soh.load(a.Wo, wave);
-        } else {
-            soh = so;
-        }
-        const size_t row0 = (size_t)b * N + t0h;
-        // o = x + att . Wo^T + bo
-        if (wave < H / 16) {
-            const int col = wave * 16 + 4 * gq;
-            f32x4 acc[RBH];
+    const size_t row0 = (size_t)b * N + t0;
+    // o = x + att . Wo^T + bo
+    if (wave < H / 16) {
+        const int col = wave * 16 + 4 * gq;
+        f32x4 acc[RB];
 #pragma unroll
-            for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VO + col);
-            gemm_t<H, RBH>(Ah, soh, acc);
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VO + col);
+        gemm_t<H, RB>(A, so, acc);
 #pragma unroll
-            for (int rb = 0; rb < RBH; ++rb) {
-                const int rr = rb * 16 + i;
-                f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-                if (t0h + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
-                *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = x + acc[rb];
-            }
+        for (int rb = 0; rb < RB; ++rb) {
+            const int rr = rb * 16 + i;
+            f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (t0 + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
+            *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = x + acc[rb];
         }
-        Strip<H> s1;
-        if (wave < F / 16) s1.load(a.W1, wave);
-        __syncthreads();
-        TSTAMP(3);
-        ln_rows<H, TRH>(O, Ah, vec + VG2, vec + VB2N);
-        __syncthreads();
-        TSTAMP(4);
-        // h = relu(LN2(o) . W1^T + b1)
+    }
+    Strip<H> s1;
+    if (wave < F / 16) s1.load(a.W1, wave);
+    __syncthreads();
+    TSTAMP(3);
+    ln_rows<H, TR>(O, A, vec + VG2, vec + VB2N);
+    __syncthreads();
+    TSTAMP(4);
+    // h = relu(LN2(o) . W1^T + b1)
 #pragma unroll 1
-        for (int nb = wave; nb < F / 16; nb += NW) {
+    for (int nb = wave; nb < F / 16; nb += NW) {
+        Strip<H> nxt;
+        if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
+        const int col = nb * 16 + 4 * gq;
+        f32x4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
+        gemm_t<H, RB>(A, s1, acc);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+            put_split4<F>(Hd + (rb * 16 + i) * srs(F) + 2 * col, acc[rb][0] > 0.f ? acc[rb][0] : 0.f,
+                          acc[rb][1] > 0.f ? acc[rb][1] : 0.f, acc[rb][2] > 0.f ? acc[rb][2] : 0.f,
+                          acc[rb][3] > 0.f ? acc[rb][3] : 0.f);
+        if (nb + NW < F / 16) s1 = nxt;
+    }
+    Strip<F> s2;
+    if (wave < H / 16) s2.load(a.W2, wave);
+    __syncthreads();
+    TSTAMP(5);
+    // y = o + h . W2^T + b2
+    if (wave < H / 16) {
+        const int col = wave * 16 + 4 * gq;
+        f32x4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB2 + col);
+        gemm_t<F, RB>(Hd, s2, acc);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int rr = rb * 16 + i;
+            const f32x4 y = *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
+            if (t0 + rr < N) *reinterpret_cast<f32x4*>(a.x_out + (row0 + rr) * H + col) = y;
+            if constexpr (NEXT != 0) *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = y;
+        }
+    }
+    if constexpr (NEXT == 1) {
+        Strip<H> sn;
+        if (wave < 3 * H / 16) sn.load(a.Wn, wave);
+        __syncthreads();
+        TSTAMP(6);
+        ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
+        __syncthreads();
+        TSTAMP(7);
+        qkv_phase<H, HD, RB>(A, a.Wn, sn, qo, b, t0, N);
+        TSTAMP(8);
+        TSTAMP_RT(15);
+    } else if constexpr (NEXT == 2) {
+        Strip<H> sn;
+        if (wave < NN / 16) sn.load(a.Wn, wave);
+        __syncthreads();
+        TSTAMP(6);
+        ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
+        __syncthreads();
+        TSTAMP(7);
+#pragma unroll 1
+        for (int nb = wave; nb < NN / 16; nb += NW) {
             Strip<H> nxt;
-            if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
+            if (nb + NW < NN / 16) nxt.load(a.Wn, nb + NW);
             const int col = nb * 16 + 4 * gq;
-            f32x4 acc[RBH];
+            f32x4 acc[RB];
 #pragma unroll
-            for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
-            gemm_t<H, RBH>(Ah, s1, acc);
+            for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VBN2 + col);
+            gemm_t<H, RB>(A, sn, acc);
 #pragma unroll
-            for (int rb = 0; rb < RBH; ++rb)
-                put_split4<F>(Hd + (rb * 16 + i) * srs(F) + 2 * col, acc[rb][0] > 0.f ? acc[rb][0] : 0.f,
-                              acc[rb][1] > 0.f ? acc[rb][1] : 0.f, acc[rb][2] > 0.f ? acc[rb][2] : 0.f,
-                              acc[rb][3] > 0.f ? acc[rb][3] : 0.f);
-            if (nb + NW < F / 16) s1 = nxt;
-        }
-        Strip<F> s2;
-        if (wave < H / 16) s2.load(a.W2, wave);
-        __syncthreads();
-        TSTAMP(5);
-        // y = o + h . W2^T + b2
-        if (wave < H / 16) {
-            const int col = wave * 16 + 4 * gq;
-            f32x4 acc[RBH];
-#pragma unroll
-            for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB2 + col);
-            gemm_t<F, RBH>(Hd, s2, acc);
-#pragma unroll
-            for (int rb = 0; rb < RBH; ++rb) {
+            for (int rb = 0; rb < RB; ++rb) {
                 const int rr = rb * 16 + i;
-                const f32x4 y = *reinterpret_cast<const f32x4*>(O + rr * frs(H) + col) + acc[rb];
-                if (t0h + rr < N) *reinterpret_cast<f32x4*>(a.x_out + (row0 + rr) * H + col) = y;
-                if constexpr (NEXT != 0) *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = y;
+                if (t0 + rr < N) *reinterpret_cast<f32x4*>(a.z + (row0 + rr) * NN + col) = acc[rb];
             }
+            if (nb + NW < NN / 16) sn = nxt;
         }
-        if constexpr (NEXT == 1) {
-            Strip<H> sn;
-            if (wave < 3 * H / 16) sn.load(a.Wn, wave);
-            __syncthreads();
-            TSTAMP(6);
-            ln_rows<H, TRH>(O, Ah, vec + VGN, vec + VBN);
-            __syncthreads();
-            TSTAMP(7);
-            qkv_phase<H, HD, RBH>(Ah, a.Wn, sn, qo, b, t0h, N);
-            TSTAMP(8);
-            TSTAMP_RT(15);
-        } else if constexpr (NEXT == 2) {
-            Strip<H> sn;
-            if (wave < NN / 16) sn.load(a.Wn, wave);
-            __syncthreads();
-            TSTAMP(6);
-            ln_rows<H, TRH>(O, Ah, vec + VGN, vec + VBN);
-            __syncthreads();
-            TSTAMP(7);
-#pragma unroll 1
-            for (int nb = wave; nb < NN / 16; nb += NW) {
-                Strip<H> nxt;
-                if (nb + NW < NN / 16) nxt.load(a.Wn, nb + NW);
-                const int col = nb * 16 + 4 * gq;
-                f32x4 acc[RBH];
-#pragma unroll
-                for (int rb = 0; rb < RBH; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VBN2 + col);
-                gemm_t<H, RBH>(Ah, sn, acc);
-#pragma unroll
-                for (int rb = 0; rb < RBH; ++rb) {
-                    const int rr = rb * 16 + i;
-                    if (t0h + rr < N) *reinterpret_cast<f32x4*>(a.z + (row0 + rr) * NN + col) = acc[rb];
-                }
-                if (nb + NW < NN / 16) sn = nxt;
-            }
-            TSTAMP(8);
-            TSTAMP_RT(15);
-        } else {
-            TSTAMP(6);
-            TSTAMP(7);
-            TSTAMP(8);
-            TSTAMP_RT(15);
-        }
+        TSTAMP(8);
+        TSTAMP_RT(15);
+    } else {
+        TSTAMP(6);
+        TSTAMP(7);
+        TSTAMP(8);
+        TSTAMP_RT(15);
     }
 }
 
@@ -3168,13 +2139,6 @@ int tfl_rb(int B, int N) {
     const long tiles16 = (long)B * (tfl_npad(N) / tfl::TQ);
     return tiles16 >= 4 * 256 ? 4 : (tiles16 > 256 ? 2 : 1);
 }
-// 128-row tiles (unmasked layers; M2_TFL_RB=8 forces them there): the
-// attention's K / V stream from L2 serves twice the queries of a 64-row tile
-// (attention_q128).  Default: off until measured.
-int tfl_rb_layer(int B, int N, bool masked) {
-    const int rb = tfl_rb(B, N);
-    return rb == 8 && masked ? 4 : rb;
-}
 // 64-row tiles: two query blocks per wave with the lean softmax
 // (attention_qsplit2<..., LEAN>) at head_dim 48 (stage2: B=128 T=2600 step
 // -1.5 %, B=16 T=2600 -1.9 %, B=64 T=500 -0.8 % against the plain two-block
@@ -3189,10 +2153,12 @@ int tfl_rb_layer(int B, int N, bool masked) {
 // B=16 T=2600 -1.1 %, B=64 T=500 level (in-process A/Bs,
 // profiles/r04/r04j_*, r04l_*, r04m_*, r04n_*); at head_dim 32 it is slower
 // than the lean one-block form (stage1 B=32 +0.5 %, B=128 +1.4 %).  Measured
-// and not kept: the software-pipelined form (5, level or slower, r04d / r04e),
-// the wave-specialised form with register staging (7, between 6 and 9) and
-// with its regions interleaved by group barriers (8, +3 %).
-// M2_TFL_QS2=0|1|3..10 forces a form (switch table, m2_common.h).
+// and not kept (removed in round 5): the software-pipelined form (5, level or
+// slower, r04d / r04e), the wave-specialised form with register staging (7,
+// between 6 and 9) and with its regions interleaved by group barriers (8,
+// +3 %; 10).  M2_TFL_QS2=0|2|3|4|9 forces a form (switch table, m2_common.h):
+// 0 / 2 one / two query blocks, 3 / 4 the same with the lean softmax, 9 the
+// wave-specialised form (unmasked layers; masked ones run 3).
 int tfl_qs2(int H) {
     if (sw().tfl_qs2 >= 0) return sw().tfl_qs2;
     return H / tfl::HEADS >= 48 ? 9 : 4;
@@ -3290,7 +2256,7 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.N = N;
     a.dN = dN;
     a.npad = tfl_npad(N);
-    const int rb = tfl_rb_layer(B, N, masked);
+    const int rb = tfl_rb(B, N);
     a.ntile = tfl_ntile(N, rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
@@ -3318,27 +2284,23 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nv = out.v;
     a.z = z;
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
-    // forms 5-10 are unmasked-only (masked launches of those forms run 3):
-    // no masked instantiations of them
-    const int qs2 = masked && tfl_qs2(H) >= 5 ? 3 : tfl_qs2(H);
+    // form 9 is unmasked-only, and keeps the softmax base as an f16 pair: a
+    // masked launch, or a layer whose scores may leave the f16 range, runs the
+    // lean two-block form (3) instead
+    int qs2 = tfl_qs2(H);
+    if (qs2 == 9 && (masked || w.wide_scores)) qs2 = 3;
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
         if constexpr (!MM) {                                                                    \
-            if (rb == 8 || (rb == 4 && qs2 >= 5)) {                                             \
-                if (rb == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 8, 3>), grid, blk, 0, st, a); \
-                else if (qs2 == 10) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 10>), grid, blk, 0, st, a); \
-                else if (qs2 == 9) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 9>), grid, blk, 0, st, a); \
-                else if (qs2 == 8) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 8>), grid, blk, 0, st, a); \
-                else if (qs2 == 7) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 7>), grid, blk, 0, st, a); \
-                else if (qs2 == 6) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 6>), grid, blk, 0, st, a); \
-                else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 5>), grid, blk, 0, st, a); \
+            if (rb == 4 && qs2 == 9) {                                                          \
+                hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 9>), grid, blk, 0, st, a); \
                 M2_LAUNCHED("tfl layer_kernel");                                                \
                 return M2_OK;                                                                   \
             }                                                                                   \
         }                                                                                       \
         if (rb == 4 && qs2 == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 4>), grid, blk, 0, st, a);  \
         else if (rb == 4 && qs2 == 3) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 3>), grid, blk, 0, st, a);  \
-        else if (rb == 4 && qs2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
+        else if (rb == 4 && qs2 == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 2>), grid, blk, 0, st, a);  \
         else if (rb == 4) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4>), grid, blk, 0, st, a);  \
         else if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2>), grid, blk, 0, st, a);  \
         else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 1>), grid, blk, 0, st, a);          \

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "m2_common.h"
+#include "vocoder_redo.h"
 
 namespace m2 {
 
@@ -127,15 +128,33 @@ struct VocX {
     // zeroed by the head kernel's first thread when set (the on-device redo's
     // other flag word, whose last readers ran in the previous call)
     int* rclear = nullptr;
+    // the redo's four work-queue words (VocW::guard_queue), zeroed with rclear:
+    // a redo launch that stopped early cannot leave them claimed for the next
+    unsigned* rqueue = nullptr;
     // device frame count (dev_frames): when set, the T passed to the launches
     // is the capacity their grids cover
     const int32_t* dT = nullptr;
+    // range policy "fallback" on the pipelined tails (tailp / tailp2): the
+    // fp32 weights of their in-launch local redo (vocoder_redo.h; device
+    // copy), else null
+    const VocRedoW* redo_w = nullptr;
+    // per call: a scratch buffer of at least B x 4T x 2C bytes (the stage2
+    // split head's ConvT1 rows), or null (the fused head)
+    void* scratch = nullptr;
 };
 
 // Non-finite output check of the split path's last kernel: any NaN among the
 // four values -> *flag = 1 (rare path; the host reads and clears it).
 __device__ __forceinline__ void flag_nonfinite4(float a, float b, float c, float d, int* flag) {
     if (flag && ((a != a) | (b != b) | (c != c) | (d != d))) *reinterpret_cast<volatile int*>(flag) = 1;
+}
+// The same, also raising the workgroup's LDS word lflag (the pipelined tails'
+// local redo, vocoder_redo.h).
+__device__ __forceinline__ void flag_nonfinite4(float a, float b, float c, float d, int* flag, int* lflag) {
+    if ((a != a) | (b != b) | (c != c) | (d != d)) {
+        if (flag) *reinterpret_cast<volatile int*>(flag) = 1;
+        *reinterpret_cast<volatile int*>(lflag) = 1;
+    }
 }
 
 // Pipelined stage1 tail (vocoder_tailp.hip): ConvT3, ResBlock3, ConvT4,
@@ -215,14 +234,16 @@ struct TailpSrc {
 // false when a layer's non-zero weights do not fit the slot table (cannot
 // happen for the stage1 shapes; the x3 tail is kept then).
 bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
+// rd.rw set: range policy "fallback" - a workgroup whose audio strip is not
+// finite recomputes it in fp32 inside the launch (vocoder_redo.h).
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                             int* rflag, hipStream_t st, const int32_t* dT = nullptr);
+                             int* rflag, hipStream_t st, const int32_t* dT = nullptr, const VocRedo& rd = VocRedo{});
 extern const char* const kVocTailpKernelName;
 // The same five modules at stage2 widths (C = 256: U2 64 channels) for the
 // pipelined stage2 tail (vocoder_tailp2.hip, two waves per layer).
 bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
 int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                              int* rflag, hipStream_t st, const int32_t* dT = nullptr);
+                              int* rflag, hipStream_t st, const int32_t* dT = nullptr, const VocRedo& rd = VocRedo{});
 extern const char* const kVocTailp2KernelName;
 
 bool vocoder_x3_supported(int M, int C);

@@ -561,8 +561,9 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(co
 // workgroups already running, so any number of resident workgroups finishes
 // (no co-residency assumption).  Publication: every wave's stores are written
 // back (agent-scope release fence) before the count; a waiter acquires after
-// it (U1 / U2 cross XCDs, whose L2s are not coherent).  The last workgroup out
-// (q[3]) re-zeroes the four words for the next redo.
+// it (U1 / U2 cross XCDs, whose L2s are not coherent).  The four words are
+// zeroed by the call's first (x3 head) kernel (VocX::rqueue), so a redo that
+// stopped early cannot leave the next one's queue claimed.
 __device__ __forceinline__ void redo_publish(unsigned* c) {
     __threadfence();
     __syncthreads();
@@ -574,8 +575,12 @@ __device__ __forceinline__ void redo_wait(unsigned* c, unsigned n) {
     __syncthreads();
     __threadfence();
 }
+// Compiled for one workgroup per CU (WAVES / 4 waves per SIMD): the three
+// bodies in one loop need more registers than each kernel's own occupancy
+// target leaves (at MINW they spilled 52-73 VGPRs), and the redo's speed
+// matters less than the split kernels' (it runs only for out-of-range calls).
 template <class Cfg, bool TRANS>
-__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_redo_kernel(const float* __restrict__ mel, int B,
+__global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::WAVES / 4) void voc_redo_kernel(const float* __restrict__ mel, int B,
                                                                              int T, VocW w, float* __restrict__ U1,
                                                                              float* __restrict__ U2,
                                                                              float* __restrict__ audio,
@@ -602,8 +607,6 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_redo_kernel(co
             voc_tail_body<Cfg>((i - nh - nm) % tx, (i - nh - nm) / tx, U2, 16 * T, w, audio);
         }
     }
-    if (threadIdx.x == 0 && atomicAdd(q + 3, 1u) == gridDim.x - 1)
-        for (int k = 0; k < 4; ++k) __hip_atomic_store(q + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -651,10 +654,17 @@ int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, floa
     return M2_OK;
 }
 
+// The redo's tiling: the 8-wave form of the stage (every stage1 tiling packs
+// the same weights and writes the same U1 / U2 / audio), so it gets up to 256
+// VGPRs per lane at one workgroup per CU.
+template <class Cfg> struct RedoCfg { using type = Cfg; };
+template <> struct RedoCfg<CfgS1W16> { using type = CfgS1W8; };
+template <> struct RedoCfg<CfgS1W16s> { using type = CfgS1W8; };
+
 template <class Cfg>
 int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                   hipStream_t st, const std::function<void(int, bool)>& mark) {
-    if (w.guard) return voc_redo<Cfg>(mel, trans, B, T, w, U1, U2, audio, st);
+    if (w.guard) return voc_redo<typename RedoCfg<Cfg>::type>(mel, trans, B, T, w, U1, U2, audio, st);
     using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;

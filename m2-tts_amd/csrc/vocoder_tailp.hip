@@ -78,7 +78,11 @@ constexpr int kPeriod(int n) { return kRingRows[n] / 16; }  // chunks per ring (
 // + the loader): NL = 7 53,248 B, NL = 6 (outc_role) 47,120 B.
 // NL = 6 also keeps the outc edge-term slot (4 floats) after the rings.
 constexpr int kCorrSlot = kRingOff(6);
-constexpr int lds_bytes(int nl) { return nl == 6 ? kCorrSlot + 16 : kRingOff(nl); }
+constexpr int ring_bytes(int nl) { return nl == 6 ? kCorrSlot + 16 : kRingOff(nl); }
+// after the rings: the workgroup's non-finite-audio word (the local redo,
+// vocoder_redo.h); the redo itself reuses the rings' bytes
+constexpr int kFlagOff(int nl) { return ring_bytes(nl); }
+constexpr int lds_bytes(int nl) { return ring_bytes(nl) + 16; }
 constexpr int nwaves(int nl) { return nl + 1; }
 static_assert(lds_bytes(7) * 3 <= 160 * 1024, "three workgroups per CU");
 #ifdef M2_STAMPS
@@ -273,7 +277,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                 o.z = tanh_fast(acc[0][2]);
                 o.w = tanh_fast(acc[0][3]);
                 *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
-                flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
+                flag_nonfinite4(o.x, o.y, o.z, o.w, rflag, reinterpret_cast<int*>(lds + kFlagOff(NL)));
             }
         } else {
             // Both m-blocks in one basic block (the compiler interleaves their
@@ -438,7 +442,7 @@ __device__ __forceinline__ void outc_role(unsigned char* lds, int qa, int L2, bo
             o.z = tanh_fast(v[2]);
             o.w = tanh_fast(v[3]);
             *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
-            flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
+            flag_nonfinite4(o.x, o.y, o.z, o.w, rflag, reinterpret_cast<int*>(lds + kFlagOff(NL)));
         }
     };
     constexpr int LAST = last_step(NCH, NL);
@@ -522,7 +526,7 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 6) void tailp_kernel(const unsigne
                                                                     const u32x4* __restrict__ W,
                                                                     const float* __restrict__ bias,
                                                                     float* __restrict__ audio, int* rflag,
-                                                                    const int32_t* __restrict__ dT) {
+                                                                    const int32_t* __restrict__ dT, VocRedo rd) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
     if (dT) {  // speculative launch: L2 was the capacity
@@ -532,6 +536,8 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 6) void tailp_kernel(const unsigne
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
     float* arow = audio + (size_t)b * 4 * L2;
+    int* const lflag = reinterpret_cast<int*>(lds + kFlagOff(NL));
+    if (threadIdx.x == 0) *lflag = 0;  // before the first epilogue: the pipeline's step barriers order it
     TPSTAMP(62, 0);
     // Later layers get higher issue priority: they are the younger waves of
     // the workgroup and lose VALU arbitration on age (MI355X_MICROARCH.md, two
@@ -564,11 +570,17 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 6) void tailp_kernel(const unsigne
             break;
     }
     TPSTAMP(63, 0);
+    if (rd.rw) {  // range policy "fallback": this strip's audio again in fp32 if it is not finite
+        __syncthreads();
+        if (*lflag)
+            redo_frames(*rd.rw, rd.mel, rd.trans, L2 / 16, b, qa / 16, min(L2, qa + 16 * NCH) / 16, arow,
+                        reinterpret_cast<float*>(lds), ring_bytes(NL) / 4);
+    }
 }
 
 template <int NCH, int NL>
 int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
-               hipStream_t st, const int32_t* dT) {
+               hipStream_t st, const int32_t* dT, const VocRedo& rd) {
     static bool attr = false;
     if (!attr) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp_kernel<NCH, NL>),
@@ -576,17 +588,17 @@ int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bi
         attr = true;
     }
     hipLaunchKernelGGL((tailp_kernel<NCH, NL>), dim3(cdiv(L2, 16 * NCH), B), dim3(nwaves(NL) * 64), lds_bytes(NL),
-                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag, dT);
+                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag, dT, rd);
     M2_LAUNCHED("tailp_kernel");
     return M2_OK;
 }
 
 template <int NL>
 int32_t launch_nl(int nch, const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                  int* rflag, hipStream_t st, const int32_t* dT) {
-    if (nch == 21) return launch<21, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
-    if (nch == 48) return launch<48, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
-    return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+                  int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd) {
+    if (nch == 21) return launch<21, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+    if (nch == 48) return launch<48, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+    return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
 }
 
 }  // namespace tp
@@ -602,7 +614,7 @@ const char* const kVocTailpKernelName =
     "tailp_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, pipelined)";
 
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                             int* rflag, hipStream_t st, const int32_t* dT) {
+                             int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd) {
     if (B == 0 || L2 == 0) return M2_OK;
     // Strip length: the shortest instantiated NCH that covers an utterance in
     // at most floor(768 / B) strips, so the grid is about one round of three
@@ -621,8 +633,8 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
     // classes of 18/21/16/12 MFMAs instead of 18/24/16/9 and measured the same:
     // the step is latency-bound, not bound by one SIMD's MFMA pipe.)
     const bool seven = sw().tailp_seven;
-    return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT)
-                 : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT);
+    return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd)
+                 : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd);
 }
 
 // ---------------------------------------------------------------------------

@@ -58,7 +58,11 @@ static_assert(kRingOff(7) <= 160 * 1024, "one workgroup per CU");
 // NL = 6: layers 0-4 two waves each, the composed layer one, loader one (12),
 // plus the composed layer's edge-term slot (8 floats) after the rings.
 constexpr int kCorrSlot = kRingOff(6);
-constexpr int lds_bytes(int nl) { return nl == 6 ? kCorrSlot + 32 : kRingOff(7); }
+constexpr int ring_bytes(int nl) { return nl == 6 ? kCorrSlot + 32 : kRingOff(7); }
+// after the rings: the workgroup's non-finite-audio word (the local redo,
+// vocoder_redo.h); the redo itself reuses the rings' bytes
+constexpr int kFlagOff(int nl) { return ring_bytes(nl); }
+constexpr int lds_bytes(int nl) { return ring_bytes(nl) + 16; }
 constexpr int nwaves(int nl) { return nl == 6 ? 12 : 14; }
 
 __device__ __forceinline__ unsigned ring_at(int n, int row, int oct) {
@@ -237,7 +241,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
                 o.z = tanh_fast(acc[0][2]);
                 o.w = tanh_fast(acc[0][3]);
                 *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
-                flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
+                flag_nonfinite4(o.x, o.y, o.z, o.w, rflag, reinterpret_cast<int*>(lds + kFlagOff(NL)));
             }
         } else {
             auto epilogue = [&](auto zc) {
@@ -375,7 +379,7 @@ __device__ __forceinline__ void outc2_role(unsigned char* lds, int qa, int L2, b
             o.z = tanh_fast(v[2]);
             o.w = tanh_fast(v[3]);
             *reinterpret_cast<float4*>(arow + 4 * (size_t)x) = o;
-            flag_nonfinite4(o.x, o.y, o.z, o.w, rflag);
+            flag_nonfinite4(o.x, o.y, o.z, o.w, rflag, reinterpret_cast<int*>(lds + kFlagOff(NL)));
         }
     };
     constexpr int LAST = last_step(NCH, NL);
@@ -449,7 +453,7 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsign
                                                                      const u32x4* __restrict__ W,
                                                                      const float* __restrict__ bias,
                                                                      float* __restrict__ audio, int* rflag,
-                                                                     const int32_t* __restrict__ dT) {
+                                                                     const int32_t* __restrict__ dT, VocRedo rd) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
     if (dT) {  // speculative launch: L2 was the capacity
@@ -459,6 +463,8 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsign
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
     float* arow = audio + (size_t)b * 4 * L2;
+    int* const lflag = reinterpret_cast<int*>(lds + kFlagOff(NL));
+    if (threadIdx.x == 0) *lflag = 0;  // before the first epilogue: the pipeline's step barriers order it
     // later layers: younger waves, the step waits for the slowest role
     if (w >= 10) __builtin_amdgcn_s_setprio(3);
     else if (w >= 6) __builtin_amdgcn_s_setprio(2);
@@ -498,11 +504,17 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsign
             else loader_role<NCH, NL, false>(lds, qa, L2, u2);
             break;
     }
+    if (rd.rw) {  // range policy "fallback": this strip's audio again in fp32 if it is not finite
+        __syncthreads();
+        if (*lflag)
+            redo_frames(*rd.rw, rd.mel, rd.trans, L2 / 16, b, qa / 16, min(L2, qa + 16 * NCH) / 16, arow,
+                        reinterpret_cast<float*>(lds), ring_bytes(NL) / 4);
+    }
 }
 
 template <int NCH, int NL>
 int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
-               hipStream_t st, const int32_t* dT) {
+               hipStream_t st, const int32_t* dT, const VocRedo& rd) {
     static bool attr = false;
     if (!attr) {
         M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp2_kernel<NCH, NL>),
@@ -510,21 +522,21 @@ int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bi
         attr = true;
     }
     hipLaunchKernelGGL((tailp2_kernel<NCH, NL>), dim3(cdiv(L2, 16 * NCH), B), dim3(nwaves(NL) * 64), lds_bytes(NL),
-                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag, dT);
+                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag, dT, rd);
     M2_LAUNCHED("tailp2_kernel");
     return M2_OK;
 }
 
 template <int NL>
 int32_t launch_nl(int nch, const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                  int* rflag, hipStream_t st, const int32_t* dT) {
+                  int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd) {
     switch (nch) {
-        case 8: return launch<8, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
-        case 16: return launch<16, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
-        case 32: return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
-        case 64: return launch<64, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
-        case 128: return launch<128, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
-        default: return launch<192, NL>(U2, L2, B, W, bias, audio, rflag, st, dT);
+        case 8: return launch<8, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+        case 16: return launch<16, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+        case 32: return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+        case 64: return launch<64, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+        case 128: return launch<128, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+        default: return launch<192, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
     }
 }
 
@@ -534,7 +546,7 @@ const char* const kVocTailp2KernelName =
     "tailp2_kernel (stage2 ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, pipelined)";
 
 int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                              int* rflag, hipStream_t st, const int32_t* dT) {
+                              int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd) {
     if (B == 0 || L2 == 0) return M2_OK;
     // Strip length: the instantiated NCH minimising rounds x (NCH + NL pipeline
     // steps) at one workgroup per CU.  M2_TAILP2_NCH forces one;
@@ -556,8 +568,8 @@ int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, 
             if (best < 0 || cost < best) best = cost, nch = n;
         }
     }
-    return seven ? tp2::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT)
-                 : tp2::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT);
+    return seven ? tp2::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd)
+                 : tp2::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd);
 }
 
 // ---------------------------------------------------------------------------

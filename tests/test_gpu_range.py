@@ -24,6 +24,25 @@ def _mel(stage, T, scale, seed=5):
     return torch.randn(2, stage_config(stage).mel_channels, T, generator=torch.Generator().manual_seed(seed)) * scale
 
 
+# The fallback's recomputation: the pipelined tails (stage1 tailp, stage2
+# tailp2) redo their own non-finite strips in fp32 inside the launch
+# (vocoder_redo.h; direct convolutions, another fp32 summation order than the
+# exact-f32 kernels); the guarded exact-f32 launch (M2_REDO_LAUNCH=1, or a
+# model without a pipelined tail) is bit-equal to those kernels.  Inputs that
+# overflow the split range are far outside the reference's normalised mel
+# range, and there the audio is ill-conditioned: activations of ~1e5 stored
+# in fp32 carry ~1e-2 of rounding each, which reaches the audio near tanh's
+# zero crossings.  So such outputs are checked against a float64 evaluation
+# of the reference's op sequence, within the distance the reference's own
+# fp32 CPU path (the oracle) lands from it on the same input (at least the
+# 1e-4 waveform bound).
+def _assert_like_reference(out, sd, mel_bmt):
+    sd64 = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
+    ref64 = orc.vocoder(sd64, mel_bmt.double())
+    cond = rms(orc.vocoder(sd, mel_bmt), ref64)  # the reference's fp32 path on this input
+    assert rms(out, ref64) <= max(AUDIO_RMS_TOL, 2 * cond), (rms(out, ref64), cond)
+
+
 @pytest.mark.parametrize("stage", ["s1", "s2"])
 def test_huge_mel_fallback_matches_exact_f32_and_oracle(gpu, stage):
     mel = _mel(stage, 45, 1e5)
@@ -32,11 +51,42 @@ def test_huge_mel_fallback_matches_exact_f32_and_oracle(gpu, stage):
     m.set_range_policy("fallback")
     out = m.vocoder(mel.to(gpu))
     assert torch.isfinite(out).all()
+    _assert_like_reference(out, golden_state(stage), mel)
     m.set_vocoder_precision("f32")
-    exact = m.vocoder(mel.to(gpu))
-    assert torch.equal(out, exact)
-    ref = orc.vocoder(golden_state(stage), mel)
-    assert rms(out, ref) <= AUDIO_RMS_TOL
+    _assert_like_reference(m.vocoder(mel.to(gpu)), golden_state(stage), mel)  # the exact-f32 kernels alike
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_local_redo_only_touches_non_finite_strips(gpu, stage):
+    """One utterance with an out-of-range stretch (frames 30-33 of
+    70): the other utterance's audio is the split path's, bit for bit; the
+    overflowing one matches the reference's op sequence (float64) as closely
+    as the reference's own fp32 path does."""
+    mel = _mel(stage, 70, 1.0)
+    clean = mel.clone()
+    mel[0, :, 30:34] *= 1e6
+    m = build_model(stage, gpu)
+    m.set_range_policy("report")
+    split_clean = m.vocoder(clean.to(gpu))
+    m.set_range_policy("fallback")
+    out = m.vocoder(mel.to(gpu))
+    assert torch.isfinite(out).all()
+    assert torch.equal(out[1], split_clean[1])
+    _assert_like_reference(out, golden_state(stage), mel)
+    m.check_numerics()
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+def test_guarded_launch_still_available(gpu, monkeypatch, stage):
+    """M2_REDO_LAUNCH=1 keeps the guarded exact-f32 launch behind the split
+    kernels (no local redo): the fallback equals the exact-f32 audio."""
+    monkeypatch.setenv("M2_REDO_LAUNCH", "1")
+    mel = _mel(stage, 45, 1e5)
+    m = build_model(stage, gpu)
+    m.set_range_policy("fallback")
+    out = m.vocoder(mel.to(gpu))
+    m.set_vocoder_precision("f32")
+    assert torch.equal(out, m.vocoder(mel.to(gpu)))
 
 
 @pytest.mark.parametrize("stage", ["s1", "s2"])
@@ -62,7 +112,8 @@ def test_huge_mel_report_raises(gpu, stage):
 @pytest.mark.parametrize("stage", ["s1", "s2"])
 def test_huge_activation_inside_the_vocoder(gpu, stage):
     """A finite mel, but input_conv's bias puts its activations near 1e5: the
-    split path flags it and the fallback gives the exact-f32 result (== oracle)."""
+    split path flags it and the fallback's fp32 recomputation matches the
+    reference's op sequence (as closely as the reference's fp32 path does)."""
     sd = golden_state(stage)
     sd["vocoder.input_conv.bias"] = sd["vocoder.input_conv.bias"] + 1e5
     m = build_model(stage, gpu, sd)
@@ -71,8 +122,7 @@ def test_huge_activation_inside_the_vocoder(gpu, stage):
     m.set_range_policy("fallback")
     out = m.vocoder(mel.to(gpu))
     assert torch.isfinite(out).all()
-    ref = orc.vocoder(sd, mel)
-    assert rms(out, ref) <= AUDIO_RMS_TOL
+    _assert_like_reference(out, sd, mel)
 
 
 @pytest.mark.parametrize("stage", ["s1", "s2"])
@@ -87,16 +137,13 @@ def test_default_policy_inference_never_nan(gpu, stage):
     ids, lens = torch.from_numpy(g["ids"]), torch.from_numpy(g["lengths"])
     mel, audio = m.inference(ids.to(gpu), lens.to(gpu))
     assert torch.isfinite(audio).all()
-    ref_mel, ref_audio = orc.inference(sd, stage_config(stage), ids, lens, as_written=False)
+    ref_mel, _ = orc.inference(sd, stage_config(stage), ids, lens, as_written=False)
     assert maxabs(mel, ref_mel) <= MEL_MAXABS_TOL
-    assert rms(audio, ref_audio) <= AUDIO_RMS_TOL
     # the second call of the shape runs the speculative back half (T from the
     # device, the redo kernels sized for the capacity): the same audio
     mel2, audio2 = m.inference(ids.to(gpu), lens.to(gpu))
     assert torch.equal(mel2, mel) and torch.equal(audio2, audio)
-    m.set_vocoder_precision("f32")
-    _, exact = m.inference(ids.to(gpu), lens.to(gpu))
-    assert torch.equal(audio, exact)
+    _assert_like_reference(audio, sd, mel.transpose(1, 2).cpu())
     m.check_numerics()  # nothing left pending
 
 
@@ -111,13 +158,18 @@ def test_fallback_on_device_alternating_calls(gpu, stage):
     ref = build_model(stage, gpu)
     ref.set_range_policy("report")
     split_ok = ref.vocoder(ok)
-    ref.set_vocoder_precision("f32")
-    exact_bad = ref.vocoder(bad)
     m = build_model(stage, gpu)
     m.set_range_policy("fallback")
+    first_bad = None
     for x in ("bad", "ok", "bad", "bad", "ok", "ok", "bad", "ok"):
         out = m.vocoder(bad if x == "bad" else ok)
-        assert torch.equal(out, exact_bad if x == "bad" else split_ok), x
+        if x == "ok":
+            assert torch.equal(out, split_ok), x
+        elif first_bad is None:
+            _assert_like_reference(out, golden_state(stage), bad.cpu())
+            first_bad = out
+        else:
+            assert torch.equal(out, first_bad)  # deterministic
     torch.cuda.synchronize()
     m.check_numerics()
 
@@ -133,7 +185,7 @@ def test_fallback_on_device_chunked(gpu, stage):
     m.set_vocoder_chunking(16)
     out = m.vocoder(mel.to(gpu))
     assert torch.isfinite(out).all()
-    assert rms(out, orc.vocoder(golden_state(stage), mel)) <= AUDIO_RMS_TOL
+    _assert_like_reference(out, golden_state(stage), mel)
     m.check_numerics()
 
 
@@ -166,6 +218,50 @@ def test_transformer_range_bound_selects_f32(gpu):
     ref_mel, ref_audio = orc.inference(sd, orc.STAGE1, ids, lens, as_written=False)
     assert maxabs(mel, ref_mel) <= MEL_MAXABS_TOL
     assert rms(audio, ref_audio) <= AUDIO_RMS_TOL
+
+
+@pytest.mark.parametrize("stage", ["s1", "s2"])
+@pytest.mark.parametrize("scale", [0.3, 10.0])
+@pytest.mark.parametrize("form", ["auto", "3", "4"])
+def test_attention_scores_large(gpu, monkeypatch, stage, scale, form):
+    """Decoder layer 0 with every q and k row = scale u (q_d = k_d = scale
+    u.LN1(x)): attention scores spread over > 128 log2 units (scale 0.3) or
+    past the f16 maximum (scale 10, with q / k still inside the split range,
+    so the creation-time activation bound passes).  The 64-row query-split
+    forms (M2_TFL_RB=4) keep an unnormalised base and move it only when a
+    weight's f16 hi half exceeds 2^8 - a later chunk scoring more than 16
+    above the base makes that hi half +inf, which the move must catch (a
+    float compare of packed f16 maxima missed it: NaN output).  At scale 10
+    the head_dim-48 default form, whose base is an f16 pair, gives way to
+    the f32-base form (m2_transformer_path 2).  "auto" is the
+    per-head-dim default (stage1 4, stage2 9), "3" / "4" the lean two- /
+    one-block forms."""
+    from m2amd import _lib
+    import torch.nn.functional as F
+    lib = _lib.load()
+    monkeypatch.setenv("M2_TFL_RB", "4")  # 64-row query-split tiles at this size
+    if form != "auto":
+        monkeypatch.setenv("M2_TFL_QS2", form)
+    cfg = stage_config(stage)
+    H, hd = cfg.hidden_dim, cfg.hidden_dim // 2
+    sd = golden_state(stage)
+    w = sd["decoder.layers.0.self_attn.qkv.weight"].clone()
+    u = torch.randn(H, generator=torch.Generator().manual_seed(3))
+    w[: 2 * H] = scale * u
+    sd["decoder.layers.0.self_attn.qkv.weight"] = w
+    x = torch.randn(2, 300, H, generator=torch.Generator().manual_seed(4))
+    xn = F.layer_norm(x, (H,), sd["decoder.layers.0.norm1.weight"], sd["decoder.layers.0.norm1.bias"])
+    q = xn @ w[:hd].T
+    sc = (q @ q.transpose(1, 2)) / hd ** 0.5 * 1.4426950408889634  # log2 units, as the kernels see them
+    assert float((sc.amax(-1) - sc.amin(-1)).amax()) > 128
+    m = build_model(stage, gpu, sd)
+    if scale > 1:
+        assert float(sc.amax()) > 65520
+        assert lib.m2_transformer_path(m._hip(gpu).handle) == 2
+        assert lib.m2_transformer_path(build_model(stage, gpu)._hip(gpu).handle) == 1
+    mel = m.decoder(x.to(gpu))
+    assert torch.isfinite(mel).all()
+    assert maxabs(mel, orc.mel_decoder(sd, cfg, x)) <= MEL_MAXABS_TOL
 
 
 def test_frame_count_overflow_is_an_error(gpu):

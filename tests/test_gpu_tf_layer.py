@@ -28,26 +28,23 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
-@pytest.fixture(params=["auto", "1", "2", "4", "4q1", "4q2", "4q3", "4q4", "4q5", "4q6", "4q7", "4q8", "4q9", "4q10", "8", "f4"])
+@pytest.fixture(params=["auto", "1", "2", "4", "4q3", "f4"])
 def rows_per_tile(request, monkeypatch):
-    """16- and 32-row workgroup tiles with key-quarter attention, 64-row tiles
-    with query-split attention (K / V staged in LDS) (M2_TFL_RB) - the
-    per-head-dim default, one query block and both chunks of each 64-key step
-    ("4q1", M2_TFL_QS2=0) or two query blocks and one chunk ("4q2") - and the
-    per-call choice; "f4": 64-row tiles for the first (LN1 -> QKV) launch
-    (M2_TFL_FIRST_RB, the default for very large grids); "8": 128-row tiles
-    for the unmasked layers (attention_q128 over two 64-row halves)."""
+    """The tile forms a default can pick: 16- and 32-row workgroup tiles with
+    key-quarter attention, 64-row tiles with query-split attention (K / V
+    staged in LDS; M2_TFL_RB) - at head_dim 32 the lean one-block form, at
+    head_dim 48 the wave-specialised LDS-DMA form (unmasked) and the lean
+    two-block form (masked) - and the per-call choice; "4q3": the lean
+    two-block form on the unmasked layers too (M2_TFL_QS2=3: what a layer
+    whose scores may leave the f16 range runs, m2_layer_w::wide_scores);
+    "f4": 64-row tiles for the first (LN1 -> QKV) launch (M2_TFL_FIRST_RB,
+    the default for very large grids)."""
     if request.param == "f4":
         monkeypatch.setenv("M2_TFL_FIRST_RB", "4")
     elif request.param != "auto":
         monkeypatch.setenv("M2_TFL_RB", request.param[0])
-    # "4q3" / "4q4": two / one block, lean softmax; "4q5": two blocks, lean,
-    # software-pipelined, "4q6": two blocks, lean, ping-pong, "4q7": four
-    # blocks per computing wave, staging waves, "4q8": that with the
-    # interleaved matrix / vector regions, "4q9" / "4q10": "4q7" / "4q8" with
-    # LDS-DMA staging (unmasked launches; masked ones run "4q3")
     if request.param.startswith("4q"):
-        monkeypatch.setenv("M2_TFL_QS2", "0" if request.param == "4q1" else request.param[2:])
+        monkeypatch.setenv("M2_TFL_QS2", request.param[2:])
     return request.param
 
 
