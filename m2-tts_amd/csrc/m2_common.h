@@ -47,7 +47,6 @@ struct Switches {
     bool tailp2_seven = false;  // M2_TAILP2_SEVEN
     bool head_inconv = false;   // M2_HEAD_INCONV
     bool s2_head_tf16 = false;  // M2_S2_HEAD_TF16
-    int s2_head_split = 0;      // M2_S2_HEAD_SPLIT=0|1: the stage2 head as two launches (vocoder_x3.hip)
     int redo_grid = -1;         // M2_REDO_GRID: workgroups of the guarded redo launch (-1: one per CU)
     bool redo_launch = false;   // M2_REDO_LAUNCH: the guarded exact-f32 launch also where the tail redoes locally
     bool dur_split = true;      // M2_DUR_SPLIT=0: the duration convs on the exact-f32 MFMA always

@@ -83,7 +83,6 @@ void reload_switches() {
     s.tailp2_seven = env_set("M2_TAILP2_SEVEN");
     s.head_inconv = env_set("M2_HEAD_INCONV");
     s.s2_head_tf16 = env_set("M2_S2_HEAD_TF16");
-    s.s2_head_split = env_int("M2_S2_HEAD_SPLIT", 0) ? 1 : 0;
     s.redo_grid = env_int("M2_REDO_GRID", -1);
     s.redo_launch = env_set("M2_REDO_LAUNCH");
     s.dur_split = env_on("M2_DUR_SPLIT", true);
@@ -1666,7 +1665,6 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
         VocX vx = m->vx;
         VocW vw = m->vw;
         vx.dT = vw.dT = dT;
-        vx.scratch = buf[2];
         if (x3 && redo >= 0) {
             vx.rflag = m->rflag_dev + redo;
             vx.rclear = m->rflag_dev + (redo ^ 1);

@@ -138,9 +138,6 @@ struct VocX {
     // fp32 weights of their in-launch local redo (vocoder_redo.h; device
     // copy), else null
     const VocRedoW* redo_w = nullptr;
-    // per call: a scratch buffer of at least B x 4T x 2C bytes (the stage2
-    // split head's ConvT1 rows), or null (the fused head)
-    void* scratch = nullptr;
 };
 
 // Non-finite output check of the split path's last kernel: any NaN among the

@@ -425,31 +425,27 @@ __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float
 // The composed input_conv o ConvT1 on the generic item path (the stage2
 // head): head_convT1c_planar's layer over (phase, m-block, chunk) items, 4
 // mel taps (frames q + d0 + 1 - k), per-phase bias, edge terms from `corr`.
-// MBS > 0: only m-blocks mb0 .. mb0 + MBS - 1 (a slice of the output
-// channels; the split head's first launch); GO: the tiles go straight to
-// global rows of 4 COUT bytes (gout, positions t < 4T) instead of `out`.
-template <int MP, int COUT, int NT, int RSI, int RSO, int NQ, int PDM = 4, int MBS = 0, bool GO = false>
+template <int MP, int COUT, int NT, int RSI, int RSO, int NQ, int PDM = 4>
 __device__ __forceinline__ void xconvT1c(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
-                                         const unsigned char* corr, XW mel, XW out, int q0, int T, int mb0 = 0,
-                                         unsigned char* gout = nullptr) {
-    constexpr int R = 4, MB = (COUT + 15) / 16, NKB = nkb_of<MP, 4>(), MBI = MBS > 0 ? MBS : MB;
+                                         const unsigned char* corr, XW mel, XW out, int q0, int T) {
+    constexpr int R = 4, MB = (COUT + 15) / 16, NKB = nkb_of<MP, 4>();
     using CH = Chunks<(NQ + 15) / 16, NT>;
-    constexpr int N = R * MBI * CH::NCH;
+    constexpr int N = R * MB * CH::NCH;
     const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
 #pragma unroll 1
     for (int item = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); item < N; item += blockDim.x >> 6) {
-        const int rg = item % (R * MBI), k = item / (R * MBI), ph = rg / MBI, mb = mb0 + rg - ph * MBI;
+        const int rg = item % (R * MB), k = item / (R * MB), ph = rg / MB, mb = rg - ph * MB;
         const int tile0 = CH::lo(k), nt = CH::lo(k + 1) - tile0, d0 = ph < 2 ? 0 : 1, co0 = mb * 16 + 4 * g;
         const u32x4* wp = Wp + (size_t)(ph * MB + mb) * NKB * 128 + lane;
         const unsigned char* bp = mel.p + (q0 + tile0 * 16 + li + d0 + 1 - mel.start) * RSI;
         const int qe = ph < 2 ? 0 : T - 1;
         u32x4 al[pd_of<MP, 4, 1, PDM>()][1][2];
         if (nt == CH::QHI)
-            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, 1, false, GO, PDM>(
-                wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, gout, corr, qe);
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM>(
+                wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
         else
-            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, 1, false, GO, PDM>(
-                wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, gout, corr, qe);
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM>(
+                wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
     }
 }
 
@@ -1212,93 +1208,6 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
     XSTAMP(0, 11);
 }
 
-// Split stage2 head (S2_HEAD_SPLIT): the fused head streams its whole weight
-// set (1.18 MB of hi / lo fragments: the composed input_conv o ConvT1 786 KB,
-// ResBlock1 393 KB) through one CU per 16-frame window - at ~60 GB/s of L2
-// per CU that alone is ~19 us of every round of windows, against ~6 us of
-// MFMA work.  Split in two launches, each workgroup streams less per frame:
-//   A (x3_ct1_kernel): the composed ConvT1 (+ leaky) for TFA frames and one
-//     of NSL slices of its output channels: 786 / NSL KB of weights per
-//     TFA-frame window; its rows go to global (Ut, the U1 row format);
-//   B (x3_rb1_kernel): ResBlock1 on TFB-frame windows of those rows (its
-//     393 KB per window), U1 out - the fused kernel's last two layers.
-// Same operation sequence per output as the fused head (bit-identical).
-template <class Cfg, int TFA, int NSL>
-struct Ct1Plan {
-    static constexpr int M = Cfg::M, MP = Cfg::MP, C1 = Cfg::C / 2;
-    static constexpr int RS_M = rs_for(MP), MEL_N = TFA + 6;  // frames f0 - 3 .. f0 + TFA + 2
-    static constexpr int MBS = C1 / 16 / NSL;                  // m-blocks per slice
-    static_assert(MBS * 16 * NSL == C1, "whole m-blocks per slice");
-    static constexpr int CORR_OFF = MEL_N * RS_M;
-    static constexpr int LDS_BYTES = CORR_OFF + 4 * 4 * C1;
-};
-template <class Cfg, bool TRANS, int TFA, int NSL>
-__global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_ct1_kernel(const float* __restrict__ mel, int T, VocX w,
-                                                                           unsigned char* __restrict__ Ut) {
-    using Pl = Ct1Plan<Cfg, TFA, NSL>;
-    constexpr int C1 = Pl::C1;
-    static_assert(4 * C1 <= Cfg::HW * 64, "one thread per edge term");
-    if (w.rclear && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 5) {  // as x3_head_kernel
-        if (threadIdx.x == 0) *reinterpret_cast<volatile int*>(w.rclear) = 0;
-        else if (w.rqueue) reinterpret_cast<volatile unsigned*>(w.rqueue)[threadIdx.x - 1] = 0u;
-    }
-    const int sl = blockIdx.x % NSL, b = blockIdx.y, f0 = (blockIdx.x / NSL) * TFA;
-    if (w.dT) {  // speculative launch: T was the capacity
-        T = dev_frames(w.dT, T);
-        if (f0 >= T) return;
-    }
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const XW melA{lds, f0 - 3};
-    unsigned char* corr = lds + Pl::CORR_OFF;
-    // ConvT1's input columns here are [f0, f0 + TFA)
-    const bool left = f0 == 0, right = T - 1 >= f0 && T - 1 < f0 + TFA;
-    gload_mel<TRANS, Pl::M, Pl::MP, Pl::RS_M, Pl::MEL_N, Cfg::HW * 64>(mel + (size_t)b * Pl::M * T, T, melA);
-    __syncthreads();
-    if (left || right) {
-        head_edge_terms_s2<Pl::M, Pl::MP, C1, Pl::RS_M>(w.hce, melA, T, left, right, corr);
-        __syncthreads();
-    }
-    xconvT1c<Pl::MP, C1, Cfg::NT_T1, Pl::RS_M, Pl::RS_M, TFA, Cfg::PDM, Pl::MBS, true>(
-        w.hc, w.hcb, (left || right) ? corr : nullptr, melA, melA, f0, T, sl * Pl::MBS,
-        Ut + (size_t)b * 4 * T * 4 * C1);
-}
-template <class Cfg, int TFB>
-struct Rb1Plan {
-    static constexpr int C1 = Cfg::C / 2, RS_1 = rs_for(C1);
-    static constexpr int H_N = 4 * TFB + 2, O_N = 4 * TFB;
-    static constexpr int CAP_U = rup16(H_N) + 4;  // u rows from 4 f0 - 4 (the conv1 tiles' read extent)
-    static constexpr int RA = H_N * RS_1;
-    static constexpr int LDS_BYTES = RA + CAP_U * RS_1;
-};
-template <class Cfg, int TFB>
-__global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_rb1_kernel(const unsigned char* __restrict__ Ut, int T,
-                                                                           VocX w, unsigned char* __restrict__ U1) {
-    using Pl = Rb1Plan<Cfg, TFB>;
-    constexpr int C1 = Pl::C1;
-    int wx, wy;
-    head_tile(wx, wy);
-    if (w.dT) {  // speculative launch: T was the capacity
-        T = dev_frames(w.dT, T);
-        if (wx * TFB >= T) return;
-    }
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int b = wy, f0 = wx * TFB;
-    const XW hw{lds, 4 * f0 - 1};
-    const XW uw{lds + Pl::RA, 4 * f0 - 4};
-    gload_rows<C1, Pl::RS_1, Pl::CAP_U, Cfg::HW * 64>(Ut + (size_t)b * 4 * T * 4 * C1, 4 * T, uw);
-    __syncthreads();
-    xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N, 1, 0, false, Cfg::PDM>(
-        w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1, 4 * T);
-    __syncthreads();
-    xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, 0, true, Cfg::PDM>(
-        w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T, nullptr, nullptr, U1 + (size_t)b * 4 * T * 4 * C1);
-}
-#ifndef S2_SPLIT_TFA  // split head tilings (A/B builds)
-#define S2_SPLIT_TFA 64
-#define S2_SPLIT_NSL 4
-#define S2_SPLIT_TFB 16
-#endif
-
 template <class Cfg>
 __global__ __launch_bounds__(Cfg::MW * 64, Cfg::MMIN) void x3_mid_kernel(const unsigned char* __restrict__ U1,
                                                                            int L1, VocX w,
@@ -1452,11 +1361,6 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         if ((rc = set_lds(x3_mid_kernel<Cfg>, MP::LDS_BYTES))) return rc;
         if ((rc = set_lds(x3_tail_kernel<Cfg>, TP::LDS_BYTES))) return rc;
         if constexpr (S2) {
-            using PA = Ct1Plan<CfgS2, S2_SPLIT_TFA, S2_SPLIT_NSL>;
-            using PB = Rb1Plan<CfgS2, S2_SPLIT_TFB>;
-            if ((rc = set_lds(x3_ct1_kernel<CfgS2, false, S2_SPLIT_TFA, S2_SPLIT_NSL>, PA::LDS_BYTES))) return rc;
-            if ((rc = set_lds(x3_ct1_kernel<CfgS2, true, S2_SPLIT_TFA, S2_SPLIT_NSL>, PA::LDS_BYTES))) return rc;
-            if ((rc = set_lds(x3_rb1_kernel<CfgS2, S2_SPLIT_TFB>, PB::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_head_kernel<CfgS2H24, false, true>, HP24::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_head_kernel<CfgS2H24, true, true>, HP24::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_mid_kernel<CfgS2Alt>, MPA::LDS_BYTES))) return rc;
@@ -1487,26 +1391,7 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     const dim3 hg(cdiv(T, Cfg::TF), B), hb(Cfg::HW * 64);
     bool wide = false;  // stage2, composed head, large grid: 24-frame windows
     if constexpr (S2) wide = comp && (long)cdiv(T, Cfg::TF) * B >= kS2WideHeadWGs && !sw().s2_head_tf16;
-    // stage2, composed head: the split head (two launches, x3_ct1_kernel /
-    // x3_rb1_kernel) when a scratch buffer for ConvT1's rows is given
-    // (M2_S2_HEAD_SPLIT=0|1 forces it off / on)
-    const bool split = S2 && comp && w.scratch && sw().s2_head_split > 0;
-    if (split) {
-        if constexpr (S2) {
-            using PA = Ct1Plan<CfgS2, S2_SPLIT_TFA, S2_SPLIT_NSL>;
-            using PB = Rb1Plan<CfgS2, S2_SPLIT_TFB>;
-            auto* ut = static_cast<unsigned char*>(w.scratch);
-            const dim3 ga(cdiv(T, S2_SPLIT_TFA) * S2_SPLIT_NSL, B), gb(cdiv(T, S2_SPLIT_TFB), B);
-            if (trans)
-                hipLaunchKernelGGL((x3_ct1_kernel<CfgS2, true, S2_SPLIT_TFA, S2_SPLIT_NSL>), ga, hb, PA::LDS_BYTES, st,
-                                   mel, T, w, ut);
-            else
-                hipLaunchKernelGGL((x3_ct1_kernel<CfgS2, false, S2_SPLIT_TFA, S2_SPLIT_NSL>), ga, hb, PA::LDS_BYTES, st,
-                                   mel, T, w, ut);
-            M2_LAUNCHED("x3_ct1_kernel");
-            hipLaunchKernelGGL((x3_rb1_kernel<CfgS2, S2_SPLIT_TFB>), gb, hb, PB::LDS_BYTES, st, ut, T, w, u1);
-        }
-    } else if (wide) {
+    if (wide) {
         if constexpr (S2) {
             const dim3 hg24(cdiv(T, CfgS2H24::TF), B);
             if (trans)

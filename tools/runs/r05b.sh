@@ -1,3 +1,4 @@
+# (run at commit f29dcf2, where the split head existed behind M2_S2_HEAD_SPLIT)
 # Round 5: the split stage2 head (M2_S2_HEAD_SPLIT) - parity, in-process A/B
 # on the configs[3] share (B=8 S=100), B=64, long form, and a B=8 kernel trace.
 set -u
