@@ -51,7 +51,8 @@ def main():
     import bench
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    m = bench.fixture_model(bench.STAGE2, dev)
+    import os
+    m = bench.fixture_model(bench.STAGE1 if os.environ.get("M2_TRACE_STAGE") == "s1" else bench.STAGE2, dev)
     g = torch.Generator().manual_seed(2024)
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     S = int(sys.argv[3]) if len(sys.argv) > 3 else 100
