@@ -103,8 +103,9 @@ constexpr int pd_of() {
 // TB: tap k's rows start at tb[k] (this lane's row and lane-group chunk, the
 // plane swizzle applied) instead of bp + k*STEP*RSI - the phase-planar
 // layouts of the head.
+// BP: see below.
 template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE, bool TB = false,
-          int PDM = 4>
+          int PDM = 4, bool BP = false>
 __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
                                        const unsigned char* xr, f32x4 (&acc)[NMB][NT],
                                        u32x4 (&a)[pd_of<CIN, NTAP, NMB, PDM>()][NMB][2], const u32x4* wp_next,
@@ -140,34 +141,50 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
             a[kb][m][0] = wp[m * WS + kb * 128];
             a[kb][m][1] = wp[m * WS + kb * 128 + 64];
         }
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-        const unsigned char* b0;
+    auto bbase = [&](int kb) {
         if constexpr (TB) {
             static_assert(NOCT >= 4 && !XR, "tap bases: whole octet rows only");
-            b0 = tb[kb / (NOCT / 4)] + (kb % (NOCT / 4)) * 64;  // tb: the lane group's chunk included
+            return tb[kb / (NOCT / 4)] + (kb % (NOCT / 4)) * 64;  // tb: the lane group's chunk included
         } else {
-            b0 = kb == NKB - 1 ? b_last : bl + koff(kb);
+            return kb == NKB - 1 ? b_last : bl + koff(kb);
         }
-        u32x4 bh[NT], blo[NT];
+    };
+    // BP: k-block kb + 1's B fragments are read from LDS before k-block kb's
+    // MFMAs are issued (two register buffers, 8 NT more VGPRs), so their LDS
+    // latency hides behind the MFMAs instead of sitting before each k-block's
+    // first.  Taken where it measured faster (the stage2 head, see CfgS2)
+    constexpr int NB = BP ? 2 : 1;
+    u32x4 bh[NB][NT], blo[NB][NT];
+    auto bread = [&](int kb, int q) {
+        const unsigned char* b0 = bbase(kb);
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            bh[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI);
-            blo[n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
+            bh[q][n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI);
+            blo[q][n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
+        }
+    };
+    if constexpr (BP) bread(0, 0);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        const int q = BP ? (kb & 1) : 0;
+        if constexpr (BP) {
+            if (kb + 1 < NKB) bread(kb + 1, (kb + 1) & 1);
+        } else {
+            bread(kb, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 0; m < NMB; ++m)
 #pragma unroll
-            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], bh[n], acc[m][n]);
+            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], bh[q][n], acc[m][n]);
 #pragma unroll
         for (int m = 0; m < NMB; ++m)
 #pragma unroll
-            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], blo[n], acc[m][n]);
+            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], blo[q][n], acc[m][n]);
 #pragma unroll
         for (int m = 0; m < NMB; ++m)
 #pragma unroll
-            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][1], bh[n], acc[m][n]);
+            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][1], bh[q][n], acc[m][n]);
         if (kb + PD < NKB) {
 #pragma unroll
             for (int m = 0; m < NMB; ++m) {
@@ -246,7 +263,7 @@ constexpr bool kFold = res_fold_channels(C);
 // corr (the composed stage2 head): per-(phase, channel) terms subtracted from
 // the outputs of input column qe (an utterance edge), before the activation.
 template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int ACT, bool RES, bool XR, int RR,
-          int JMAX, int NMB, bool PRE, bool GO = false, int PDM = 4>
+          int JMAX, int NMB, bool PRE, bool GO = false, int PDM = 4, bool BP = false>
 __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
                                          const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
                                          int ph, int tile0, int L, u32x4 (&a)[pd_of<CIN, NTAP, NMB, PDM>()][NMB][2],
@@ -262,7 +279,7 @@ __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const flo
 #pragma unroll
         for (int n = 0; n < NTT; ++n) acc[m][n] = bv;
     }
-    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR, NMB, WS, PRE, false, PDM>(wp, bp, xr, acc, a, wp_next);
+    mma_x3<CIN, NTAP, STEP, RSI, NTT, XR, NMB, WS, PRE, false, PDM, BP>(wp, bp, xr, acc, a, wp_next);
     const bool edge = (p0 + tile0 * 16) * RR < 0 || (p0 + (tile0 + NTT) * 16) * RR > L;
     const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
     if (corr) {  // wave-uniform
@@ -340,7 +357,7 @@ struct ConvTItems {
 // 8/16 channels, read back in the epilogue otherwise.
 // GO: store the output tiles to global rows (gout) instead of `out`.
 template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS, int NMB = 1, int ONE = 0,
-          bool GO = false, int PDM = 4>
+          bool GO = false, int PDM = 4, bool BP = false>
 __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
                                        int a0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr,
                                        unsigned char* gout = nullptr) {
@@ -366,10 +383,10 @@ __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float
             else return al;
         }();
         if (nt == CH::QHI)
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO, PDM>(
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QHI, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO, PDM, BP>(
                 wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next, gout);
         else
-            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO, PDM>(
+            run_item<CIN, COUT, 3, 1, RSI, RSO, CH::QLO, ACT, RES && !FOLD, FOLD, 1, NPOS, NMB, PRE, GO, PDM, BP>(
                 wp, bias, bp, xr, out, co0, a0, 0, tile0, L, a, wp_next, gout);
     };
     if constexpr (ONE) {
@@ -425,7 +442,7 @@ __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float
 // The composed input_conv o ConvT1 on the generic item path (the stage2
 // head): head_convT1c_planar's layer over (phase, m-block, chunk) items, 4
 // mel taps (frames q + d0 + 1 - k), per-phase bias, edge terms from `corr`.
-template <int MP, int COUT, int NT, int RSI, int RSO, int NQ, int PDM = 4>
+template <int MP, int COUT, int NT, int RSI, int RSO, int NQ, int PDM = 4, bool BP = false>
 __device__ __forceinline__ void xconvT1c(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
                                          const unsigned char* corr, XW mel, XW out, int q0, int T) {
     constexpr int R = 4, MB = (COUT + 15) / 16, NKB = nkb_of<MP, 4>();
@@ -441,10 +458,10 @@ __device__ __forceinline__ void xconvT1c(const u32x4* __restrict__ Wp, const flo
         const int qe = ph < 2 ? 0 : T - 1;
         u32x4 al[pd_of<MP, 4, 1, PDM>()][1][2];
         if (nt == CH::QHI)
-            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM>(
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QHI, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM, BP>(
                 wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
         else
-            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM>(
+            run_item<MP, COUT, 4, -1, RSI, RSO, CH::QLO, ACT_LEAKY, false, false, R, NQ, 1, false, false, PDM, BP>(
                 wp, bias + ph * COUT, bp, nullptr, out, co0, q0, ph, tile0, 4 * T, al, nullptr, nullptr, corr, qe);
     }
 }
@@ -879,6 +896,9 @@ struct CfgS1 {
 #ifndef X3S2_HW  // stage2 head waves per workgroup (tiling experiments)
 #define X3S2_HW 8
 #endif
+#ifndef X3S2_HBP  // stage2 head: B-fragment reads one k-block ahead (CfgS2::HBP)
+#define X3S2_HBP 1
+#endif
 #ifndef X3S2_PDM  // stage2 weight-fragment k-blocks in flight per item (mma_x3)
 #define X3S2_PDM 4
 #endif
@@ -897,6 +917,12 @@ struct CfgS2 {
     // the stage2 head and mid are not bound by the latency of their weight
     // stream
     static constexpr int PDM = X3S2_PDM;
+    // head B fragments one k-block ahead (mma_x3 BP; 116 -> 156 VGPRs, one
+    // workgroup per CU either way): head 26.5 -> 25.0 us at 8x500; in the mid
+    // kernels it measured slower (24.0 -> 26.0 us at 8x500, 186 -> 212 us at
+    // 16x2600: 4 -> 3 waves per SIMD), in the 16-wave H24 head level (172 ->
+    // 175 us, spills) - profiles/r05/r05g_bpipe_ab.txt
+    static constexpr bool HBP = X3S2_HBP;
 };
 // Stage2 mid / tail tilings for small grids (run<CfgS2> picks per call): at
 // B=8, T=500 the default windows make 576 mid workgroups (1.1 rounds of 512
@@ -920,6 +946,7 @@ constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
 struct CfgS2H24 : CfgS2 {
     static constexpr int TF = 24, HW = 16;
     static constexpr int PDM = 4;  // 16 waves: 128 VGPRs per wave
+    static constexpr bool HBP = false;
 };
 constexpr long kS2WideHeadWGs = 1024;
 
@@ -1050,17 +1077,17 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         XSTAMP(0, 2);
         XSTAMP(0, 3);
         XSTAMP(0, 4);
-        xconvT1c<MP, C1, Cfg::NT_T1, Pl::RS_M, Pl::RS_1, Pl::NQ, Cfg::PDM>(w.hc, w.hcb, (left || right) ? corr : nullptr, melA,
+        xconvT1c<MP, C1, Cfg::NT_T1, Pl::RS_M, Pl::RS_1, Pl::NQ, Cfg::PDM, Cfg::HBP>(w.hc, w.hcb, (left || right) ? corr : nullptr, melA,
                                                               uw, f0 - 1, T);
         XSTAMP(0, 5);
         __syncthreads();
         XSTAMP(0, 6);
-        xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N, 1, 0, false, Cfg::PDM>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1,
+        xconv3<C1, C1, Cfg::NT_R1, ACT_LEAKY, false, Pl::RS_1, Pl::RS_1, Pl::H_N, 1, 0, false, Cfg::PDM, Cfg::HBP>(w.w1[0], w.b1[0], uw, hw, 4 * f0 - 1,
                                                                                  4 * T);
         XSTAMP(0, 7);
         __syncthreads();
         XSTAMP(0, 8);
-        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, 0, true, Cfg::PDM>(
+        xconv3<C1, C1, Cfg::NT_R1, ACT_NONE, true, Pl::RS_1, Pl::RS_1, Pl::O_N, 1, 0, true, Cfg::PDM, Cfg::HBP>(
             w.w2[0], w.b2[0], hw, uw, 4 * f0, 4 * T, nullptr, nullptr, U1 + (size_t)b * 4 * T * 4 * C1);
         XSTAMP(0, 9);
         return;
