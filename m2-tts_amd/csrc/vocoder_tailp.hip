@@ -632,6 +632,9 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
     // rotation r per co-resident workgroup, tools/probe/simd_map.hip — gave
     // classes of 18/21/16/12 MFMAs instead of 18/24/16/9 and measured the same:
     // the step is latency-bound, not bound by one SIMD's MFMA pipe.)
+    if (sw().tailr)  // the register-hand-off form: its units and biases follow these
+        return launch_vocoder_tailr(U2, L2, B, W + (size_t)(tp::kUnits + tp::kOutcUnits) * 128,
+                                    bias + tp::kBiasFloats, audio, rflag, st, dT, rd);
     const bool seven = sw().tailp_seven;
     return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd)
                  : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd);
@@ -742,7 +745,7 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
     const int cper[tp::kLayers] = {16, 16, 16, 8, 8, 8, 1};
     for (int l = 0; l < tp::kLayers; ++l)
         for (int R = 0; R < nrows[l]; ++R) (*bout)[l * 32 + R] = bsrc[l][tp::prow(l, R) % cper[l]];
-    return pack_outc(s, wout, bout, range_ok);
+    return pack_outc(s, wout, bout, range_ok) && pack_tailr(s, wout, bout, range_ok);
 }
 
 // The composed ResBlock4-conv2 + output_conv layer (outc_role), in double:
@@ -751,8 +754,17 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
 // Wo[c][d] b2[c]; on the 4-phase columns (row p = output phase, input row
 // p2*8 + c at column q + dq).  Edge terms: the y the composed form sees at
 // t = -1 is b2 + W2[.][.][2] h[., 0], at t = L4 it is b2 + W2[.][.][0] h[., L4-1].
-bool pack_outc(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
-    double dh[4][3][32] = {}, dx[4][3][32] = {};
+namespace {
+// The composed layer's dense matrices on the 4-phase columns (dh on ResBlock4's
+// intermediate h, dx on ConvT4's output x: [output phase][dq + 1][input row]),
+// its bias and the edge terms vL[8], vR[8], kL, kR.
+struct OutcDense {
+    double dh[4][3][32] = {}, dx[4][3][32] = {}, bo = 0.0, corr[18] = {};
+};
+OutcDense outc_dense(const TailpSrc& s) {
+    OutcDense o;
+    auto& dh = o.dh;
+    auto& dx = o.dx;
     auto wo = [&](int c, int k) { return (double)s.wo[c * 3 + k]; };
     auto w2 = [&](int c, int ci, int k) { return (double)s.w42[(c * 8 + ci) * 3 + k]; };
     for (int p = 0; p < 4; ++p)
@@ -766,6 +778,32 @@ bool pack_outc(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float
                         dh[p][qh + 1][(th - 4 * qh) * 8 + ci] += wo(c, d + 1) * w2(c, ci, e + 1);
                     }
             }
+    double bo = s.bo[0], kl = 0.0, kr = 0.0;
+    for (int c = 0; c < 8; ++c) {
+        for (int k = 0; k < 3; ++k) bo += wo(c, k) * s.b42[c];
+        kl += wo(c, 0) * s.b42[c];
+        kr += wo(c, 2) * s.b42[c];
+    }
+    o.bo = bo;
+    for (int ci = 0; ci < 8; ++ci) {
+        double vl = 0.0, vr = 0.0;
+        for (int c = 0; c < 8; ++c) {
+            vl += wo(c, 0) * w2(c, ci, 2);
+            vr += wo(c, 2) * w2(c, ci, 0);
+        }
+        o.corr[ci] = vl;
+        o.corr[8 + ci] = vr;
+    }
+    o.corr[16] = kl;
+    o.corr[17] = kr;
+    return o;
+}
+}  // namespace
+
+bool pack_outc(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
+    const OutcDense o = outc_dense(s);
+    const auto& dh = o.dh;
+    const auto& dx = o.dx;
     // every non-zero on a slot (fragments 0, 1: h; 2, 3: x)
     for (int p = 0; p < 4; ++p)
         for (int dq = -1; dq <= 1; ++dq)
@@ -791,24 +829,71 @@ bool pack_outc(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float
                 put_split(*wout, (((size_t)(tp::kOutcUnit0 + f) * 2) * 64 + lane) * 8 + e, (float)v, range_ok);
             }
         }
-    double bo = s.bo[0], kl = 0.0, kr = 0.0;
-    for (int c = 0; c < 8; ++c) {
-        for (int k = 0; k < 3; ++k) bo += wo(c, k) * s.b42[c];
-        kl += wo(c, 0) * s.b42[c];
-        kr += wo(c, 2) * s.b42[c];
-    }
-    for (int r = 0; r < 4; ++r) (*bout)[tp::kOutcBias + r] = (float)bo;
-    for (int ci = 0; ci < 8; ++ci) {
-        double vl = 0.0, vr = 0.0;
-        for (int c = 0; c < 8; ++c) {
-            vl += wo(c, 0) * w2(c, ci, 2);
-            vr += wo(c, 2) * w2(c, ci, 0);
+    for (int r = 0; r < 4; ++r) (*bout)[tp::kOutcBias + r] = (float)o.bo;
+    for (int i = 0; i < 18; ++i) (*bout)[tp::kOutcCorr + i] = (float)o.corr[i];
+    return true;
+}
+
+// The register-hand-off tail's units (tr:: slot tables), appended to wout /
+// bout.  Same dense matrices, other slots; every non-zero must sit on a slot
+// of its row's m-block.
+bool pack_tailr(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
+    Dense d[5];
+    dense_convT2(d[0], s.wt3, 1, 32, 16);
+    dense_conv3(d[1], s.w31, 2, 16, 16);
+    dense_conv3(d[2], s.w32, 2, 16, 16);
+    dense_convT2(d[3], s.wt4, 2, 16, 8);
+    dense_conv3(d[4], s.w41, 4, 8, 8);
+    const OutcDense o = outc_dense(s);
+    auto D = [&](int l, int src, int row, int dq, int in) -> double {
+        if (l < 5) return d[l].at(row, dq, in);
+        return (src ? o.dx : o.dh)[row][dq + 1][in];
+    };
+    for (int l = 0; l < tr::kLayers; ++l)
+        for (int R = 0; R < 16 * tr::nmb(l); ++R) {
+            const int row = tr::rrow(l, R), mb = R / 16;
+            if (row < 0) continue;
+            for (int src = 0; src < (l == 5 ? 2 : 1); ++src)
+                for (int dq = -1; dq <= 1; ++dq)
+                    for (int in = 0; in < 32; ++in) {
+                        if (D(l, src, row, dq, in) == 0.0) continue;
+                        bool found = false;
+                        for (int kb = 0; kb < tr::nkbm(l, mb); ++kb)
+                            for (int g = 0; g < 4; ++g) {
+                                const tr::Slot sl = tr::fslot(l, tr::frag(l, mb, kb), g);
+                                found = found || (sl.src == src && sl.dq == dq && sl.oct == in / 8);
+                            }
+                        if (!found) return false;
+                    }
         }
-        (*bout)[tp::kOutcCorr + ci] = (float)vl;
-        (*bout)[tp::kOutcCorr + 8 + ci] = (float)vr;
-    }
-    (*bout)[tp::kOutcCorr + 16] = (float)kl;
-    (*bout)[tp::kOutcCorr + 17] = (float)kr;
+    const size_t base = wout->size();
+    wout->resize(base + (size_t)tr::kUnits * 2 * 64 * 8, 0);
+    for (int l = 0; l < tr::kLayers; ++l)
+        for (int mb = 0; mb < tr::nmb(l); ++mb)
+            for (int kb = 0; kb < tr::nkbm(l, mb); ++kb) {
+                const int u = tr::unit(l, mb, kb);
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int row = tr::rrow(l, mb * 16 + (lane & 15)), g = lane >> 4;
+                    const tr::Slot sl = tr::fslot(l, tr::frag(l, mb, kb), g);
+                    bool dup = sl.oct < 0;  // an (src, dq, octet) the m-block already reads gets zeros
+                    for (int j = 0; !dup && j < kb * 4 + g; ++j) {
+                        const tr::Slot e = tr::fslot(l, tr::frag(l, mb, j / 4), j % 4);
+                        dup = e.src == sl.src && e.dq == sl.dq && e.oct == sl.oct;
+                    }
+                    for (int e = 0; e < 8; ++e) {
+                        const double v = row >= 0 && !dup ? D(l, sl.src, row, sl.dq, 8 * sl.oct + e) : 0.0;
+                        put_split(*wout, base + (((size_t)u * 2) * 64 + lane) * 8 + e, (float)v, range_ok);
+                    }
+                }
+            }
+    const size_t b0 = bout->size();
+    bout->resize(b0 + tr::kBiasFloats, 0.f);
+    const float* bsrc[5] = {s.bt3, s.b31, s.b32, s.bt4, s.b41};
+    const int cper[5] = {16, 16, 16, 8, 8};
+    for (int l = 0; l < 5; ++l)
+        for (int R = 0; R < 32; ++R) (*bout)[b0 + l * 32 + R] = bsrc[l][tr::rrow(l, R) % cper[l]];
+    for (int R = 0; R < 4; ++R) (*bout)[b0 + 5 * 32 + R] = (float)o.bo;
+    for (int i = 0; i < 18; ++i) (*bout)[b0 + 6 * 32 + i] = (float)o.corr[i];
     return true;
 }
 
