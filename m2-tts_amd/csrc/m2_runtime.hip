@@ -79,7 +79,8 @@ void reload_switches() {
     const int tn = env_int("M2_TAILP_NCH", 0);
     s.tailp_nch = (tn == 21 || tn == 32 || tn == 48) ? tn : 0;
     s.tailp_seven = env_set("M2_TAILP_SEVEN");
-    s.tailr = env_on("M2_TAILR", false);
+    const int tr = env_int("M2_TAILR", 0);
+    s.tailr = tr >= 1 && tr <= 3 ? tr : 0;
     const int rn = env_int("M2_TAILR_NCH", 0);
     s.tailr_nch = rn > 0 && rn <= 256 ? rn : 0;
     s.tailp2_nch = env_int("M2_TAILP2_NCH", 0);

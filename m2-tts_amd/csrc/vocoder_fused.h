@@ -169,6 +169,19 @@ struct Slot {
     int dq, oct;
 };
 constexpr int kLayers = 7, kUnits = 22;
+// The composed ResBlock4-conv2 + output_conv layer (six-layer form): weight
+// units after the 22 of the seven-layer form, its bias (rows 0..3) and the
+// edge terms (vL[8], vR[8], kL, kR) after the seven layers' biases.
+constexpr int kOutcUnit0 = kUnits, kOutcUnits = 4, kOutcBias = kLayers * 32, kOutcCorr = kOutcBias + 32;
+constexpr int kBiasFloats = kOutcCorr + 32;
+// Fragment f, lane group g: 0, 1 on ring R5 (ResBlock4's intermediate h),
+// 2, 3 on ring R4 (ConvT4's output x); slots of f = 3 repeated in f = 2 carry
+// zero weights.
+constexpr Slot outc_slot(int f, int g) {
+    return f == 0 || f == 2 ? Slot{0, g}
+                            : (f == 1 ? (g < 2 ? Slot{-1, 2 + g} : Slot{1, g - 2})
+                                      : (g == 0 ? Slot{-1, 3} : (g == 1 ? Slot{1, 0} : Slot{0, g})));
+}
 constexpr int nmb(int l) { return l == 6 ? 1 : 2; }
 constexpr int nkb(int l) { return (l == 4 || l == 5) ? 1 : 2; }
 // ConvT4 (layer 3): output phases 1 and 2 read column q only (t3 = 2q, 2q + 1),
@@ -198,49 +211,6 @@ constexpr Slot fslot(int l, int f, int g) {
 constexpr Slot kslot(int l, int mb, int kb, int g) { return fslot(l, frag(l, mb, kb), g); }
 }  // namespace tp
 
-// Register-hand-off stage1 tail (vocoder_tailr.hip): the same six layers
-// (ConvT3, ResBlock3 conv1 / conv2, ConvT4, ResBlock4 conv1, the composed
-// ResBlock4-conv2 + output_conv) over the same 16-column chunks, with their
-// own slot tables: B fragments are built in registers by DPP row shifts of a
-// layer's output (one shift for all four lane groups wherever it can be), so
-// a fragment slot here is (source, dq, octet) with the octets in the order the
-// producing layer's register layout holds them.  src 1: ConvT4's output (x)
-// of the composed layer (src 0: its ResBlock4 intermediate h, or the layer's
-// only input); oct -1: a zero-weight slot.  rrow(l, R): the dense (phase,
-// channel) row MFMA row R computes (-1: none).
-namespace tr {
-struct Slot {
-    int src, dq, oct;
-};
-constexpr int kLayers = 6, kUnits = 21, kBiasFloats = 7 * 32;  // 6 layers' rows + the composed layer's edge terms
-constexpr int nmb(int l) { return l == 5 ? 1 : 2; }
-constexpr int nkbm(int l, int mb) { return l == 3 ? (mb == 0 ? 2 : 1) : (l == 4 ? 1 : (l == 5 ? 4 : 2)); }
-constexpr int unit(int l, int mb, int kb) {
-    return (l <= 2 ? 4 * l : (l == 3 ? 12 : (l == 4 ? 15 : 17))) + mb * nkbm(l, 0) + kb;
-}
-// ConvT3 / ResBlock3 convs: fragments 0, 1, 2 = columns q, q-1, q+1, all four
-// octets in order; ConvT3's phase 0 reads q, q-1 and phase 1 q+1, q; the
-// ResBlock3 convs' phase 0 q, q-1 and phase 1 q, q+1.  ConvT4: m-block 0 holds
-// phases 3, 0 (rows 0-7, 8-15), m-block 1 phases 1, 2; fragment 0 = column q,
-// fragment 1 = (q-1, phase 1 | q+1, phase 0) (m-block 0 only).  ResBlock4
-// conv1 and the composed layer read ConvT4's output in the lane-group orders
-// (3, 0, 1, 2) / (1, 2, 3, 0) and ResBlock4's intermediate in (2, 3, 0, 1).
-constexpr int frag(int l, int mb, int kb) {
-    return l == 0 ? (mb == 0 ? kb : (kb == 0 ? 2 : 0))
-                  : (l <= 2 ? (kb == 0 ? 0 : (mb == 0 ? 1 : 2)) : (l == 3 ? kb : (l == 4 ? mb : kb)));
-}
-constexpr Slot fslot(int l, int f, int g) {
-    if (l <= 2) return Slot{0, f == 0 ? 0 : (f == 1 ? -1 : 1), g};
-    if (l == 3) return f == 0 ? Slot{0, 0, g} : (g < 2 ? Slot{0, -1, 2 + g} : Slot{0, 1, g - 2});
-    if (l == 4)
-        return f == 0 ? (g == 0 ? Slot{0, -1, 3} : Slot{0, 0, g - 1}) : (g == 3 ? Slot{0, 1, 0} : Slot{0, 0, g + 1});
-    if (f == 0) return Slot{0, 0, (g + 2) & 3};
-    if (f == 1) return g < 2 ? Slot{0, -1, 2 + g} : Slot{0, 1, g - 2};
-    if (f == 2) return Slot{1, 0, (g + 3) & 3};
-    return g == 0 ? Slot{1, -1, 3} : (g == 1 ? Slot{1, 1, 0} : Slot{1, 0, -1});
-}
-constexpr int rrow(int l, int R) { return l == 3 ? (R < 8 ? 24 + R : R - 8) : (l == 5 ? (R < 4 ? R : -1) : R); }
-}  // namespace tr
 
 // Pipelined stage1 mid stage (vocoder_midp.hip): ConvT2 (layer 0), ResBlock2
 // conv1 / conv2 (layers 1, 2) in polyphase form over the columns q of U1, 8
@@ -280,10 +250,8 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>*
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                              int* rflag, hipStream_t st, const int32_t* dT = nullptr, const VocRedo& rd = VocRedo{});
 extern const char* const kVocTailpKernelName;
-// The register-hand-off form of the same tail (tr:: tables above): pack_tailp
-// appends its units and biases (launch_vocoder_tailp passes them on when
-// M2_TAILR is set).
-bool pack_tailr(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);
+// The same tail with three layers chained per wave (vocoder_tailr.hip, same
+// packed weights; launch_vocoder_tailp passes them on when M2_TAILR is set).
 int32_t launch_vocoder_tailr(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                              int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd);
 extern const char* const kVocTailrKernelName;

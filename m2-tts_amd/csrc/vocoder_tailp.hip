@@ -89,20 +89,6 @@ static_assert(lds_bytes(7) * 3 <= 160 * 1024, "three workgroups per CU");
 constexpr int NWAVES = 8;  // stamp buffer size (the larger variant)
 #endif
 
-// The composed ResBlock4-conv2 + output_conv layer (outc_role): weight units
-// after the 22 of the seven-layer form, its bias (rows 0..3) and the edge
-// terms (vL[8], vR[8], kL, kR) after the seven layers' biases.
-constexpr int kOutcUnit0 = kUnits, kOutcUnits = 4, kOutcBias = kLayers * 32, kOutcCorr = kOutcBias + 32;
-constexpr int kBiasFloats = kOutcCorr + 32;
-// Fragment f, lane group g: 0, 1 on ring R5 (ResBlock4's intermediate h),
-// 2, 3 on ring R4 (ConvT4's output x); slots of f = 3 repeated in f = 2 carry
-// zero weights.
-__host__ __device__ constexpr Slot outc_slot(int f, int g) {
-    return f == 0 || f == 2 ? Slot{0, g}
-                            : (f == 1 ? (g < 2 ? Slot{-1, 2 + g} : Slot{1, g - 2})
-                                      : (g == 0 ? Slot{-1, 3} : (g == 1 ? Slot{1, 0} : Slot{0, g})));
-}
-
 // Byte offset of (row, octet) in ring n's hi plane; row in [0, kRingRows[n]).
 __device__ __forceinline__ unsigned ring_at(int n, int row, int oct) {
     return kRingOff(n) + row * 64 + 16 * (oct ^ ((row >> 1) & 3));
@@ -632,9 +618,8 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
     // rotation r per co-resident workgroup, tools/probe/simd_map.hip — gave
     // classes of 18/21/16/12 MFMAs instead of 18/24/16/9 and measured the same:
     // the step is latency-bound, not bound by one SIMD's MFMA pipe.)
-    if (sw().tailr)  // the register-hand-off form: its units and biases follow these
-        return launch_vocoder_tailr(U2, L2, B, W + (size_t)(tp::kUnits + tp::kOutcUnits) * 128,
-                                    bias + tp::kBiasFloats, audio, rflag, st, dT, rd);
+    if (sw().tailr)  // three layers per wave (vocoder_tailr.hip)
+        return launch_vocoder_tailr(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
     const bool seven = sw().tailp_seven;
     return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd)
                  : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd);
@@ -745,7 +730,7 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<floa
     const int cper[tp::kLayers] = {16, 16, 16, 8, 8, 8, 1};
     for (int l = 0; l < tp::kLayers; ++l)
         for (int R = 0; R < nrows[l]; ++R) (*bout)[l * 32 + R] = bsrc[l][tp::prow(l, R) % cper[l]];
-    return pack_outc(s, wout, bout, range_ok) && pack_tailr(s, wout, bout, range_ok);
+    return pack_outc(s, wout, bout, range_ok);
 }
 
 // The composed ResBlock4-conv2 + output_conv layer (outc_role), in double:
@@ -831,69 +816,6 @@ bool pack_outc(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float
         }
     for (int r = 0; r < 4; ++r) (*bout)[tp::kOutcBias + r] = (float)o.bo;
     for (int i = 0; i < 18; ++i) (*bout)[tp::kOutcCorr + i] = (float)o.corr[i];
-    return true;
-}
-
-// The register-hand-off tail's units (tr:: slot tables), appended to wout /
-// bout.  Same dense matrices, other slots; every non-zero must sit on a slot
-// of its row's m-block.
-bool pack_tailr(const TailpSrc& s, std::vector<uint16_t>* wout, std::vector<float>* bout, bool* range_ok) {
-    Dense d[5];
-    dense_convT2(d[0], s.wt3, 1, 32, 16);
-    dense_conv3(d[1], s.w31, 2, 16, 16);
-    dense_conv3(d[2], s.w32, 2, 16, 16);
-    dense_convT2(d[3], s.wt4, 2, 16, 8);
-    dense_conv3(d[4], s.w41, 4, 8, 8);
-    const OutcDense o = outc_dense(s);
-    auto D = [&](int l, int src, int row, int dq, int in) -> double {
-        if (l < 5) return d[l].at(row, dq, in);
-        return (src ? o.dx : o.dh)[row][dq + 1][in];
-    };
-    for (int l = 0; l < tr::kLayers; ++l)
-        for (int R = 0; R < 16 * tr::nmb(l); ++R) {
-            const int row = tr::rrow(l, R), mb = R / 16;
-            if (row < 0) continue;
-            for (int src = 0; src < (l == 5 ? 2 : 1); ++src)
-                for (int dq = -1; dq <= 1; ++dq)
-                    for (int in = 0; in < 32; ++in) {
-                        if (D(l, src, row, dq, in) == 0.0) continue;
-                        bool found = false;
-                        for (int kb = 0; kb < tr::nkbm(l, mb); ++kb)
-                            for (int g = 0; g < 4; ++g) {
-                                const tr::Slot sl = tr::fslot(l, tr::frag(l, mb, kb), g);
-                                found = found || (sl.src == src && sl.dq == dq && sl.oct == in / 8);
-                            }
-                        if (!found) return false;
-                    }
-        }
-    const size_t base = wout->size();
-    wout->resize(base + (size_t)tr::kUnits * 2 * 64 * 8, 0);
-    for (int l = 0; l < tr::kLayers; ++l)
-        for (int mb = 0; mb < tr::nmb(l); ++mb)
-            for (int kb = 0; kb < tr::nkbm(l, mb); ++kb) {
-                const int u = tr::unit(l, mb, kb);
-                for (int lane = 0; lane < 64; ++lane) {
-                    const int row = tr::rrow(l, mb * 16 + (lane & 15)), g = lane >> 4;
-                    const tr::Slot sl = tr::fslot(l, tr::frag(l, mb, kb), g);
-                    bool dup = sl.oct < 0;  // an (src, dq, octet) the m-block already reads gets zeros
-                    for (int j = 0; !dup && j < kb * 4 + g; ++j) {
-                        const tr::Slot e = tr::fslot(l, tr::frag(l, mb, j / 4), j % 4);
-                        dup = e.src == sl.src && e.dq == sl.dq && e.oct == sl.oct;
-                    }
-                    for (int e = 0; e < 8; ++e) {
-                        const double v = row >= 0 && !dup ? D(l, sl.src, row, sl.dq, 8 * sl.oct + e) : 0.0;
-                        put_split(*wout, base + (((size_t)u * 2) * 64 + lane) * 8 + e, (float)v, range_ok);
-                    }
-                }
-            }
-    const size_t b0 = bout->size();
-    bout->resize(b0 + tr::kBiasFloats, 0.f);
-    const float* bsrc[5] = {s.bt3, s.b31, s.b32, s.bt4, s.b41};
-    const int cper[5] = {16, 16, 16, 8, 8};
-    for (int l = 0; l < 5; ++l)
-        for (int R = 0; R < 32; ++R) (*bout)[b0 + l * 32 + R] = bsrc[l][tr::rrow(l, R) % cper[l]];
-    for (int R = 0; R < 4; ++R) (*bout)[b0 + 5 * 32 + R] = (float)o.bo;
-    for (int i = 0; i < 18; ++i) (*bout)[b0 + 6 * 32 + i] = (float)o.corr[i];
     return true;
 }
 
