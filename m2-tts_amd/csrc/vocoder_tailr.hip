@@ -113,22 +113,25 @@ struct Layer {
         }
     }
 
-    // chunk k (ring slot J): columns x0 .. x0 + 15 of this layer's output
+    // B fragments of chunk k (ring slot J); RES: x too (slot NF)
+    struct Frags {
+        u32x4 h[NF + RES], l[NF + RES];
+    };
     template <int J>
-    __device__ __forceinline__ void work(unsigned char* lds, int x0, int L2, bool edge, const float* cp) const {
-        const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
-        u32x4 bh[NF], bl[NF];
+    __device__ __forceinline__ Frags load(const unsigned char* lds) const {
+        Frags F;
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-            bh[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J]);
-            bl[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J] + kPlane);
+            F.h[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J]);
+            F.l[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J] + kPlane);
         }
-        u32x4 xh, xl;
         if constexpr (RES) {
-            xh = *reinterpret_cast<const u32x4*>(lds + xadr[J]);
-            xl = *reinterpret_cast<const u32x4*>(lds + xadr[J] + kPlane);
+            F.h[NF] = *reinterpret_cast<const u32x4*>(lds + xadr[J]);
+            F.l[NF] = *reinterpret_cast<const u32x4*>(lds + xadr[J] + kPlane);
         }
-        f32x4 acc[2];
+        return F;
+    }
+    __device__ __forceinline__ void mma(const Frags& F, f32x4 (&acc)[2]) const {
 #pragma unroll
         for (int m = 0; m < 2; ++m) acc[m] = f32x4{bv[m][0], bv[m][1], bv[m][2], bv[m][3]};
 #pragma unroll
@@ -139,14 +142,21 @@ struct Layer {
                 for (int m = 0; m < 2; ++m)
                     if (kb < tp::nkbm(L, m)) {
                         const int f = tp::frag(L, m, kb);
-                        acc[m] = mfma_h(a[m][kb][pr == 2], pr == 1 ? bl[f] : bh[f], acc[m]);
+                        acc[m] = mfma_h(a[m][kb][pr == 2], pr == 1 ? F.l[f] : F.h[f], acc[m]);
                     }
         if constexpr (RES) {
 #pragma unroll
-            for (int m = 0; m < 2; ++m) acc[m] = mfma_h(aid[m], xh, acc[m]);
+            for (int m = 0; m < 2; ++m) acc[m] = mfma_h(aid[m], F.h[NF], acc[m]);
 #pragma unroll
-            for (int m = 0; m < 2; ++m) acc[m] = mfma_h(aid[m], xl, acc[m]);
+            for (int m = 0; m < 2; ++m) acc[m] = mfma_h(aid[m], F.l[NF], acc[m]);
         }
+    }
+    // the epilogue of chunk k (ring slot J): columns x0 .. x0 + 15 of this
+    // layer's output into ring R(L + 1)
+    template <int J>
+    __device__ __forceinline__ void store(unsigned char* lds, const f32x4 (&acc)[2], int x0, int L2, bool edge,
+                                          const float* cp) const {
+        const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
         auto epilogue = [&](auto zc) {
             constexpr bool ZERO = decltype(zc)::value;
             float v[2][4];
@@ -224,21 +234,29 @@ struct Outc {
             }
     }
 
+    struct Frags {
+        u32x4 h[4], l[4];
+    };
     template <int J>
-    __device__ __forceinline__ void work(unsigned char* lds, int x0, int L2, bool edge, float* __restrict__ arow,
-                                         int* rflag) const {
-        const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
-        u32x4 bh[4], bl[4];
+    __device__ __forceinline__ Frags load(const unsigned char* lds) const {
+        Frags F;
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            bh[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J]);
-            bl[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J] + kPlane);
+            F.h[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J]);
+            F.l[f] = *reinterpret_cast<const u32x4*>(lds + radr[f][J] + kPlane);
         }
-        f32x4 acc = f32x4{bv[0], bv[1], bv[2], bv[3]};
+        return F;
+    }
+    __device__ __forceinline__ void mma(const Frags& F, f32x4& acc) const {
+        acc = f32x4{bv[0], bv[1], bv[2], bv[3]};
 #pragma unroll
         for (int f = 0; f < 4; ++f)
 #pragma unroll
-            for (int pr = 0; pr < 3; ++pr) acc = mfma_h(a[f][pr == 2], pr == 1 ? bl[f] : bh[f], acc);
+            for (int pr = 0; pr < 3; ++pr) acc = mfma_h(a[f][pr == 2], pr == 1 ? F.l[f] : F.h[f], acc);
+    }
+    __device__ __forceinline__ void store(unsigned char* lds, const f32x4& acc, int x0, int L2, bool edge,
+                                          float* __restrict__ arow, int* rflag) const {
+        const int li = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
         const int x = x0 + li;
         float v[4] = {acc[0], acc[1], acc[2], acc[3]};
         if (edge && (x0 <= 0 || x0 + 16 >= L2)) {  // wave-uniform
@@ -308,20 +326,16 @@ struct Loader {
     }
 };
 
-// The step loop of role R of NW: step s = 3i + u computes chunk k = s - 2 - R
-// (ring slot k mod 3 = (u + 1 - R) mod 3, a compile-time index), then the
-// workgroup barrier; body(s, k, ic<u>, ic<slot>) with k in [-1, nch) or -2
-// (nothing to compute).  The last role's chunk nch - 1 is done in step
-// nch + NW - 1 + ... = nch + NW.
-template <int R, int NW, class Body>
+// The step loop: step s = 3i + u (u compile-time, so every ring slot is a
+// compile-time index), then the workgroup barrier; the last step is
+// nch + kSkew + 1 (the composed layer's chunk nch - 1).
+constexpr int kLast = 6;  // last step - nch
+template <class Body>
 __device__ __forceinline__ void run_steps(int nch, Body&& body) {
-    const int last = nch + NW;
+    const int last = nch + kLast;
     auto step = [&](int s, auto uc) {
-        constexpr int u = decltype(uc)::value;
         if (s <= last) {
-            int k = s - 2 - R;
-            if (k < -1 || k >= nch) k = -2;
-            body(s, k, uc, ic<(u + 4 - R) % 3>{});
+            body(s, uc);
             step_barrier();
         }
     };
@@ -333,89 +347,126 @@ __device__ __forceinline__ void run_steps(int nch, Body&& body) {
     }
 }
 
-// NW = 2.  Wave 0: ConvT3, ResBlock3 conv1, conv2 (+ x) of chunk s - 2 (its U2
-// columns stored by wave 1 in steps s - 2 and s - 1).  Wave 1: the loader,
-// ConvT4, ResBlock4 conv1 and the composed layer of chunk s - 3 (ring R3's
-// chunk written by wave 0 in step s - 1).
-// NW = 3.  Wave 0: ConvT3, conv1 (chunk s - 2); wave 1: conv2, ConvT4 (chunk
-// s - 3; rings R1 / R2 from wave 0); wave 2: the loader, ResBlock4 conv1 and
-// the composed layer (chunk s - 4; ring R4 from wave 1).  Layer l's chunk k
-// starts at column qa + 5 - l + 16 k.
-template <int NW>
-__device__ __forceinline__ void role(int w, unsigned char* lds, int qa, int L2, int nch, bool edge,
-                                     const u32x4* __restrict__ W, const float* __restrict__ bias,
-                                     const unsigned char* __restrict__ u2, float* __restrict__ arow, int* rflag) {
-    const float* cp = bias + tp::kOutcCorr;
-    if (w == 0) {
-        Layer<0> l0;
-        Layer<1> l1;
-        l0.init(W, bias);
-        l1.init(W, bias);
-        if constexpr (NW == 2) {
-            Layer<2> l2;
-            l2.init(W, bias);
-            run_steps<0, NW>(nch, [&](int, int k, auto, auto jc) {
-                constexpr int j = decltype(jc)::value;
-                if (k == -2) return;
-                l0.template work<j>(lds, qa + 5 + 16 * k, L2, edge, nullptr);
-                l1.template work<j>(lds, qa + 4 + 16 * k, L2, edge, nullptr);
-                l2.template work<j>(lds, qa + 3 + 16 * k, L2, edge, nullptr);
-            });
-        } else {
-            run_steps<0, NW>(nch, [&](int, int k, auto, auto jc) {
-                constexpr int j = decltype(jc)::value;
-                if (k == -2) return;
-                l0.template work<j>(lds, qa + 5 + 16 * k, L2, edge, nullptr);
-                l1.template work<j>(lds, qa + 4 + 16 * k, L2, edge, nullptr);
-            });
+// Skewed schedule: in step s each layer l works on its own chunk k_l (front:
+// ConvT3 s - 2, conv1 s - 3, conv2 s - 4; back: ConvT4 s - 5, ResBlock4 conv1
+// s - 6, the composed layer s - 7), whose inputs were all written in earlier
+// steps, so a wave's three layers are independent within the step: all their
+// fragment loads are issued first (before any store of the step: a ring slot
+// a later layer still reads for its previous chunk's last columns may be
+// rewritten in the same step, and LDS operations of one wave complete in
+// order), then the three MFMA chains (six accumulators), then the epilogues.
+// Layer l's chunk k starts at column qa + 5 - l + 16 k (the composed layer's
+// at qa + 16 k); ring slot = k mod 3 = (u + 3 - offset mod 3) mod 3.
+template <int OFF, int U>
+using slot_of = ic<(U + 3 * 3 - OFF) % 3>;
+
+__device__ __forceinline__ bool live(int k, int nch) { return k >= -1 && k < nch; }
+
+// Wave 0: ConvT3 (chunk s - 2; its U2 columns stored by wave 1 in steps s - 2,
+// s - 1), ResBlock3 conv1 (s - 3), conv2 (s - 4; ring R3 to wave 1).
+__device__ __forceinline__ void front_role(unsigned char* lds, int qa, int L2, int nch, bool edge,
+                                           const u32x4* __restrict__ W, const float* __restrict__ bias) {
+    Layer<0> l0;
+    Layer<1> l1;
+    Layer<2> l2;
+    l0.init(W, bias);
+    l1.init(W, bias);
+    l2.init(W, bias);
+    run_steps(nch, [&](int s, auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int j0 = slot_of<2, u>::value, j1 = slot_of<3, u>::value, j2 = slot_of<4, u>::value;
+        const int k0 = s - 2, k1 = s - 3, k2 = s - 4;
+        const bool a0 = live(k0, nch), a1 = live(k1, nch), a2 = live(k2, nch);
+        if (a0 && a1 && a2) {  // the steady state: all three
+            const auto F2 = l2.load<j2>(lds);
+            const auto F1 = l1.load<j1>(lds);
+            const auto F0 = l0.load<j0>(lds);
+            f32x4 c0[2], c1[2], c2[2];
+            l2.mma(F2, c2);
+            l1.mma(F1, c1);
+            l0.mma(F0, c0);
+            l2.store<j2>(lds, c2, qa + 3 + 16 * k2, L2, edge, nullptr);
+            l1.store<j1>(lds, c1, qa + 4 + 16 * k1, L2, edge, nullptr);
+            l0.store<j0>(lds, c0, qa + 5 + 16 * k0, L2, edge, nullptr);
+        } else {  // fill and drain: one layer at a time, loads before stores as above
+            f32x4 c[2];
+            const auto F2 = l2.load<j2>(lds);
+            const auto F1 = l1.load<j1>(lds);
+            const auto F0 = l0.load<j0>(lds);
+            if (a2) {
+                l2.mma(F2, c);
+                l2.store<j2>(lds, c, qa + 3 + 16 * k2, L2, edge, nullptr);
+            }
+            if (a1) {
+                l1.mma(F1, c);
+                l1.store<j1>(lds, c, qa + 4 + 16 * k1, L2, edge, nullptr);
+            }
+            if (a0) {
+                l0.mma(F0, c);
+                l0.store<j0>(lds, c, qa + 5 + 16 * k0, L2, edge, nullptr);
+            }
         }
-    } else if (NW == 3 && w == 1) {
-        Layer<2> l2;
-        Layer<3> l3;
-        l2.init(W, bias);
-        l3.init(W, bias);
-        run_steps<1, NW>(nch, [&](int, int k, auto, auto jc) {
-            constexpr int j = decltype(jc)::value;
-            if (k == -2) return;
-            l2.template work<j>(lds, qa + 3 + 16 * k, L2, edge, nullptr);
-            l3.template work<j>(lds, qa + 2 + 16 * k, L2, edge, nullptr);
-        });
-    } else {
-        Loader ld;
-        ld.init(u2, qa, L2, nch);
-        Layer<4> l4;
-        Outc oc;
-        l4.init(W, bias);
-        oc.init(W, bias);
-        if constexpr (NW == 2) {
-            Layer<3> l3;
-            l3.init(W, bias);
-            run_steps<1, NW>(nch, [&](int s, int k, auto uc, auto jc) {
-                constexpr int u = decltype(uc)::value, j = decltype(jc)::value;
-                ld.template step<u>(lds, s);
-                if (k == -2) return;
-                l3.template work<j>(lds, qa + 2 + 16 * k, L2, edge, nullptr);
-                l4.template work<j>(lds, qa + 1 + 16 * k, L2, edge, cp);
-                if (k >= 0) oc.template work<j>(lds, qa + 16 * k, L2, edge, arow, rflag);  // chunk -1 feeds nothing
-            });
-        } else {
-            run_steps<2, NW>(nch, [&](int s, int k, auto uc, auto jc) {
-                constexpr int u = decltype(uc)::value, j = decltype(jc)::value;
-                ld.template step<u>(lds, s);
-                if (k == -2) return;
-                l4.template work<j>(lds, qa + 1 + 16 * k, L2, edge, cp);
-                if (k >= 0) oc.template work<j>(lds, qa + 16 * k, L2, edge, arow, rflag);
-            });
-        }
-    }
+    });
 }
 
-template <int NW>
-__global__ __launch_bounds__(NW * 64, NW == 2 ? 2 : 3) void tailr_kernel(const unsigned char* __restrict__ U2, int L2,
-                                                                          int nch, const u32x4* __restrict__ W,
-                                                                          const float* __restrict__ bias,
-                                                                          float* __restrict__ audio, int* rflag,
-                                                                          const int32_t* __restrict__ dT, VocRedo rd) {
+// Wave 1: the loader (U2 chunk s - 1), ConvT4 (chunk s - 5: ring R3's chunk
+// written by wave 0 in step s - 1), ResBlock4 conv1 (s - 6), the composed
+// layer (s - 7; chunk -1 feeds nothing).
+__device__ __forceinline__ void back_role(unsigned char* lds, int qa, int L2, int nch, bool edge,
+                                          const u32x4* __restrict__ W, const float* __restrict__ bias,
+                                          const unsigned char* __restrict__ u2, float* __restrict__ arow,
+                                          int* rflag) {
+    Loader ld;
+    ld.init(u2, qa, L2, nch);
+    Layer<3> l3;
+    Layer<4> l4;
+    Outc oc;
+    l3.init(W, bias);
+    l4.init(W, bias);
+    oc.init(W, bias);
+    const float* cp = bias + tp::kOutcCorr;
+    run_steps(nch, [&](int s, auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int j3 = slot_of<5, u>::value, j4 = slot_of<6, u>::value, j5 = slot_of<7, u>::value;
+        const int k3 = s - 5, k4 = s - 6, k5 = s - 7;
+        const bool a3 = live(k3, nch), a4 = live(k4, nch), a5 = k5 >= 0 && k5 < nch;
+        // all loads of the step first (the composed layer's x reads ring R4's
+        // slot ConvT4 rewrites in this step), then the loader's store
+        const auto F5 = oc.load<j5>(lds);
+        const auto F4 = l4.load<j4>(lds);
+        const auto F3 = l3.load<j3>(lds);
+        ld.template step<u>(lds, s);
+        if (a3 && a4 && a5) {
+            f32x4 c3[2], c4[2], c5;
+            oc.mma(F5, c5);
+            l4.mma(F4, c4);
+            l3.mma(F3, c3);
+            // ResBlock4 conv1 before the composed layer's epilogue: its edge terms
+            oc.store(lds, c5, qa + 16 * k5, L2, edge, arow, rflag);
+            l4.store<j4>(lds, c4, qa + 1 + 16 * k4, L2, edge, cp);
+            l3.store<j3>(lds, c3, qa + 2 + 16 * k3, L2, edge, nullptr);
+        } else {
+            f32x4 c[2], c5;
+            if (a5) {
+                oc.mma(F5, c5);
+                oc.store(lds, c5, qa + 16 * k5, L2, edge, arow, rflag);
+            }
+            if (a4) {
+                l4.mma(F4, c);
+                l4.store<j4>(lds, c, qa + 1 + 16 * k4, L2, edge, cp);
+            }
+            if (a3) {
+                l3.mma(F3, c);
+                l3.store<j3>(lds, c, qa + 2 + 16 * k3, L2, edge, nullptr);
+            }
+        }
+    });
+}
+
+__global__ __launch_bounds__(128, 2) void tailr_kernel(const unsigned char* __restrict__ U2, int L2, int nch,
+                                                        const u32x4* __restrict__ W, const float* __restrict__ bias,
+                                                        float* __restrict__ audio, int* rflag,
+                                                        const int32_t* __restrict__ dT, VocRedo rd) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, qa = blockIdx.x * 16 * nch;
     if (dT) {  // speculative launch: L2 was the capacity
@@ -427,7 +478,8 @@ __global__ __launch_bounds__(NW * 64, NW == 2 ? 2 : 3) void tailr_kernel(const u
     float* arow = audio + (size_t)b * 4 * L2;
     int* const lflag = reinterpret_cast<int*>(lds + kFlagOff);
     if (threadIdx.x == 0) *lflag = 0;  // before the first audio store: the step barriers order it
-    role<NW>(w, lds, qa, L2, nch, edge, W, bias, U2 + (size_t)b * L2 * 128, arow, rflag);
+    if (w == 0) front_role(lds, qa, L2, nch, edge, W, bias);
+    else back_role(lds, qa, L2, nch, edge, W, bias, U2 + (size_t)b * L2 * 128, arow, rflag);
     if (rd.rw) {  // range policy "fallback": this strip's audio again in fp32 if it is not finite
         __syncthreads();
         if (*lflag)
@@ -436,37 +488,30 @@ __global__ __launch_bounds__(NW * 64, NW == 2 ? 2 : 3) void tailr_kernel(const u
     }
 }
 
-template <int NW>
-static int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
-                      hipStream_t st, const int32_t* dT, const VocRedo& rd) {
-    static bool attr = false;
-    if (!attr) {
-        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailr_kernel<NW>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
-        attr = true;
-    }
-    // Strip length: about one round of four workgroups per CU (stage1 B = 32,
-    // L2 = 8000: 32 strips of 16 chunks per utterance), at least 8 chunks
-    // (each strip pays NW + 1 steps of pipeline fill).
-    const int chunks = cdiv(L2, 16);
-    int nch = sw().tailr_nch;
-    if (!nch) nch = std::max(8, cdiv(chunks, std::max(1, 4 * 256 / B)));
-    hipLaunchKernelGGL(tailr_kernel<NW>, dim3(cdiv(chunks, nch), B), dim3(NW * 64), kLdsBytes, st,
-                       static_cast<const unsigned char*>(U2), L2, nch, W, bias, audio, rflag, dT, rd);
-    M2_LAUNCHED("tailr_kernel");
-    return M2_OK;
-}
-
 }  // namespace tr
 
 const char* const kVocTailrKernelName =
-    "tailr_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, layers chained per wave)";
+    "tailr_kernel (ConvT3 + ResBlock3 + ConvT4 + ResBlock4 + output_conv, skewed layers per wave)";
 
 int32_t launch_vocoder_tailr(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                              int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd) {
     if (B == 0 || L2 == 0) return M2_OK;
-    return sw().tailr == 3 ? tr::launch<3>(U2, L2, B, W, bias, audio, rflag, st, dT, rd)
-                           : tr::launch<2>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+    static bool attr = false;
+    if (!attr) {
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tr::tailr_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, tr::kLdsBytes));
+        attr = true;
+    }
+    // Strip length: about one round of four workgroups per CU (stage1 B = 32,
+    // L2 = 8000: 32 strips of 16 chunks per utterance), at least 8 chunks
+    // (each strip pays 7 steps of pipeline fill and drain).
+    const int chunks = cdiv(L2, 16);
+    int nch = sw().tailr_nch;
+    if (!nch) nch = std::max(8, cdiv(chunks, std::max(1, 4 * 256 / B)));
+    hipLaunchKernelGGL(tr::tailr_kernel, dim3(cdiv(chunks, nch), B), dim3(128), tr::kLdsBytes, st,
+                       static_cast<const unsigned char*>(U2), L2, nch, W, bias, audio, rflag, dT, rd);
+    M2_LAUNCHED("tailr_kernel");
+    return M2_OK;
 }
 
 }  // namespace m2

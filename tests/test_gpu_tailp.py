@@ -58,12 +58,11 @@ def test_tailp_outc_vs_seven_layers(gpu, monkeypatch, B, T):
 
 
 
-# ---- layers chained per wave (vocoder_tailr.hip, M2_TAILR=1: two waves, 3: three) --
+# ---- three layers per wave, skewed (vocoder_tailr.hip, M2_TAILR=1) ---------------
 
-@pytest.mark.parametrize("waves", ["1", "3"])
 @pytest.mark.parametrize("B,T", [(3, 1), (2, 2), (2, 7), (3, 61), (1, 137)])
-def test_tailr_vs_oracle(gpu, monkeypatch, B, T, waves):
-    monkeypatch.setenv("M2_TAILR", waves)
+def test_tailr_vs_oracle(gpu, monkeypatch, B, T):
+    monkeypatch.setenv("M2_TAILR", "1")
     m = build_model(gpu)
     assert kernel_names(m, gpu)[2].startswith("tailr_kernel")
     mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(300 + T))
@@ -76,15 +75,14 @@ def test_tailr_vs_oracle(gpu, monkeypatch, B, T, waves):
 
 @pytest.mark.parametrize("B,T,nch", [(32, 500, 0), (8, 500, 0), (2, 2600, 0), (5, 333, 0), (1, 3, 0), (3, 41, 1),
                                      (2, 97, 5), (4, 200, 13)])
-@pytest.mark.parametrize("waves", ["1", "3"])
-def test_tailr_vs_tailp(gpu, monkeypatch, B, T, nch, waves):
+def test_tailr_vs_tailp(gpu, monkeypatch, B, T, nch):
     """The same packed weights, slot tables and per-chunk MFMA sequence on
     another schedule: bit-identical audio, at the default strips and at forced
     strip lengths (M2_TAILR_NCH) that put strip ends everywhere."""
     mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(7 * B + T))
     m = build_model(gpu)
     ref = m.vocoder(mel.to(gpu))
-    monkeypatch.setenv("M2_TAILR", waves)
+    monkeypatch.setenv("M2_TAILR", "1")
     if nch:
         monkeypatch.setenv("M2_TAILR_NCH", str(nch))
     out = m.vocoder(mel.to(gpu))
