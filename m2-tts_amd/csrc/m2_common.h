@@ -43,8 +43,6 @@ struct Switches {
     int midp_nch = 16;          // M2_MIDP_NCH=8|16|32
     int tailp_nch = 0;          // M2_TAILP_NCH=21|32|48
     bool tailp_seven = false;   // M2_TAILP_SEVEN
-    int tailr = 0;              // M2_TAILR=1|2|3: the stage1 tail with layers chained per wave (vocoder_tailr.hip; 3: three waves)
-    int tailr_nch = 0;          // M2_TAILR_NCH: its strip length in 16-column chunks (0: by grid)
     int tailp2_nch = 0;         // M2_TAILP2_NCH
     bool tailp2_seven = false;  // M2_TAILP2_SEVEN
     bool head_inconv = false;   // M2_HEAD_INCONV

@@ -79,10 +79,6 @@ void reload_switches() {
     const int tn = env_int("M2_TAILP_NCH", 0);
     s.tailp_nch = (tn == 21 || tn == 32 || tn == 48) ? tn : 0;
     s.tailp_seven = env_set("M2_TAILP_SEVEN");
-    const int tr = env_int("M2_TAILR", 0);
-    s.tailr = tr >= 1 && tr <= 3 ? tr : 0;
-    const int rn = env_int("M2_TAILR_NCH", 0);
-    s.tailr_nch = rn > 0 && rn <= 256 ? rn : 0;
     s.tailp2_nch = env_int("M2_TAILP2_NCH", 0);
     s.tailp2_seven = env_set("M2_TAILP2_SEVEN");
     s.head_inconv = env_set("M2_HEAD_INCONV");
@@ -1791,8 +1787,7 @@ const char* m2_profile_kernel_name(int32_t index) {
 
 const char* m2_profile_kernel_name_for(const m2_model* m, int32_t index) {
     if (!m || index < 0 || index >= kVocKernels) return "";
-    if (m->x3 && m->tailp && index == 2)
-        return m->vx.tp2 ? kVocTailp2KernelName : (sw().tailr ? kVocTailrKernelName : kVocTailpKernelName);
+    if (m->x3 && m->tailp && index == 2) return m->vx.tp2 ? kVocTailp2KernelName : kVocTailpKernelName;
     if (m->x3 && m->midp && index == 1) return kVocMidpKernelName;
     return m->x3 ? kVocX3KernelNames[index] : kVocKernelNames[index];
 }

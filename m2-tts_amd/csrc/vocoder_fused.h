@@ -250,11 +250,6 @@ bool pack_tailp(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>*
 int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                              int* rflag, hipStream_t st, const int32_t* dT = nullptr, const VocRedo& rd = VocRedo{});
 extern const char* const kVocTailpKernelName;
-// The same tail with three layers chained per wave (vocoder_tailr.hip, same
-// packed weights; launch_vocoder_tailp passes them on when M2_TAILR is set).
-int32_t launch_vocoder_tailr(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
-                             int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd);
-extern const char* const kVocTailrKernelName;
 // The same five modules at stage2 widths (C = 256: U2 64 channels) for the
 // pipelined stage2 tail (vocoder_tailp2.hip, two waves per layer).
 bool pack_tailp2(const TailpSrc& s, std::vector<uint16_t>* w, std::vector<float>* bias, bool* range_ok);

@@ -618,8 +618,6 @@ int32_t launch_vocoder_tailp(const void* U2, int L2, int B, const vx_u32x4* W, c
     // rotation r per co-resident workgroup, tools/probe/simd_map.hip — gave
     // classes of 18/21/16/12 MFMAs instead of 18/24/16/9 and measured the same:
     // the step is latency-bound, not bound by one SIMD's MFMA pipe.)
-    if (sw().tailr)  // three layers per wave (vocoder_tailr.hip)
-        return launch_vocoder_tailr(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
     const bool seven = sw().tailp_seven;
     return seven ? tp::launch_nl<7>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd)
                  : tp::launch_nl<6>(nch, U2, L2, B, W, bias, audio, rflag, st, dT, rd);

@@ -57,34 +57,3 @@ def test_tailp_outc_vs_seven_layers(gpu, monkeypatch, B, T):
     assert float((out - ref).abs().max()) <= 2e-6
 
 
-
-# ---- three layers per wave, skewed (vocoder_tailr.hip, M2_TAILR=1) ---------------
-
-@pytest.mark.parametrize("B,T", [(3, 1), (2, 2), (2, 7), (3, 61), (1, 137)])
-def test_tailr_vs_oracle(gpu, monkeypatch, B, T):
-    monkeypatch.setenv("M2_TAILR", "1")
-    m = build_model(gpu)
-    assert kernel_names(m, gpu)[2].startswith("tailr_kernel")
-    mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(300 + T))
-    out = m.vocoder(mel.to(gpu)).cpu()
-    ref = orc.vocoder(golden_state("s1"), mel)
-    assert out.shape == ref.shape
-    assert rms(out, ref) <= AUDIO_RMS_TOL and maxabs(out, ref) <= 1e-4
-    assert maxabs(out[..., :4], ref[..., :4]) <= 1e-5 and maxabs(out[..., -4:], ref[..., -4:]) <= 1e-5
-
-
-@pytest.mark.parametrize("B,T,nch", [(32, 500, 0), (8, 500, 0), (2, 2600, 0), (5, 333, 0), (1, 3, 0), (3, 41, 1),
-                                     (2, 97, 5), (4, 200, 13)])
-def test_tailr_vs_tailp(gpu, monkeypatch, B, T, nch):
-    """The same packed weights, slot tables and per-chunk MFMA sequence on
-    another schedule: bit-identical audio, at the default strips and at forced
-    strip lengths (M2_TAILR_NCH) that put strip ends everywhere."""
-    mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(7 * B + T))
-    m = build_model(gpu)
-    ref = m.vocoder(mel.to(gpu))
-    monkeypatch.setenv("M2_TAILR", "1")
-    if nch:
-        monkeypatch.setenv("M2_TAILR_NCH", str(nch))
-    out = m.vocoder(mel.to(gpu))
-    assert torch.isfinite(out).all()
-    assert torch.equal(out, ref)
