@@ -536,7 +536,9 @@ def vocoder_line(cx: Ctx, stage: str, B: int, T: int, args, settle_ms: float, se
         _, all_ms = cx.timed(step, min(args.steps, 20), 2, hm, kernel_mask=(1 << cx.nk) - 1)
         per_kernel = cx.kernel_table(hm, all_ms, cfg["vocoder_channels"], cfg["mel_channels"], B, T)
         dom_i = max(per_kernel, key=lambda d: d["avg_ms"])["index"] if per_kernel else 0
-        stride = max(1, args.steps // 32)
+        # every 16th call carries the events: a sampled call pays ~4.5 us before
+        # and after its timed kernel (profiles/r05/r05o_gaps.txt), unsampled none
+        stride = max(1, args.steps // 16)
         elapsed, kern_ms = cx.timed(step, args.steps, args.warmup, hm, kernel_mask=1 << dom_i, stride=stride)
         path = cx.lib.m2_vocoder_path(hm.handle)
     finally:
@@ -588,10 +590,11 @@ def vocoder_line(cx: Ctx, stage: str, B: int, T: int, args, settle_ms: float, se
 
 def report_policy_line(cx: Ctx, B: int, T: int, args, head: dict):
     """The headline vocoder workload on the opt-in "report" range policy (a
-    non-finite split-f16 result raises on the next call; nothing is enqueued
-    behind the split kernels) - what the default "fallback" policy of the
-    headline costs per call: its one guarded exact-f32 redo launch, whose
-    workgroups return at once when the audio is finite.  Measured like for
+    non-finite split-f16 result raises on the next call) - what the default
+    "fallback" policy of the headline costs per call: the pipelined tail's
+    workgroup-local non-finite word and the barrier before its in-launch fp32
+    redo, which runs only for a strip whose audio is not finite (round 5; a
+    guarded exact-f32 launch behind the tail with M2_REDO_LAUNCH=1).  Measured like for
     like: both policies timed exactly as the headline is (same steps, the
     same fence-free events on the dominant kernel every stride-th call),
     alternated three times in this process; the cost is the difference of
