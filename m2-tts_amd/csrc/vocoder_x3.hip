@@ -105,7 +105,7 @@ constexpr int pd_of() {
 // layouts of the head.
 // BP: see below.
 template <int CIN, int NTAP, int STEP, int RSI, int NT, bool XR, int NMB, int WS, bool PRE, bool TB = false,
-          int PDM = 4, bool BP = false>
+          int PDM = 4, int BP = 0>
 __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsigned char* bp,
                                        const unsigned char* xr, f32x4 (&acc)[NMB][NT],
                                        u32x4 (&a)[pd_of<CIN, NTAP, NMB, PDM>()][NMB][2], const u32x4* wp_next,
@@ -149,28 +149,37 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
             return kb == NKB - 1 ? b_last : bl + koff(kb);
         }
     };
-    // BP: k-block kb + 1's B fragments are read from LDS before k-block kb's
-    // MFMAs are issued (two register buffers, 8 NT more VGPRs), so their LDS
-    // latency hides behind the MFMAs instead of sitting before each k-block's
-    // first.  Taken where it measured faster (the stage2 head, see CfgS2)
-    constexpr int NB = BP ? 2 : 1;
-    u32x4 bh[NB][NT], blo[NB][NT];
-    auto bread = [&](int kb, int q) {
+    // BP 1: k-block kb + 1's B fragments are read from LDS before k-block
+    // kb's MFMAs are issued (two register buffers, 8 NT more VGPRs), so their
+    // LDS latency hides behind the MFMAs instead of sitting before each
+    // k-block's first; BP 2: only the hi fragments one k-block ahead (4 NT
+    // more VGPRs).  Taken where it measured faster (the stage2 head, CfgS2).
+    constexpr int NBH = BP ? 2 : 1, NBL = BP == 1 ? 2 : 1;
+    u32x4 bh[NBH][NT], blo[NBL][NT];
+    auto readh = [&](int kb, int q) {
         const unsigned char* b0 = bbase(kb);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-            bh[q][n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI);
-            blo[q][n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
-        }
+        for (int n = 0; n < NT; ++n) bh[q][n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI);
     };
-    if constexpr (BP) bread(0, 0);
+    auto readl = [&](int kb, int q) {
+        const unsigned char* b0 = bbase(kb);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) blo[q][n] = *reinterpret_cast<const u32x4*>(b0 + n * 16 * RSI + 2 * CIN);
+    };
+    if constexpr (BP) readh(0, 0);
+    if constexpr (BP == 1) readl(0, 0);
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-        const int q = BP ? (kb & 1) : 0;
+        const int q = BP ? (kb & 1) : 0, ql = BP == 1 ? (kb & 1) : 0;
+        if constexpr (BP == 2) readl(kb, 0);
         if constexpr (BP) {
-            if (kb + 1 < NKB) bread(kb + 1, (kb + 1) & 1);
+            if (kb + 1 < NKB) {
+                readh(kb + 1, (kb + 1) & 1);
+                if constexpr (BP == 1) readl(kb + 1, (kb + 1) & 1);
+            }
         } else {
-            bread(kb, 0);
+            readh(kb, 0);
+            readl(kb, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -180,7 +189,7 @@ __device__ __forceinline__ void mma_x3(const u32x4* __restrict__ wp, const unsig
 #pragma unroll
         for (int m = 0; m < NMB; ++m)
 #pragma unroll
-            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], blo[q][n], acc[m][n]);
+            for (int n = 0; n < NT; ++n) acc[m][n] = mfma_h(a[kb % PD][m][0], blo[ql][n], acc[m][n]);
 #pragma unroll
         for (int m = 0; m < NMB; ++m)
 #pragma unroll
@@ -263,7 +272,7 @@ constexpr bool kFold = res_fold_channels(C);
 // corr (the composed stage2 head): per-(phase, channel) terms subtracted from
 // the outputs of input column qe (an utterance edge), before the activation.
 template <int CIN, int COUT, int NTAP, int STEP, int RSI, int RSO, int NTT, int ACT, bool RES, bool XR, int RR,
-          int JMAX, int NMB, bool PRE, bool GO = false, int PDM = 4, bool BP = false>
+          int JMAX, int NMB, bool PRE, bool GO = false, int PDM = 4, int BP = 0>
 __device__ __forceinline__ void run_item(const u32x4* __restrict__ wp, const float* __restrict__ bias,
                                          const unsigned char* bp, const unsigned char* xr, XW out, int co0, int p0,
                                          int ph, int tile0, int L, u32x4 (&a)[pd_of<CIN, NTAP, NMB, PDM>()][NMB][2],
@@ -357,7 +366,7 @@ struct ConvTItems {
 // 8/16 channels, read back in the epilogue otherwise.
 // GO: store the output tiles to global rows (gout) instead of `out`.
 template <int CIN, int COUT, int NT, int ACT, bool RES, int RSI, int RSO, int NPOS, int NMB = 1, int ONE = 0,
-          bool GO = false, int PDM = 4, bool BP = false>
+          bool GO = false, int PDM = 4, int BP = 0>
 __device__ __forceinline__ void xconv3(const u32x4* __restrict__ Wp, const float* __restrict__ bias, XW in, XW out,
                                        int a0, int L, APipe* ap = nullptr, const u32x4* wp_next = nullptr,
                                        unsigned char* gout = nullptr) {
@@ -442,7 +451,7 @@ __device__ __forceinline__ void xconvT(const u32x4* __restrict__ Wp, const float
 // The composed input_conv o ConvT1 on the generic item path (the stage2
 // head): head_convT1c_planar's layer over (phase, m-block, chunk) items, 4
 // mel taps (frames q + d0 + 1 - k), per-phase bias, edge terms from `corr`.
-template <int MP, int COUT, int NT, int RSI, int RSO, int NQ, int PDM = 4, bool BP = false>
+template <int MP, int COUT, int NT, int RSI, int RSO, int NQ, int PDM = 4, int BP = 0>
 __device__ __forceinline__ void xconvT1c(const u32x4* __restrict__ Wp, const float* __restrict__ bias,
                                          const unsigned char* corr, XW mel, XW out, int q0, int T) {
     constexpr int R = 4, MB = (COUT + 15) / 16, NKB = nkb_of<MP, 4>();
@@ -896,8 +905,11 @@ struct CfgS1 {
 #ifndef X3S2_HW  // stage2 head waves per workgroup (tiling experiments)
 #define X3S2_HW 8
 #endif
-#ifndef X3S2_HBP  // stage2 head: B-fragment reads one k-block ahead (CfgS2::HBP)
+#ifndef X3S2_HBP  // stage2 head: B-fragment reads one k-block ahead (CfgS2::HBP, mma_x3 BP)
 #define X3S2_HBP 1
+#endif
+#ifndef X3S2W_HBP  // the 16-wave stage2 head of large grids (CfgS2H24::HBP)
+#define X3S2W_HBP 2
 #endif
 #ifndef X3S2_PDM  // stage2 weight-fragment k-blocks in flight per item (mma_x3)
 #define X3S2_PDM 4
@@ -921,8 +933,9 @@ struct CfgS2 {
     // workgroup per CU either way): head 26.5 -> 25.0 us at 8x500; in the mid
     // kernels it measured slower (24.0 -> 26.0 us at 8x500, 186 -> 212 us at
     // 16x2600: 4 -> 3 waves per SIMD), in the 16-wave H24 head level (172 ->
-    // 175 us, spills) - profiles/r05/r05g_bpipe_ab.txt
-    static constexpr bool HBP = X3S2_HBP;
+    // 175 us, spills; its hi-only form, BP 2, 173.6 -> 171.5 us: CfgS2H24) -
+    // profiles/r05/r05g_bpipe_ab.txt, r05r_head_bp2_ab.txt
+    static constexpr int HBP = X3S2_HBP;
 };
 // Stage2 mid / tail tilings for small grids (run<CfgS2> picks per call): at
 // B=8, T=500 the default windows make 576 mid workgroups (1.1 rounds of 512
@@ -946,7 +959,7 @@ constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
 struct CfgS2H24 : CfgS2 {
     static constexpr int TF = 24, HW = 16;
     static constexpr int PDM = 4;  // 16 waves: 128 VGPRs per wave
-    static constexpr bool HBP = false;
+    static constexpr int HBP = X3S2W_HBP;
 };
 constexpr long kS2WideHeadWGs = 1024;
 
