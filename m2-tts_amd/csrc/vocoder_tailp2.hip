@@ -150,8 +150,8 @@ constexpr Slot outc_slot(int f, int g) {
 // strip, LDS addresses precomputed per ring phase (the step loop is unrolled by
 // the lcm of the ring periods), one fp32 accumulator per m-block for the three
 // split products, identity-A MFMAs for the ResBlock residual.
-template <int L, int W, int NCH, int NL>
-__device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, bool edge,
+template <int L, int W, int NL>
+__device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, int nch, bool edge,
                                            const u32x4* __restrict__ W_, const float* __restrict__ bias,
                                            float* __restrict__ arow, int* rflag) {
     constexpr int NMB = nmbw(L), NKB = nkb(L), NF = nfrag(L, W);
@@ -296,11 +296,11 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
             else epilogue(std::false_type{});
         }
     };
-    constexpr int LAST = last_step(NCH, NL);
+    const int LAST = last_step(nch, NL);
     auto step = [&](int s, auto jc) {
         if (s <= LAST) {
             const int k = s - off_l(L);
-            if (k >= -1 && k < NCH) work(k, jc);
+            if (k >= -1 && k < nch) work(k, jc);
             step_barrier();
         }
     };
@@ -324,8 +324,7 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L2, b
 // wave, in place of ResBlock4 conv2 (two waves of 2 x 2 x 3 + 4) and the
 // output conv (9).  The utterance's two edge samples subtract the y the
 // reference pads with zeros (terms from layer 4, LDS slot kCorrSlot).
-template <int NCH>
-__device__ __forceinline__ void outc2_role(unsigned char* lds, int qa, int L2, bool edge,
+__device__ __forceinline__ void outc2_role(unsigned char* lds, int qa, int L2, int nch, bool edge,
                                            const u32x4* __restrict__ W_, const float* __restrict__ bias,
                                            float* __restrict__ arow, int* rflag) {
     constexpr int L = 5, NL = 6, NF = kOutcF, P = 4;
@@ -382,11 +381,11 @@ __device__ __forceinline__ void outc2_role(unsigned char* lds, int qa, int L2, b
             flag_nonfinite4(o.x, o.y, o.z, o.w, rflag, reinterpret_cast<int*>(lds + kFlagOff(NL)));
         }
     };
-    constexpr int LAST = last_step(NCH, NL);
+    const int LAST = last_step(nch, NL);
     auto step = [&](int s, auto jc) {
         if (s <= LAST) {
             const int k = s - off_l(L);
-            if (k >= 0 && k < NCH) work(k, jc);  // chunk -1 feeds no later layer
+            if (k >= 0 && k < nch) work(k, jc);  // chunk -1 feeds no later layer
             step_barrier();
         }
     };
@@ -404,8 +403,9 @@ __device__ __forceinline__ void outc2_role(unsigned char* lds, int qa, int L2, b
 // columns [qa + 7 + 16c, +16), zero outside [0, L2).  Lane (r = lane >> 4, pc =
 // lane & 15) moves 16 B of columns r, r + 4, r + 8, r + 12 (pc < 8: hi octet pc,
 // else lo octet pc - 8); loads unconditional (clamped) so their waits are counted.
-template <int NCH, int NL, bool EDGE>
-__device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, const unsigned char* __restrict__ u2) {
+template <int NL, bool EDGE>
+__device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, int nch,
+                                            const unsigned char* __restrict__ u2) {
     const int lane = threadIdx.x & 63, r = lane >> 4, pc = lane & 15;
     auto fetch = [&](int c, u32x4 (&v)[4]) {
 #pragma unroll
@@ -423,8 +423,8 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
         for (int h = 0; h < 4; ++h) wadr[j][h] = (pc >> 3) * kLoOff(0) + ring_at(0, ring_row(0, j, r + 4 * h), pc & 7);
     auto step = [&](int s, auto jc, u32x4 (&cur)[4], u32x4 (&ahead)[4]) {
         constexpr int j = decltype(jc)::value;
-        fetch(min(s + 2, NCH - 1), ahead);
-        if (s < NCH) {
+        fetch(min(s + 2, nch - 1), ahead);
+        if (s < nch) {
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
                 const int col = qa + NL + 16 * s + r + 4 * h;
@@ -439,29 +439,29 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     fetch(0, buf[1]);
     int s = -1;
 #pragma unroll 1
-    for (; s + 2 <= last_step(NCH, NL); s += 3) {
+    for (; s + 2 <= last_step(nch, NL); s += 3) {
         step(s, ic<2>{}, buf[0], buf[2]);
         step(s + 1, ic<0>{}, buf[1], buf[0]);
         step(s + 2, ic<1>{}, buf[2], buf[1]);
     }
 #pragma unroll 1
-    for (; s <= last_step(NCH, NL); ++s) step_barrier();
+    for (; s <= last_step(nch, NL); ++s) step_barrier();
 }
 
-template <int NCH, int NL>
+template <int NL>
 __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsigned char* __restrict__ U2, int L2,
-                                                                     const u32x4* __restrict__ W,
+                                                                     int nch, const u32x4* __restrict__ W,
                                                                      const float* __restrict__ bias,
                                                                      float* __restrict__ audio, int* rflag,
                                                                      const int32_t* __restrict__ dT, VocRedo rd) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
+    const int b = blockIdx.y, qa = blockIdx.x * 16 * nch;
     if (dT) {  // speculative launch: L2 was the capacity
         L2 = 16 * dev_frames(dT, L2 / 16);
         if (qa >= L2) return;
     }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool edge = qa < 32 || qa + 16 * NCH + 32 > L2;
+    const bool edge = qa < 32 || qa + 16 * nch + 32 > L2;
     float* arow = audio + (size_t)b * 4 * L2;
     int* const lflag = reinterpret_cast<int*>(lds + kFlagOff(NL));
     if (threadIdx.x == 0) *lflag = 0;  // before the first epilogue: the pipeline's step barriers order it
@@ -471,73 +471,60 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsign
     else if (w >= 2) __builtin_amdgcn_s_setprio(1);
     const unsigned char* u2 = U2 + (size_t)b * L2 * 256;
     switch (w) {
-        case 0: layer_role<0, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 1: layer_role<0, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 2: layer_role<1, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 3: layer_role<1, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 4: layer_role<2, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 5: layer_role<2, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 6: layer_role<3, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 7: layer_role<3, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 8: layer_role<4, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
-        case 9: layer_role<4, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag); break;
+        case 0: layer_role<0, 0, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 1: layer_role<0, 1, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 2: layer_role<1, 0, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 3: layer_role<1, 1, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 4: layer_role<2, 0, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 5: layer_role<2, 1, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 6: layer_role<3, 0, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 7: layer_role<3, 1, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 8: layer_role<4, 0, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
+        case 9: layer_role<4, 1, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag); break;
         case 10:
-            if constexpr (NL == 7) layer_role<5, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
-            else outc2_role<NCH>(lds, qa, L2, edge, W, bias, arow, rflag);
+            if constexpr (NL == 7) layer_role<5, 0, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag);
+            else outc2_role(lds, qa, L2, nch, edge, W, bias, arow, rflag);
             break;
         case 11:
             if constexpr (NL == 7) {
-                layer_role<5, 1, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
+                layer_role<5, 1, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag);
                 break;
             }
             [[fallthrough]];
         case 12:
             if constexpr (NL == 7) {
                 if (w == 12) {
-                    layer_role<6, 0, NCH, NL>(lds, qa, L2, edge, W, bias, arow, rflag);
+                    layer_role<6, 0, NL>(lds, qa, L2, nch, edge, W, bias, arow, rflag);
                     break;
                 }
             }
             [[fallthrough]];
         default:
-            if (edge) loader_role<NCH, NL, true>(lds, qa, L2, u2);
-            else loader_role<NCH, NL, false>(lds, qa, L2, u2);
+            if (edge) loader_role<NL, true>(lds, qa, L2, nch, u2);
+            else loader_role<NL, false>(lds, qa, L2, nch, u2);
             break;
     }
     if (rd.rw) {  // range policy "fallback": this strip's audio again in fp32 if it is not finite
         __syncthreads();
         if (*lflag)
-            redo_frames(*rd.rw, rd.mel, rd.trans, L2 / 16, b, qa / 16, min(L2, qa + 16 * NCH) / 16, arow,
+            redo_frames(*rd.rw, rd.mel, rd.trans, L2 / 16, b, qa / 16, min(L2, qa + 16 * nch) / 16, arow,
                         reinterpret_cast<float*>(lds), ring_bytes(NL) / 4);
     }
-}
-
-template <int NCH, int NL>
-int32_t launch(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio, int* rflag,
-               hipStream_t st, const int32_t* dT, const VocRedo& rd) {
-    static bool attr = false;
-    if (!attr) {
-        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp2_kernel<NCH, NL>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes(NL)));
-        attr = true;
-    }
-    hipLaunchKernelGGL((tailp2_kernel<NCH, NL>), dim3(cdiv(L2, 16 * NCH), B), dim3(nwaves(NL) * 64), lds_bytes(NL),
-                       st, static_cast<const unsigned char*>(U2), L2, W, bias, audio, rflag, dT, rd);
-    M2_LAUNCHED("tailp2_kernel");
-    return M2_OK;
 }
 
 template <int NL>
 int32_t launch_nl(int nch, const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                   int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd) {
-    switch (nch) {
-        case 8: return launch<8, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
-        case 16: return launch<16, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
-        case 32: return launch<32, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
-        case 64: return launch<64, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
-        case 128: return launch<128, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
-        default: return launch<192, NL>(U2, L2, B, W, bias, audio, rflag, st, dT, rd);
+    static bool attr = false;
+    if (!attr) {
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tailp2_kernel<NL>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes(NL)));
+        attr = true;
     }
+    hipLaunchKernelGGL((tailp2_kernel<NL>), dim3(cdiv(L2, 16 * nch), B), dim3(nwaves(NL) * 64), lds_bytes(NL), st,
+                       static_cast<const unsigned char*>(U2), L2, nch, W, bias, audio, rflag, dT, rd);
+    M2_LAUNCHED("tailp2_kernel");
+    return M2_OK;
 }
 
 }  // namespace tp2
@@ -548,22 +535,19 @@ const char* const kVocTailp2KernelName =
 int32_t launch_vocoder_tailp2(const void* U2, int L2, int B, const vx_u32x4* W, const float* bias, float* audio,
                               int* rflag, hipStream_t st, const int32_t* dT, const VocRedo& rd) {
     if (B == 0 || L2 == 0) return M2_OK;
-    // Strip length: the instantiated NCH minimising rounds x (NCH + NL pipeline
-    // steps) at one workgroup per CU.  M2_TAILP2_NCH forces one;
-    // M2_TAILP2_SEVEN=1 the seven-layer form (switch table, m2_common.h).
+    // Strip length (chunks of 16 columns): the one minimising rounds x (nch +
+    // NL pipeline steps) at one workgroup per CU, any length from 8 to 256
+    // (the kernel takes it at run time: 16 x 2600 gets 256 strips of 163
+    // chunks, one round, where the instantiated lengths of round 4 gave 224
+    // strips of 192).  M2_TAILP2_NCH forces one; M2_TAILP2_SEVEN=1 the
+    // seven-layer form (switch table, m2_common.h).
     const bool seven = sw().tailp2_seven;
     const int nl = seven ? 7 : 6;
-    static constexpr int kN[] = {8, 16, 32, 64, 128, 192};
-    const int forced = [] {
-        for (int n : kN)
-            if (sw().tailp2_nch == n) return n;
-        return 0;
-    }();
-    int nch = forced;
+    int nch = sw().tailp2_nch > 0 ? std::min(sw().tailp2_nch, 4096) : 0;
     if (!nch) {
         const long chunks = cdiv(L2, 16);
         long best = -1;
-        for (int n : kN) {
+        for (int n = 8; n <= 256; ++n) {
             const long wgs = (long)cdiv((int)chunks, n) * B, rounds = (wgs + 255) / 256, cost = rounds * (n + nl);
             if (best < 0 || cost < best) best = cost, nch = n;
         }

@@ -3,7 +3,7 @@ ResBlock3, ConvT4, ResBlock4 and output_conv at C = 256 in polyphase form,
 two waves per layer) against the CPU oracle (the reference's
 SimpleVocoder.forward, tts_model.py:279-297) and against the x3 tail kernel it
 replaces (M2_VOC_TAIL_X3=1), over ragged lengths that put utterance ends in
-every position of a 16-column chunk and strips of every instantiated length.
+every position of a 16-column chunk, and at forced strip lengths.
 """
 import pytest
 import torch
@@ -42,8 +42,8 @@ def test_tailp2_vs_oracle(gpu, B, T):
 @pytest.mark.parametrize("B,T", [(8, 500), (2, 2600), (16, 2600), (5, 333)])
 def test_tailp2_vs_x3_tail(gpu, monkeypatch, B, T):
     """Same split-f16 products as the x3 tail in another summation order:
-    agreement to fp32 rounding.  (16, 2600) takes 192-chunk strips, (8, 500)
-    16-chunk strips, (2, 2600) 32."""
+    agreement to fp32 rounding.  (16, 2600) takes 163-chunk strips (one
+    round of 256 workgroups), (8, 500) 16-chunk strips."""
     mel = torch.randn(B, stage_config("s2").mel_channels, T, generator=torch.Generator().manual_seed(B * T))
     m = build_model(gpu)
     out = m.vocoder(mel.to(gpu))
@@ -77,3 +77,16 @@ def test_tailp2_outc_vs_seven_layers(gpu, monkeypatch, B, T):
     ref = m.vocoder(mel.to(gpu))
     assert torch.isfinite(out).all()
     assert float((out - ref).abs().max()) <= 2e-6
+
+
+@pytest.mark.parametrize("nch", [1, 7, 13, 100])
+def test_tailp2_strip_lengths(gpu, monkeypatch, nch):
+    """The strip length is a launch argument (M2_TAILP2_NCH forces one): every
+    column's arithmetic is the same whatever strip holds it, so the audio is
+    bit-identical to the default strips, with strip ends everywhere."""
+    mel = torch.randn(3, stage_config("s2").mel_channels, 97, generator=torch.Generator().manual_seed(nch))
+    m = build_model(gpu)
+    ref = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_TAILP2_NCH", str(nch))
+    out = m.vocoder(mel.to(gpu))
+    assert torch.equal(out, ref)
