@@ -40,10 +40,10 @@ struct Switches {
     bool voc_tail_x3 = false;   // M2_VOC_TAIL_X3 (handle creation)
     bool voc_mid_x3 = false;    // M2_VOC_MID_X3 (handle creation)
     int voc_plan = -1;          // M2_VOC_PLAN
-    int midp_nch = 16;          // M2_MIDP_NCH=8|16|32
-    int tailp_nch = 0;          // M2_TAILP_NCH=21|32|48
+    int midp_nch = 0;           // M2_MIDP_NCH: the stage1 mid's strip length in 16-column chunks (0: by grid)
+    int tailp_nch = 0;          // M2_TAILP_NCH: strip length in 16-column chunks (0: by grid)
     bool tailp_seven = false;   // M2_TAILP_SEVEN
-    int tailp2_nch = 0;         // M2_TAILP2_NCH
+    int tailp2_nch = 0;         // M2_TAILP2_NCH: the same for the stage2 tail
     bool tailp2_seven = false;  // M2_TAILP2_SEVEN
     bool head_inconv = false;   // M2_HEAD_INCONV
     bool s2_head_tf16 = false;  // M2_S2_HEAD_TF16

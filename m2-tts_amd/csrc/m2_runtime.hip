@@ -74,10 +74,10 @@ void reload_switches() {
     s.voc_tail_x3 = env_set("M2_VOC_TAIL_X3");
     s.voc_mid_x3 = env_set("M2_VOC_MID_X3");
     s.voc_plan = env_int("M2_VOC_PLAN", -1);
-    const int mn = env_int("M2_MIDP_NCH", 16);
-    s.midp_nch = (mn == 8 || mn == 32) ? mn : 16;
+    const int mn = env_int("M2_MIDP_NCH", 0);
+    s.midp_nch = mn > 0 ? mn : 0;
     const int tn = env_int("M2_TAILP_NCH", 0);
-    s.tailp_nch = (tn == 21 || tn == 32 || tn == 48) ? tn : 0;
+    s.tailp_nch = tn > 0 ? tn : 0;
     s.tailp_seven = env_set("M2_TAILP_SEVEN");
     s.tailp2_nch = env_int("M2_TAILP2_NCH", 0);
     s.tailp2_seven = env_set("M2_TAILP2_SEVEN");

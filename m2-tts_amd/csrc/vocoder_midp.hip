@@ -74,8 +74,8 @@ using ic = std::integral_constant<int, V>;
 // utterance end, and conv2's residual (ConvT2's output, ring R1, two columns
 // ahead: channels 32S .. 32S+31 = one fragment shared by both m-blocks) as
 // two identity-A MFMAs per m-block instead of 24 VALU.
-template <int L, int S, int NCH>
-__device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, bool edge,
+template <int L, int S>
+__device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, int nch, bool edge,
                                            const u32x4* __restrict__ W, const float* __restrict__ bias,
                                            unsigned char* __restrict__ u2row) {
     constexpr int NKB = mkb(L);
@@ -180,11 +180,11 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
             }
         }
     };
-    constexpr int LAST = NCH + 2;  // conv2 computes chunk NCH - 1 in step NCH + 2
+    const int LAST = nch + 2;  // conv2 computes chunk nch - 1 in step nch + 2
     auto step = [&](int s, auto jc) {
         if (s <= LAST) {
             const int k = s - (L + 1);
-            if (k >= -1 && k < NCH) work(k, jc);
+            if (k >= -1 && k < nch) work(k, jc);
             step_barrier();
         }
     };
@@ -201,8 +201,9 @@ __device__ __forceinline__ void layer_role(unsigned char* lds, int qa, int L1, b
 // U1 rows (256 B) into ring R0, two chunks ahead: chunk c = columns
 // [qa + 3 + 16c, +16), zero outside [0, L1).  Four 16-B pieces per lane per
 // chunk, loads issued unconditionally (clamped) so their waits are counted.
-template <int NCH, bool EDGE>
-__device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L1, const unsigned char* __restrict__ u1) {
+template <bool EDGE>
+__device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L1, int nch,
+                                            const unsigned char* __restrict__ u1) {
     const int lane = threadIdx.x & 63, cr = lane >> 4, pc = lane & 15;
     auto fetch = [&](int c, u32x4 (&v)[4]) {
 #pragma unroll
@@ -214,8 +215,8 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L1, 
     };
     u32x4 buf[3][4];
     auto step = [&](int s, u32x4 (&cur)[4], u32x4 (&ahead)[4]) {
-        fetch(min(s + 2, NCH - 1), ahead);
-        if (s < NCH) {
+        fetch(min(s + 2, nch - 1), ahead);
+        if (s < nch) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int col = qa + 3 + 16 * s + 4 * j + cr;
@@ -231,63 +232,65 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L1, 
     fetch(0, buf[1]);
     int s = -1;
 #pragma unroll 1
-    for (; s + 2 <= NCH + 2; s += 3) {
+    for (; s + 2 <= nch + 2; s += 3) {
         step(s, buf[0], buf[2]);
         step(s + 1, buf[1], buf[0]);
         step(s + 2, buf[2], buf[1]);
     }
 #pragma unroll 1
-    for (; s <= NCH + 2; ++s) step_barrier();
+    for (; s <= nch + 2; ++s) step_barrier();
 }
 
-template <int NCH>
-__global__ __launch_bounds__(NWAVES * 64, 4) void midp_kernel(const unsigned char* __restrict__ U1, int L1,
+// NCHC > 0: the strip length as a compile-time constant (the headline's 16); 0: nch.
+template <int NCHC>
+__global__ __launch_bounds__(NWAVES * 64, 4) void midp_kernel(const unsigned char* __restrict__ U1, int L1, int nch_arg,
                                                                const u32x4* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                unsigned char* __restrict__ U2,
                                                                const int32_t* __restrict__ dT) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int b = blockIdx.y, qa = blockIdx.x * 16 * NCH;
+    const int nch = NCHC ? NCHC : nch_arg;
+    const int b = blockIdx.y, qa = blockIdx.x * 16 * nch;
     if (dT) {  // speculative launch: L1 was the capacity
         L1 = 4 * dev_frames(dT, L1 / 4);
         if (qa >= L1) return;
     }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool edge = qa < 16 || qa + 16 * NCH + 16 > L1;
+    const bool edge = qa < 16 || qa + 16 * nch + 16 > L1;
     unsigned char* u2row = U2 + (size_t)b * 4 * L1 * 128;
     if (w >= 8) __builtin_amdgcn_s_setprio(2);  // later layers: younger waves, the step waits for them
     else if (w >= 4) __builtin_amdgcn_s_setprio(1);
     switch (w) {
-        case 0: layer_role<0, 0, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 1: layer_role<0, 1, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 2: layer_role<0, 2, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 3: layer_role<0, 3, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 4: layer_role<1, 0, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 5: layer_role<1, 1, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 6: layer_role<1, 2, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 7: layer_role<1, 3, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 8: layer_role<2, 0, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 9: layer_role<2, 1, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 10: layer_role<2, 2, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
-        case 11: layer_role<2, 3, NCH>(lds, qa, L1, edge, W, bias, u2row); break;
+        case 0: layer_role<0, 0>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 1: layer_role<0, 1>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 2: layer_role<0, 2>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 3: layer_role<0, 3>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 4: layer_role<1, 0>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 5: layer_role<1, 1>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 6: layer_role<1, 2>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 7: layer_role<1, 3>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 8: layer_role<2, 0>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 9: layer_role<2, 1>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 10: layer_role<2, 2>(lds, qa, L1, nch, edge, W, bias, u2row); break;
+        case 11: layer_role<2, 3>(lds, qa, L1, nch, edge, W, bias, u2row); break;
         default:
-            if (edge) loader_role<NCH, true>(lds, qa, L1, U1 + (size_t)b * L1 * 256);
-            else loader_role<NCH, false>(lds, qa, L1, U1 + (size_t)b * L1 * 256);
+            if (edge) loader_role<true>(lds, qa, L1, nch, U1 + (size_t)b * L1 * 256);
+            else loader_role<false>(lds, qa, L1, nch, U1 + (size_t)b * L1 * 256);
             break;
     }
 }
 
-template <int NCH>
-int32_t launch(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2, hipStream_t st,
-               const int32_t* dT) {
+template <int NCHC>
+int32_t launch(int nch, const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2,
+               hipStream_t st, const int32_t* dT) {
     static bool attr = false;
     if (!attr) {
-        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(midp_kernel<NCH>),
+        M2_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(midp_kernel<NCHC>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
         attr = true;
     }
-    hipLaunchKernelGGL((midp_kernel<NCH>), dim3(cdiv(L1, 16 * NCH), B), dim3(NWAVES * 64), LDS_BYTES, st,
-                       static_cast<const unsigned char*>(U1), L1, W, bias, static_cast<unsigned char*>(U2), dT);
+    hipLaunchKernelGGL(midp_kernel<NCHC>, dim3(cdiv(L1, 16 * nch), B), dim3(NWAVES * 64), LDS_BYTES, st,
+                       static_cast<const unsigned char*>(U1), L1, nch, W, bias, static_cast<unsigned char*>(U2), dT);
     M2_LAUNCHED("midp_kernel");
     return M2_OK;
 }
@@ -299,10 +302,22 @@ const char* const kVocMidpKernelName = "midp_kernel (ConvT2 + ResBlock2, pipelin
 int32_t launch_vocoder_midp(const void* U1, int L1, int B, const vx_u32x4* W, const float* bias, void* U2,
                             hipStream_t st, const int32_t* dT) {
     if (B == 0 || L1 == 0) return M2_OK;
-    const int nch = sw().midp_nch;
-    if (nch == 8) return mp::launch<8>(U1, L1, B, W, bias, U2, st, dT);
-    if (nch == 32) return mp::launch<32>(U1, L1, B, W, bias, U2, st, dT);
-    return mp::launch<16>(U1, L1, B, W, bias, U2, st, dT);
+    // Strip length (16-column chunks of U1 per workgroup, a launch argument):
+    // the one from 4 to 256 minimising rounds of 256 workgroups (one per CU)
+    // x pipeline steps (stage1 B = 32, L1 = 2000: 8 strips of 16 chunks, one
+    // round; the round-4 sweep at 8 / 16 / 32 measured 23.1 / 20.0 / 29.9 us).
+    // M2_MIDP_NCH forces one.
+    int nch = sw().midp_nch > 0 ? std::min(sw().midp_nch, 4096) : 0;
+    if (!nch) {
+        const long chunks = cdiv(L1, 16);
+        long best = -1;
+        for (int n = 4; n <= 256; ++n) {
+            const long wgs = (long)cdiv((int)chunks, n) * B, rounds = (wgs + 255) / 256, cost = rounds * (n + 4);
+            if (best < 0 || cost < best) best = cost, nch = n;
+        }
+    }
+    return nch == 16 ? mp::launch<16>(nch, U1, L1, B, W, bias, U2, st, dT)
+                     : mp::launch<0>(nch, U1, L1, B, W, bias, U2, st, dT);
 }
 
 // ---------------------------------------------------------------------------

@@ -46,8 +46,8 @@ def test_tailp_outc_vs_oracle(gpu, B, T):
 @pytest.mark.parametrize("B,T", [(32, 500), (8, 500), (2, 2600), (5, 333), (1, 3)])
 def test_tailp_outc_vs_seven_layers(gpu, monkeypatch, B, T):
     """The composed layer reorders fp32 sums of the same products: agreement
-    to fp32 rounding.  (32, 500) takes 21-chunk strips, (8, 500) 32, (2, 2600)
-    48."""
+    to fp32 rounding.  (32, 500) takes 21-chunk strips, (8, 500) 8, (2, 2600)
+    8 (the grid model's choices)."""
     mel = torch.randn(B, stage_config("s1").mel_channels, T, generator=torch.Generator().manual_seed(B * T))
     m = build_model(gpu)
     out = m.vocoder(mel.to(gpu))
@@ -57,3 +57,29 @@ def test_tailp_outc_vs_seven_layers(gpu, monkeypatch, B, T):
     assert float((out - ref).abs().max()) <= 2e-6
 
 
+
+
+@pytest.mark.parametrize("nch", [1, 5, 21, 77])
+def test_tailp_strip_lengths(gpu, monkeypatch, nch):
+    """The strip length is a launch argument (M2_TAILP_NCH forces one): every
+    column's arithmetic is the same whatever strip holds it, so the audio is
+    bit-identical to the default strips, with strip ends everywhere."""
+    mel = torch.randn(3, stage_config("s1").mel_channels, 83, generator=torch.Generator().manual_seed(nch))
+    m = build_model(gpu)
+    ref = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_TAILP_NCH", str(nch))
+    out = m.vocoder(mel.to(gpu))
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("nch", [1, 3, 16, 41])
+def test_midp_strip_lengths(gpu, monkeypatch, nch):
+    """The pipelined stage1 mid (vocoder_midp.hip) takes its strip length as a
+    launch argument too (M2_MIDP_NCH forces one): bit-identical audio."""
+    mel = torch.randn(2, stage_config("s1").mel_channels, 71, generator=torch.Generator().manual_seed(50 + nch))
+    m = build_model(gpu)
+    assert kernel_names(m, gpu)[1].startswith("midp_kernel")
+    ref = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_MIDP_NCH", str(nch))
+    out = m.vocoder(mel.to(gpu))
+    assert torch.equal(out, ref)
