@@ -424,9 +424,11 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// One workgroup per utterance: n[s] = max(0, trunc(d[s]*scale)); exclusive
-// scan into cum[b, 0..S]; T[b] = cum[b,S]; atomicMax into Tmax (zeroed by the
-// launcher's memset node).
+// One wave per utterance: n[s] = max(0, trunc(d[s]*scale)) for ceil(S/64)
+// consecutive phonemes per lane, a shuffle scan of the lanes' sums (no LDS,
+// no barrier: was 256 threads and a Hillis-Steele scan in LDS, 16 barriers,
+// 6.0 us at stage1 B=32 S=100), exclusive prefix sums into cum[b, 0..S],
+// T[b] = cum[b, S]; atomicMax into Tmax (zeroed by the launcher's memset node).
 
 
 // SYNC: no pre-zeroed Tmax / atomicMax: the last workgroup to finish (a
@@ -438,60 +440,50 @@ __global__ __launch_bounds__(64 * DUR_WAVES) void duration_kernel(
 // stored prefix sums and totals saturate at INT32_MAX (the host rejects a
 // T_max above m2's frame limit with M2_E_SHAPE instead of wrapping).
 template <bool SYNC>
-__global__ __launch_bounds__(256) void lr_count_kernel(const void* __restrict__ dur, int is_int,
-                                                       float scale, int S, int32_t* __restrict__ cum,
-                                                       int32_t* __restrict__ T,
-                                                       int32_t* __restrict__ Tmax, unsigned* __restrict__ ticket,
-                                                       int32_t* __restrict__ mbox, int32_t seq) {
-    __shared__ long long part[256];
-    const int b = blockIdx.x, tid = threadIdx.x;
-    const int chunk = (S + 255) / 256;
-    const int lo = min(S, tid * chunk), hi = min(S, lo + chunk);
+__global__ __launch_bounds__(64) void lr_count_kernel(const void* __restrict__ dur, int is_int, float scale, int S,
+                                                      int32_t* __restrict__ cum, int32_t* __restrict__ T,
+                                                      int32_t* __restrict__ Tmax, unsigned* __restrict__ ticket,
+                                                      int32_t* __restrict__ mbox, int32_t seq) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int per = (S + 63) / 64, lo = min(S, lane * per), hi = min(S, lo + per);
     const size_t base = (size_t)b * S;
     long long sum = 0;
     for (int s = lo; s < hi; ++s) sum += frames_of(dur, is_int, scale, base + s);
-    part[tid] = sum;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over the 256 partials.
-    for (int off = 1; off < 256; off <<= 1) {
-        const long long v = tid >= off ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    long long inc = sum;  // inclusive scan over the lanes
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long v = __shfl_up(inc, off);
+        if (lane >= off) inc += v;
     }
-    long long run = part[tid] - sum;  // exclusive prefix of this thread's chunk
+    long long run = inc - sum;  // exclusive prefix of this lane's phonemes
     int32_t* c = cum + (size_t)b * (S + 1);
-    if (tid == 0) c[0] = 0;
+    if (lane == 0) c[0] = 0;
     for (int s = lo; s < hi; ++s) {
         run += frames_of(dur, is_int, scale, base + s);
         c[s + 1] = sat32(run);
     }
-    const int32_t total = sat32(part[255]);
+    const int32_t total = sat32(__shfl(inc, 63));
     if constexpr (!SYNC) {
-        if (tid == 255) {
+        if (lane == 0) {
             T[b] = total;
             atomicMax(Tmax, total);
         }
     } else {
-        __shared__ bool last;
-        if (tid == 255) {
+        bool last = false;
+        if (lane == 0) {
             __hip_atomic_store(T + b, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __atomic_thread_fence(__ATOMIC_RELEASE);  // totals before the ticket
             last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
         }
-        __syncthreads();
-        if (last) {  // every other workgroup's total is visible
+        if (__shfl(last ? 1 : 0, 0)) {  // every other workgroup's total is visible
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (all lanes: lane 0's ticket was the acquire)
             long long m = 0;
-            for (int i = tid; i < (int)gridDim.x; i += 256)
+            for (int i = lane; i < (int)gridDim.x; i += 64)
                 m = max(m, (long long)__hip_atomic_load(T + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            part[tid] = m;
-            __syncthreads();
-            for (int off = 128; off > 0; off >>= 1) {
-                if (tid < off) part[tid] = max(part[tid], part[tid + off]);
-                __syncthreads();
-            }
-            if (tid == 0) {
-                const int32_t tm = sat32(part[0]);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+            if (lane == 0) {
+                const int32_t tm = sat32(m);
                 *Tmax = tm;
                 __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (mbox) {  // null: T_max stays on the device (m2_inference_front_dev)
@@ -651,7 +643,7 @@ int32_t launch_lr_count(const void* dur, int is_int, float scale, int B, int S, 
                         int32_t* T, int32_t* Tmax, hipStream_t st) {
     M2_HIP(hipMemsetAsync(Tmax, 0, sizeof(int32_t), st));
     if (B == 0) return M2_OK;
-    hipLaunchKernelGGL(lr_count_kernel<false>, dim3(B), dim3(256), 0, st, dur, is_int, scale, S, cum, T,
+    hipLaunchKernelGGL(lr_count_kernel<false>, dim3(B), dim3(64), 0, st, dur, is_int, scale, S, cum, T,
                        Tmax, nullptr, nullptr, 0);
     M2_LAUNCHED("lr_count_kernel");
     return M2_OK;
@@ -659,7 +651,7 @@ int32_t launch_lr_count(const void* dur, int is_int, float scale, int B, int S, 
 
 int32_t launch_lr_count_sync(const void* dur, int is_int, float scale, int B, int S, int32_t* cum, int32_t* T,
                              int32_t* Tmax, unsigned* ticket, int32_t* mbox, int32_t seq, hipStream_t st) {
-    hipLaunchKernelGGL(lr_count_kernel<true>, dim3(B), dim3(256), 0, st, dur, is_int, scale, S, cum, T, Tmax,
+    hipLaunchKernelGGL(lr_count_kernel<true>, dim3(B), dim3(64), 0, st, dur, is_int, scale, S, cum, T, Tmax,
                        ticket, mbox, seq);
     M2_LAUNCHED("lr_count_kernel");
     return M2_OK;
