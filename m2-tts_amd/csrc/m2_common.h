@@ -46,7 +46,8 @@ struct Switches {
     int tailp2_nch = 0;         // M2_TAILP2_NCH: the same for the stage2 tail
     bool tailp2_seven = false;  // M2_TAILP2_SEVEN
     bool head_inconv = false;   // M2_HEAD_INCONV
-    bool s2_head_tf16 = false;  // M2_S2_HEAD_TF16
+    int s2_mid_alt = -1;        // M2_S2_MID_ALT=0|1: the 30- / 33-position stage2 mid (-1: by grid)
+    int s2_head_tf = 0;         // M2_S2_HEAD_TF=16|19|24|27 (M2_S2_HEAD_TF16: 16)
     int redo_grid = -1;         // M2_REDO_GRID: workgroups of the guarded redo launch (-1: one per CU)
     bool redo_launch = false;   // M2_REDO_LAUNCH: the guarded exact-f32 launch also where the tail redoes locally
     bool dur_split = true;      // M2_DUR_SPLIT=0: the duration convs on the exact-f32 MFMA always

@@ -82,7 +82,10 @@ void reload_switches() {
     s.tailp2_nch = env_int("M2_TAILP2_NCH", 0);
     s.tailp2_seven = env_set("M2_TAILP2_SEVEN");
     s.head_inconv = env_set("M2_HEAD_INCONV");
-    s.s2_head_tf16 = env_set("M2_S2_HEAD_TF16");
+    const int malt = env_int("M2_S2_MID_ALT", -1);
+    s.s2_mid_alt = (malt == 0 || malt == 1) ? malt : -1;
+    const int htf = env_int("M2_S2_HEAD_TF", env_set("M2_S2_HEAD_TF16") ? 16 : 0);
+    s.s2_head_tf = (htf == 16 || htf == 19 || htf == 24 || htf == 27) ? htf : 0;
     s.redo_grid = env_int("M2_REDO_GRID", -1);
     s.redo_launch = env_set("M2_REDO_LAUNCH");
     s.dur_split = env_on("M2_DUR_SPLIT", true);

@@ -894,7 +894,7 @@ struct CfgS1 {
 #define X3S2_NT_R1 5
 #endif
 #ifndef X3S2_W2
-#define X3S2_W2 28
+#define X3S2_W2 30
 #define X3S2_NT_R2 4
 #endif
 #ifndef X3S2_W3
@@ -910,6 +910,12 @@ struct CfgS1 {
 #endif
 #ifndef X3S2W_HBP  // the 16-wave stage2 head of large grids (CfgS2H24::HBP)
 #define X3S2W_HBP 2
+#endif
+#ifndef X3S2W_TF  // the 16-wave stage2 head's window (CfgS2H24::TF)
+#define X3S2W_TF 24
+#endif
+#ifndef X3S2A_W2  // the small-grid stage2 mid window (CfgS2Alt::W2)
+#define X3S2A_W2 33
 #endif
 #ifndef X3S2_PDM  // stage2 weight-fragment k-blocks in flight per item (mma_x3)
 #define X3S2_PDM 4
@@ -943,9 +949,10 @@ struct CfgS2 {
 // per CU); 32 / 125 make 504 and 512 (one and two full rounds), at 1.20x /
 // 1.075x the time per workgroup (5-tile chunks where 4 were enough).
 // Measured B=8 T=500: mid 26.4 -> 22.9 us, tail 35.5 -> 26.1 us; large grids
-// keep the defaults (tools/probe/s2_tiles.sh).
+// keep the defaults (tools/probe/s2_tiles.sh).  Since round 5 the windows
+// are 30 and 33 positions (same tiles, fewer workgroups: below).
 struct CfgS2Alt : CfgS2 {
-    static constexpr int W2 = 32, NT_R2 = 5;
+    static constexpr int W2 = X3S2A_W2, NT_R2 = 5;
     static constexpr int W3 = 125, NT_T3 = 5, NT_R3 = 5;
 };
 constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
@@ -957,11 +964,30 @@ constexpr double kAltMidCost = 1.20, kAltTailCost = 1.075;
 // head 140.8 -> 135.2 us at 64x500, 170.6 -> 165.4 at 16x2600; at 8x500 the
 // 16-frame, 8-wave head stays, tools/probe/s2_tiles.sh with X3S2_HW=16).
 struct CfgS2H24 : CfgS2 {
-    static constexpr int TF = 24, HW = 16;
+    static constexpr int TF = X3S2W_TF, HW = 16;
     static constexpr int PDM = 4;  // 16 waves: 128 VGPRs per wave
     static constexpr int HBP = X3S2W_HBP;
 };
-constexpr long kS2WideHeadWGs = 1024;
+constexpr long kS2WideHeadWGs = 1024;  // in 16-frame windows
+// Each window's layers run whole 16-row m-tiles: the head's ResBlock1 covers
+// 4 TF + 2 rows (16 and 19 frames: 5 tiles, 24 and 27: 7), the mid's
+// ResBlock2 4 W + 2 and its ConvT2 W + 2 rows per phase (28 and 30
+// positions: 8 and 2 tiles, 32 and 33: 10 with NT_R2 = 5, and 3).  So the
+// 19 / 27-frame heads and the 30 / 33-position mids cost what the 16 / 24 /
+// 28 / 32 ones do per workgroup and make fewer workgroups; run<CfgS2> takes
+// the fewer rounds of workgroup slots, the smaller window when the rounds tie.
+// Bit-identical audio either way (every output sums the same products in the
+// same order).  Alternated twice (profiles/r05/r05ab_windows_ab.txt): head
+// 38.9 -> 27.2 us at 16x262 (272 -> 224 workgroups: one round of 256),
+// 146.3 -> 132.9 at 128x262, 141.2 -> 128.0 at 64x500; mid 184.4 -> 176.6 us
+// at 16x2600, 149.1 -> 145.2 at 128x262, 26.7 -> 25.2 at 16x262 (W33:
+// 512 workgroups, one round of two per CU).
+struct CfgS2T19 : CfgS2 {
+    static constexpr int TF = 19;
+};
+struct CfgS2H27 : CfgS2H24 {
+    static constexpr int TF = 27;
+};
 
 // Diagnostic build only (-DM2_STAMPS): per-wave s_memtime stamps at phase
 // boundaries, [kernel][workgroup][wave][16] (tools/probe/stamps.py --x3).
@@ -1386,6 +1412,8 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
             hipStream_t st, const std::function<void(int, bool)>& mark) {
     using HP = HeadPlan<Cfg::MP, Cfg::C, Cfg::TF, head_planar<Cfg>()>;
     using HP24 = HeadPlan<CfgS2H24::MP, CfgS2H24::C, CfgS2H24::TF, false>;
+    using HP19 = HeadPlan<CfgS2T19::MP, CfgS2T19::C, CfgS2T19::TF, false>;
+    using HP27 = HeadPlan<CfgS2H27::MP, CfgS2H27::C, CfgS2H27::TF, false>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
     using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
     constexpr bool S2 = std::is_same<Cfg, CfgS2>::value;
@@ -1403,6 +1431,10 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
         if constexpr (S2) {
             if ((rc = set_lds(x3_head_kernel<CfgS2H24, false, true>, HP24::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_head_kernel<CfgS2H24, true, true>, HP24::LDS_BYTES))) return rc;
+            if ((rc = set_lds(x3_head_kernel<CfgS2T19, false, true>, HP19::LDS_BYTES))) return rc;
+            if ((rc = set_lds(x3_head_kernel<CfgS2T19, true, true>, HP19::LDS_BYTES))) return rc;
+            if ((rc = set_lds(x3_head_kernel<CfgS2H27, false, true>, HP27::LDS_BYTES))) return rc;
+            if ((rc = set_lds(x3_head_kernel<CfgS2H27, true, true>, HP27::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_mid_kernel<CfgS2Alt>, MPA::LDS_BYTES))) return rc;
             if ((rc = set_lds(x3_tail_kernel<CfgS2Alt>, TPA::LDS_BYTES))) return rc;
         }
@@ -1414,7 +1446,9 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
                           sm1 = grid_slots(x3_mid_kernel<CfgS2Alt>, Cfg::MW * 64, MPA::LDS_BYTES),
                           st0 = grid_slots(x3_tail_kernel<Cfg>, Cfg::TW * 64, TP::LDS_BYTES),
                           st1 = grid_slots(x3_tail_kernel<CfgS2Alt>, Cfg::TW * 64, TPA::LDS_BYTES);
-        if (!w.mp)
+        if (!w.mp && sw().s2_mid_alt >= 0)
+            alt_mid = sw().s2_mid_alt == 1;
+        else if (!w.mp)
             alt_mid = rounds_of((long)cdiv(4 * T, CfgS2Alt::W2) * B, sm1) * kAltMidCost <
                       (double)rounds_of((long)cdiv(4 * T, Cfg::W2) * B, sm0);
         if (!w.tp && !w.tp2)
@@ -1429,16 +1463,40 @@ int32_t run(const float* mel, bool trans, int B, int T, const VocX& w, void* U1,
     // layers (A/B and test switch, m2_common.h switch table)
     const bool comp = w.hc && !sw().head_inconv;
     const dim3 hg(cdiv(T, Cfg::TF), B), hb(Cfg::HW * 64);
-    bool wide = false;  // stage2, composed head, large grid: 24-frame windows
-    if constexpr (S2) wide = comp && (long)cdiv(T, Cfg::TF) * B >= kS2WideHeadWGs && !sw().s2_head_tf16;
-    if (wide) {
+    // stage2, composed head: the 16-wave heads (24 / 27 frames) on large
+    // grids, the 8-wave heads (16 / 19) below; within a pair the fewer rounds
+    // of workgroup slots, the smaller window on a tie (M2_S2_HEAD_TF forces)
+    int hv = 16;
+    if constexpr (S2) {
+        static const long s16 = grid_slots(x3_head_kernel<Cfg, false, true>, Cfg::HW * 64, HP::LDS_BYTES),
+                          s19 = grid_slots(x3_head_kernel<CfgS2T19, false, true>, CfgS2T19::HW * 64, HP19::LDS_BYTES),
+                          s24 = grid_slots(x3_head_kernel<CfgS2H24, false, true>, CfgS2H24::HW * 64, HP24::LDS_BYTES),
+                          s27 = grid_slots(x3_head_kernel<CfgS2H27, false, true>, CfgS2H27::HW * 64, HP27::LDS_BYTES);
+        auto rounds = [&](int tf, long slots) { return rounds_of((long)cdiv(T, tf) * B, slots); };
+        if (sw().s2_head_tf)
+            hv = sw().s2_head_tf;
+        else if ((long)cdiv(T, 16) * B >= kS2WideHeadWGs)
+            hv = rounds(27, s27) < rounds(24, s24) ? 27 : 24;
+        else
+            hv = rounds(19, s19) < rounds(16, s16) ? 19 : 16;
+    }
+    auto head = [&](auto cfg) {
+        using HC = decltype(cfg);
+        using HPc = HeadPlan<HC::MP, HC::C, HC::TF, false>;
+        const dim3 g(cdiv(T, HC::TF), B), b(HC::HW * 64);
+        if (trans)
+            hipLaunchKernelGGL((x3_head_kernel<HC, true, true>), g, b, HPc::LDS_BYTES, st, mel, T, w, u1);
+        else
+            hipLaunchKernelGGL((x3_head_kernel<HC, false, true>), g, b, HPc::LDS_BYTES, st, mel, T, w, u1);
+    };
+    if (S2 && comp && hv != 16) {
         if constexpr (S2) {
-            const dim3 hg24(cdiv(T, CfgS2H24::TF), B);
-            if (trans)
-                hipLaunchKernelGGL((x3_head_kernel<CfgS2H24, true, true>), hg24, hb, HP24::LDS_BYTES, st, mel, T, w, u1);
+            if (hv == 19)
+                head(CfgS2T19{});
+            else if (hv == 24)
+                head(CfgS2H24{});
             else
-                hipLaunchKernelGGL((x3_head_kernel<CfgS2H24, false, true>), hg24, hb, HP24::LDS_BYTES, st, mel, T, w,
-                                   u1);
+                head(CfgS2H27{});
         }
     } else if (comp && trans)
         hipLaunchKernelGGL((x3_head_kernel<Cfg, true, true>), hg, hb, HP::LDS_BYTES, st, mel, T, w, u1);

@@ -85,3 +85,33 @@ def test_head_comp_s2_vs_two_layers(gpu, monkeypatch, B, T):
     ref = m.vocoder(mel.to(gpu))
     assert torch.isfinite(out).all()
     assert float((out - ref).abs().max()) <= 2e-5 and rms(out.cpu(), ref.cpu()) <= 2e-6
+
+
+@pytest.mark.parametrize("B,T", [(3, 33), (2, 263), (1, 54), (16, 262)])
+def test_head_s2_windows_bit_identical(gpu, monkeypatch, B, T):
+    """The stage2 head's four windows (16 / 19 frames, 8 waves; 24 / 27, 16
+    waves; run<CfgS2> picks by rounds of workgroup slots, M2_S2_HEAD_TF
+    forces) sum the same products in the same order: identical audio, and the
+    27-frame one against the oracle."""
+    mel = torch.randn(B, stage_config("s2").mel_channels, T, generator=torch.Generator().manual_seed(B * T + 3))
+    m = build_s2(gpu)
+    auto = m.vocoder(mel.to(gpu))
+    for tf in (16, 19, 24, 27):
+        monkeypatch.setenv("M2_S2_HEAD_TF", str(tf))
+        assert torch.equal(m.vocoder(mel.to(gpu)), auto), tf
+    if B * T <= 100:
+        ref = orc.vocoder(golden_state("s2"), mel)
+        out = auto.cpu()
+        assert rms(out, ref) <= AUDIO_RMS_TOL and maxabs(out, ref) <= 1e-4
+
+
+@pytest.mark.parametrize("B,T", [(3, 33), (8, 500), (16, 262)])
+def test_mid_s2_windows_bit_identical(gpu, monkeypatch, B, T):
+    """The stage2 mid's 30- and 33-position windows (M2_S2_MID_ALT forces
+    either): identical audio."""
+    mel = torch.randn(B, stage_config("s2").mel_channels, T, generator=torch.Generator().manual_seed(B * T + 4))
+    m = build_s2(gpu)
+    monkeypatch.setenv("M2_S2_MID_ALT", "0")
+    a = m.vocoder(mel.to(gpu))
+    monkeypatch.setenv("M2_S2_MID_ALT", "1")
+    assert torch.equal(m.vocoder(mel.to(gpu)), a)
