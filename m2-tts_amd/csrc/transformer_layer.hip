@@ -596,7 +596,9 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
 
     // chunks kq, kq + 4, ... through a two-slot register ring.  The scheduling
     // barriers keep each slot's loads in program order (slot 0 before slot 1),
-    // so the wait at the top of an iteration is for the older slot only.
+    // so the wait at the top of an iteration is for the older slot only.  (A
+    // three-slot ring for the 16-row tiles measured slower: B=8 decoder
+    // attention 12.2k -> 18.6k cycles, profiles/r05/r05ae_*.)
     const int nj = kq < nchl ? (nchl - kq + WPH - 1) / WPH : 0;
     Frag f0, f1;
     load(f0, kq);
@@ -1796,11 +1798,24 @@ struct LArgs {
 // RB = 1 (16-row tiles) while the grid fits one round of the CUs, else 2
 // (32-row tiles: every K / V and weight fragment a workgroup reads serves
 // twice the rows), 4 (64-row query-split tiles; QV picks the attention form).
+#ifndef TFL_ONE  // A/B builds: 0 = the 16-row tiles compiled like the others
+#define TFL_ONE 1
+#endif
+// 16-row tiles run only on grids of at most one workgroup per CU (tfl_rb):
+// there they request every weight strip a phase ahead - both FFN1 strips of
+// a wave before the attention merge, the FFN2 and QKV' strips before FFN1 -
+// and the residual rows at the start (ONE; 232-236 VGPRs for H = 96, no
+// scratch).  B=8 S=100 stage2, alternated twice: the six layer launches
+// 78.2 -> 75.9 us; stage1 B=32 encoder layers 9.9 -> 9.0 and 7.7 -> 7.4 us
+// (profiles/r05/r05af_*).
+constexpr bool tfl_one(int rb) { return TFL_ONE && rb == 1; }
 template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     static_assert(RB == 1 || RB == 2 || RB == 4, "16-, 32- or 64-row tiles");
     static_assert(QV != 9 || !MASKED, "the wave-specialised attention is unmasked-only");
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
+    constexpr bool ONE = tfl_one(RB);
+    constexpr int NBQ = 3 * H / 16, NQK = 2 * H / 16;  // QKV' column blocks, of them Q / K
     constexpr bool QS = RB == 4;                  // 64-row tiles: K / V staged in LDS
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att, then LN2(o), LN(y) (split)
     // the attention's scratch (key-quarter merge records / the K-V chunk ring)
@@ -1844,6 +1859,12 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     int len = N;
     if constexpr (MASKED) len = (int)max((int64_t)0, min(a.lengths[b], (int64_t)N));  // mask[b, s] = s < lengths[b]
     Strip<H> so;
+    Strip<H> s1, s1b;  // FFN1 strips (ONE: both of this wave's, requested before the merge)
+    f32x4 xres = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (ONE) {  // the out projection's residual rows (here: measured 0.4 us better than beside Wo)
+        if (wave < H / 16 && t0 + i < N)
+            xres = *reinterpret_cast<const f32x4*>(a.x_in + ((size_t)b * N + t0 + i) * H + wave * 16 + 4 * gq);
+    }
     if constexpr (QS) {
         if constexpr (QV == 9) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
@@ -1859,6 +1880,10 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     } else {
         attention_tile<H, HD, MASKED, RB>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs, [&] {
             if (wave < H / 16) so.load(a.Wo, wave);
+            if constexpr (ONE) {
+                if (wave < F / 16) s1.load(a.W1, wave);
+                if (wave + NW < F / 16) s1b.load(a.W1, wave + NW);
+            }
         });
     }
     const size_t row0 = (size_t)b * N + t0;
@@ -1873,36 +1898,59 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         for (int rb = 0; rb < RB; ++rb) {
             const int rr = rb * 16 + i;
             f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (t0 + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
+            if constexpr (ONE) x = xres;
+            else if (t0 + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
             *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = x + acc[rb];
         }
     }
-    Strip<H> s1;
-    if (wave < F / 16) s1.load(a.W1, wave);
+    Strip<F> s2;
+    if constexpr (ONE) {
+        if (wave < H / 16) s2.load(a.W2, wave);
+    } else if (wave < F / 16) {
+        s1.load(a.W1, wave);
+    }
     __syncthreads();
     TSTAMP(3);
     ln_rows<H, TR>(O, A, vec + VG2, vec + VB2N);
     __syncthreads();
     TSTAMP(4);
     // h = relu(LN2(o) . W1^T + b1)
-#pragma unroll 1
-    for (int nb = wave; nb < F / 16; nb += NW) {
-        Strip<H> nxt;
-        if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
+    auto ffn1 = [&](int nb, const Strip<H>& st) {
         const int col = nb * 16 + 4 * gq;
         f32x4 acc[RB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc[rb] = *reinterpret_cast<const f32x4*>(vec + VB1 + col);
-        gemm_t<H, RB>(A, s1, acc);
+        gemm_t<H, RB>(A, st, acc);
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
             put_split4<F>(Hd + (rb * 16 + i) * srs(F) + 2 * col, acc[rb][0] > 0.f ? acc[rb][0] : 0.f,
                           acc[rb][1] > 0.f ? acc[rb][1] : 0.f, acc[rb][2] > 0.f ? acc[rb][2] : 0.f,
                           acc[rb][3] > 0.f ? acc[rb][3] : 0.f);
-        if (nb + NW < F / 16) s1 = nxt;
+    };
+    // ONE: the QKV' strips of this wave, requested before FFN1 (the
+    // final-projection strip for NEXT 2)
+    Strip<H> sq[(NBQ + NW - 1) / NW];
+    if constexpr (ONE) {
+        if constexpr (NEXT == 1) {
+#pragma unroll
+            for (int k = 0; k < (NBQ + NW - 1) / NW; ++k)
+                if (wave + NW * k < NBQ) sq[k].load(a.Wn, wave + NW * k);
+        } else if constexpr (NEXT == 2) {
+            if (wave < NN / 16) sq[0].load(a.Wn, wave);
+        }
+        static_assert(F / 16 <= 2 * NW, "two FFN1 blocks per wave at most");
+        if (wave < F / 16) ffn1(wave, s1);
+        if (wave + NW < F / 16) ffn1(wave + NW, s1b);
+    } else {
+#pragma unroll 1
+        for (int nb = wave; nb < F / 16; nb += NW) {
+            Strip<H> nxt;
+            if (nb + NW < F / 16) nxt.load(a.W1, nb + NW);
+            ffn1(nb, s1);
+            if (nb + NW < F / 16) s1 = nxt;
+        }
+        if (wave < H / 16) s2.load(a.W2, wave);
     }
-    Strip<F> s2;
-    if (wave < H / 16) s2.load(a.W2, wave);
     __syncthreads();
     TSTAMP(5);
     // y = o + h . W2^T + b2
@@ -1922,18 +1970,36 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     }
     if constexpr (NEXT == 1) {
         Strip<H> sn;
-        if (wave < 3 * H / 16) sn.load(a.Wn, wave);
+        if (!ONE && wave < 3 * H / 16) sn.load(a.Wn, wave);
         __syncthreads();
         TSTAMP(6);
         ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
         __syncthreads();
         TSTAMP(7);
-        qkv_phase<H, HD, RB>(A, a.Wn, sn, qo, b, t0, N);
+        if constexpr (ONE) {
+#pragma unroll
+            for (int k = 0; k < (NBQ + NW - 1) / NW; ++k) {
+                const int nb = wave + NW * k;
+                if (nb < NBQ) {
+                    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+                    if (nb < NQK) {
+                        gemm_t<H, 1>(A, sq[k], acc);
+                        store_qk<H, HD>(qo, b, t0, N, nb, acc[0]);
+                    } else {
+                        gemm_n<H, 1>(A, sq[k], acc);
+                        store_v<H, HD>(qo, b, t0, N, nb, acc[0]);
+                    }
+                }
+            }
+        } else {
+            qkv_phase<H, HD, RB>(A, a.Wn, sn, qo, b, t0, N);
+        }
         TSTAMP(8);
         TSTAMP_RT(15);
     } else if constexpr (NEXT == 2) {
         Strip<H> sn;
-        if (wave < NN / 16) sn.load(a.Wn, wave);
+        if constexpr (ONE) sn = sq[0];
+        else if (wave < NN / 16) sn.load(a.Wn, wave);
         __syncthreads();
         TSTAMP(6);
         ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);

@@ -1,0 +1,28 @@
+# Round 5 (r05af with the residual rows requested beside the Wo strip): the 16-row-tile layer form for grids of <= one workgroup per CU
+# (TFL_ONE: weight strips and residual rows requested a phase ahead, three
+# K / V chunks in flight) against the same tree built with TFL_ONE=0: layer
+# tile / parity / range tests, phase stamps of both, B=8 S=100 kernel traces
+# and stage1 pipeline kernel stats, alternated twice.
+set -u
+tag=r05ag
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+NEW=m2-tts_amd/src/m2amd/libm2tts_hip.so
+OLD=m2-tts_amd/csrc/build_one0/libm2tts_hip_one0.so
+timeout -k 10 500 python -u -m pytest tests/test_gpu_tf_layer.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { tail -n 30 gpurun_out/${tag}_tests.log; exit 1; }
+tail -n 1 gpurun_out/${tag}_tests.log
+for v in tst tst0; do
+  M2TTS_HIP_LIB=m2-tts_amd/csrc/build_$v/libm2tts_hip_$v.so timeout -k 10 120 python -u tools/probe/tfl_stamps.py s2 enc8x100 8x500 > gpurun_out/${tag}_stamps_$v.txt 2>&1 || exit 1
+done
+for i in 1 2; do
+for v in new old; do
+  L=$NEW; [ $v = old ] && L=$OLD
+  d=gpurun_out/${tag}_tr8_${v}_$i
+  M2TTS_HIP_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python3 tools/probe/s2_small_trace.py 8 dev 100 > $d.log 2>&1 || exit 1
+  python3 tools/probe/s2_small_trace.py --summarize $d/run_kernel_trace.csv 20 > $d.txt || exit 1
+  rm -f $d/run_kernel_trace.csv
+  M2TTS_HIP_LIB=$L timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_pipe_${v}_$i -o run -- \
+      python3 bench.py --workload pipeline --steps 100 --warmup 20 --no-cpu-baseline --no-extras > gpurun_out/${tag}_pipe_${v}_$i.json 2>/dev/null || exit 1
+  rm -f gpurun_out/${tag}_pipe_${v}_$i/run_kernel_trace.csv
+done
+done
