@@ -31,7 +31,6 @@ struct Switches {
     bool tf_unfused = false;  // M2_TF_UNFUSED: five-linear layers (handle creation)
     int tf_waves = 0;         // M2_TF_WAVES=4|8
     int tfl_rb = 0;           // M2_TFL_RB=1|2|4
-    int tfl_split = -1;       // M2_TFL_SPLIT=0|1 (key-split small-grid tiles; -1: by grid)
     int tfl_first_rb = 0;     // M2_TFL_FIRST_RB=1|2|4
     int tfl_qs2 = -1;         // M2_TFL_QS2=0|2|3|4|9
     int att_qt = 0;           // M2_ATT_QT

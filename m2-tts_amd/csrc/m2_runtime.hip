@@ -63,8 +63,6 @@ void reload_switches() {
     const int trb = env_int("M2_TFL_RB", 0);
     s.tfl_rb = rb124(trb);
     s.tfl_first_rb = rb124(env_int("M2_TFL_FIRST_RB", 0));
-    const int tsp = env_int("M2_TFL_SPLIT", -1);
-    s.tfl_split = (tsp == 0 || tsp == 1) ? tsp : -1;
     if (const char* e = std::getenv("M2_TFL_QS2"); e && *e) {
         const int v = std::atoi(e);
         s.tfl_qs2 = (v == 2 || v == 3 || v == 4 || v == 9) ? v : 0;
@@ -297,10 +295,6 @@ struct m2_model {
     // sequence whose parity picks their set (one stream per model)
     unsigned* tflq = nullptr;
     mutable unsigned tfl_seq = 0;
-    // key-split layer launches: tickets (in tflq, after the count ticket) and
-    // the softmax-record buffer (TflQueue::tick / part)
-    unsigned* tfl_tick = nullptr;
-    float* tfl_part = nullptr;
     // device-T path: the count kernel's ticket word (after the queue words in
     // tflq) and the host-mapped [seq, T] pair the back half's first launch
     // posts (m2_frames_wait)
@@ -471,12 +465,10 @@ bool tf_first_fused(const m2_model* m, const std::vector<m2_layer_w>& layers) {
 }
 
 // The next launch's work queue (its parity alternates the counter sets).
-TflQueue tfl_queue(const m2_model* m) { return TflQueue{m->tflq, m->tfl_seq++, m->tfl_tick, m->tfl_part}; }
-// A launch that failed may not have zeroed the next counter set: restart both
-// (and the split tickets, which a failed launch may have left raised).
+TflQueue tfl_queue(const m2_model* m) { return TflQueue{m->tflq, m->tfl_seq++}; }
+// A launch that failed may not have zeroed the next counter set: restart both.
 int32_t tfl_reset(const m2_model* m, hipStream_t st, int32_t rc) {
     (void)hipMemsetAsync(m->tflq, 0, kTflQueueWords * sizeof(unsigned), st);
-    if (m->tfl_tick) (void)hipMemsetAsync(m->tfl_tick, 0, kTflSplitTiles * sizeof(unsigned), st);
     m->tfl_seq = 0;
     return rc;
 }
@@ -1157,15 +1149,9 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
     }
     // work-queue counters of the one-launch transformer layers (TflQueue)
     // (+ 16 words: the count kernel's ticket of the device-T front half)
-    // (+ kTflSplitTiles words: the key-split layer launches' tickets)
-    e = hipMalloc(&m->tflq, (kTflQueueWords + 16 + kTflSplitTiles) * sizeof(unsigned));
-    if (e == hipSuccess)
-        e = hipMemsetAsync(m->tflq, 0, (kTflQueueWords + 16 + kTflSplitTiles) * sizeof(unsigned), st);
-    if (e == hipSuccess) {
-        m->cnt_ticket = m->tflq + kTflQueueWords;
-        m->tfl_tick = m->tflq + kTflQueueWords + 16;
-        e = hipMalloc(&m->tfl_part, kTflPartFloats * sizeof(float));
-    }
+    e = hipMalloc(&m->tflq, (kTflQueueWords + 16) * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemsetAsync(m->tflq, 0, (kTflQueueWords + 16) * sizeof(unsigned), st);
+    if (e == hipSuccess) m->cnt_ticket = m->tflq + kTflQueueWords;
     if (e == hipSuccess) {
         void* h = nullptr;
         e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
@@ -1198,7 +1184,6 @@ int32_t m2_model_destroy(m2_model* model) {
     if (model->rflag_host) (void)hipHostFree(model->rflag_host);
     if (model->rflag_dev) (void)hipFree(model->rflag_dev);
     if (model->tflq) (void)hipFree(model->tflq);
-    if (model->tfl_part) (void)hipFree(model->tfl_part);
     if (model->fpost_host) (void)hipHostFree(model->fpost_host);
     if (model->redo_w) (void)hipFree(const_cast<VocRedoW*>(model->redo_w));
     hipError_t e = hipFree(model->buf);

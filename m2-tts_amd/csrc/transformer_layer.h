@@ -24,18 +24,9 @@ struct TflBufs {
 // parity); a launch's workgroup 0 zeroes the other set for the next one.
 // One stream per counter buffer.
 constexpr int kTflQueueWords = 2 * 8 * 32;
-// Key-split layer launches (small grids): at most kTflSplitTiles query tiles,
-// two workgroups each; a workgroup's softmax records take kTflRecFloats
-// (8 waves x 2 row blocks x 64 lanes x (2 + 4 x 3) floats at H = 96) in
-// `part`, and `tick` holds one zero-at-rest ticket per tile.
-constexpr int kTflSplitTiles = 128;
-constexpr size_t kTflRecFloats = 8 * 2 * 64 * 14;
-constexpr size_t kTflPartFloats = 2 * kTflSplitTiles * kTflRecFloats;
 struct TflQueue {
     unsigned* cnt = nullptr;
     unsigned seq = 0;
-    unsigned* tick = nullptr;  // kTflSplitTiles words, zero
-    float* part = nullptr;     // kTflPartFloats
 };
 
 // True when the fused layer path covers (H, heads): heads == 2, H in {32, 64, 96}.

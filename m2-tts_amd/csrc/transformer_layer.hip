@@ -400,23 +400,10 @@ __device__ __forceinline__ void claim_tile(int B, int ntile, unsigned* __restric
 // as split LDS rows A [16 RB][srs(H)] (the out projection's B operand).  The
 // caller's `between` runs after the chunk loop, before the merge (the first
 // GEMM's weight strip is requested there).
-// SPL: the tile's key quarters are split between two workgroups (`half` h
-// runs quarters 2h and 2h + 1 of both heads, each over the same chunks in the
-// same order as without the split; its other four waves idle); each writes
-// its per-wave softmax records to `part` (slot 2 tix + half), and the second
-// to arrive (ticket `tick[tix]`) merges the four quarters in the usual order
-// - bit-identical to the unsplit tile - and returns true; the first returns
-// false and its workgroup ends.
-struct Split {
-    float* part;
-    unsigned* tick;
-    int tix, half;
-};
-template <int H, int HD, bool MASKED, int RB, bool SPL = false, typename Between>
-__device__ __forceinline__ bool attention_tile(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
+template <int H, int HD, bool MASKED, int RB, typename Between>
+__device__ __forceinline__ void attention_tile(const unsigned char* __restrict__ qb, const unsigned char* __restrict__ kb,
                                                const unsigned char* __restrict__ vb, int b, int t0, int N, int npad,
-                                               int len, float sl2, unsigned char* A, float* xs, Between between,
-                                               const Split& sp = Split{}) {
+                                               int len, float sl2, unsigned char* A, float* xs, Between between) {
     using G = Geo<HD>;
     constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, VCH = G::VCH, XW = G::XW;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -424,7 +411,6 @@ __device__ __forceinline__ bool attention_tile(const unsigned char* __restrict__
     const int h = wave / WPH, kq = wave - h * WPH;
     const int nch = npad / KC, nchl = (N + KC - 1) / KC;  // layout chunks, chunks holding live keys
     const size_t bh = (size_t)__builtin_amdgcn_readfirstlane(b * HEADS + h);
-    const bool act = !SPL || (kq >> 1) == sp.half;  // this wave's quarter runs in this workgroup
 
     // B = Q^T fragments: lane (query li of block qt, dims 32 ks + 8 g .. + 7)
     u32x4 qh[RB][KSA], ql[RB][KSA], qxh[RB], qxl[RB];
@@ -613,22 +599,21 @@ __device__ __forceinline__ bool attention_tile(const unsigned char* __restrict__
     // so the wait at the top of an iteration is for the older slot only.  (A
     // three-slot ring for the 16-row tiles measured slower: B=8 decoder
     // attention 12.2k -> 18.6k cycles, profiles/r05/r05ae_*.)
-    const int c0 = act ? kq : nchl;  // an idle wave's loads read zeros without traffic
-    const int nj = c0 < nchl ? (nchl - c0 + WPH - 1) / WPH : 0;
+    const int nj = kq < nchl ? (nchl - kq + WPH - 1) / WPH : 0;
     Frag f0, f1;
-    load(f0, c0);
+    load(f0, kq);
     __builtin_amdgcn_sched_barrier(0);
-    load(f1, c0 + WPH);
+    load(f1, kq + WPH);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll 1
     for (int j = 0; j < nj; j += 2) {
-        process(f0, c0 + WPH * j);
+        process(f0, kq + WPH * j);
         __builtin_amdgcn_sched_barrier(0);
-        load(f0, c0 + WPH * (j + 2));
+        load(f0, kq + WPH * (j + 2));
         __builtin_amdgcn_sched_barrier(0);
-        if (j + 1 < nj) process(f1, c0 + WPH * (j + 1));  // wave-uniform
+        if (j + 1 < nj) process(f1, kq + WPH * (j + 1));  // wave-uniform
         __builtin_amdgcn_sched_barrier(0);
-        load(f1, c0 + WPH * (j + 3));
+        load(f1, kq + WPH * (j + 3));
         __builtin_amdgcn_sched_barrier(0);
     }
     TSTAMP(1);
@@ -639,8 +624,6 @@ __device__ __forceinline__ bool attention_tile(const unsigned char* __restrict__
 #pragma unroll
         for (int qt = 0; qt < RB; ++qt) m[qt] = -INFINITY;
     }
-    constexpr int REC = NW * RB * 64 * XW;  // floats of one workgroup's records
-    float* const own = SPL ? sp.part + (size_t)(2 * sp.tix + sp.half) * REC : nullptr;
 #pragma unroll
     for (int qt = 0; qt < RB; ++qt) {
         float* xw = xs + ((wave * RB + qt) * 64 + lane) * XW;
@@ -650,64 +633,26 @@ __device__ __forceinline__ bool attention_tile(const unsigned char* __restrict__
         for (int t = 0; t < MT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) xw[2 + 4 * t + r] = acc[qt][t][r];
-        if (SPL && act) {  // field-major ([wave][qt][field][lane]): one 256-B row per store
-            float* gw = own + (wave * RB + qt) * XW * 64 + lane;
-            auto put = [](float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-            put(gw, m[qt]);
-            put(gw + 64, lsum[qt]);
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) put(gw + 64 * (2 + 4 * t + r), acc[qt][t][r]);
-        }
     }
-    const float* other = nullptr;
-    if constexpr (SPL) {
-        // Records out (agent-scope stores: written through past this XCD's
-        // L2), completed, then the ticket; the second workgroup to arrive
-        // reads the other's records with agent-scope loads.  No agent-scope
-        // fences: their L2 writeback / invalidate, once per workgroup, made
-        // the layer ~60 us slower (profiles/r05/r05ah_split_fence_ab.txt).
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        __shared__ int flag_s;
-        int* flag = &flag_s;
-        if (threadIdx.x == 0) {
-            const unsigned got = __hip_atomic_fetch_add(sp.tick + sp.tix, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (got != 0) __hip_atomic_store(sp.tick + sp.tix, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *flag = (int)got;
-        }
-        __syncthreads();
-        if (*flag == 0) return false;
-        other = sp.part + (size_t)(2 * sp.tix + (sp.half ^ 1)) * REC;
-    } else {
-        __syncthreads();
-    }
+    __syncthreads();
     if (kq < MT) {  // wave (h, j = kq): output dims 16 j .. 16 j + 15 of head h
         const int j = kq;
-        constexpr int NQ = WPH;
 #pragma unroll
         for (int qt = 0; qt < RB; ++qt) {
-            // record field k of quarter q: this workgroup's from LDS, the
-            // other half's (SPL) from its agent-scope stores
-            auto fld = [&](int q, int k) -> float {
-                const int w = (h * WPH + q) * RB + qt;
-                if (!SPL || (q >> 1) == sp.half) return xs[(w * 64 + lane) * XW + k];
-                return __hip_atomic_load(other + (w * XW + k) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            };
-            float mi[NQ], mx = -INFINITY;
+            float mi[WPH], mx = -INFINITY;
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                mi[q] = fld(q, 0);
+            for (int q = 0; q < WPH; ++q) {
+                mi[q] = xs[(((h * WPH + q) * RB + qt) * 64 + lane) * XW];
                 mx = vmax(mx, mi[q]);
             }
             float ls = 0.f, o[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
+            for (int q = 0; q < WPH; ++q) {
+                const float* xq = xs + (((h * WPH + q) * RB + qt) * 64 + lane) * XW;
                 const float fq = __builtin_amdgcn_exp2f(mi[q] - mx);
-                ls += fld(q, 1) * fq;
+                ls += xq[1] * fq;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] += fld(q, 2 + 4 * j + r) * fq;
+                for (int r = 0; r < 4; ++r) o[r] += xq[2 + 4 * j + r] * fq;
             }
             ls += __shfl_xor(ls, 16);
             ls += __shfl_xor(ls, 32);
@@ -718,7 +663,6 @@ __device__ __forceinline__ bool attention_tile(const unsigned char* __restrict__
     }
     __syncthreads();
     TSTAMP(2);
-    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -1849,8 +1793,6 @@ struct LArgs {
     const float *bo, *g2, *b2n, *b1, *b2, *gn, *bn, *bn2;
     unsigned char *nq, *nk, *nv;
     float* z;
-    float* part;  // SPL: per-workgroup softmax records (TflQueue::part)
-    unsigned* tick;
 };
 
 // RB = 1 (16-row tiles) while the grid fits one round of the CUs, else 2
@@ -1867,11 +1809,10 @@ struct LArgs {
 // 78.2 -> 75.9 us; stage1 B=32 encoder layers 9.9 -> 9.0 and 7.7 -> 7.4 us
 // (profiles/r05/r05af_*).
 constexpr bool tfl_one(int rb) { return TFL_ONE && rb == 1; }
-template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1, bool SPL = false>
+template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     static_assert(RB == 1 || RB == 2 || RB == 4, "16-, 32- or 64-row tiles");
     static_assert(QV != 9 || !MASKED, "the wave-specialised attention is unmasked-only");
-    static_assert(!SPL || RB <= 2, "key-split tiles are 16 or 32 rows");
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
     constexpr bool ONE = tfl_one(RB);
     constexpr int NBQ = 3 * H / 16, NQK = 2 * H / 16;  // QKV' column blocks, of them Q / K
@@ -1892,9 +1833,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     __shared__ __attribute__((aligned(16))) float vec[6 * H + F + (NN > 0 ? NN : 4)];
     __shared__ int item;
     int b, tile;
-    claim_tile(a.B, SPL ? 2 * a.ntile : a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
-    const int half = SPL ? tile & 1 : 0;  // SPL: which half of the keys
-    if constexpr (SPL) tile >>= 1;
+    claim_tile(a.B, a.ntile, a.qcnt, a.qseq, &item, &b, &tile);
     const int t0 = tile * TR, N = a.dN ? dev_frames(a.dN, a.N) : a.N;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, gq = lane >> 4;
     const QkvOut qo{a.nq, a.nk, a.nv, a.npad, a.npad / KC, MASKED ? 1.f : a.sl2};
@@ -1939,17 +1878,13 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         __syncthreads();
         TSTAMP(2);
     } else {
-        const bool go = attention_tile<H, HD, MASKED, RB, SPL>(
-            a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs,
-            [&] {
-                if (wave < H / 16) so.load(a.Wo, wave);
-                if constexpr (ONE) {
-                    if (wave < F / 16) s1.load(a.W1, wave);
-                    if (wave + NW < F / 16) s1b.load(a.W1, wave + NW);
-                }
-            },
-            Split{a.part, a.tick, b * a.ntile + tile, half});
-        if (!go) return;  // SPL: the other half's workgroup finishes the tile
+        attention_tile<H, HD, MASKED, RB>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, xs, [&] {
+            if (wave < H / 16) so.load(a.Wo, wave);
+            if constexpr (ONE) {
+                if (wave < F / 16) s1.load(a.W1, wave);
+                if (wave + NW < F / 16) s1b.load(a.W1, wave + NW);
+            }
+        });
     }
     const size_t row0 = (size_t)b * N + t0;
     // o = x + att . Wo^T + bo
@@ -2295,28 +2230,6 @@ int tfl_qs2(int H) {
     return H / tfl::HEADS >= 48 ? 9 : 4;
 }
 int tfl_ntile(int N, int rb) { return (tfl_npad(N) + tfl::TQ * rb - 1) / (tfl::TQ * rb); }
-// Key-split tiles (layer_kernel SPL): on a grid of at most one workgroup per
-// CU every workgroup reads all of its utterance's K / V (two bytes per
-// element and plane) at the CU's L2 rate - the 16-row tiles' attention at
-// B=8 T=500 moves 448 KB per workgroup in ~12k cycles (~37 B/clk, the rate
-// tools/probe/l2bw.hip measures).  Two workgroups per tile, each on two of
-// the four key quarters, halve that (bit-identical results); the smallest
-// tile (16, else 32 rows) whose doubled grid still fits one round (and the
-// record buffer) is taken, from 8 chunks of live keys on (M2_TFL_SPLIT=0
-// never, 1 whenever a tile fits).
-constexpr int kTflSplitMinChunks = 8;
-bool tfl_split(int B, int N, const TflQueue& q, int& rb) {
-    const int mode = sw().tfl_split;
-    if (!q.tick || !q.part || mode == 0 || rb == 4) return false;
-    const long t16 = (long)B * (tfl_npad(N) / tfl::TQ);
-    if (mode < 0 && (sw().tfl_rb || t16 > 256 || (N + tfl::KC - 1) / tfl::KC < kTflSplitMinChunks)) return false;
-    for (int r = rb; r <= 2; r *= 2)
-        if ((long)B * tfl_ntile(N, r) <= kTflSplitTiles) {
-            rb = r;
-            return true;
-        }
-    return false;
-}
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * tfl_ntile(N, rb)); }
 float tfl_sl2(int H) {
     const float scale = (float)(1.0 / std::sqrt((double)(H / tfl::HEADS)));  // components.py:52, fp32 at the mul
@@ -2409,11 +2322,8 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.N = N;
     a.dN = dN;
     a.npad = tfl_npad(N);
-    int rb = tfl_rb(B, N);
-    const bool spl = tfl_split(B, N, q, rb);
+    const int rb = tfl_rb(B, N);
     a.ntile = tfl_ntile(N, rb);
-    a.part = q.part;
-    a.tick = q.tick;
     a.qcnt = q.cnt;
     a.qseq = q.seq;
     a.sl2 = tfl_sl2(H);
@@ -2439,7 +2349,7 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nk = out.k;
     a.nv = out.v;
     a.z = z;
-    const dim3 grid(B * a.ntile * (spl ? 2 : 1)), blk(tfl::NW * 64);
+    const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
     // form 9 is unmasked-only, and keeps the softmax base as an f16 pair: a
     // masked launch, or a layer whose scores may leave the f16 range, runs the
     // lean two-block form (3) instead
@@ -2447,12 +2357,6 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     if (qs2 == 9 && (masked || w.wide_scores)) qs2 = 3;
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
-        if (spl) {                                                                              \
-            if (rb == 2) hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 2, 1, true>), grid, blk, 0, st, a); \
-            else hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 1, 1, true>), grid, blk, 0, st, a);      \
-            M2_LAUNCHED("tfl layer_kernel");                                                    \
-            return M2_OK;                                                                       \
-        }                                                                                       \
         if constexpr (!MM) {                                                                    \
             if (rb == 4 && qs2 == 9) {                                                          \
                 hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 9>), grid, blk, 0, st, a); \
