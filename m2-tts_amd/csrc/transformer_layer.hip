@@ -346,6 +346,40 @@ __device__ __forceinline__ void qkv_phase(const unsigned char* Xn, const u32x4* 
     }
 }
 
+// The 16-row tiles' QKV projection with every strip of the wave requested
+// beforehand (qkv_strips): no strip load on the chain between the blocks.
+template <int H>
+struct QkvStrips {
+    static constexpr int NB = 3 * H / 16, NK = (NB + NW - 1) / NW;
+    Strip<H> s[NK];
+    __device__ __forceinline__ void load(const u32x4* __restrict__ W) {
+        const int wave = threadIdx.x >> 6;
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+            if (wave + NW * k < NB) s[k].load(W, wave + NW * k);
+    }
+};
+template <int H, int HD>
+__device__ __forceinline__ void qkv_phase_pre(const unsigned char* Xn, const QkvStrips<H>& sq, const QkvOut& o, int b,
+                                              int t0, int N) {
+    constexpr int NQK = 2 * H / 16;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < QkvStrips<H>::NK; ++k) {
+        const int nb = wave + NW * k;
+        if (nb < QkvStrips<H>::NB) {
+            f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+            if (nb < NQK) {
+                gemm_t<H, 1>(Xn, sq.s[k], acc);
+                store_qk<H, HD>(o, b, t0, N, nb, acc[0]);
+            } else {
+                gemm_n<H, 1>(Xn, sq.s[k], acc);
+                store_v<H, HD>(o, b, t0, N, nb, acc[0]);
+            }
+        }
+    }
+}
+
 // A tile wholly past the utterance's end: its rows of the next attention
 // buffers are zeros (no GEMM).
 template <int H, int HD, int RB, int NWV = NW>
@@ -1815,7 +1849,6 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     static_assert(QV != 9 || !MASKED, "the wave-specialised attention is unmasked-only");
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
     constexpr bool ONE = tfl_one(RB);
-    constexpr int NBQ = 3 * H / 16, NQK = 2 * H / 16;  // QKV' column blocks, of them Q / K
     constexpr bool QS = RB == 4;                  // 64-row tiles: K / V staged in LDS
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att, then LN2(o), LN(y) (split)
     // the attention's scratch (key-quarter merge records / the K-V chunk ring)
@@ -1929,14 +1962,12 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     };
     // ONE: the QKV' strips of this wave, requested before FFN1 (the
     // final-projection strip for NEXT 2)
-    Strip<H> sq[(NBQ + NW - 1) / NW];
+    QkvStrips<H> sq;
     if constexpr (ONE) {
         if constexpr (NEXT == 1) {
-#pragma unroll
-            for (int k = 0; k < (NBQ + NW - 1) / NW; ++k)
-                if (wave + NW * k < NBQ) sq[k].load(a.Wn, wave + NW * k);
+            sq.load(a.Wn);
         } else if constexpr (NEXT == 2) {
-            if (wave < NN / 16) sq[0].load(a.Wn, wave);
+            if (wave < NN / 16) sq.s[0].load(a.Wn, wave);
         }
         static_assert(F / 16 <= 2 * NW, "two FFN1 blocks per wave at most");
         if (wave < F / 16) ffn1(wave, s1);
@@ -1977,20 +2008,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         __syncthreads();
         TSTAMP(7);
         if constexpr (ONE) {
-#pragma unroll
-            for (int k = 0; k < (NBQ + NW - 1) / NW; ++k) {
-                const int nb = wave + NW * k;
-                if (nb < NBQ) {
-                    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
-                    if (nb < NQK) {
-                        gemm_t<H, 1>(A, sq[k], acc);
-                        store_qk<H, HD>(qo, b, t0, N, nb, acc[0]);
-                    } else {
-                        gemm_n<H, 1>(A, sq[k], acc);
-                        store_v<H, HD>(qo, b, t0, N, nb, acc[0]);
-                    }
-                }
-            }
+            qkv_phase_pre<H, HD>(A, sq, qo, b, t0, N);
         } else {
             qkv_phase<H, HD, RB>(A, a.Wn, sn, qo, b, t0, N);
         }
@@ -1998,7 +2016,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         TSTAMP_RT(15);
     } else if constexpr (NEXT == 2) {
         Strip<H> sn;
-        if constexpr (ONE) sn = sq[0];
+        if constexpr (ONE) sn = sq.s[0];
         else if (wave < NN / 16) sn.load(a.Wn, wave);
         __syncthreads();
         TSTAMP(6);
@@ -2091,8 +2109,12 @@ __global__ __launch_bounds__(fk_nw(RB) * 64, FK_MINW) void first_kernel(FArgs a)
         zero_tile<H, HD, RB, FNW>(qo, b, t0);
         return;
     }
+    // 16-row tiles (tfl_one): all of the wave's QKV strips at the start
+    constexpr bool ONE = tfl_one(RB) && FNW == NW;
     Strip<H> sq;
-    if (wave < 3 * H / 16) sq.load(a.W, wave);
+    QkvStrips<H> sqa;
+    if constexpr (ONE) sqa.load(a.W);
+    else if (wave < 3 * H / 16) sq.load(a.W, wave);
     for (int e = threadIdx.x; e < H; e += FNW * 64) {
         vec[e] = a.g[e];
         vec[H + e] = a.bln[e];
@@ -2152,7 +2174,8 @@ __global__ __launch_bounds__(fk_nw(RB) * 64, FK_MINW) void first_kernel(FArgs a)
     __syncthreads();
     ln_rows<H, TR, FNW * 64>(O, A, vec, vec + H);
     __syncthreads();
-    qkv_phase<H, HD, RB, FNW>(A, a.W, sq, qo, b, t0, N);
+    if constexpr (ONE) qkv_phase_pre<H, HD>(A, sqa, qo, b, t0, N);
+    else qkv_phase<H, HD, RB, FNW>(A, a.W, sq, qo, b, t0, N);
 }
 
 }  // namespace tfl
