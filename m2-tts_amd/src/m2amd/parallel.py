@@ -413,6 +413,9 @@ class _LaneResult:
         self._res = None
 
     def wait(self):
+        if self._out is not None and self._stream is None:  # host stages: no stream to join
+            self._res = self._out.wait() if isinstance(self._out, PendingGather) else self._out
+            self._out = None
         if self._out is not None:
             # the gather's wait and the assembly of rank 0's outputs run on the
             # lane's stream, where the gathered buffers were allocated
@@ -437,22 +440,33 @@ class ShardedPipeline:
     vocoder, and step i's gather beside step i + 1's compute.  Every rank
     submits the same sequence, so the lanes' collectives are issued in the
     same order everywhere (torch's process group runs them on one
-    communicator stream).  Results are identical to sharded_inference."""
+    communicator stream).  Results are identical to sharded_inference.
+
+    ``model`` may also be a host ``Stages`` (the oracle-backed stages of the
+    CPU tests): the lanes then share it and have no stream; the lane
+    rotation and the in-flight gathers are the same."""
 
     def __init__(self, model, depth: int = 2, group=None, gather_to: Optional[int] = 0):
-        tcap: dict = {}
-        # lanes 1..depth: lane 0 is the model's default handle, which
-        # model.inference() / forward() use on the caller's stream, and a
-        # handle's device state (work-queue counters, frame mailbox, redo
-        # words) is ordered on one stream
-        self.lanes = [(HipStages(model, lane=i + 1, tcap=tcap), torch.cuda.Stream()) for i in range(depth)]
+        if isinstance(model, Stages):
+            self.lanes = [(model, None) for _ in range(depth)]
+        else:
+            tcap: dict = {}
+            # lanes 1..depth: lane 0 is the model's default handle, which
+            # model.inference() / forward() use on the caller's stream, and a
+            # handle's device state (work-queue counters, frame mailbox, redo
+            # words) is ordered on one stream
+            self.lanes = [(HipStages(model, lane=i + 1, tcap=tcap), torch.cuda.Stream()) for i in range(depth)]
         self.group, self.gather_to = group, gather_to
         self._next = 0
 
-    def submit(self, phoneme_ids: Tensor, phoneme_lengths: Optional[Tensor],
+    def submit(self, phoneme_ids: Optional[Tensor], phoneme_lengths: Optional[Tensor],
                duration_scale: float = 1.0) -> _LaneResult:
         st, stream = self.lanes[self._next % len(self.lanes)]
         self._next += 1
+        if stream is None:
+            out = sharded_inference(st, phoneme_ids, phoneme_lengths, duration_scale, group=self.group,
+                                    gather_to=self.gather_to, async_gather=True, one_call_world1=False)
+            return _LaneResult(out, None, None)
         caller = torch.cuda.current_stream(phoneme_ids.device)
         stream.wait_stream(caller)  # the inputs were produced on the caller's stream
         for t in (phoneme_ids, phoneme_lengths):

@@ -5,6 +5,7 @@ the unmasked decoder makes observable."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -121,3 +122,85 @@ def test_shard_bounds_cover_batch():
             assert spans[0][0] == 0 and spans[-1][1] == B
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _global_batch(B: int, seed: int):
+    """B utterances of the s1 fixture's phoneme vocabulary with ragged lengths."""
+    g = torch.Generator().manual_seed(seed)
+    S = 24
+    ids = torch.randint(1, 42, (B, S), generator=g)
+    lens = torch.randint(3, S + 1, (B,), generator=g)
+    lens[0] = S  # one full-length utterance: T_max is set by a known row
+    return ids, lens
+
+
+def _worker_wide(rank, world, port, outfile):
+    """The multi-rank layouts the driver's N = 4 / 8 runs use, each written
+    out per case so the parent compares them with the unsharded oracle."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import numpy as np
+        from m2amd.parallel import ShardedPipeline, sharded_inference
+        torch.set_num_threads(1)
+        st = oracle_stages(golden_state("s1"), orc.STAGE1)
+        big = _global_batch(8 * world, 7)      # 8 utterances per rank
+        small = _global_batch(5, 11)           # B = 5 < world: world - 5 empty shards
+        res = {}
+        res["big_all"] = sharded_inference(st, *big)                       # all_gather
+        res["small_all"] = sharded_inference(st, *small)
+        res["small_to0"] = sharded_inference(st, *small, gather_to=0)      # gather to rank 0 only
+        res["small_src"] = sharded_inference(st, small[0] if rank == 0 else None,
+                                             small[1] if rank == 0 else None, src=0, gather_to=0)
+        res["big_src_s"] = sharded_inference(st, big[0] if rank == 0 else None, big[1] if rank == 0 else None,
+                                             src=0, duration_scale=1.3, gather_to=0)
+        # two global batches in flight: submit, submit, wait, wait (gathers overlap)
+        pipe = ShardedPipeline(st, depth=2, gather_to=0)
+        p1 = pipe.submit(*big)
+        p2 = pipe.submit(*small)
+        p3 = pipe.submit(*big)
+        res["pipe_big"], res["pipe_small"], res["pipe_big2"] = p1.wait(), p2.wait(), p3.wait()
+        for k in ("small_to0", "small_src", "big_src_s", "pipe_big", "pipe_small", "pipe_big2"):
+            assert (res[k][0] is None) == (rank != 0), k
+        if rank == 0:
+            np.savez(outfile, **{f"{k}_{j}": v[j].numpy() for k, v in res.items() for j in range(2)})
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_inference_wide_worlds(tmp_path, world):
+    """the sharded flow at the rank counts of the driver's
+    scaling run, on gloo with the oracle as the stages - B = 8 per rank,
+    B = 5 with empty shards, broadcast from rank 0, gather to rank 0 and
+    ShardedPipeline at depth 2 - each bit-equal to the unsharded oracle
+    (tts_model.py:165-176, 402-438)."""
+    import numpy as np
+    outfile = str(tmp_path / "wide.npz")
+    mp.spawn(_worker_wide, args=(world, _free_port(), outfile), nprocs=world, join=True)
+    z = np.load(outfile)
+    sd = golden_state("s1")
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)  # the ranks' thread count: ATen's CPU reductions split by thread
+    want = {}
+    for tag, (ids, lens), scale in (("big", _global_batch(8 * world, 7), 1.0), ("small", _global_batch(5, 11), 1.0),
+                                    ("big_s", _global_batch(8 * world, 7), 1.3)):
+        mel, audio = orc.inference(sd, orc.STAGE1, ids, lens, duration_scale=scale, as_written=False)
+        # each rank vocodes its own rows: ATen's CPU conv may sum a batch of
+        # one in another order than a larger batch (~1e-6), so the bit-exact
+        # expectation is the oracle vocoder over the same shard layout, on the
+        # full-batch mel; the full-batch audio is checked within 1e-5 below
+        from m2amd.parallel import shard_bounds
+        shards = [shard_bounds(ids.shape[0], world, r) for r in range(world)]
+        audio_sh = torch.cat([orc.vocoder(sd, mel[lo:hi].transpose(1, 2)) for lo, hi in shards if hi > lo])
+        want[tag] = (mel.numpy(), audio_sh.numpy(), audio.numpy())
+    torch.set_num_threads(nt)
+    cases = {"big_all": "big", "small_all": "small", "small_to0": "small", "small_src": "small",
+             "big_src_s": "big_s", "pipe_big": "big", "pipe_small": "small", "pipe_big2": "big"}
+    for k, ref in cases.items():
+        for j in range(2):
+            got, exp = z[f"{k}_{j}"], want[ref][j]
+            assert got.shape == exp.shape, (k, j)
+            assert np.array_equal(got, exp), (k, j, float(abs(got - exp).max()))
+        assert float(abs(z[f"{k}_1"] - want[ref][2]).max()) <= 1e-5, k
