@@ -319,7 +319,11 @@ def cpu_baseline(B: int, S: int, T: int, runs: int = 7, min_s: float = 1.5, ids_
     unstable = lambda d: spread(d) >= 0.2  # noqa: E731
     # value = the median of the runs; the best run (other tenants' load on the
     # shared host only slows a run down) and the spread are reported beside it
+    busy = sorted(r["busy"] for r in voc["runs"])
     return {"value": voc["median"], "best": voc["max"], "unit": "audio samples/s", "cores": len(cpus),
+            "effective_cores": round(busy[len(busy) // 2] * len(cpus), 2),
+            "effective_cores_def": "median over the runs of busy (process CPU s / (wall s x threads)) x threads: "
+                                   "the cores the reference's op sequence actually kept busy",
             "kind": "port",
             "sockets": sockets, "host_logical_cpus": ncpu, "affinity_cpus": aff,
             "physical_cores_in_affinity": len(phys), "cgroup_cpu_quota": quota,
@@ -852,6 +856,13 @@ def run(args):
             f32 = vocoder_line(cx, "s1", B, 5 * S, args, 100.0, 1000, f32=True)
             extras["vocoder_exact_f32"] = {k: f32[k] for k in ("value", "ms_per_step", "dtype", "roofline",
                                                               "vocoder_kernels", "vocoder_tflops")}
+            # the strict-fp32 figure's own roofline at the top level (fp32 MFMA
+            # peak 157.3 TF): the credited number for a reader who does not
+            # accept the split-f16 arithmetic
+            strict = f32.get("roofline")
+            if strict:
+                strict = {**strict, "value": f32["value"], "ms_per_step": f32["ms_per_step"], "dtype": f32["dtype"]}
+            extras["roofline_exact_f32"] = strict
         if wl != "s2_vocoder":
             s2v = vocoder_line(cx, "s2", 8, 500, args, 100.0, 3000)
             extras["s2_vocoder_b8_t500"] = s2v
@@ -894,6 +905,10 @@ def run(args):
         if k in head:
             out[k] = head[k]
     out.update(extras)
+    # the driver keeps only the contract keys of the line: the strict-fp32
+    # roofline rides inside `roofline` so it reaches the record
+    if isinstance(out.get("roofline"), dict) and extras.get("roofline_exact_f32"):
+        out["roofline"]["exact_f32"] = extras["roofline_exact_f32"]
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("vocoder", "pipeline"):
         pipe = out.get("pipeline") if wl == "vocoder" else head

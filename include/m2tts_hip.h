@@ -183,14 +183,21 @@ size_t m2_vocoder_chunk_workspace_bytes(const m2_model* model, int32_t B, int32_
  *     next m2_vocoder / m2_inference* call on the model returns M2_E_RANGE
  *     (and clears the flag); m2_model_check synchronises `stream` and
  *     reports it at once (*flagged = 1, flag cleared).
- *   policy 1 (fallback): the call is recomputed on the exact-f32 kernels
- *     when its split audio came out non-finite (the reference's fp32 result,
- *     non-finite only if the reference's is).  With the fused vocoder kernels
- *     (the model's own shapes) this happens on the device, without a host
- *     wait: the split kernels raise a device flag word and the exact-f32
- *     kernels, enqueued behind them, return at once unless it is raised (two
- *     words alternate between calls; the next call's first kernel zeroes the
- *     other).  Otherwise m2_vocoder synchronises `stream` and re-runs. */
+ *   policy 1 (fallback): the non-finite part of the call is recomputed in
+ *     fp32 on the device, without a host wait.  On the pipelined tails (the
+ *     stage1 / stage2 split-f16 defaults) each workgroup whose strip stored a
+ *     non-finite sample recomputes only that strip's frames inside the tail
+ *     launch by direct fp32 convolution in the reference's layer order
+ *     (csrc/vocoder_redo.h): the reference's op sequence in fp32, in another
+ *     summation order than the exact-f32 kernels, so within the
+ *     reference-conditioned tolerance of tests/test_gpu_range.py, NOT
+ *     bit-equal to them; non-finite only if the reference's result is.
+ *     M2_REDO_LAUNCH=1 (and the windowed x3 tails) instead enqueue the
+ *     guarded exact-f32 launch behind the split kernels (it returns at once
+ *     unless their device flag word is raised; two words alternate between
+ *     calls, the next call's first kernel zeroes the other), whose output is
+ *     bit-equal to the exact-f32 kernels.  Other shapes: m2_vocoder
+ *     synchronises `stream` and re-runs the call on the exact-f32 kernels. */
 int32_t m2_set_range_policy(m2_model* model, int32_t policy);
 int32_t m2_model_check(m2_model* model, void* stream, int32_t* flagged);
 
