@@ -429,50 +429,183 @@ class _LaneResult:
         return self._res
 
 
+class _SplitStep:
+    """A step of ShardedPipeline's split-stream schedule: ``wait()`` reads T
+    (posted by the back half's first launch), joins the step's back-half
+    event into the caller's stream and returns (mel, audio) (None on
+    non-destination ranks).  A step whose T outgrew the capacity is re-run
+    on the host-T path (every rank sees the same T and capacity)."""
+
+    def __init__(self, pipe, lane, **kw):
+        self.pipe, self.lane = pipe, lane
+        self.__dict__.update(kw)
+        self._res = None
+
+    def wait(self):
+        if self._res is not None:
+            return self._res
+        p = self.pipe
+        if p._pending[self.lane] is self:
+            p._pending[self.lane] = None
+        caller = self.caller
+        caller.wait_event(self.done)
+        st = p.lanes[self.lane]
+        T = self.hm.frames_wait() if self.b else max(1, int(self.tw.item()))
+        _learn_cap(st.tcap, self.key, T)
+        if T > self.cap:  # rare: re-run the step for the exact T on the host-T path
+            if self.work is not None:
+                self.work.wait()
+            with torch.no_grad():
+                out = sharded_inference(st, self.ids, self.lens, self.scale, group=p.group,
+                                        gather_to=p.gather_to, one_call_world1=False, device_T=False)
+            self._res = out
+            return out
+        if self.work is not None:
+            self.work.wait()  # the caller's stream waits for the gather
+        M, moff, B, world = self.M, self.moff, self.B, self.world
+
+        def view(flat, n):
+            return flat[: n * T * M].view(n, T, M), flat[moff: moff + n * 64 * T].view(n, 1, 64 * T)
+
+        if world == 1:
+            self.buf.record_stream(caller)
+            self._res = view(self.buf, self.b)
+        elif self.parts is None:
+            self._res = (None, None)
+        else:
+            counts = [shard_bounds(B, world, r)[1] - shard_bounds(B, world, r)[0] for r in range(world)]
+            for t in self.parts:
+                t.record_stream(caller)
+            vs = [view(self.parts[r], counts[r]) for r in range(world) if counts[r]]
+            self._res = (torch.cat([v[0] for v in vs]), torch.cat([v[1] for v in vs]))
+        return self._res
+
+
 class ShardedPipeline:
     """Sharded inference with ``depth`` global batches in flight per rank.
 
-    Each lane has its own model handle and HIP stream; ``submit`` runs one
-    step (sharded_inference on the device-T path, gather left in flight) on
-    the next lane and returns at once with a _LaneResult.  Step i + 1's
-    front half (encoder, durations: small launches that leave most CUs idle
-    at a per-GPU share of 8 utterances) then runs beside step i's decoder and
-    vocoder, and step i's gather beside step i + 1's compute.  Every rank
-    submits the same sequence, so the lanes' collectives are issued in the
-    same order everywhere (torch's process group runs them on one
-    communicator stream).  Results are identical to sharded_inference.
+    Two streams per pipeline, shared by all lanes: every step's front half
+    (encoder, durations, the shard's T_max into a device word) and the ranks'
+    all_reduce(MAX) of that word go on the FRONT stream, its back half
+    (expansion, decoder, vocoder reading T from the word) and the gather of
+    mel / audio on the BACK stream, behind an event of its front half.  So
+    step i + 1's front half (a few small launches: 50 workgroups at configs[3]'s
+    8-utterance share) runs beside step i's back half, and the back halves run
+    back to back.  Each lane has its own model handle (a handle's front
+    buffer, workspace and device words are reused by its next step, whose
+    front half waits for this step's back-half event).  With several ranks
+    the gathers use a communicator of their own, so step i + 1's T exchange
+    is not queued behind step i's gather.  ``submit`` returns at once; the
+    device-T path needs a capacity, so the first step of a (B, S) shape runs
+    as one sharded_inference on the back stream.  Every rank submits the
+    same sequence, so the collectives of each communicator are issued in the
+    same order everywhere.  Results are identical to sharded_inference.
 
     ``model`` may also be a host ``Stages`` (the oracle-backed stages of the
     CPU tests): the lanes then share it and have no stream; the lane
     rotation and the in-flight gathers are the same."""
 
     def __init__(self, model, depth: int = 2, group=None, gather_to: Optional[int] = 0):
-        if isinstance(model, Stages):
-            self.lanes = [(model, None) for _ in range(depth)]
-        else:
-            tcap: dict = {}
-            # lanes 1..depth: lane 0 is the model's default handle, which
-            # model.inference() / forward() use on the caller's stream, and a
-            # handle's device state (work-queue counters, frame mailbox, redo
-            # words) is ordered on one stream
-            self.lanes = [(HipStages(model, lane=i + 1, tcap=tcap), torch.cuda.Stream()) for i in range(depth)]
         self.group, self.gather_to = group, gather_to
         self._next = 0
+        self.host = isinstance(model, Stages)
+        if self.host:
+            self.lanes = [model for _ in range(depth)]
+            return
+        tcap: dict = {}
+        # lanes 1..depth: lane 0 is the model's default handle, which
+        # model.inference() / forward() use on the caller's stream
+        self.lanes = [HipStages(model, lane=i + 1, tcap=tcap) for i in range(depth)]
+        self.front_stream, self.back_stream = torch.cuda.Stream(), torch.cuda.Stream()
+        self._pending = [None] * depth
+        self._free = [None] * depth  # per lane: event after its last back half
+        self._tw = [None] * depth
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.ggroup = None
+        if world > 1:  # collective: every rank constructs the pipeline
+            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
+            self.ggroup = dist.new_group(ranks=ranks)
 
     def submit(self, phoneme_ids: Optional[Tensor], phoneme_lengths: Optional[Tensor],
-               duration_scale: float = 1.0) -> _LaneResult:
-        st, stream = self.lanes[self._next % len(self.lanes)]
+               duration_scale: float = 1.0):
+        h = self._next % len(self.lanes)
         self._next += 1
-        if stream is None:
+        st = self.lanes[h]
+        if self.host:
             out = sharded_inference(st, phoneme_ids, phoneme_lengths, duration_scale, group=self.group,
                                     gather_to=self.gather_to, async_gather=True, one_call_world1=False)
             return _LaneResult(out, None, None)
-        caller = torch.cuda.current_stream(phoneme_ids.device)
-        stream.wait_stream(caller)  # the inputs were produced on the caller's stream
+        if self._pending[h] is not None:  # the lane's buffers are reused below
+            self._pending[h].wait()
+        dev = phoneme_ids.device
+        caller = torch.cuda.current_stream(dev)
+        B, S = phoneme_ids.shape
+        key = (B, S, float(duration_scale))
+        cap = st.tcap.get(key, 0)
+        hm = st.dev_handle(dev, cap) if cap > 0 else None
+        fs, bs = self.front_stream, self.back_stream
+        fs.wait_stream(caller)  # the inputs were produced on the caller's stream
+        if self._free[h] is not None:
+            fs.wait_event(self._free[h])
         for t in (phoneme_ids, phoneme_lengths):
             if t is not None:
-                t.record_stream(stream)
-        with torch.cuda.stream(stream):
-            out = sharded_inference(st, phoneme_ids, phoneme_lengths, duration_scale, group=self.group,
-                                    gather_to=self.gather_to, async_gather=True, one_call_world1=False)
-        return _LaneResult(out, stream, caller)
+                t.record_stream(fs)
+                t.record_stream(bs)
+        if hm is None:  # no capacity yet: one whole step on the back stream
+            bs.wait_stream(fs)
+            with torch.cuda.stream(bs):
+                out = sharded_inference(st, phoneme_ids, phoneme_lengths, duration_scale, group=self.group,
+                                        gather_to=self.gather_to, async_gather=True, one_call_world1=False)
+            ev = torch.cuda.Event()
+            ev.record(bs)
+            self._free[h] = ev
+            return _LaneResult(out, bs, caller)
+        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        rank = dist.get_rank(self.group) if dist.is_initialized() else 0
+        lo, hi = shard_bounds(B, world, rank)
+        b = hi - lo
+        M = st.mel_channels()
+        if self._tw[h] is None:
+            self._tw[h] = torch.empty(1, dtype=torch.int32, device=dev)
+        tw = self._tw[h]
+        lens = phoneme_lengths
+        with torch.no_grad():
+            with torch.cuda.stream(fs):
+                state = hm.inference_front_dev(phoneme_ids[lo:hi], lens[lo:hi] if lens is not None else None,
+                                               duration_scale, tw) if b else None
+                if not b:
+                    tw.zero_()
+                if world > 1:
+                    if dist.get_backend(self.group) == "nccl":
+                        dist.all_reduce(tw, op=dist.ReduceOp.MAX, group=self.group)
+                    else:  # gloo: staged through the host
+                        t = tw.cpu()
+                        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                        tw.copy_(t)
+            ev = torch.cuda.Event()
+            ev.record(fs)
+            bs.wait_event(ev)
+            rows = -(-B // world) if world > 1 else b
+            moff = (rows * cap * M + 63) // 64 * 64
+            parts, work = None, None
+            with torch.cuda.stream(bs):
+                buf = torch.empty(moff + rows * 64 * cap, dtype=torch.float32, device=dev)
+                if b:
+                    hm.inference_back_dev(state, cap, tw, buf[: b * cap * M], buf[moff: moff + b * 64 * cap])
+                if world > 1:
+                    me = dist.get_rank(self.ggroup)
+                    if self.gather_to is None or me == self.gather_to:
+                        parts = [torch.empty_like(buf) for _ in range(world)]
+                    if self.gather_to is None:
+                        work = dist.all_gather(parts, buf, group=self.ggroup, async_op=True)
+                    else:
+                        dst = dist.get_global_rank(self.ggroup, self.gather_to)
+                        work = dist.gather(buf, parts, dst=dst, group=self.ggroup, async_op=True)
+            done = torch.cuda.Event()
+            done.record(bs)
+        self._free[h] = done
+        step = _SplitStep(self, h, caller=caller, done=done, hm=hm, b=b, tw=tw, key=key, cap=cap, work=work,
+                          ids=phoneme_ids, lens=phoneme_lengths, scale=duration_scale, M=M, moff=moff, B=B,
+                          world=world, buf=buf, parts=parts)
+        self._pending[h] = step
+        return step
