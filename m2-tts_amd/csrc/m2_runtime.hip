@@ -1299,7 +1299,13 @@ constexpr int kMaxDevices = 64;
 std::mutex g_mb_mu;
 LrMailbox g_mb[kMaxDevices];
 
-int32_t mailbox_for(int dev, LrMailbox** out) {
+// The mailbox's device ticket is zeroed on the caller's stream `st` (and
+// waited for): a blocking hipMemset would go to the null stream, which a
+// non-blocking stream (e.g. a torch side stream) does not wait for, so the
+// first count kernel could take its ticket before the zero landed and never
+// post (seen as "stream idle but T_max not posted" on a first call from a
+// side stream).
+int32_t mailbox_for(int dev, hipStream_t st, LrMailbox** out) {
     LrMailbox& mb = g_mb[dev];
     if (!mb.host) {
         int cur = 0;
@@ -1311,8 +1317,9 @@ int32_t mailbox_for(int dev, LrMailbox** out) {
         if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
         void* t = nullptr;
         if (e == hipSuccess) e = hipMalloc(&t, sizeof(unsigned));
-        if (e == hipSuccess) e = hipMemset(t, 0, sizeof(unsigned));
         (void)hipSetDevice(cur);
+        if (e == hipSuccess) e = hipMemsetAsync(t, 0, sizeof(unsigned), st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return hip_status(e, "m2_length_regulator_count_sync: mailbox allocation");
         std::memset(h, 0, 64);
         mb.host = static_cast<int32_t*>(h);
@@ -1366,7 +1373,7 @@ int32_t m2_length_regulator_count_sync(const void* dur, int32_t dur_is_int, floa
     if (rc0) return rc0;
     std::lock_guard<std::mutex> lk(g_mb_mu);
     LrMailbox* mb = nullptr;
-    int32_t rc = mailbox_for(dev, &mb);
+    int32_t rc = mailbox_for(dev, st, &mb);
     if (rc) return rc;
     mb->seq = mb->seq == INT_MAX ? 1 : mb->seq + 1;
     const int32_t seq = mb->seq;
@@ -1999,7 +2006,7 @@ int32_t m2_inference(const m2_model* m, const int64_t* ids, const int64_t* lengt
         if ((rc = stream_device(st, &dev))) return rc;
         std::lock_guard<std::mutex> lk(g_mb_mu);
         LrMailbox* mb = nullptr;
-        if ((rc = mailbox_for(dev, &mb))) return rc;
+        if ((rc = mailbox_for(dev, st, &mb))) return rc;
         mb->seq = mb->seq == INT_MAX ? 1 : mb->seq + 1;
         const int32_t seq = mb->seq;
         const CountFuse cf{scale, nullptr, mb->ticket, mb->dev, seq};

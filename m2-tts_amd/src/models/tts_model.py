@@ -244,16 +244,19 @@ class M2TTSModel(nn.Module):
         """The split-f16 vocoder carries fp32 values as f16 hi/lo pairs; an
         input or activation of magnitude >= 65520 turns its audio non-finite
         (never silently wrong).  "fallback" (the default, also without this
-        call; M2_RANGE_POLICY overrides it for new handles): a vocoder call
-        whose split audio is not finite is recomputed on the exact-f32 kernels
-        before anything behind it on the stream runs, so a call never returns
-        non-finite audio for an input the reference's fp32 path handles - on
-        the device, without a host wait (the exact kernels are enqueued behind
-        the split ones and return at once unless the call was flagged; their
-        empty launches are the per-call cost, bench.py's
-        ``vocoder_default_policy``).
-        "report" (opt-in, what the throughput benchmarks use): asynchronous -
-        the next call raises, check_numerics() reports it at once."""
+        call; M2_RANGE_POLICY overrides it for new handles): the non-finite
+        part of a vocoder call is recomputed in fp32 on the device before
+        anything behind it on the stream runs, so a call never returns
+        non-finite audio for an input the reference's fp32 path handles.  On
+        the pipelined tails (the defaults) each strip whose split audio is not
+        finite is recomputed inside the tail launch by direct fp32 convolution
+        in the reference's layer order (within the reference-conditioned
+        tolerance, not bit-equal to the exact-f32 kernels); M2_REDO_LAUNCH=1
+        and the windowed tails use the guarded exact-f32 launch behind the
+        split kernels instead (bit-equal to those kernels).  The per-call cost
+        is bench.py's ``vocoder_report_policy`` difference.
+        "report" (opt-in): asynchronous - the next call raises,
+        check_numerics() reports it at once."""
         if policy not in runtime.RANGE_POLICIES:
             raise ValueError(f"range policy {policy!r}: expected one of {sorted(runtime.RANGE_POLICIES)}")
         self.__dict__["_m2_range_policy"] = policy

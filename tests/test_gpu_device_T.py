@@ -412,3 +412,42 @@ def test_duration_persistent_tiles(gpu, stage, B, S, monkeypatch):
         enc, _ = orc.text_encoder(sd, cfg, ids.cpu(), lens.cpu())
         dref = orc.duration_predictor(sd, enc)
     assert maxabs(d, dref) <= 1e-4
+
+
+_FIRST_CALL_SIDE_STREAM = r"""
+import sys, torch
+sys.path[:0] = [sys.argv[1] + "/m2-tts_amd/src", sys.argv[1] + "/tests", sys.argv[1] + "/oracle"]
+from test_gpu_device_T import build_model
+from m2amd.parallel import ShardedPipeline
+dev = torch.device("cuda", 0)
+m = build_model("s2", dev)
+g = torch.Generator().manual_seed(9)
+ids = torch.randint(0, 42, (8, 100), generator=g).to(dev)
+lens = torch.randint(30, 101, (8,), generator=g).to(dev)
+pipe = ShardedPipeline(m, depth=2)
+outs = [pipe.submit(ids, lens) for _ in range(2)]   # the process's first library calls: side streams
+outs = [o.wait() for o in outs]
+ref = m.inference(ids, lens)
+assert all(torch.equal(o[0], ref[0]) and torch.equal(o[1], ref[1]) for o in outs)
+side = torch.cuda.Stream()
+with torch.cuda.stream(side):
+    mel, audio = m.inference(ids, lens)
+torch.cuda.current_stream().wait_stream(side)
+assert torch.equal(mel, ref[0]) and torch.equal(audio, ref[1])
+print("ok")
+"""
+
+
+def test_first_call_from_a_side_stream(gpu):
+    """The process's first T_max read from a non-blocking stream
+    (ShardedPipeline's first submit): the per-device mailbox ticket is zeroed
+    on the caller's stream, not by a null-stream memset that stream does not
+    wait for (which left the first count kernel without its post: "stream
+    idle but T_max not posted").  A fresh process, so the mailbox is new."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parents[1])
+    p = subprocess.run([sys.executable, "-c", _FIRST_CALL_SIDE_STREAM, root], capture_output=True, text=True,
+                       timeout=180)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-2000:]
