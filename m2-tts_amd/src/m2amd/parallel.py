@@ -38,8 +38,12 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Any, Callable, Optional, Tuple
 
+import ctypes
+
 import torch
 import torch.distributed as dist
+
+from . import _lib
 
 Tensor = torch.Tensor
 
@@ -436,9 +440,13 @@ class _SplitStep:
     non-destination ranks).  A step whose T outgrew the capacity is re-run
     on the host-T path (every rank sees the same T and capacity)."""
 
-    def __init__(self, pipe, lane, **kw):
-        self.pipe, self.lane = pipe, lane
-        self.__dict__.update(kw)
+    __slots__ = ("pipe", "lane", "caller", "bind", "b", "key", "cap", "work", "ids", "lens", "scale", "moff", "B",
+                 "world", "buf", "parts", "_res")
+
+    def __init__(self, pipe, lane, caller, bind, b, key, cap, work, ids, lens, scale, moff, B, world, buf, parts):
+        self.pipe, self.lane, self.caller, self.bind, self.b, self.key, self.cap = pipe, lane, caller, bind, b, key, cap
+        self.work, self.ids, self.lens, self.scale, self.moff, self.B = work, ids, lens, scale, moff, B
+        self.world, self.buf, self.parts = world, buf, parts
         self._res = None
 
     def wait(self):
@@ -448,9 +456,14 @@ class _SplitStep:
         if p._pending[self.lane] is self:
             p._pending[self.lane] = None
         caller = self.caller
-        caller.wait_event(self.done)
+        caller.wait_event(p._done[self.lane])
         st = p.lanes[self.lane]
-        T = self.hm.frames_wait() if self.b else max(1, int(self.tw.item()))
+        if self.b:
+            T = ctypes.c_int32(0)
+            _lib.check(p._wait_fn(self.bind.handle, p._bs_h, ctypes.byref(T)), "m2_frames_wait")
+            T = int(T.value)
+        else:
+            T = max(1, int(self.bind.tw.item()))
         _learn_cap(st.tcap, self.key, T)
         if T > self.cap:  # rare: re-run the step for the exact T on the host-T path
             if self.work is not None:
@@ -462,13 +475,12 @@ class _SplitStep:
             return out
         if self.work is not None:
             self.work.wait()  # the caller's stream waits for the gather
-        M, moff, B, world = self.M, self.moff, self.B, self.world
+        M, moff, B, world = p._M, self.moff, self.B, self.world
 
         def view(flat, n):
             return flat[: n * T * M].view(n, T, M), flat[moff: moff + n * 64 * T].view(n, 1, 64 * T)
 
         if world == 1:
-            self.buf.record_stream(caller)
             self._res = view(self.buf, self.b)
         elif self.parts is None:
             self._res = (None, None)
@@ -479,6 +491,20 @@ class _SplitStep:
             vs = [view(self.parts[r], counts[r]) for r in range(world) if counts[r]]
             self._res = (torch.cat([v[0] for v in vs]), torch.cat([v[1] for v in vs]))
         return self._res
+
+
+class _LaneBind:
+    """A lane's handle and buffers for one (B, S, scale, capacity): the
+    library is called with these raw pointers and the pipeline's raw stream
+    handles (no per-step wrapper work)."""
+
+    def __init__(self, hm, b, S, cap, dev):
+        self.hm, self.handle = hm, hm.handle
+        self.front = hm._scratch("_front", hm._size("m2_front_bytes", max(b, 1), S))
+        self.ws = hm._scratch("_ws", hm._size("m2_inference_workspace_bytes", max(b, 1), S, cap))
+        self.tw = torch.empty(1, dtype=torch.int32, device=dev)
+        self.args = (self.front.data_ptr(), self.front.numel(), self.ws.data_ptr(), self.ws.numel(),
+                     self.tw.data_ptr())
 
 
 class ShardedPipeline:
@@ -500,6 +526,10 @@ class ShardedPipeline:
     as one sharded_inference on the back stream.  Every rank submits the
     same sequence, so the collectives of each communicator are issued in the
     same order everywhere.  Results are identical to sharded_inference.
+    A step calls the library with raw pointers on the two streams' raw
+    handles (the host enqueue is ~0.1 ms per step at configs[3]'s share,
+    under its GPU time); the weights are re-validated every step (the
+    model's handle cache), as ``inference()`` does.
 
     ``model`` may also be a host ``Stages`` (the oracle-backed stages of the
     CPU tests): the lanes then share it and have no stream; the lane
@@ -517,14 +547,24 @@ class ShardedPipeline:
         # model.inference() / forward() use on the caller's stream
         self.lanes = [HipStages(model, lane=i + 1, tcap=tcap) for i in range(depth)]
         self.front_stream, self.back_stream = torch.cuda.Stream(), torch.cuda.Stream()
+        self._fs_h, self._bs_h = self.front_stream.cuda_stream, self.back_stream.cuda_stream
         self._pending = [None] * depth
-        self._free = [None] * depth  # per lane: event after its last back half
-        self._tw = [None] * depth
-        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._front_ev = [torch.cuda.Event() for _ in range(depth)]
+        self._done = [torch.cuda.Event() for _ in range(depth)]
+        self._used = [False] * depth  # a lane's done event has been recorded
+        self._binds = [{} for _ in range(depth)]
+        self._M = self.lanes[0].mel_channels()
+        lib = _lib.load()
+        self._front_fn, self._back_fn, self._wait_fn = (lib.m2_inference_front_dev, lib.m2_inference_back_dev,
+                                                        lib.m2_frames_wait)
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.ggroup = None
-        if world > 1:  # collective: every rank constructs the pipeline
-            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
+        self._nccl = False
+        if self.world > 1:  # collective: every rank constructs the pipeline
+            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.world))
             self.ggroup = dist.new_group(ranks=ranks)
+            self._nccl = dist.get_backend(group) == "nccl"
 
     def submit(self, phoneme_ids: Optional[Tensor], phoneme_lengths: Optional[Tensor],
                duration_scale: float = 1.0):
@@ -542,57 +582,70 @@ class ShardedPipeline:
         B, S = phoneme_ids.shape
         key = (B, S, float(duration_scale))
         cap = st.tcap.get(key, 0)
+        # the lane's handle, re-validated against the model's weights every step
         hm = st.dev_handle(dev, cap) if cap > 0 else None
         fs, bs = self.front_stream, self.back_stream
         fs.wait_stream(caller)  # the inputs were produced on the caller's stream
-        if self._free[h] is not None:
-            fs.wait_event(self._free[h])
-        for t in (phoneme_ids, phoneme_lengths):
-            if t is not None:
-                t.record_stream(fs)
-                t.record_stream(bs)
+        if self._used[h]:
+            fs.wait_event(self._done[h])
         if hm is None:  # no capacity yet: one whole step on the back stream
+            for t in (phoneme_ids, phoneme_lengths):
+                if t is not None:
+                    t.record_stream(bs)
             bs.wait_stream(fs)
             with torch.cuda.stream(bs):
                 out = sharded_inference(st, phoneme_ids, phoneme_lengths, duration_scale, group=self.group,
                                         gather_to=self.gather_to, async_gather=True, one_call_world1=False)
-            ev = torch.cuda.Event()
-            ev.record(bs)
-            self._free[h] = ev
+            self._done[h].record(bs)
+            self._used[h] = True
             return _LaneResult(out, bs, caller)
-        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
-        rank = dist.get_rank(self.group) if dist.is_initialized() else 0
-        lo, hi = shard_bounds(B, world, rank)
+        world, M = self.world, self._M
+        lo, hi = shard_bounds(B, world, self.rank)
         b = hi - lo
-        M = st.mel_channels()
-        if self._tw[h] is None:
-            self._tw[h] = torch.empty(1, dtype=torch.int32, device=dev)
-        tw = self._tw[h]
+        bind = self._binds[h].get((key, cap))
+        if bind is None or bind.hm is not hm:
+            if bind is not None:  # the weights changed: a new handle
+                self._binds[h].clear()
+            bind = self._binds[h][(key, cap)] = _LaneBind(hm, b, S, cap, dev)
+        fr, fn, wsp, wsn, twp = bind.args
+        ids = phoneme_ids if phoneme_ids.dtype == torch.int64 and phoneme_ids.is_contiguous() else \
+            phoneme_ids.to(torch.int64).contiguous()
         lens = phoneme_lengths
+        if lens is not None and (lens.dtype != torch.int64 or not lens.is_contiguous()):
+            lens = lens.to(torch.int64).contiguous()
+        for t in (ids, lens):
+            if t is not None:
+                t.record_stream(fs)
         with torch.no_grad():
-            with torch.cuda.stream(fs):
-                state = hm.inference_front_dev(phoneme_ids[lo:hi], lens[lo:hi] if lens is not None else None,
-                                               duration_scale, tw) if b else None
-                if not b:
-                    tw.zero_()
-                if world > 1:
-                    if dist.get_backend(self.group) == "nccl":
-                        dist.all_reduce(tw, op=dist.ReduceOp.MAX, group=self.group)
-                    else:  # gloo: staged through the host
-                        t = tw.cpu()
-                        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-                        tw.copy_(t)
-            ev = torch.cuda.Event()
-            ev.record(fs)
-            bs.wait_event(ev)
+            if b:
+                _lib.check(self._front_fn(bind.handle, ids.data_ptr() + lo * S * 8,
+                                          None if lens is None else lens.data_ptr() + lo * 8, b, S,
+                                          float(duration_scale), fr, fn, wsp, wsn, twp, self._fs_h),
+                           "m2_inference_front_dev")
+            if world > 1 or not b:
+                with torch.cuda.stream(fs):
+                    if not b:
+                        bind.tw.zero_()
+                    if world > 1:
+                        if self._nccl:
+                            dist.all_reduce(bind.tw, op=dist.ReduceOp.MAX, group=self.group)
+                        else:  # gloo: staged through the host
+                            t = bind.tw.cpu()
+                            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                            bind.tw.copy_(t)
+            self._front_ev[h].record(fs)
+            bs.wait_event(self._front_ev[h])
             rows = -(-B // world) if world > 1 else b
             moff = (rows * cap * M + 63) // 64 * 64
+            buf = torch.empty(moff + rows * 64 * cap, dtype=torch.float32, device=dev)
+            buf.record_stream(bs)
+            if b:
+                bp = buf.data_ptr()
+                _lib.check(self._back_fn(bind.handle, b, S, cap, twp, fr, fn, bp, bp + moff * 4, wsp, wsn,
+                                         self._bs_h), "m2_inference_back_dev")
             parts, work = None, None
-            with torch.cuda.stream(bs):
-                buf = torch.empty(moff + rows * 64 * cap, dtype=torch.float32, device=dev)
-                if b:
-                    hm.inference_back_dev(state, cap, tw, buf[: b * cap * M], buf[moff: moff + b * 64 * cap])
-                if world > 1:
+            if world > 1:
+                with torch.cuda.stream(bs):
                     me = dist.get_rank(self.ggroup)
                     if self.gather_to is None or me == self.gather_to:
                         parts = [torch.empty_like(buf) for _ in range(world)]
@@ -601,11 +654,9 @@ class ShardedPipeline:
                     else:
                         dst = dist.get_global_rank(self.ggroup, self.gather_to)
                         work = dist.gather(buf, parts, dst=dst, group=self.ggroup, async_op=True)
-            done = torch.cuda.Event()
-            done.record(bs)
-        self._free[h] = done
-        step = _SplitStep(self, h, caller=caller, done=done, hm=hm, b=b, tw=tw, key=key, cap=cap, work=work,
-                          ids=phoneme_ids, lens=phoneme_lengths, scale=duration_scale, M=M, moff=moff, B=B,
-                          world=world, buf=buf, parts=parts)
+            self._done[h].record(bs)
+            self._used[h] = True
+        step = _SplitStep(self, h, caller, bind, b, key, cap, work, phoneme_ids, phoneme_lengths, duration_scale,
+                          moff, B, world, buf, parts)
         self._pending[h] = step
         return step

@@ -188,15 +188,21 @@ def mel_decoder(sd: Dict[str, Tensor], cfg: OracleConfig, x: Tensor) -> Tensor:
     return F.linear(x, sd["decoder.mel_projection.weight"], sd["decoder.mel_projection.bias"])
 
 
-def vocoder(sd: Dict[str, Tensor], mel_bmt: Tensor) -> Tensor:
-    """SimpleVocoder.forward, tts_model.py:279-297; mel [B,M,T] -> audio [B,1,64T].
-    Convs pad kernel_size // 2 (tts_model.py:246, 272; kernel_size 3 in M2TTSModel)."""
+def vocoder_pre_tanh(sd: Dict[str, Tensor], mel_bmt: Tensor) -> Tensor:
+    """SimpleVocoder.forward up to the output conv (tts_model.py:279-296), the
+    value tanh is applied to at :297 (the stress tests' conditioning check)."""
     ks = sd["vocoder.input_conv.weight"].shape[-1]
     x = F.conv1d(mel_bmt, sd["vocoder.input_conv.weight"], sd["vocoder.input_conv.bias"], padding=ks // 2)
     for k, r in enumerate(UPSAMPLE_RATES):
         x = F.leaky_relu(conv_transpose(sd, f"vocoder.upsamples.{k}", x, r), LEAKY)
         x = resblock(sd, f"vocoder.resblocks.{k}", x)
-    return torch.tanh(F.conv1d(x, sd["vocoder.output_conv.weight"], sd["vocoder.output_conv.bias"], padding=ks // 2))
+    return F.conv1d(x, sd["vocoder.output_conv.weight"], sd["vocoder.output_conv.bias"], padding=ks // 2)
+
+
+def vocoder(sd: Dict[str, Tensor], mel_bmt: Tensor) -> Tensor:
+    """SimpleVocoder.forward, tts_model.py:279-297; mel [B,M,T] -> audio [B,1,64T].
+    Convs pad kernel_size // 2 (tts_model.py:246, 272; kernel_size 3 in M2TTSModel)."""
+    return torch.tanh(vocoder_pre_tanh(sd, mel_bmt))
 
 
 def forward(sd: Dict[str, Tensor], cfg: OracleConfig, ids: Tensor,

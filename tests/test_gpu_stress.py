@@ -14,9 +14,21 @@ Tolerances: mel max-abs 1e-3 relative to the oracle mel's magnitude (the
 north-star bound is absolute at the reference's unit-scale outputs; scaled
 weights scale the mel); audio against a float64 evaluation of the
 reference's vocoder on the oracle mel, within the distance the reference's
-own fp32 path lands from it (at least 1e-4 RMS), with at most 1e-4 of the
-samples allowed a sign flip: large activations make tanh's zero crossings
-ill-conditioned in any fp32 implementation."""
+own fp32 path lands from it (at least 1e-4 RMS).
+
+Samples more than 1e-2 from float64 (a tanh sign flip) are accounted for,
+not tolerated (tools/probe/stress_flips.py,
+profiles/r06/r06f_flips*.txt): their number per case is asserted exactly,
+and each must sit where fp32 itself is ill-conditioned - its float64
+pre-tanh value within 8x the error the reference's own fp32 path makes in
+the pre-tanh signal near it.  At x4 the vocoder's activations reach ~3e8,
+far past the split-f16 range (65520): every strip of the split path is
+non-finite and the default range policy recomputes all of it in fp32 inside
+the tail launch (vocoder_redo.h).  stage1 x4 has exactly one such sample,
+[3, 0, 6547]: float64 pre-tanh 64.1 where the fp32 oracle's own pre-tanh
+error is 13.7; the redo and the exact-f32 kernels both flip it, the fp32
+oracle (another summation order) does not.  stage2 x4 and both x2 cases
+have none."""
 import pytest
 import torch
 
@@ -35,6 +47,11 @@ def scaled_state(stage, f):
     sd[p + ".weight"] = torch.zeros_like(sd[p + ".weight"])
     sd[p + ".bias"] = torch.full_like(sd[p + ".bias"], 5.5)
     return sd
+
+
+# samples that land > 1e-2 from float64 (tanh sign flips at ill-conditioned
+# zero crossings), per (stage, weight scale): see the module docstring
+FAR_SAMPLES = {("s1", 2.0): 0, ("s2", 2.0): 0, ("s1", 4.0): 1, ("s2", 4.0): 0}
 
 
 @pytest.mark.parametrize("stage", ["s1", "s2"])
@@ -60,16 +77,16 @@ def test_scaled_weights_inference(gpu, stage, f):
     sd64 = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
     ref64 = orc.vocoder(sd64, mel_bmt.double())
     cond = rms(orc.vocoder(sd, mel_bmt), ref64)
-    # the GPU vocoder on the oracle's mel (so mel differences do not enter):
-    # at f = 4 the pre-tanh values reach ~1e7, where fp32's own rounding is
-    # ~1 and can flip the sign of a sample that sits near a zero crossing
-    # (the oracle's fp32 path does not flip it on these inputs, by luck: its
-    # distance to float64 here is 0); so at most 1e-4 of the samples may
-    # differ by more than 1e-2 (such a flip), the rest within the bound
+    # the GPU vocoder on the oracle's mel (so mel differences do not enter)
     out = m.vocoder(mel_bmt.to(gpu)).cpu().double()
     assert torch.isfinite(out).all()
     far = (out - ref64).abs() > 1e-2
-    assert float(far.double().mean()) <= 1e-4, int(far.sum())
+    assert int(far.sum()) == FAR_SAMPLES[(stage, f)], far.nonzero().tolist()
+    if far.any():
+        pre64 = orc.vocoder_pre_tanh(sd64, mel_bmt.double())
+        err32 = (orc.vocoder_pre_tanh(sd, mel_bmt).double() - pre64).abs()
+        err32 = torch.nn.functional.max_pool1d(err32, 65, stride=1, padding=32)  # fp32's error near each sample
+        assert (pre64.abs()[far] <= 8 * err32[far]).all(), (pre64[far], err32[far])
     assert rms(out[~far], ref64[~far]) <= max(AUDIO_RMS_TOL, 2 * cond), (rms(out[~far], ref64[~far]), cond)
     # inference()'s audio is the same vocoder on the GPU's own mel
     assert torch.equal(audio, m.vocoder(mel.transpose(1, 2).contiguous()))
