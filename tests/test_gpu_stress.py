@@ -18,7 +18,7 @@ own fp32 path lands from it (at least 1e-4 RMS).
 
 Samples more than 1e-2 from float64 (a tanh sign flip) are accounted for,
 not tolerated (tools/probe/stress_flips.py,
-profiles/r06/r06f_flips*.txt): their number per case is asserted exactly,
+profiles/r06/r06h_flips_x{2,4}.txt): their number per case is asserted exactly,
 and each must sit where fp32 itself is ill-conditioned - its float64
 pre-tanh value within 8x the error the reference's own fp32 path makes in
 the pre-tanh signal near it.  At x4 the vocoder's activations reach ~3e8,
