@@ -546,7 +546,11 @@ class ShardedPipeline:
         # lanes 1..depth: lane 0 is the model's default handle, which
         # model.inference() / forward() use on the caller's stream
         self.lanes = [HipStages(model, lane=i + 1, tcap=tcap) for i in range(depth)]
-        self.front_stream, self.back_stream = torch.cuda.Stream(), torch.cuda.Stream()
+        # the back stream at high priority: when a CU frees up, the dispatcher
+        # prefers the back half's workgroups (the critical path) over the next
+        # step's front half (B=8 share, raw calls: 0.1502 -> 0.1474 ms per
+        # step, profiles/r06/r06j_prio.txt)
+        self.front_stream, self.back_stream = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
         self._fs_h, self._bs_h = self.front_stream.cuda_stream, self.back_stream.cuda_stream
         self._pending = [None] * depth
         self._front_ev = [torch.cuda.Event() for _ in range(depth)]

@@ -110,6 +110,22 @@ def main():
         res = [run(fs, bs, steps, pipelined) for _ in range(reps)]
         return min(r[1] for r in res), min(r[0] for r in res)
 
+    def prio_stream(prio):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithPriority(ctypes.byref(s), 1, prio) == 0
+        return s
+
+    lo_p, hi_p = ctypes.c_int(0), ctypes.c_int(0)
+    hip.hipDeviceGetStreamPriorityRange(ctypes.byref(lo_p), ctypes.byref(hi_p))
+    print(f"stream priority range: least {lo_p.value}, greatest {hi_p.value}", flush=True)
+    if "--prio" in sys.argv:
+        pf, pb = stream(), stream()
+        for name, (a, c) in {"both default": (pf, pb),
+                             "front low, back high": (prio_stream(lo_p.value), prio_stream(hi_p.value)),
+                             "front high, back low": (prio_stream(hi_p.value), prio_stream(lo_p.value))}.items():
+            rs = [best(a, c) for _ in range(3)]
+            print(f"pipelined, {name}: " + ", ".join(f"{w:.4f}" for w, _ in rs) + " ms/step", flush=True)
+        return
     plain_f, plain_b = stream(), stream()
     w, h = best(plain_f, plain_f, pipelined=False)
     print(f"serial, one raw stream: {w:.4f} ms/step (host enqueue {h:.4f})", flush=True)
