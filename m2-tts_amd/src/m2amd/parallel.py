@@ -546,11 +546,14 @@ class ShardedPipeline:
         # lanes 1..depth: lane 0 is the model's default handle, which
         # model.inference() / forward() use on the caller's stream
         self.lanes = [HipStages(model, lane=i + 1, tcap=tcap) for i in range(depth)]
-        # the back stream at high priority: when a CU frees up, the dispatcher
-        # prefers the back half's workgroups (the critical path) over the next
-        # step's front half (B=8 share, raw calls: 0.1502 -> 0.1474 ms per
-        # step, profiles/r06/r06j_prio.txt)
-        self.front_stream, self.back_stream = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
+        # Two normal-priority streams (measured and dropped: the back stream at
+        # high priority, -2 % at B=8 with raw calls but up to 3x slower in other
+        # stream layouts and +35 % at B=64, profiles/r06/r06j_prio.txt,
+        # r06l_prio_ab.txt).  HIP maps streams onto GPU_MAX_HW_QUEUES (4)
+        # in-order hardware queues, so either stream can share a queue with
+        # the caller's; in the layouts measured that cost up to 1.5x at B=8
+        # (profiles/r06/r06n_q*.txt)
+        self.front_stream, self.back_stream = torch.cuda.Stream(), torch.cuda.Stream()
         self._fs_h, self._bs_h = self.front_stream.cuda_stream, self.back_stream.cuda_stream
         self._pending = [None] * depth
         self._front_ev = [torch.cuda.Event() for _ in range(depth)]
