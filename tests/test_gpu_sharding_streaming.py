@@ -42,6 +42,31 @@ def test_hip_stages_sharded_world1_matches_fixture(gpu):
     assert rms(audio[rows], ref_audio) <= AUDIO_RMS_TOL
 
 
+def test_sharded_pipeline_matches_fixture(gpu):
+    """ShardedPipeline (front halves on one stream, back halves on another,
+    two lanes) over configs[3]'s global batch fp_s2_B64_S100 and over its
+    8-utterance slices (the per-GPU share's shape): the global batch against
+    the reference fingerprints, every step bit-equal to M2TTSModel.inference
+    of the same rows, with several steps in flight."""
+    from m2amd.parallel import ShardedPipeline
+    from test_gpu_parity import _check_fingerprint
+    fp = golden("fp_s2_B64_S100")
+    m = build_model("s2", gpu)
+    ids, lens = torch.from_numpy(fp["ids"]).to(gpu), torch.from_numpy(fp["lengths"]).to(gpu)
+    pipe = ShardedPipeline(m, depth=2)
+    steps = [(slice(0, 64), pipe.submit(ids, lens))]
+    for i in range(8):
+        rows = slice(8 * i, 8 * i + 8)
+        steps.append((rows, pipe.submit(ids[rows], lens[rows])))
+    steps.append((slice(0, 64), pipe.submit(ids, lens)))
+    for rows, r in steps:
+        mel, audio = r.wait()
+        ref = m.inference(ids[rows], lens[rows])
+        assert torch.equal(mel, ref[0]) and torch.equal(audio, ref[1]), rows
+        if rows == slice(0, 64):
+            _check_fingerprint(fp, mel, audio)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
