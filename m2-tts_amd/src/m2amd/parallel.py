@@ -456,7 +456,10 @@ class _SplitStep:
         if p._pending[self.lane] is self:
             p._pending[self.lane] = None
         caller = self.caller
-        caller.wait_event(p._done[self.lane])
+        if p.host_wait:  # the host waits; the caller's (possibly shared) hardware queue gets no barrier
+            p._done[self.lane].synchronize()
+        else:
+            caller.wait_event(p._done[self.lane])
         st = p.lanes[self.lane]
         if self.b:
             T = ctypes.c_int32(0)
@@ -531,12 +534,20 @@ class ShardedPipeline:
     under its GPU time); the weights are re-validated every step (the
     model's handle cache), as ``inference()`` does.
 
+    ``host_wait`` (default): a step's ``wait()`` blocks the host until the
+    step's back half is done instead of enqueueing a wait on the caller's
+    stream.  HIP maps streams onto GPU_MAX_HW_QUEUES (4) in-order hardware
+    queues; when the caller's stream shares one with a pipeline stream, a
+    wait enqueued there holds the pipeline's next launches behind it (B=64:
+    0.673 -> 0.641 ms per step in such a layout, profiles/r06/r06p_q4.txt).
+
     ``model`` may also be a host ``Stages`` (the oracle-backed stages of the
     CPU tests): the lanes then share it and have no stream; the lane
     rotation and the in-flight gathers are the same."""
 
-    def __init__(self, model, depth: int = 2, group=None, gather_to: Optional[int] = 0):
+    def __init__(self, model, depth: int = 2, group=None, gather_to: Optional[int] = 0, host_wait: bool = True):
         self.group, self.gather_to = group, gather_to
+        self.host_wait = host_wait
         self._next = 0
         self.host = isinstance(model, Stages)
         if self.host:

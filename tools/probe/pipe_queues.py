@@ -58,7 +58,7 @@ def main():
         for kind in KINDS:
             out = []
             for B, (ids, lens) in batches.items():
-                pipe = ShardedPipeline(m, depth=2, gather_to=0)
+                pipe = ShardedPipeline(m, depth=2, gather_to=0, host_wait=(kind == "hostwait"))
                 if kind in ("lo/hi", "hi/lo"):
                     pf, pb = (1, -1) if kind == "lo/hi" else (-1, 1)
                     pipe.front_stream = prio_stream(pf)
