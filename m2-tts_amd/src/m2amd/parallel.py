@@ -434,10 +434,10 @@ class _LaneResult:
 
 
 class _SplitStep:
-    """A step of ShardedPipeline's split-stream schedule: ``wait()`` reads T
-    (posted by the back half's first launch), joins the step's back-half
-    event into the caller's stream and returns (mel, audio) (None on
-    non-destination ranks).  A step whose T outgrew the capacity is re-run
+    """A step of ShardedPipeline's split-stream schedule: ``wait()`` waits
+    for the step's back half (on the host with ``host_wait``, else by an
+    event wait on the caller's stream), reads T (posted by the back half's
+    first launch) and returns (mel, audio) (None on non-destination ranks).  A step whose T outgrew the capacity is re-run
     on the host-T path (every rank sees the same T and capacity)."""
 
     __slots__ = ("pipe", "lane", "caller", "bind", "b", "key", "cap", "work", "ids", "lens", "scale", "moff", "B",
