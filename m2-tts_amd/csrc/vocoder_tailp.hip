@@ -67,10 +67,21 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // epilogue store (ds_write_b128, 8 consecutive rows) bank-conflict free
 // without padding (tools/probe/tailp_banks.py).  The swizzle depends on row
 // bits 1-2 only, so it does not change from chunk to chunk.  Rings hold 4
-// chunks of 16 columns (3 for R0 and R6, whose only reader is one step behind
-// its writer; R1 and R4 also feed a residual reader two layers down), 53,248 B
-// in all: three workgroups per CU.
-constexpr int kRingRows[7] = {48, 64, 64, 64, 64, 64, 48};
+// chunks of 16 columns (3 for R6, whose only reader is one step behind its
+// writer, and for R0 with the register loader; R1 and R4 also feed a residual
+// reader two layers down): three workgroups per CU.
+// TAILP_DMA (default): the loader moves U2 into R0 by LDS-DMA (buffer_load
+// ... lds: L2 -> LDS, no VGPR staging, no ds_write), one chunk ahead, so R0
+// holds 4 chunks (TAILP_DMA=0 keeps the register loader
+// and a 3-chunk R0).  Alternated twice on one box (profiles/r06/
+// r06s_tail_dma_ab/): tail 21.85 / 21.76 -> 21.46 / 21.47 us under
+// rocprofv3 at B=32 (-1.6 %; the loader's two ds_write_b128 per step were
+// 2 KB of the ~12 KB each chunk writes into LDS), 141 tail / range /
+// stress / streaming / parity tests green (r06s_tests.log).
+#ifndef TAILP_DMA
+#define TAILP_DMA 1
+#endif
+constexpr int kRingRows[7] = {TAILP_DMA ? 64 : 48, 64, 64, 64, 64, 64, 48};
 constexpr int kRingOff(int n) { return n == 0 ? 0 : kRingOff(n - 1) + kRingRows[n - 1] * 128; }
 constexpr int kLoOff(int n) { return kRingRows[n] * 64; }
 constexpr int kPeriod(int n) { return kRingRows[n] / 16; }  // chunks per ring (3 or 4)
@@ -84,7 +95,8 @@ constexpr int ring_bytes(int nl) { return nl == 6 ? kCorrSlot + 16 : kRingOff(nl
 constexpr int kFlagOff(int nl) { return ring_bytes(nl); }
 constexpr int lds_bytes(int nl) { return ring_bytes(nl) + 16; }
 constexpr int nwaves(int nl) { return nl + 1; }
-static_assert(lds_bytes(7) * 3 <= 160 * 1024, "three workgroups per CU");
+static_assert(lds_bytes(6) * 3 <= 160 * 1024, "three workgroups per CU");
+static_assert(TAILP_DMA || lds_bytes(7) * 3 <= 160 * 1024, "three workgroups per CU");
 #ifdef M2_STAMPS
 constexpr int NWAVES = 8;  // stamp buffer size (the larger variant)
 #endif
@@ -507,6 +519,47 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     for (; s <= last_step(nch, NL); ++s) step_barrier();
 }
 
+// TAILP_DMA: U2 rows into ring R0 by LDS-DMA.  One buffer_load_dwordx4 ...
+// lds writes 64 lanes x 16 B = 1 KB at M0 + 16 x lane, i.e. exactly the 16
+// rows (columns) of a chunk's hi plane (or lo plane) in ring phase c mod 4;
+// lane l fills row l / 4, slot l % 4, so it loads the U2 octet ring_at
+// places there (octet (l % 4) ^ ((row >> 1) & 3)).  The descriptor spans the
+// utterance's L2 rows: columns before 0 or from L2 on are out of range and
+// land as zeros (the next conv's zero padding), so edge and interior strips
+// run the same code.  Chunk c + 1 is issued at the top of step c into the
+// slot of chunk c - 3 (read for the last time in step c - 1, before that
+// step's barrier); chunk c must have landed before step c's barrier
+// (vmcnt(2): only chunk c + 1's two loads may still be in flight).
+template <int NL>
+__device__ __forceinline__ void loader_role_dma(unsigned char* lds, int qa, int L2, int nch,
+                                                const unsigned char* __restrict__ u2) {
+    static_assert(NL > 0 && kRingRows[0] == 64, "4-chunk R0");
+    const int lane = threadIdx.x & 63, row = lane >> 2;
+    [[maybe_unused]] const int oct = (lane & 3) ^ ((row >> 1) & 3);
+    [[maybe_unused]] const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(u2), 0, L2 * 128, 0x00020000);
+    auto dma = [&](int c) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc does not know this builtin)
+        const int voff = (qa + NL + 16 * c + row) * 128 + 16 * oct;  // < 0 or >= L2 rows: out of range -> 0
+        unsigned char* dst = lds + kRingOff(0) + 1024 * (c & 3);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0,
+                                                 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + kLoOff(0)), 16,
+                                                 voff + 64, 0, 0, 0);
+#endif
+    };
+    dma(-1);
+#pragma unroll 1
+    for (int s = -1; s <= last_step(nch, NL); ++s) {
+        if (s + 1 < nch) {
+            dma(s + 1);
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        step_barrier();
+    }
+}
+
 // NCHC > 0: the strip length as a compile-time constant (the headline's 21,
 // measured 0.45 us faster than the same length as an argument); 0: nch.
 template <int NL, int NCHC>
@@ -554,7 +607,8 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 6) void tailp_kernel(const unsigne
             }
             [[fallthrough]];
         default:
-            if (edge) loader_role<NL, true>(lds, qa, L2, nch, u2);
+            if constexpr (TAILP_DMA) loader_role_dma<NL>(lds, qa, L2, nch, u2);
+            else if (edge) loader_role<NL, true>(lds, qa, L2, nch, u2);
             else loader_role<NL, false>(lds, qa, L2, nch, u2);
             break;
     }
