@@ -47,9 +47,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // later.  Octet o of row r sits at 16 * (o ^ (r & 7)): every fragment read
 // (ds_read_b128), residual read and epilogue store (ds_write_b128) of the
 // kernel is then bank-conflict free (tools/probe/tailp2_banks.py models them
-// all).  R0 and R6 hold 3 chunks of 16 columns (their only reader is one step
-// behind the writer), the others 4.
-constexpr int kRingRows[7] = {48, 64, 64, 64, 64, 64, 48};
+// all).  R6 holds 3 chunks of 16 columns (its only reader is one step behind
+// the writer; R0 too with the register loader), the others 4.
+// TAILP2_DMA (default): U2 into R0 by LDS-DMA, one chunk ahead, R0 4 chunks
+// (loader_role_dma below; TAILP2_DMA=0 keeps the register loader, R0 3 chunks).
+// Alternated twice on one box (profiles/r06/r06t_tail2_dma_ab/): tail2
+// 19.38 / 19.51 -> 18.97 / 18.84 us at B=8 T=500, 146.0 / 146.4 -> 145.4 /
+// 145.4 us at B=16 T=2600; 174 tests green (r06t_tests.log).
+#ifndef TAILP2_DMA
+#define TAILP2_DMA 1
+#endif
+constexpr int kRingRows[7] = {TAILP2_DMA ? 64 : 48, 64, 64, 64, 64, 64, 48};
 constexpr int kRingOff(int n) { return n == 0 ? 0 : kRingOff(n - 1) + kRingRows[n - 1] * 256; }
 constexpr int kLoOff(int n) { return kRingRows[n] * 128; }
 constexpr int kPeriod(int n) { return kRingRows[n] / 16; }
@@ -448,6 +456,47 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L2, 
     for (; s <= last_step(nch, NL); ++s) step_barrier();
 }
 
+// TAILP2_DMA: U2 rows into ring R0 by LDS-DMA (as vocoder_tailp.hip's
+// loader_role_dma).  A chunk's hi plane is 16 rows x 128 B = two 1-KB
+// buffer_load_dwordx4 ... lds (rows 8i .. 8i + 7: lane l fills row 8i + l / 8,
+// slot l % 8, i.e. octet (l % 8) ^ (row & 7)), its lo plane two more; columns
+// outside [0, L2) are out of the descriptor's range and land as zeros.  Chunk
+// c + 1 goes into the slot of chunk c - 3 at the top of step c, and chunk c
+// must have landed before step c's barrier (vmcnt(4)).
+template <int NL>
+__device__ __forceinline__ void loader_role_dma(unsigned char* lds, int qa, int L2, int nch,
+                                                const unsigned char* __restrict__ u2) {
+    static_assert(NL > 0 && kRingRows[0] == 64, "4-chunk R0");
+    const int lane = threadIdx.x & 63, r8 = lane >> 3;
+    [[maybe_unused]] const int oct = (lane & 7) ^ (r8 & 7);
+    [[maybe_unused]] const auto rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(u2), 0, L2 * 256, 0x00020000);
+    auto dma = [&](int c) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc does not know this builtin)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int voff = (qa + NL + 16 * c + 8 * i + r8) * 256 + 16 * oct;  // out of range -> 0
+            unsigned char* dst = lds + kRingOff(0) + 2048 * (c & 3) + 1024 * i;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0,
+                                                     0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + kLoOff(0)),
+                                                     16, voff + 128, 0, 0, 0);
+        }
+#endif
+    };
+    dma(-1);
+#pragma unroll 1
+    for (int s = -1; s <= last_step(nch, NL); ++s) {
+        if (s + 1 < nch) {
+            dma(s + 1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        step_barrier();
+    }
+}
+
 template <int NL>
 __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsigned char* __restrict__ U2, int L2,
                                                                      int nch, const u32x4* __restrict__ W,
@@ -500,7 +549,8 @@ __global__ __launch_bounds__(nwaves(NL) * 64, 1) void tailp2_kernel(const unsign
             }
             [[fallthrough]];
         default:
-            if (edge) loader_role<NL, true>(lds, qa, L2, nch, u2);
+            if constexpr (TAILP2_DMA) loader_role_dma<NL>(lds, qa, L2, nch, u2);
+            else if (edge) loader_role<NL, true>(lds, qa, L2, nch, u2);
             else loader_role<NL, false>(lds, qa, L2, nch, u2);
             break;
     }
