@@ -241,6 +241,64 @@ __device__ __forceinline__ void loader_role(unsigned char* lds, int qa, int L1, 
     for (; s <= nch + 2; ++s) step_barrier();
 }
 
+// MIDP_DMA (default): U1 rows into ring R0 by LDS-DMA (as the tails'
+// loader_role_dma): a chunk's 16 ring rows are 16 x RS0 = 4,608 contiguous
+// bytes (hi[64] lo[64] + 32 B of padding per row), written by five
+// buffer_load_dwordx4 ... lds of 64 lanes x 16 B (the fifth by lanes 0-31
+// only: EXEC-masked lanes write nothing, so the next chunk's rows are left
+// alone).  Lane l of instruction i fills 16-B unit u = 64 i + l of the
+// chunk: row u / 18, unit u % 18 of the row - units 0-15 are the U1 row's
+// 16-B pieces in order, 16-17 the padding (loaded out of range: zeros).
+// Columns outside [0, L1) are out of the descriptor's range and land as
+// zeros.  Chunk c + 1 is issued at the top of step c into the slot of chunk
+// c - 3; chunk c has landed before step c's barrier (vmcnt(5)).
+// Measured level, so not the default (MIDP_DMA=1 builds it): midp 19.74 /
+// 20.14 us against 19.83 / 19.86 us with the register loader, alternated on
+// one box, 169 tests green on it (profiles/r06/r06u_mid_dma_ab/,
+// r06u_tests.log) - the mid's loader is not on its step's critical path.
+#ifndef MIDP_DMA
+#define MIDP_DMA 0
+#endif
+__device__ __forceinline__ void loader_role_dma(unsigned char* lds, int qa, int L1, int nch,
+                                                const unsigned char* __restrict__ u1) {
+    static_assert(RROWS == 64 && RS0 == 288, "4-chunk R0 of 288-B rows");
+    const int lane = threadIdx.x & 63;
+    [[maybe_unused]] const auto rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(u1), 0, L1 * 256, 0x00020000);
+    // per instruction i: this lane's row in the chunk and byte in the U1 row (-1: padding)
+    int urow[5], ubyte[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const int u = 64 * i + lane;
+        urow[i] = u / 18;
+        ubyte[i] = u % 18 < 16 ? 16 * (u % 18) : -1;
+    }
+    [[maybe_unused]] auto dma = [&](int c) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc does not know this builtin)
+        unsigned char* dst = lds + R0_OFF + (c & 3) * 16 * RS0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int col = qa + 3 + 16 * c + urow[i];
+            const int voff = ubyte[i] < 0 ? -1 : col * 256 + ubyte[i];  // < 0 / past L1: out of range -> 0
+            if (i < 4 || lane < 32)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + 1024 * i),
+                                                         16, voff, 0, 0, 0);
+        }
+#endif
+    };
+    dma(-1);
+#pragma unroll 1
+    for (int s = -1; s <= nch + 2; ++s) {
+        if (s + 1 < nch) {
+            dma(s + 1);
+            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        step_barrier();
+    }
+}
+
 // NCHC > 0: the strip length as a compile-time constant (the headline's 16); 0: nch.
 template <int NCHC>
 __global__ __launch_bounds__(NWAVES * 64, 4) void midp_kernel(const unsigned char* __restrict__ U1, int L1, int nch_arg,
@@ -274,7 +332,8 @@ __global__ __launch_bounds__(NWAVES * 64, 4) void midp_kernel(const unsigned cha
         case 10: layer_role<2, 2>(lds, qa, L1, nch, edge, W, bias, u2row); break;
         case 11: layer_role<2, 3>(lds, qa, L1, nch, edge, W, bias, u2row); break;
         default:
-            if (edge) loader_role<true>(lds, qa, L1, nch, U1 + (size_t)b * L1 * 256);
+            if constexpr (MIDP_DMA) loader_role_dma(lds, qa, L1, nch, U1 + (size_t)b * L1 * 256);
+            else if (edge) loader_role<true>(lds, qa, L1, nch, U1 + (size_t)b * L1 * 256);
             else loader_role<false>(lds, qa, L1, nch, U1 + (size_t)b * L1 * 256);
             break;
     }
