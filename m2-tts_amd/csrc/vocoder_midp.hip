@@ -263,8 +263,11 @@ __device__ __forceinline__ void loader_role_dma(unsigned char* lds, int qa, int 
                                                 const unsigned char* __restrict__ u1) {
     static_assert(RROWS == 64 && RS0 == 288, "4-chunk R0 of 288-B rows");
     const int lane = threadIdx.x & 63;
-    [[maybe_unused]] const auto rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(u1), 0, L1 * 256, 0x00020000);
+    // descriptor from the strip's first column to the utterance's end
+    const int c0 = max(0, qa + 3 - 16);
+    [[maybe_unused]] const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(u1) + (size_t)c0 * 256, 0, (int)min((long)(L1 - c0) * 256, 0x7fffffffL),
+        0x00020000);
     // per instruction i: this lane's row in the chunk and byte in the U1 row (-1: padding)
     int urow[5], ubyte[5];
 #pragma unroll
@@ -278,7 +281,7 @@ __device__ __forceinline__ void loader_role_dma(unsigned char* lds, int qa, int 
         unsigned char* dst = lds + R0_OFF + (c & 3) * 16 * RS0;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            const int col = qa + 3 + 16 * c + urow[i];
+            const int col = qa + 3 + 16 * c + urow[i] - c0;
             const int voff = ubyte[i] < 0 ? -1 : col * 256 + ubyte[i];  // < 0 / past L1: out of range -> 0
             if (i < 4 || lane < 32)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + 1024 * i),

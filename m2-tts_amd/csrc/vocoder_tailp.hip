@@ -536,10 +536,16 @@ __device__ __forceinline__ void loader_role_dma(unsigned char* lds, int qa, int 
     static_assert(NL > 0 && kRingRows[0] == 64, "4-chunk R0");
     const int lane = threadIdx.x & 63, row = lane >> 2;
     [[maybe_unused]] const int oct = (lane & 3) ^ ((row >> 1) & 3);
-    [[maybe_unused]] const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(u2), 0, L2 * 128, 0x00020000);
+    // the descriptor starts at the strip's first column (32-bit offsets stay
+    // small for any utterance length) and ends at the utterance's last row;
+    // columns before 0 only occur in the first strip, whose base is column 0
+    const int c0 = max(0, qa + NL - 16);
+    [[maybe_unused]] const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(u2) + (size_t)c0 * 128, 0, (int)min((long)(L2 - c0) * 128, 0x7fffffffL),
+        0x00020000);
     auto dma = [&](int c) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc does not know this builtin)
-        const int voff = (qa + NL + 16 * c + row) * 128 + 16 * oct;  // < 0 or >= L2 rows: out of range -> 0
+        const int voff = (qa + NL + 16 * c + row - c0) * 128 + 16 * oct;  // < 0 or >= L2 rows: out of range -> 0
         unsigned char* dst = lds + kRingOff(0) + 1024 * (c & 3);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0,
                                                  0);

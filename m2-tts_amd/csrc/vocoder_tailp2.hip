@@ -469,13 +469,17 @@ __device__ __forceinline__ void loader_role_dma(unsigned char* lds, int qa, int 
     static_assert(NL > 0 && kRingRows[0] == 64, "4-chunk R0");
     const int lane = threadIdx.x & 63, r8 = lane >> 3;
     [[maybe_unused]] const int oct = (lane & 7) ^ (r8 & 7);
-    [[maybe_unused]] const auto rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(u2), 0, L2 * 256, 0x00020000);
+    // descriptor from the strip's first column to the utterance's end (small
+    // 32-bit offsets at any length; columns before 0 only in the first strip)
+    const int c0 = max(0, qa + NL - 16);
+    [[maybe_unused]] const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(u2) + (size_t)c0 * 256, 0, (int)min((long)(L2 - c0) * 256, 0x7fffffffL),
+        0x00020000);
     auto dma = [&](int c) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc does not know this builtin)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int voff = (qa + NL + 16 * c + 8 * i + r8) * 256 + 16 * oct;  // out of range -> 0
+            const int voff = (qa + NL + 16 * c + 8 * i + r8 - c0) * 256 + 16 * oct;  // out of range -> 0
             unsigned char* dst = lds + kRingOff(0) + 2048 * (c & 3) + 1024 * i;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0,
                                                      0, 0);

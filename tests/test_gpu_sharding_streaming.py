@@ -153,6 +153,27 @@ def test_streamed_vocoder_longform_stage2(gpu):
     assert rms(chunked, ref) <= AUDIO_RMS_TOL
 
 
+@pytest.mark.parametrize("stage,T", [("s1", 1_100_000), ("s2", 540_000)])
+def test_vocoder_u2_past_2gb(gpu, stage, T):
+    """One utterance whose U2 hand-off (16 T rows of 128 / 256 B) passes 2^31
+    bytes: the pipelined tails' LDS-DMA loaders address U2 through 32-bit
+    buffer offsets, so their descriptors start at each strip (not at the
+    utterance).  The whole call equals the same vocoder chunked by 65,536
+    frames (whose U2 is small) bit for bit."""
+    m = build_model(stage, gpu)
+    M = stage_config(stage).mel_channels
+    assert 16 * T * (128 if stage == "s1" else 256) > 2**31
+    mel = torch.randn(1, M, T, generator=torch.Generator().manual_seed(31)).to(gpu)
+    full = m.vocoder(mel)
+    m.set_vocoder_chunking(65536)
+    try:
+        chunked = m.vocoder(mel)
+    finally:
+        m.set_vocoder_chunking(0)
+    assert torch.isfinite(full).all()
+    assert torch.equal(chunked, full)
+
+
 def test_streamed_vocoder_standalone_module(gpu):
     """A SimpleVocoder outside an M2TTSModel streams through the per-op kernels
     over the same widened windows: equal to its own forward up to the per-op
