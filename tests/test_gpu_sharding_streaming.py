@@ -67,6 +67,24 @@ def test_sharded_pipeline_matches_fixture(gpu):
             _check_fingerprint(fp, mel, audio)
 
 
+def test_sharded_pipeline_no_lengths_scaled(gpu):
+    """ShardedPipeline with phoneme_lengths=None (no padding mask), int32
+    ids and a duration scale: each step bit-equal to M2TTSModel.inference
+    with the same arguments (tts_model.py:402-438)."""
+    from m2amd.parallel import ShardedPipeline
+    m = build_model("s1", gpu)
+    g = torch.Generator().manual_seed(13)
+    ids = torch.randint(0, 42, (6, 40), generator=g).to(gpu)
+    pipe = ShardedPipeline(m, depth=2)
+    for scale in (1.0, 1.3, 1.3, 0.7):
+        ref = m.inference(ids, None, duration_scale=scale)
+        r1 = pipe.submit(ids.to(torch.int32), None, scale)
+        r2 = pipe.submit(ids, None, scale)
+        for r in (r1, r2):
+            mel, audio = r.wait()
+            assert torch.equal(mel, ref[0]) and torch.equal(audio, ref[1]), scale
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
