@@ -603,16 +603,23 @@ class ShardedPipeline:
         # the lane's handle, re-validated against the model's weights every step
         hm = st.dev_handle(dev, cap) if cap > 0 else None
         fs, bs = self.front_stream, self.back_stream
+        # int64 contiguous inputs, converted on the caller's stream before the
+        # front stream waits for it
+        ids = phoneme_ids if phoneme_ids.dtype == torch.int64 and phoneme_ids.is_contiguous() else \
+            phoneme_ids.to(torch.int64).contiguous()
+        lens = phoneme_lengths
+        if lens is not None and (lens.dtype != torch.int64 or not lens.is_contiguous()):
+            lens = lens.to(torch.int64).contiguous()
         fs.wait_stream(caller)  # the inputs were produced on the caller's stream
         if self._used[h]:
             fs.wait_event(self._done[h])
         if hm is None:  # no capacity yet: one whole step on the back stream
-            for t in (phoneme_ids, phoneme_lengths):
+            for t in (ids, lens):
                 if t is not None:
                     t.record_stream(bs)
             bs.wait_stream(fs)
             with torch.cuda.stream(bs):
-                out = sharded_inference(st, phoneme_ids, phoneme_lengths, duration_scale, group=self.group,
+                out = sharded_inference(st, ids, lens, duration_scale, group=self.group,
                                         gather_to=self.gather_to, async_gather=True, one_call_world1=False)
             self._done[h].record(bs)
             self._used[h] = True
@@ -626,11 +633,6 @@ class ShardedPipeline:
                 self._binds[h].clear()
             bind = self._binds[h][(key, cap)] = _LaneBind(hm, b, S, cap, dev)
         fr, fn, wsp, wsn, twp = bind.args
-        ids = phoneme_ids if phoneme_ids.dtype == torch.int64 and phoneme_ids.is_contiguous() else \
-            phoneme_ids.to(torch.int64).contiguous()
-        lens = phoneme_lengths
-        if lens is not None and (lens.dtype != torch.int64 or not lens.is_contiguous()):
-            lens = lens.to(torch.int64).contiguous()
         for t in (ids, lens):
             if t is not None:
                 t.record_stream(fs)
