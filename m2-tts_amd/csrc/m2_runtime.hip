@@ -64,6 +64,7 @@ void reload_switches() {
     s.tfl_rb = rb124(trb);
     s.tfl_first_rb = rb124(env_int("M2_TFL_FIRST_RB", 0));
     s.tfl_rb_masked = rb124(env_int("M2_TFL_RB_MASKED", 0));
+    s.tfl_rb_unmasked = rb124(env_int("M2_TFL_RB_UNMASKED", 0));
     if (const char* e = std::getenv("M2_TFL_QS2"); e && *e) {
         const int v = std::atoi(e);
         s.tfl_qs2 = (v == 2 || v == 3 || v == 4 || v == 9) ? v : 0;

@@ -2282,6 +2282,7 @@ int32_t launch_tfl_first(const TflFirst& f, int B, int N, int H, int heads, bool
     if ((long)B * (tfl_npad(N) / tfl::TQ) >= 8L * 256) rb = 4;
     if (sw().tfl_first_rb) rb = sw().tfl_first_rb;
     if (masked && sw().tfl_rb_masked) rb = sw().tfl_rb_masked;
+    if (!masked && sw().tfl_rb_unmasked) rb = sw().tfl_rb_unmasked;
     a.ntile = tfl_ntile(N, rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;
@@ -2346,7 +2347,9 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.N = N;
     a.dN = dN;
     a.npad = tfl_npad(N);
-    const int rb = masked && sw().tfl_rb_masked ? sw().tfl_rb_masked : tfl_rb(B, N);
+    const int rb = masked && sw().tfl_rb_masked     ? sw().tfl_rb_masked
+                   : !masked && sw().tfl_rb_unmasked ? sw().tfl_rb_unmasked
+                                                     : tfl_rb(B, N);
     a.ntile = tfl_ntile(N, rb);
     a.qcnt = q.cnt;
     a.qseq = q.seq;

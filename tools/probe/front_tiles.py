@@ -17,6 +17,9 @@ ROOT = Path(__file__).resolve().parent.parent.parent
 VARIANTS = {"default": {}, "enc32": {"M2_TFL_RB_MASKED": "2"}, "enc64": {"M2_TFL_RB_MASKED": "4"},
             "dur30": {"M2_DUR_RB": "2"}, "enc64+dur30": {"M2_TFL_RB_MASKED": "4", "M2_DUR_RB": "2"},
             "enc32+dur30": {"M2_TFL_RB_MASKED": "2", "M2_DUR_RB": "2"}}
+if "--dec" in sys.argv:  # the decoder's tiles instead (its K / V stream per workgroup is the same at any rows)
+    VARIANTS = {"default": {}, "dec32": {"M2_TFL_RB_UNMASKED": "2"}, "dec64": {"M2_TFL_RB_UNMASKED": "4"}}
+ENV_KEYS = ("M2_TFL_RB_MASKED", "M2_DUR_RB", "M2_TFL_RB_UNMASKED")
 
 
 def main():
@@ -61,7 +64,7 @@ def main():
     ref = None
     for _ in range(2):
         for name, env in VARIANTS.items():
-            for k in ("M2_TFL_RB_MASKED", "M2_DUR_RB"):
+            for k in ENV_KEYS:
                 os.environ.pop(k, None)
             os.environ.update(env)
             _lib.reload_switches()
