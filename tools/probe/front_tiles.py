@@ -62,7 +62,8 @@ def main():
 
     res = {k: ([], []) for k in VARIANTS}
     ref = None
-    for _ in range(2):
+    rounds = 4 if "--dec" in sys.argv else 2
+    for _ in range(rounds):
         for name, env in VARIANTS.items():
             for k in ENV_KEYS:
                 os.environ.pop(k, None)
@@ -76,6 +77,9 @@ def main():
             d = float((mel - ref[0]).abs().max())
             print(f"{name:12s} pipelined {res[name][0][-1]:.4f}  one step {res[name][1][-1]:.4f} ms/step  "
                   f"mel max-abs vs default {d:.2e}", flush=True)
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    for name, (p, o) in res.items():
+        print(f"median {name:12s} pipelined {med(p):.4f}  one step {med(o):.4f} ms/step", flush=True)
 
 
 if __name__ == "__main__":
