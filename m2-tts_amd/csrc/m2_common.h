@@ -34,7 +34,7 @@ struct Switches {
     int tfl_first_rb = 0;     // M2_TFL_FIRST_RB=1|2|4
     int tfl_rb_masked = 0;    // M2_TFL_RB_MASKED=1|2|4: rows per tile of the masked (encoder) launches
     int tfl_rb_unmasked = 0;  // M2_TFL_RB_UNMASKED=1|2|4: rows per tile of the unmasked (decoder) launches
-    int tfl_qs2 = -1;         // M2_TFL_QS2=0|2|3|4|9
+    int tfl_qs2 = -1;         // M2_TFL_QS2=0|2|3|4|12
     int att_qt = 0;           // M2_ATT_QT
     bool att_f32 = false;     // M2_ATT_F32
     bool voc_perlayer = false;  // M2_VOCODER_PERLAYER (handle creation)

@@ -67,7 +67,7 @@ void reload_switches() {
     s.tfl_rb_unmasked = rb124(env_int("M2_TFL_RB_UNMASKED", 0));
     if (const char* e = std::getenv("M2_TFL_QS2"); e && *e) {
         const int v = std::atoi(e);
-        s.tfl_qs2 = (v == 2 || v == 3 || v == 4 || v == 9) ? v : 0;
+        s.tfl_qs2 = (v == 2 || v == 3 || v == 4 || v == 12) ? v : 0;
     }
     s.att_qt = env_int("M2_ATT_QT", 0);
     if (const char* e = std::getenv("M2_ATT_F32")) s.att_f32 = *e && *e != '0';

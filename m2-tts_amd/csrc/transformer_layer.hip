@@ -96,10 +96,8 @@ typedef vx_u32x4 u32x4;
 
 // Diagnostic builds only (-DTFL_DIAG=bits, tools/runs): attention_qsplit2's
 // lean path without 1 its global K / V loads after step 2, 2 its softmax
-// VALU, 4 its LDS stores, 8 its QK^T MFMAs, 16 its PV MFMAs; the
-// wave-specialised DMA form's producers without 32 the wait for their
-// DMAs before the step barrier, 64 the DMAs after step 0 - the per-step
-// time each piece holds (results are garbage; never the product).
+// VALU, 4 its LDS stores, 8 its QK^T MFMAs, 16 its PV MFMAs - the
+// per-step time each piece holds (results are garbage; never the product).
 #ifndef TFL_DIAG
 #define TFL_DIAG 0
 #endif
@@ -1479,103 +1477,47 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
     else fin(CI<0>{});
 }
 
-// Wave-specialised query-split attention (M2_TFL_QS2=9, unmasked; the
-// default at head_dim 48): the diagnostic builds of the lean two-block form
-// (profiles/r04/r04h_attention_diag.txt) show its 64-key step as the serial
-// sum of staging (~600 cycles of LDS stores), softmax (~600) and the MFMAs,
-// every wave doing each in turn.  Here waves 0-3 compute and waves 4-7 stage:
-// consumer wave w = (head w / 2, chunk w % 2) owns all four 16-query blocks
-// of its head over its 32-key chunk of every step (each K / V^T fragment it
-// reads from LDS feeds four blocks: half the LDS reads of the two-block
-// form), producer wave 4 + c shares a SIMD with consumer c (waves w and w + 4
-// do: tools/probe/simd_map.hip) and stages by LDS-DMA (global_load_lds_dwordx4:
-// L2 -> LDS, no VGPRs, no ds_write): step p + 1's 12 pieces per producer lane
-// are issued at the top of step p into the free half of the ring and retired
-// (vmcnt(0)) before the step's barrier.  One barrier per step, as before.
-// Consumers take their four blocks as two pairs (the two-block lean softmax
-// per pair: scores from C = -m, base moves on an f16 weight past 2^kLazyT,
-// row sums by MFMA); chunk waves (h, 0) and (h, 1) merge at the end as in
-// attention_qsplit2, wave (h, j) finalising blocks 2j, 2j + 1.  The base m
-// rides in the tail k-step as an f16 hi + lo pair (QT below), so the layer's
-// scores must stay inside the f16 range: launch_tfl_layer runs the lean
-// two-block form (f32 base) for a layer whose score bound does not
-// (TflLayer::wide_scores, set at model creation).
-// Measured and removed in round 5 (history keeps them): register staging by
-// the producer waves (7), the consumers' interleaved matrix / vector regions
-// (8, 10), a software-pipelined two-block form (5), a ping-pong two-block
-// form (6) and 128-row tiles (M2_TFL_RB=8) - DESIGN.md section 4.
+// Key-quarter attention for 64-row tiles (M2_TFL_QS2=12, unmasked; the
+// default at head_dim 48).  Each wave owns four 16-query blocks of one head
+// (every K / V^T fragment it holds feeds four blocks), takes them through the
+// lean softmax as two pairs (scores from C = -m, the base moved only when a
+// weight's f16 hi half passes 2^kLazyT, row sums by MFMA) with the base riding
+// in the head_dim-48 tail k-step, and all eight waves compute - two per SIMD,
+// so one wave's softmax VALU meets the other's MFMAs.  Wave (h, kq) takes
+// chunks kq, kq + 4, ... of head h (the key quarters of attention_tile)
+// straight from L2 into registers by buffer loads: nothing in a chunk is
+// shared between waves, so there is no staging, no ring and no barrier in the
+// chunk loop.  One fragment set: chunk c's V^T is requested at the top of its
+// iteration (first used by the first pair's PV), chunk c + 4's K right after
+// the second pair's QK^T.  The four quarters of a head merge through LDS at
+// the end, wave (h, kq) finalising block kq.
+// Round 6, against the round-4/5 default (form 9: one computing wave per SIMD
+// beside a staging wave that moved K / V into an LDS ring by LDS-DMA, one
+// barrier per 64 keys; its computing wave's dependent chain per step was the
+// bound, the MFMA pipe ~42 % busy): configs[4] step 8.67 -> 8.31 ms, B=16
+// T=2600 -7.1 %, B=64 T=500 -2.6 %, decoder layers 1.35-1.44 -> 1.24-1.33 ms,
+// MFMA busy 52 % (profiles/r06/r06ad_*, r06ae_pmc.txt).  Measured and not
+// kept: each wave moving its next chunk into a private LDS slot by LDS-DMA a
+// whole iteration ahead (step 8.23 -> 8.54 ms, r06af_*); both pairs' QK^T
+// before either softmax (+2.2 %), s_setprio 1 around each MFMA group (+0.7 %),
+// both (+2.9 %; r06ag_*).
 template <int H, int HD>
-__device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restrict__ qb,
-                                                    const unsigned char* __restrict__ kb,
-                                                    const unsigned char* __restrict__ vb, int b, int t0, int N,
-                                                    int npad, unsigned char* A, unsigned char* ring) {
+__device__ __forceinline__ void attention_quarters(const unsigned char* __restrict__ qb,
+                                                   const unsigned char* __restrict__ kb,
+                                                   const unsigned char* __restrict__ vb, int b, int t0, int N,
+                                                   int npad, unsigned char* A, unsigned char* U) {
     using G = Geo<HD>;
-    using Q = QsGeo<HD>;
-    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, CB = Q::CB, SB = Q::SB;
-    constexpr int NP = NW / 2, PT = NP * 64;           // producer waves / threads
-    constexpr int PPT = SB / (16 * PT);                // 16-B pieces per producer thread per step
-    constexpr int RW = 2 * (2 + 4 * MT);               // merge record floats per lane: two blocks
-    static_assert(SB % (16 * PT) == 0, "a step is whole producer rounds");
-    static_assert((NW / 2) * RW * 64 * 4 <= 2 * SB, "merge records fit the ring");
+    constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, VCH = G::VCH, XW = G::XW;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, g = lane >> 4;
-    const int nch = npad / KC, nsc = (N + 2 * KC - 1) / (2 * KC);
-    const bool producer = wave >= NP;  // wave-uniform
+    const int h = wave / WPH, kq = wave - h * WPH;
+    const int nch = npad / KC, nchl = (N + KC - 1) / KC;
+    const size_t bh = (size_t)__builtin_amdgcn_readfirstlane(b * HEADS + h);
 
-    if (producer) {
-        const int pt = tid - PT;  // 0 .. PT - 1
-        const unsigned char* src[PPT];
-        int sstep[PPT];
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            const int o = 16 * (pt + PT * i), jj = o / CB, oc = o - jj * CB, hh = oc / Q::HB, r = oc - hh * Q::HB;
-            const size_t bh = (size_t)b * HEADS + hh;
-            const bool isk = r < Q::KB;
-            src[i] = isk ? kb + (bh * (npad / 16) + 2 * jj) * QKBLK + r
-                         : vb + (bh * nch + jj) * G::VCH + (r - Q::KB);
-            sstep[i] = isk ? 4 * QKBLK : 2 * G::VCH;
-        }
-        {
-            // buffer_load ... lds through a descriptor of each piece's 1-KB
-            // region: the lane offset in a fixed VGPR, the step's advance in
-            // an SGPR - no per-step address VALU
-            [[maybe_unused]] const int pw = __builtin_amdgcn_readfirstlane(pt >> 6);
-            __amdgpu_buffer_rsrc_t rs[PPT];
-            int ss[PPT];
-#pragma unroll
-            for (int i = 0; i < PPT; ++i) {
-                rs[i] = wave_rsrc(src[i] - 16 * lane);
-                ss[i] = __builtin_amdgcn_readfirstlane(sstep[i]);
-            }
-            auto dma = [&](int p, int buf) {  // LDS destination: the wave's 1 KB (M0) + 16 x lane
-#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc does not know this builtin)
-#pragma unroll
-                for (int i = 0; i < PPT; ++i)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        rs[i], (__attribute__((address_space(3))) void*)(ring + buf * SB + 16 * PT * i + 1024 * pw), 16,
-                        16 * lane, p * ss[i], 0, 0);
-#endif
-            };
-            dma(0, 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_barrier();
-#pragma unroll 1
-            for (int p = 0; p < nsc; ++p) {
-                if (p + 1 < nsc && !(TFL_DIAG & 64)) dma(p + 1, (p + 1) & 1);
-                if constexpr (!(TFL_DIAG & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                lds_barrier();
-            }
-        }
-        TSTAMP(1);
-        __syncthreads();  // the consumers' merge records
-        return;
-    }
-
-    const int h = wave >> 1, j = wave & 1;
     u32x4 qh[4][KSA], ql[4][KSA], qxh[4], qxl[4];
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
-        const unsigned char* qp8 = qb + ((size_t)(b * HEADS + h) * (npad / 16) + t0 / 16 + qq) * QKBLK + 16 * lane;
+        const unsigned char* qp8 = qb + (bh * (npad / 16) + t0 / 16 + qq) * QKBLK + 16 * lane;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             qh[qq][ks] = *reinterpret_cast<const u32x4*>(qp8 + 2048 * ks);
@@ -1587,6 +1529,39 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
         }
     }
+    // chunk c's fragments through descriptors of its two K blocks / V^T chunk
+    // (lane l reads 16 B at 16 l of each 1-KB piece: the layout the QKV
+    // epilogues write)
+    const int loff = 16 * lane, xoff = G::TAIL + 512 - 512 * (lane >> 5) + 16 * lane;
+    u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
+    auto load_k = [&](int c) {
+        const auto rk = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<unsigned char*>(kb) + (bh * (npad / 16) + (size_t)c * 2) * QKBLK, 0, 2 * QKBLK, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                kf[u][ks][0] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff, u * QKBLK + 2048 * ks, 0));
+                kf[u][ks][1] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff, u * QKBLK + 2048 * ks + 1024, 0));
+            }
+            if constexpr (KT) {
+                kx[u][0] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff, u * QKBLK + G::TAIL, 0));
+                kx[u][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, xoff, u * QKBLK, 0));
+            }
+        }
+    };
+    auto load_v = [&](int c) {
+        const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(vb) + (bh * nch + c) * VCH, 0,
+                                                          VCH, 0x00020000);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            vf[t][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, loff, t * 2048, 0));
+            vf[t][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, loff, t * 2048 + 1024, 0));
+        }
+    };
     f32x4 acc[4][MT], lacc[4];
     float m[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1601,12 +1576,12 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
     // k-elements of which only 16 are head dims (lane groups 2, 3 carry zero
     // Q).  Lane group 2's first two elements become A = (1, 1) (every key)
     // and B = (hi, lo) of -m (its query): the QK^T chain then delivers
-    // q.k - m itself, from C = 0 - no per-step -m vector build (16 VALU per
-    // query pair).  The base is kept as the value those two f16 halves
-    // represent (hi + lo, exact in f32), so every use of m stays consistent.
+    // q.k - m itself, from C = 0 - no per-step -m vector build.  The base is
+    // kept as the value those two f16 halves represent (hi + lo, exact in
+    // f32), so every use of m stays consistent.
     constexpr bool QT = KT == 1 && KS >= 1;
     const bool g2 = (lane >> 4) == 2;
-    auto set_base = [&](int qq, float mnew) {  // m[qq] := mnew (as the tail's halves hold it)
+    auto set_base = [&](int qq, float mnew) {
         if constexpr (QT) {
             const _Float16 hi = (_Float16)(-mnew);
             const _Float16 lo = (_Float16)(-mnew - (float)hi);
@@ -1618,21 +1593,12 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             m[qq] = mnew;
         }
     };
-    auto fix_tail = [&](u32x4 (&kx)[2][2]) {  // lane group 2: A = (1, 1) for kxh, 0 for kxl
-        if constexpr (QT)
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                kx[u][0][0] = g2 ? 0x3C003C00u : kx[u][0][0];
-                kx[u][1][0] = g2 ? 0u : kx[u][1][0];
-            }
-    };
     auto c0 = [&](int qq) { return QT ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{-m[qq], -m[qq], -m[qq], -m[qq]}; };
 
-    // blocks Q0, Q0 + 1 of this wave's chunk of step p, K / V^T fragments in registers
-    auto pair = [&](auto Q0c, int p, const u32x4 (&kf)[2][KSA][2], const u32x4 (&kx)[2][2],
-                    const u32x4 (&vf)[MT][2], bool first) {
+    // QK^T of blocks Q0, Q0 + 1 over the chunk in registers: s[qq][u][r] =
+    // key 16 u + 4 g + r of query li of block Q0 + qq (base-2, minus the base)
+    auto qk = [&](auto Q0c, float (&s)[2][2][4]) {
         constexpr int Q0 = decltype(Q0c)::value;
-        float s[2][2][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             f32x4 st[2] = {c0(Q0), c0(Q0 + 1)};
@@ -1656,7 +1622,11 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
 #pragma unroll
                 for (int r = 0; r < 4; ++r) s[qq][u][r] = st[qq][r];
         }
-        const int k0 = p * 2 * KC + j * KC;
+    };
+    // the lean softmax of blocks Q0, Q0 + 1 over chunk c and their PV
+    auto smpv = [&](auto Q0c, int c, bool first, float (&s)[2][2][4]) {
+        constexpr int Q0 = decltype(Q0c)::value;
+        const int k0 = c * KC;
         if (N - k0 < KC) {  // the chunk straddles N (wave-uniform)
 #pragma unroll
             for (int u = 0; u < 2; ++u)
@@ -1731,85 +1701,67 @@ __device__ __forceinline__ void attention_qsplit_ws(const unsigned char* __restr
             }
     };
 
-    lds_barrier();  // step 0 staged
-
+    const int nj = kq < nchl ? (nchl - kq + WPH - 1) / WPH : 0;  // this wave's chunks
+    if (nj > 0) load_k(kq);
 #pragma unroll 1
-    for (int p = 0; p < nsc; ++p) {
-        if (2 * KC * p + KC * j < N) {  // wave-uniform
-            const unsigned char* sb = ring + (p & 1) * SB + j * CB + h * Q::HB + 16 * lane;
-            u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
+    for (int j = 0; j < nj; ++j) {
+        const int c = kq + WPH * j;
+        load_v(c);
+        if constexpr (QT)  // lane group 2: A = (1, 1) for the hi tail, 0 for the lo tail
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    kf[u][ks][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks);
-                    kf[u][ks][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + 2048 * ks + 1024);
-                }
-                if constexpr (KT) {
-                    kx[u][0] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL);
-                    kx[u][1] = *reinterpret_cast<const u32x4*>(sb + u * QKBLK + G::TAIL + 512 - 512 * (lane >> 5));
-                }
+                kx[u][0][0] = g2 ? 0x3C003C00u : kx[u][0][0];
+                kx[u][1][0] = g2 ? 0u : kx[u][1][0];
             }
-            fix_tail(kx);
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                vf[t][0] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048);
-                vf[t][1] = *reinterpret_cast<const u32x4*>(sb + Q::KB + t * 2048 + 1024);
-            }
-            pair(CI<0>{}, p, kf, kx, vf, fresh);
-            pair(CI<2>{}, p, kf, kx, vf, fresh);
-            fresh = false;
-        }
-        lds_barrier();
+        float s0[2][2][4], s2[2][2][4];
+        qk(CI<0>{}, s0);
+        smpv(CI<0>{}, c, fresh, s0);
+        qk(CI<2>{}, s2);
+        if (j + 1 < nj) load_k(c + WPH);  // wave-uniform: the K fragments are dead
+        smpv(CI<2>{}, c, fresh, s2);
+        fresh = false;
     }
     TSTAMP(1);
     if (fresh) {  // this wave saw no key
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) m[qq] = -INFINITY;
     }
-    // merge the chunk waves (h, 0), (h, 1): wave (h, j) finalises blocks
-    // 2j, 2j + 1 and hands its state of the other two to its partner
-    float* rec = reinterpret_cast<float*>(ring);
-    auto put = [&](auto J) {
-        constexpr int q0 = 2 * (1 - decltype(J)::value);
-        float* w = rec + (size_t)wave * RW * 64 + lane;
+    // merge: every wave leaves (m, row sum, acc) of its four blocks; wave
+    // (h, kq) combines block kq over the head's four quarters
+    float* rec = reinterpret_cast<float*>(U);
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            float* we = w + e * (2 + 4 * MT) * 64;
-            we[0] = m[q0 + e];
-            we[64] = lacc[q0 + e][0];
+    for (int qq = 0; qq < 4; ++qq) {
+        float* w = rec + (size_t)(wave * 4 + qq) * XW * 64 + lane;
+        w[0] = m[qq];
+        w[64] = lacc[qq][0];
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
+        for (int t = 0; t < MT; ++t)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) we[(2 + 4 * t + r) * 64] = acc[q0 + e][t][r];
-        }
-    };
-    auto fin = [&](auto J) {
-        constexpr int q0 = 2 * decltype(J)::value;
-        const float* o = rec + (size_t)(wave ^ 1) * RW * 64 + lane;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float* oe = o + e * (2 + 4 * MT) * 64;
-            const int qq = q0 + e;
-            const float mo = oe[0];
-            const float mx = vmax(m[qq], mo);  // finite: chunk 0 of step 0 holds key 0 < N
-            const float fm = __builtin_amdgcn_exp2f(m[qq] - mx), fo = __builtin_amdgcn_exp2f(mo - mx);
-            const float ls = lacc[qq][0] * fm + oe[64] * fo;
-            const float inv = 1.0f / ls;
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = (acc[qq][t][r] * fm + oe[(2 + 4 * t + r) * 64] * fo) * inv;
-                put_split4<H>(A + (16 * qq + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), v[0], v[1], v[2], v[3]);
-            }
-        }
-    };
-    if (j) put(CI<1>{});
-    else put(CI<0>{});
+            for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qq][t][r];
+    }
     __syncthreads();
-    if (j) fin(CI<1>{});
-    else fin(CI<0>{});
+    float mi[WPH], mx = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < WPH; ++q) {
+        mi[q] = rec[(size_t)((h * WPH + q) * 4 + kq) * XW * 64 + lane];
+        mx = vmax(mx, mi[q]);  // finite: quarter 0 holds key 0 < N
+    }
+    float ls = 0.f, o[MT][4] = {};
+#pragma unroll
+    for (int q = 0; q < WPH; ++q) {
+        const float* r0 = rec + (size_t)((h * WPH + q) * 4 + kq) * XW * 64 + lane;
+        const float f = __builtin_amdgcn_exp2f(mi[q] - mx);
+        ls += r0[64] * f;
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[t][r] += r0[(2 + 4 * t + r) * 64] * f;
+    }
+    const float inv = 1.0f / ls;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+        put_split4<H>(A + (16 * kq + li) * srs(H) + 2 * (h * HD + 16 * t + 4 * g), o[t][0] * inv, o[t][1] * inv,
+                      o[t][2] * inv, o[t][3] * inv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1846,7 +1798,7 @@ constexpr bool tfl_one(int rb) { return TFL_ONE && rb == 1; }
 template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     static_assert(RB == 1 || RB == 2 || RB == 4, "16-, 32- or 64-row tiles");
-    static_assert(QV != 9 || !MASKED, "the wave-specialised attention is unmasked-only");
+    static_assert(QV != 12 || !MASKED, "the key-quarter form is unmasked-only");
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
     constexpr bool ONE = tfl_one(RB);
     constexpr bool QS = RB == 4;                  // 64-row tiles: K / V staged in LDS
@@ -1854,7 +1806,9 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     // the attention's scratch (key-quarter merge records / the K-V chunk ring)
     // and, after it, o / y (fp32, O) and relu(FFN1) (split, Hd)
     constexpr int OB = TR * frs(H) * 4, HB = TR * srs(F);
-    constexpr int XB = QS ? 2 * QsGeo<HD>::SB : NW * RB * 64 * Geo<HD>::XW * 4;
+    constexpr int XB = QV == 12 ? NW * 4 * 64 * Geo<HD>::XW * 4  // form 12: merge records
+                       : QS     ? 2 * QsGeo<HD>::SB
+                                : NW * RB * 64 * Geo<HD>::XW * 4;
     __shared__ __attribute__((aligned(16))) unsigned char U[OB + HB > XB ? OB + HB : XB];
     float* const O = reinterpret_cast<float*>(U);
     unsigned char* const Hd = U + OB;
@@ -1899,7 +1853,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
             xres = *reinterpret_cast<const f32x4*>(a.x_in + ((size_t)b * N + t0 + i) * H + wave * 16 + 4 * gq);
     }
     if constexpr (QS) {
-        if constexpr (QV == 9) attention_qsplit_ws<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        if constexpr (QV == 12) attention_quarters<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
         else if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
@@ -2245,12 +2199,18 @@ int tfl_rb(int B, int N) {
 // and not kept (removed in round 5): the software-pipelined form (5, level or
 // slower, r04d / r04e), the wave-specialised form with register staging (7,
 // between 6 and 9) and with its regions interleaved by group barriers (8,
-// +3 %; 10).  M2_TFL_QS2=0|2|3|4|9 forces a form (switch table, m2_common.h):
-// 0 / 2 one / two query blocks, 3 / 4 the same with the lean softmax, 9 the
-// wave-specialised form (unmasked layers; masked ones run 3).
+// +3 %; 10).  Round 6: the key-quarter form (12, attention_quarters) for
+// every unmasked layer - at head_dim 48 it replaces 9 (configs[4] step -4.2 %,
+// B=16 T=2600 -7.1 %, B=64 T=500 -2.6 %; 9 removed, history keeps it), at
+// head_dim 32 the lean one-block form (stage1 B=128 S=130 -3.2 %, B=32 S=520
+// -9.1 %; profiles/r06/r06ad_*, r06ah_*).  Masked layers, and layers whose
+// scores may leave the f16 range (12's base is an f16 pair), keep the
+// previous default: 3 at head_dim 48, 4 below.  M2_TFL_QS2=0|2|3|4|12 forces
+// a form (switch table, m2_common.h): 0 / 2 one / two query blocks, 3 / 4 the
+// same with the lean softmax, 12 the key-quarter form (unmasked layers).
 int tfl_qs2(int H) {
     if (sw().tfl_qs2 >= 0) return sw().tfl_qs2;
-    return H / tfl::HEADS >= 48 ? 9 : 4;
+    return 12;
 }
 int tfl_ntile(int N, int rb) { return (tfl_npad(N) + tfl::TQ * rb - 1) / (tfl::TQ * rb); }
 dim3 tfl_grid(int B, int N, int rb) { return dim3(B * tfl_ntile(N, rb)); }
@@ -2377,16 +2337,17 @@ int32_t launch_tfl_layer(const TflLayer& w, int B, int N, int H, int heads, bool
     a.nv = out.v;
     a.z = z;
     const dim3 grid = tfl_grid(B, N, rb), blk(tfl::NW * 64);
-    // form 9 is unmasked-only, and keeps the softmax base as an f16 pair: a
-    // masked launch, or a layer whose scores may leave the f16 range, runs the
-    // lean two-block form (3) instead
+    // form 12 is unmasked-only, and at head_dim 48 keeps the softmax base as
+    // an f16 pair: a masked launch, or a layer whose scores may leave the f16
+    // range, runs the previous default instead (the lean two-block form 3 at
+    // head_dim 48, the one-block form 4 below)
     int qs2 = tfl_qs2(H);
-    if (qs2 == 9 && (masked || w.wide_scores)) qs2 = 3;
+    if (qs2 == 12 && (masked || w.wide_scores)) qs2 = H / tfl::HEADS >= 48 ? 3 : 4;
 #define M2_TFL(HH, MM, NX, NNN)                                                                 \
     if (H == HH && masked == MM && next == NX && (NX != 2 || NN == NNN)) {                      \
         if constexpr (!MM) {                                                                    \
-            if (rb == 4 && qs2 == 9) {                                                          \
-                hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 9>), grid, blk, 0, st, a); \
+            if (rb == 4 && qs2 == 12) {                                                         \
+                hipLaunchKernelGGL((tfl::layer_kernel<HH, MM, NX, NNN, 4, 12>), grid, blk, 0, st, a); \
                 M2_LAUNCHED("tfl layer_kernel");                                                \
                 return M2_OK;                                                                   \
             }                                                                                   \

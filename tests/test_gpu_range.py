@@ -222,7 +222,8 @@ def test_transformer_range_bound_selects_f32(gpu):
 
 @pytest.mark.parametrize("stage", ["s1", "s2"])
 @pytest.mark.parametrize("scale", [0.3, 10.0])
-@pytest.mark.parametrize("rb,form", [("1", "auto"), ("2", "auto"), ("4", "auto"), ("4", "3"), ("4", "4")])
+@pytest.mark.parametrize("rb,form", [("1", "auto"), ("2", "auto"), ("4", "auto"), ("4", "3"), ("4", "4"),
+                                     ("4", "12")])
 def test_attention_scores_large(gpu, monkeypatch, stage, scale, rb, form):
     """Decoder layer 0 with every q and k row = scale u (q_d = k_d = scale
     u.LN1(x)): attention scores spread over > 128 log2 units (scale 0.3) or
@@ -234,8 +235,9 @@ def test_attention_scores_large(gpu, monkeypatch, stage, scale, rb, form):
     float compare of packed f16 maxima missed it: NaN output).  At scale 10
     the head_dim-48 default form, whose base is an f16 pair, gives way to
     the f32-base form (m2_transformer_path 2).  "auto" is the
-    per-head-dim default (stage1 4, stage2 9), "3" / "4" the lean two- /
-    one-block forms.  M2_TFL_RB=1 / 2 run the same layer on the 16- / 32-row
+    default (12 on unmasked layers at both head dims), "3" / "4" the lean two- /
+    one-block forms, "12" the key-quarter form (base an f16 pair at
+    head_dim 48).  M2_TFL_RB=1 / 2 run the same layer on the 16- / 32-row
     tile forms (attention_tile), whose softmax base is fp32 in every form
     (the wide-score claim is checked on every tile form)."""
     from m2amd import _lib

@@ -28,15 +28,17 @@ def build_model(stage, dev):
     return m.to(dev).eval()
 
 
-@pytest.fixture(params=["auto", "1", "2", "4", "4q3", "f4"])
+@pytest.fixture(params=["auto", "1", "2", "4", "4q3", "4q12", "f4"])
 def rows_per_tile(request, monkeypatch):
     """The tile forms a default can pick: 16- and 32-row workgroup tiles with
     key-quarter attention, 64-row tiles with query-split attention (K / V
-    staged in LDS; M2_TFL_RB) - at head_dim 32 the lean one-block form, at
-    head_dim 48 the wave-specialised LDS-DMA form (unmasked) and the lean
-    two-block form (masked) - and the per-call choice; "4q3": the lean
+    staged in LDS; M2_TFL_RB) - the key-quarter form on unmasked layers
+    (eight computing waves, fragments straight from L2), on masked ones the
+    lean one-block form at head_dim 32 and the lean two-block form at
+    head_dim 48 - and the per-call choice; "4q3": the lean
     two-block form on the unmasked layers too (M2_TFL_QS2=3: what a layer
     whose scores may leave the f16 range runs, m2_layer_w::wide_scores);
+    "4q12": M2_TFL_QS2=12 forced (the masked layers still fall back);
     "f4": 64-row tiles for the first (LN1 -> QKV) launch (M2_TFL_FIRST_RB,
     the default for very large grids)."""
     if request.param == "f4":
