@@ -1477,30 +1477,38 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
     else fin(CI<0>{});
 }
 
-// Key-quarter attention for 64-row tiles (M2_TFL_QS2=12, unmasked; the
-// default at head_dim 48).  Each wave owns four 16-query blocks of one head
-// (every K / V^T fragment it holds feeds four blocks), takes them through the
-// lean softmax as two pairs (scores from C = -m, the base moved only when a
-// weight's f16 hi half passes 2^kLazyT, row sums by MFMA) with the base riding
-// in the head_dim-48 tail k-step, and all eight waves compute - two per SIMD,
-// so one wave's softmax VALU meets the other's MFMAs.  Wave (h, kq) takes
-// chunks kq, kq + 4, ... of head h (the key quarters of attention_tile)
+// Key-quarter attention for 64-row tiles (M2_TFL_QS2=12; the default for
+// unmasked layers).  Each wave owns four 16-query blocks of one head (every
+// K / V^T fragment it holds feeds four blocks) and takes them through the lean
+// softmax as two pairs (scores from C = -m, the base moved only when a
+// weight's f16 hi half passes 2^kLazyT); all eight waves compute - two per
+// SIMD, so one wave's softmax VALU meets the other's MFMAs.  Wave (h, kq)
+// takes chunks kq, kq + 4, ... of head h (the key quarters of attention_tile)
 // straight from L2 into registers by buffer loads: nothing in a chunk is
 // shared between waves, so there is no staging, no ring and no barrier in the
 // chunk loop.  One fragment set: chunk c's V^T is requested at the top of its
 // iteration (first used by the first pair's PV), chunk c + 4's K right after
-// the second pair's QK^T.  The four quarters of a head merge through LDS at
-// the end, wave (h, kq) finalising block kq.
+// the second pair's QK^T.  At head_dim 48 the 16-dim tail k-step is two MFMAs,
+// not three: [k hi | k lo] . [q hi | q hi], then [k hi | (1, 1)] . [q lo | -m]
+// - the second's lane group 2 carries the base, so the QK^T chain returns
+// q.k - m from C = 0.  Row sums are per-lane fp32 sums of the exponentials,
+// reduced over the query's four lane groups once, at the merge.  The four
+// quarters of a head merge through LDS at the end, wave (h, kq) finalising
+// block kq.
 // Round 6, against the round-4/5 default (form 9: one computing wave per SIMD
 // beside a staging wave that moved K / V into an LDS ring by LDS-DMA, one
 // barrier per 64 keys; its computing wave's dependent chain per step was the
 // bound, the MFMA pipe ~42 % busy): configs[4] step 8.67 -> 8.31 ms, B=16
 // T=2600 -7.1 %, B=64 T=500 -2.6 %, decoder layers 1.35-1.44 -> 1.24-1.33 ms,
-// MFMA busy 52 % (profiles/r06/r06ad_*, r06ae_pmc.txt).  Measured and not
-// kept: each wave moving its next chunk into a private LDS slot by LDS-DMA a
-// whole iteration ahead (step 8.23 -> 8.54 ms, r06af_*); both pairs' QK^T
-// before either softmax (+2.2 %), s_setprio 1 around each MFMA group (+0.7 %),
-// both (+2.9 %; r06ag_*).
+// MFMA busy 52 % (profiles/r06/r06ad_*, r06ae_pmc.txt); then the two-MFMA
+// tail (three before: 92 -> 84 MFMAs per chunk; configs[4] step -1.4 %, B=16
+// T=2600 -1.6 %, r06ai_*) and the VALU row sums (two MFMAs per block pair on
+// an all-ones fragment before: 84 -> 76; layers 1,261 / 1,203 -> 1,241 /
+// 1,179 us, step -2.0 %, r06aj_*, r06ak_*).  Measured and not kept: each wave
+// moving its next chunk into a private LDS slot by LDS-DMA a whole iteration
+// ahead (step 8.23 -> 8.54 ms, r06af_*); both pairs' QK^T before either
+// softmax (+2.2 %), s_setprio 1 around each MFMA group (+0.7 %), both (+2.9 %;
+// r06ag_*).
 template <int H, int HD>
 __device__ __forceinline__ void attention_quarters(const unsigned char* __restrict__ qb,
                                                    const unsigned char* __restrict__ kb,
@@ -1525,14 +1533,14 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
         }
         if constexpr (KT) {
             const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-            qxh[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL) : z;
+            qxh[qq] = *reinterpret_cast<const u32x4*>(qp8 - 16 * lane + 16 * (lane & 31) + G::TAIL);  // both halves
             qxl[qq] = lane < 32 ? *reinterpret_cast<const u32x4*>(qp8 + G::TAIL + 512) : z;
         }
     }
     // chunk c's fragments through descriptors of its two K blocks / V^T chunk
     // (lane l reads 16 B at 16 l of each 1-KB piece: the layout the QKV
     // epilogues write)
-    const int loff = 16 * lane, xoff = G::TAIL + 512 - 512 * (lane >> 5) + 16 * lane;
+    const int loff = 16 * lane, toff = tail_off(lane);
     u32x4 kf[2][KSA][2], kx[2][2], vf[MT][2];
     auto load_k = [&](int c) {
         const auto rk = __builtin_amdgcn_make_buffer_rsrc(
@@ -1549,7 +1557,8 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
             if constexpr (KT) {
                 kx[u][0] = __builtin_bit_cast(
                     u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, loff, u * QKBLK + G::TAIL, 0));
-                kx[u][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, xoff, u * QKBLK, 0));
+                kx[u][1] = __builtin_bit_cast(  // hi | zeros
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, toff, u * QKBLK + G::TAIL, 0));
             }
         }
     };
@@ -1562,23 +1571,20 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
             vf[t][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, loff, t * 2048 + 1024, 0));
         }
     };
-    f32x4 acc[4][MT], lacc[4];
-    float m[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[4][MT];
+    float m[4] = {0.f, 0.f, 0.f, 0.f}, lsum[4] = {0.f, 0.f, 0.f, 0.f};  // lsum: per-lane partial row sums
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
+    for (int qq = 0; qq < 4; ++qq)
 #pragma unroll
         for (int t = 0; t < MT; ++t) acc[qq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        lacc[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const u32x4 ones = u32x4{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};  // f16 1.0 x 8
     bool fresh = true;
-    // QT (head_dim 48): the base rides in the tail k-step.  Its MFMA sums 32
-    // k-elements of which only 16 are head dims (lane groups 2, 3 carry zero
-    // Q).  Lane group 2's first two elements become A = (1, 1) (every key)
-    // and B = (hi, lo) of -m (its query): the QK^T chain then delivers
-    // q.k - m itself, from C = 0 - no per-step -m vector build.  The base is
-    // kept as the value those two f16 halves represent (hi + lo, exact in
-    // f32), so every use of m stays consistent.
+    // QT (head_dim 48): the base rides in the tail's second MFMA, whose lane
+    // groups 2, 3 carry no head dims (zeros loaded).  Lane group 2's first
+    // two elements become A = (1, 1) (every key) and B = (hi, lo) of -m (its
+    // query): the QK^T chain then delivers q.k - m itself, from C = 0 - no
+    // per-step -m vector build.  The base is kept as the value those two f16
+    // halves represent (hi + lo, exact in f32), so every use of m stays
+    // consistent.
     constexpr bool QT = KT == 1 && KS >= 1;
     const bool g2 = (lane >> 4) == 2;
     auto set_base = [&](int qq, float mnew) {
@@ -1588,7 +1594,7 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
             m[qq] = -((float)hi + (float)lo);
             const unsigned w = (unsigned)__builtin_bit_cast(unsigned short, hi) |
                                ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
-            if (g2) qxh[qq][0] = w;
+            if (g2) qxl[qq][0] = w;
         } else {
             m[qq] = mnew;
         }
@@ -1610,12 +1616,11 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
                     st[qq] = mfma(kf[u][ks][0], ql[Q0 + qq][ks], st[qq]);
                     st[qq] = mfma(kf[u][ks][1], qh[Q0 + qq][ks], st[qq]);
                 }
-            if constexpr (KT)
+            if constexpr (KT)  // [k hi | k lo] . [q hi | q hi], then [k hi | (1, 1)] . [q lo | -m]
 #pragma unroll
                 for (int qq = 0; qq < 2; ++qq) {
                     st[qq] = mfma(kx[u][0], qxh[Q0 + qq], st[qq]);
-                    st[qq] = mfma(kx[u][0], qxl[Q0 + qq], st[qq]);
-                    st[qq] = mfma(kx[u][1], qxh[Q0 + qq], st[qq]);
+                    st[qq] = mfma(kx[u][1], qxl[Q0 + qq], st[qq]);
                 }
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq)
@@ -1651,6 +1656,7 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
             }
         }
         u32x4 bh4[2], bl4[2];
+        float esum[2];
         auto exp_split = [&]() {
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
@@ -1659,6 +1665,7 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) e[u][r] = __builtin_amdgcn_exp2f(s[qq][u][r]);
+                esum[qq] = ((e[0][0] + e[0][1]) + (e[0][2] + e[0][3])) + ((e[1][0] + e[1][1]) + (e[1][2] + e[1][3]));
                 unsigned ph[4], pl[4];
                 split2u(e[0][0], e[0][1], ph[0], pl[0]);
                 split2u(e[0][2], e[0][3], ph[1], pl[1]);
@@ -1676,7 +1683,7 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
                 set_base(Q0 + qq, mold + vmax(grp4_max(chunk_max(qq)), 0.f));
                 const float d = m[Q0 + qq] - mold;
                 const float corr = __builtin_amdgcn_exp2f(-d);
-                lacc[Q0 + qq] *= corr;
+                lsum[Q0 + qq] *= corr;
 #pragma unroll
                 for (int t = 0; t < MT; ++t) acc[Q0 + qq][t] *= corr;
 #pragma unroll
@@ -1687,10 +1694,7 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
             exp_split();
         }
 #pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            lacc[Q0 + qq] = mfma(ones, bh4[qq], lacc[Q0 + qq]);
-            lacc[Q0 + qq] = mfma(ones, bl4[qq], lacc[Q0 + qq]);
-        }
+        for (int qq = 0; qq < 2; ++qq) lsum[Q0 + qq] += esum[qq];
 #pragma unroll
         for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -1707,12 +1711,9 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
     for (int j = 0; j < nj; ++j) {
         const int c = kq + WPH * j;
         load_v(c);
-        if constexpr (QT)  // lane group 2: A = (1, 1) for the hi tail, 0 for the lo tail
+        if constexpr (QT)  // lane group 2 of the second tail MFMA: A = (1, 1) (zeros loaded)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                kx[u][0][0] = g2 ? 0x3C003C00u : kx[u][0][0];
-                kx[u][1][0] = g2 ? 0u : kx[u][1][0];
-            }
+            for (int u = 0; u < 2; ++u) kx[u][1][0] |= g2 ? 0x3C003C00u : 0u;
         float s0[2][2][4], s2[2][2][4];
         qk(CI<0>{}, s0);
         smpv(CI<0>{}, c, fresh, s0);
@@ -1733,7 +1734,8 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
     for (int qq = 0; qq < 4; ++qq) {
         float* w = rec + (size_t)(wave * 4 + qq) * XW * 64 + lane;
         w[0] = m[qq];
-        w[64] = lacc[qq][0];
+        const float l = lsum[qq] + __shfl_xor(lsum[qq], 16);  // over the query's four lane groups
+        w[64] = l + __shfl_xor(l, 32);
 #pragma unroll
         for (int t = 0; t < MT; ++t)
 #pragma unroll

@@ -1,0 +1,14 @@
+# Round 6: form 12's tail k-step in two MFMAs instead of three ([k hi | k lo] .
+# [q hi | q hi], [k hi | (1, 1)] . [q lo | -m]; temporary form 17) - tile /
+# range / parity tests with it forced, in-process A/Bs against 12.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+M2_TFL_QS2=17 timeout -k 10 400 python -u -m pytest tests/test_gpu_tf_layer.py tests/test_gpu_range.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r06ai_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r06ai_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/probe/env_ab.py M2_TFL_QS2 12,17 s2 128 520 4 2 > gpurun_out/r06ai_ab_lf.txt 2>&1 || exit 1
+cat gpurun_out/r06ai_ab_lf.txt
+timeout -k 10 300 python -u tools/probe/env_ab.py M2_TFL_QS2 12,17 s2 16 520 6 4 > gpurun_out/r06ai_ab_16.txt 2>&1 || exit 1
+cat gpurun_out/r06ai_ab_16.txt
+timeout -k 10 300 python -u tools/probe/env_ab.py M2_TFL_QS2 12,17 s2 64 100 6 10 > gpurun_out/r06ai_ab_64.txt 2>&1 || exit 1
+cat gpurun_out/r06ai_ab_64.txt
