@@ -357,7 +357,7 @@ struct QkvStrips {
             if (wave + NW * k < NB) s[k].load(W, wave + NW * k);
     }
 };
-template <int H, int HD>
+template <int H, int HD, int RB = 1>
 __device__ __forceinline__ void qkv_phase_pre(const unsigned char* Xn, const QkvStrips<H>& sq, const QkvOut& o, int b,
                                               int t0, int N) {
     constexpr int NQK = 2 * H / 16;
@@ -366,13 +366,17 @@ __device__ __forceinline__ void qkv_phase_pre(const unsigned char* Xn, const Qkv
     for (int k = 0; k < QkvStrips<H>::NK; ++k) {
         const int nb = wave + NW * k;
         if (nb < QkvStrips<H>::NB) {
-            f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+            f32x4 acc[RB];
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (nb < NQK) {
-                gemm_t<H, 1>(Xn, sq.s[k], acc);
-                store_qk<H, HD>(o, b, t0, N, nb, acc[0]);
+                gemm_t<H, RB>(Xn, sq.s[k], acc);
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) store_qk<H, HD>(o, b, t0 + 16 * rb, N, nb, acc[rb]);
             } else {
-                gemm_n<H, 1>(Xn, sq.s[k], acc);
-                store_v<H, HD>(o, b, t0, N, nb, acc[0]);
+                gemm_n<H, RB>(Xn, sq.s[k], acc);
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) store_v<H, HD>(o, b, t0 + 16 * rb, N, nb, acc[rb]);
             }
         }
     }
@@ -1508,12 +1512,17 @@ __device__ __forceinline__ void attention_qsplit2(const unsigned char* __restric
 // moving its next chunk into a private LDS slot by LDS-DMA a whole iteration
 // ahead (step 8.23 -> 8.54 ms, r06af_*); both pairs' QK^T before either
 // softmax (+2.2 %), s_setprio 1 around each MFMA group (+0.7 %), both (+2.9 %;
-// r06ag_*).
-template <int H, int HD>
+// r06ag_*); a barrier of all eight waves every 1 / 2 / 4 / 8 chunks (+3.3 to
+// +4.4 %, r06an_ab_lf.txt); the issue priority to whichever SIMD partner lags
+// (each wave posting its chunk index in LDS: +0.6 % / +1.5 %, r06ap_*) - the
+// older wave of each SIMD pair finishes its quarter ~11k cycles first
+// (r06ao_stamps.txt), and neither evens that out for a gain.
+template <int H, int HD, typename Between>
 __device__ __forceinline__ void attention_quarters(const unsigned char* __restrict__ qb,
                                                    const unsigned char* __restrict__ kb,
                                                    const unsigned char* __restrict__ vb, int b, int t0, int N,
-                                                   int npad, unsigned char* A, unsigned char* U) {
+                                                   int npad, unsigned char* A, unsigned char* U,
+                                                   Between between) {
     using G = Geo<HD>;
     constexpr int KS = G::KS, KSA = G::KSA, KT = G::KT, MT = G::MT, QKBLK = G::QKBLK, VCH = G::VCH, XW = G::XW;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1741,6 +1750,7 @@ __device__ __forceinline__ void attention_quarters(const unsigned char* __restri
 #pragma unroll
             for (int r = 0; r < 4; ++r) w[(2 + 4 * t + r) * 64] = acc[qq][t][r];
     }
+    between();  // the caller's next loads, in flight across the merge
     __syncthreads();
     float mi[WPH], mx = -INFINITY;
 #pragma unroll
@@ -1797,6 +1807,9 @@ struct LArgs {
 // 78.2 -> 75.9 us; stage1 B=32 encoder layers 9.9 -> 9.0 and 7.7 -> 7.4 us
 // (profiles/r05/r05af_*).
 constexpr bool tfl_one(int rb) { return TFL_ONE && rb == 1; }
+#ifndef TFL_PRE12  // A/B builds: 0 = form 12's tiles load each strip in the phase that uses it
+#define TFL_PRE12 1
+#endif
 template <int H, bool MASKED, int NEXT, int NN, int RB, int QV = 1>
 __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     static_assert(RB == 1 || RB == 2 || RB == 4, "16-, 32- or 64-row tiles");
@@ -1804,6 +1817,9 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     constexpr int HD = H / HEADS, F = 2 * H, TR = 16 * RB;
     constexpr bool ONE = tfl_one(RB);
     constexpr bool QS = RB == 4;                  // 64-row tiles: K / V staged in LDS
+    // every weight strip requested a phase ahead (the registers are free once
+    // the attention is done): the 16-row tiles, and form 12's 64-row tiles
+    constexpr bool PRE = ONE || (TFL_PRE12 && QV == 12);
     __shared__ __attribute__((aligned(16))) unsigned char A[TR * srs(H)];   // att, then LN2(o), LN(y) (split)
     // the attention's scratch (key-quarter merge records / the K-V chunk ring)
     // and, after it, o / y (fp32, O) and relu(FFN1) (split, Hd)
@@ -1850,12 +1866,26 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     Strip<H> so;
     Strip<H> s1, s1b;  // FFN1 strips (ONE: both of this wave's, requested before the merge)
     f32x4 xres = f32x4{0.f, 0.f, 0.f, 0.f};
+    [[maybe_unused]] f32x4 xres4[RB];  // form 12: the residual rows, requested before the merge
     if constexpr (ONE) {  // the out projection's residual rows (here: measured 0.4 us better than beside Wo)
         if (wave < H / 16 && t0 + i < N)
             xres = *reinterpret_cast<const f32x4*>(a.x_in + ((size_t)b * N + t0 + i) * H + wave * 16 + 4 * gq);
     }
     if constexpr (QS) {
-        if constexpr (QV == 12) attention_quarters<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U);
+        if constexpr (QV == 12)
+            attention_quarters<H, HD>(a.q, a.k, a.v, b, t0, N, a.npad, A, U, [&] {
+                if (wave < F / 16) s1.load(a.W1, wave);  // both FFN1 strips of this wave
+                if (wave + NW < F / 16) s1b.load(a.W1, wave + NW);
+                if (wave < H / 16) {  // the out projection's strip and residual rows
+                    so.load(a.Wo, wave);
+#pragma unroll
+                    for (int rb = 0; rb < RB; ++rb)
+                        xres4[rb] = t0 + rb * 16 + i < N ? *reinterpret_cast<const f32x4*>(
+                                                               a.x_in + ((size_t)b * N + t0 + rb * 16 + i) * H +
+                                                               wave * 16 + 4 * gq)
+                                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            });
         else if constexpr (QV == 3) attention_qsplit2<H, HD, MASKED, true>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else if constexpr (QV == 2) attention_qsplit2<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         // (lean one-block form for the unmasked decoder only: masked, its MFMA
@@ -1863,7 +1893,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         // to just over the tile tests' 2e-5 bound, for no measured gain)
         else if constexpr (QV == 4) attention_qsplit<H, HD, MASKED, !MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
         else attention_qsplit<H, HD, MASKED>(a.q, a.k, a.v, b, t0, N, a.npad, len, a.sl2, A, U);
-        if (wave < H / 16) so.load(a.Wo, wave);
+        if (QV != 12 && wave < H / 16) so.load(a.Wo, wave);
         __syncthreads();
         TSTAMP(2);
     } else {
@@ -1888,12 +1918,13 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
             const int rr = rb * 16 + i;
             f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
             if constexpr (ONE) x = xres;
+            else if constexpr (QV == 12) x = xres4[rb];
             else if (t0 + rr < N) x = *reinterpret_cast<const f32x4*>(a.x_in + (row0 + rr) * H + col);
             *reinterpret_cast<f32x4*>(O + rr * frs(H) + col) = x + acc[rb];
         }
     }
     Strip<F> s2;
-    if constexpr (ONE) {
+    if constexpr (PRE) {
         if (wave < H / 16) s2.load(a.W2, wave);
     } else if (wave < F / 16) {
         s1.load(a.W1, wave);
@@ -1916,10 +1947,10 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
                           acc[rb][1] > 0.f ? acc[rb][1] : 0.f, acc[rb][2] > 0.f ? acc[rb][2] : 0.f,
                           acc[rb][3] > 0.f ? acc[rb][3] : 0.f);
     };
-    // ONE: the QKV' strips of this wave, requested before FFN1 (the
+    // PRE: the QKV' strips of this wave, requested before FFN1 (the
     // final-projection strip for NEXT 2)
     QkvStrips<H> sq;
-    if constexpr (ONE) {
+    if constexpr (PRE) {
         if constexpr (NEXT == 1) {
             sq.load(a.Wn);
         } else if constexpr (NEXT == 2) {
@@ -1957,14 +1988,14 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
     }
     if constexpr (NEXT == 1) {
         Strip<H> sn;
-        if (!ONE && wave < 3 * H / 16) sn.load(a.Wn, wave);
+        if (!PRE && wave < 3 * H / 16) sn.load(a.Wn, wave);
         __syncthreads();
         TSTAMP(6);
         ln_rows<H, TR>(O, A, vec + VGN, vec + VBN);
         __syncthreads();
         TSTAMP(7);
-        if constexpr (ONE) {
-            qkv_phase_pre<H, HD>(A, sq, qo, b, t0, N);
+        if constexpr (PRE) {
+            qkv_phase_pre<H, HD, RB>(A, sq, qo, b, t0, N);
         } else {
             qkv_phase<H, HD, RB>(A, a.Wn, sn, qo, b, t0, N);
         }
@@ -1972,7 +2003,7 @@ __global__ __launch_bounds__(512, 2) void layer_kernel(LArgs a) {
         TSTAMP_RT(15);
     } else if constexpr (NEXT == 2) {
         Strip<H> sn;
-        if constexpr (ONE) sn = sq.s[0];
+        if constexpr (PRE) sn = sq.s[0];
         else if (wave < NN / 16) sn.load(a.Wn, wave);
         __syncthreads();
         TSTAMP(6);

@@ -74,6 +74,7 @@ def main():
             print(f"   attention-end spread over waves {np.median(spread):8.0f} cycles; merge after the last wave "
                   f"{np.median(after):8.0f}; per-wave attention min/median/max {np.median(att.min(axis=1)):.0f} / "
                   f"{np.median(np.median(att, axis=1)):.0f} / {np.median(att.max(axis=1)):.0f}")
+            print("   attention loop by wave index (median): " + " ".join(f"{np.median(att[:, w]):.0f}" for w in range(8)))
         last = max(i for i in range(1, 9) if (st[:, :, i] != 0).all(axis=1).any())
         tot = (st[:, :, last] - st[:, :, 0]).max(axis=1)
         print(f"   total            {np.median(tot):8.0f} cycles")
