@@ -641,6 +641,11 @@ __device__ __forceinline__ void attention_tile(const unsigned char* __restrict__
     __builtin_amdgcn_sched_barrier(0);
     load(f1, kq + WPH);
     __builtin_amdgcn_sched_barrier(0);
+    // (The head-1 waves, the younger of each SIMD pair, finish their
+    // quarters ~4k cycles after the head-0 waves at B=8 T=500 - phase stamps,
+    // profiles/r06/r06at_stamps.txt - and the merge waits for them; the two
+    // waves of a SIMD taking the issue priority in turn, one chunk each,
+    // measured level: r06au_*.)
 #pragma unroll 1
     for (int j = 0; j < nj; j += 2) {
         process(f0, kq + WPH * j);
