@@ -540,17 +540,20 @@ def vocoder_line(cx: Ctx, stage: str, B: int, T: int, args, settle_ms: float, se
         _, all_ms = cx.timed(step, min(args.steps, 20), 2, hm, kernel_mask=(1 << cx.nk) - 1)
         per_kernel = cx.kernel_table(hm, all_ms, cfg["vocoder_channels"], cfg["mel_channels"], B, T)
         dom_i = max(per_kernel, key=lambda d: d["avg_ms"])["index"] if per_kernel else 0
-        # every 16th call carries the events: a sampled call pays ~4.5 us before
-        # and after its timed kernel (profiles/r05/r05o_gaps.txt), unsampled none
-        stride = max(1, args.steps // 16)
+        # every stride-th call carries the events (at least every 4th: 5 of the
+        # driver's 20 steps): a sampled call pays ~4.5 us before and after its
+        # timed kernel (profiles/r05/r05o_gaps.txt), unsampled none; every call
+        # sampled cost the driver-form line ~3 % (profiles/r06/r06as_bench*.json)
+        stride = max(4, args.steps // 16)
         elapsed, kern_ms = cx.timed(step, args.steps, args.warmup, hm, kernel_mask=1 << dom_i, stride=stride)
         path = cx.lib.m2_vocoder_path(hm.handle)
+        # (before the path is restored: the table's kernel names and peak are this path's)
+        live = cx.kernel_table(hm, kern_ms, cfg["vocoder_channels"], cfg["mel_channels"], B, T)
     finally:
         hm.vocoder_select(2)
     dtype, peak, note = VOC_PATHS[path]
     value = samples_per(B, T) * args.steps * cx.world / elapsed
     ms = elapsed / args.steps * 1e3
-    live = cx.kernel_table(hm, kern_ms, cfg["vocoder_channels"], cfg["mel_channels"], B, T)
     roof = None
     if live:
         d = live[0]

@@ -76,6 +76,8 @@ void reload_switches() {
     s.voc_tail_x3 = env_set("M2_VOC_TAIL_X3");
     s.voc_mid_x3 = env_set("M2_VOC_MID_X3");
     s.voc_plan = env_int("M2_VOC_PLAN", -1);
+    s.f32_mt = env_int("M2_F32_MT", 0);
+    s.f32_pair = env_int("M2_F32_PAIR", 0) != 0;
     const int mn = env_int("M2_MIDP_NCH", 0);
     s.midp_nch = mn > 0 ? mn : 0;
     const int tn = env_int("M2_TAILP_NCH", 0);
@@ -924,6 +926,11 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
             auto w2 = fetch(r + ".conv2.weight");
             add(pack_conv3(w2.data(), ch, ch), &m->vw.w2[k]);
             add(fetch(r + ".conv2.bias"), &m->vw.b2[k]);
+            if (k == 3 && ch == 8 && kRates[3] == 2) {  // the two-phase forms of the last stage
+                add(pack_convT2_paired(wt.data(), 2 * ch), &m->vw.wt4p);
+                add(pack_conv3_2p(w1.data()), &m->vw.w1p);
+                add(pack_conv3_2p(w2.data()), &m->vw.w2p);
+            }
         }
         size_t tot = 0;
         std::vector<size_t> offs;

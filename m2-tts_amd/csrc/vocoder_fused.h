@@ -16,6 +16,10 @@ struct VocW {
     const float *wt[4], *bt[4];
     const float *w1[4], *b1[4], *w2[4], *b2[4];
     const float *wo, *bo;
+    // stage1's 8-channel tail layers in the two-phase forms (M2_F32_PAIR):
+    // ConvT4 (pack_convT2_paired) and ResBlock4's convs (pack_conv3_2p);
+    // null when the last stage does not have 8 channels
+    const float *wt4p = nullptr, *w1p = nullptr, *w2p = nullptr;
     // device word; when set, the call is the range policy's on-device redo
     // of a split-path call whose audio came out non-finite: ONE persistent
     // launch (voc_redo_kernel) whose workgroups return at once unless it is
@@ -43,6 +47,8 @@ extern const char* const kVocX3KernelNames[kVocKernels];
 // convT:  per phase ph, A[co][tap*Cin + ci] = W[ci][co][k_tap(ph)]   (W: [Cin][Cout][2R])
 std::vector<float> pack_conv3(const float* W, int Cout, int Cin);
 std::vector<float> pack_convT(const float* W, int Cin, int Cout, int R);
+std::vector<float> pack_convT2_paired(const float* W, int Cin);  // Cout = 8, R = 2
+std::vector<float> pack_conv3_2p(const float* W);                 // 8 -> 8 channels
 
 // ---------------------------------------------------------------------------
 // Split-f16 vocoder (vocoder_x3.hip): conv / convT weights packed as f16

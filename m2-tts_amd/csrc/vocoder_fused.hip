@@ -74,7 +74,7 @@ struct KPlan {
     static constexpr int NB = KSP / KB;
 };
 
-template <int KC, int NTAP, int NT, int P, int OFFSTEP>
+template <int KC, int NTAP, int NT, int P, int OFFSTEP, int CS = 16>
 __device__ __forceinline__ void mma_run(const float* __restrict__ wp, const float* __restrict__ bp, int nt,
                                         f32x4 (&acc)[NT]) {
     constexpr int KS = NTAP * KC;
@@ -98,7 +98,7 @@ __device__ __forceinline__ void mma_run(const float* __restrict__ wp, const floa
             if (NB > 1 || s < KS) {
                 const float* br = bp + (s % KC) * 4 * P + (s / KC) * OFFSTEP;
 #pragma unroll
-                for (int n = 0; n < NT; ++n) bv[i][n] = (n < nt) ? br[n * 16] : 0.f;
+                for (int n = 0; n < NT; ++n) bv[i][n] = (n < nt) ? br[n * CS] : 0.f;
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -247,6 +247,93 @@ __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float
     }
 }
 
+// Two-phase forms of the 8-channel layers (stage1's ConvT4 and ResBlock4,
+// M2_F32_PAIR): an 8-channel output fills half of a 16-row m-block, so two
+// output phases share one: row (p, co) = 8p + co.
+// ConvT4 paired: leaky(ConvTranspose1d(k=4, stride 2, pad 1)) as a k3 conv
+// over its input positions q whose 16 output rows are (phase, channel),
+// output t = 2q + p: 12 k-steps per 16 columns instead of 2 x 8
+// (pack_convT2_paired: out[2q] = x[q] W1 + x[q-1] W3, out[2q+1] = x[q+1] W0 + x[q] W2).
+template <int CIN, int NT, int PIN>
+__device__ __forceinline__ void lconvT2p(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
+                                         LB out, int q0, int nq, int L, int* ctr) {
+    static_assert(CIN % 4 == 0, "CIN must be a multiple of 4");
+    constexpr int KC = CIN / 4;
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int ntiles = (nq + 15) >> 4;
+    const int nch = (ntiles + NT - 1) / NT;
+    for (int item = first_item(ctr); item < nch; item = next_item(ctr, item)) {
+        const int tile0 = item * NT;
+        const int nt = min(NT, ntiles - tile0);
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = bias[(lk * 4 + r) & 7];
+        f32x4 acc[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma_run<KC, 3, NT, PIN, 1>(Wp + lane * 4, in.p + lk * PIN + (q0 + tile0 * 16 + li - in.start - 1), nt, acc);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (n < nt) {
+                const int j = (tile0 + n) * 16 + li;
+                if (j < nq) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = lk * 4 + r, ph = row >> 3, co = row & 7;
+                        const int t = 2 * (q0 + j) + ph;
+                        const float v = act_t<ACT_LEAKY>(acc[n][r] + bv[r]);
+                        out.p[co * out.P + (t - out.start)] = (t >= 0 && t < L) ? v : 0.f;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ResBlock4's k3 convs in the two-phase form: column j covers positions
+// a0 + 2j + p (p = 0, 1), K = taps at a0 + 2j - 1 .. a0 + 2j + 2 x 8 input
+// channels (8 k-steps per 32 positions instead of 12).  The B reads step two
+// positions per lane, so the windows these read take an odd row stride
+// (ostride: conflict-free 32-lane groups).  Packed by pack_conv3_2p.
+template <int NT, int ACT, bool RES, int PIN>
+__device__ __forceinline__ void lconv3_2p(const float* __restrict__ Wp, const float* __restrict__ bias, LB in,
+                                          LB out, int a0, int npos, int L, int* ctr) {
+    constexpr int KC = 2;  // 8 input channels
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int ncol = (npos + 1) >> 1;
+    const int ntiles = (ncol + 15) >> 4;
+    const int nch = (ntiles + NT - 1) / NT;
+    for (int item = first_item(ctr); item < nch; item = next_item(ctr, item)) {
+        const int tile0 = item * NT;
+        const int nt = min(NT, ntiles - tile0);
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = bias[(lk * 4 + r) & 7];
+        f32x4 acc[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma_run<KC, 4, NT, PIN, 1, 32>(Wp + lane * 4, in.p + lk * PIN + (a0 + 2 * (tile0 * 16 + li) - in.start - 1), nt,
+                                       acc);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (n < nt) {
+                const int j = (tile0 + n) * 16 + li;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = lk * 4 + r, p = row >> 3, co = row & 7;
+                    const int jj = 2 * j + p, t = a0 + jj;
+                    if (jj < npos) {
+                        float v = act_t<ACT>(acc[n][r] + bv[r]);
+                        float* o = out.p + co * out.P + (t - out.start);
+                        if (RES) v += *o;
+                        *o = (t >= 0 && t < L) ? v : 0.f;
+                    }
+                }
+            }
+        }
+    }
+}
+
 // Global [rows][Lg] (or [Lg][rows] when TRANS) -> LDS window cols [0, ncols),
 // zero outside [0, Lg).
 template <bool TRANS>
@@ -311,7 +398,9 @@ struct MidPlan {  // U1 (CI ch, res 4) -> U2 (CI/2 ch, res 16); W res-4 position
     static constexpr int LDS_FLOATS = R0 + R1;
 };
 
-template <int CI, int W>
+// Odd row stride >= cols (the two-phase layers' stride-2 B reads).
+constexpr int ostride(int cols) { return ((cols + 15) / 32) * 32 + 17; }
+template <int CI, int W, bool PAIR = false>
 struct TailPlan {  // U2 (CI ch, res 16) -> audio (res 64); W res-16 positions
     static constexpr int C3 = CI / 2, C4 = CI / 4;
     static constexpr int IN_N = W + 8;             // [p0-4, p0+W+4)
@@ -325,8 +414,10 @@ struct TailPlan {  // U2 (CI ch, res 16) -> audio (res 64); W res-16 positions
     static constexpr int P_IN = pstride(cmax(IN_N, rup16(NQ3) + 2));
     static constexpr int P_U3 = pstride(cmax(2 * NQ3, cmax(rup16(H3_N) + 3, rup16(NQ4) + 5)));
     static constexpr int P_H3 = pstride(cmax(H3_N, rup16(O3_N) + 2));
-    static constexpr int P_U4 = pstride(cmax(2 * NQ4, rup16(H4_N) + 3));
-    static constexpr int P_H4 = pstride(cmax(H4_N, rup16(O4_N) + 2));
+    // (PAIR: the two-phase ResBlock4 reads up to 2 x 16 columns past its last
+    // needed position pair)
+    static constexpr int P_U4 = PAIR ? ostride(cmax(2 * NQ4, 4 * W + 40)) : pstride(cmax(2 * NQ4, rup16(H4_N) + 3));
+    static constexpr int P_H4 = PAIR ? ostride(cmax(H4_N, 4 * W + 40)) : pstride(cmax(H4_N, rup16(O4_N) + 2));
     // region A: U2in -> H3 -> U4 ; region B: U3 -> H4
     static constexpr int RA = cmax(CI * P_IN, cmax(C3 * P_H3, C4 * P_U4));
     static constexpr int RB = cmax(C3 * P_U3, C4 * P_H4);
@@ -351,6 +442,15 @@ struct CfgS1W16s {  // CfgS1W16 with ~2-3 smaller work items per wave for the dy
     static constexpr int M = 64, C = 128, TF = 63, W2 = 125, W3 = 500, WAVES = 16, MINW = 4;
     static constexpr bool CP = false;
     static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 2, NT_T2 = 2, NT_R2 = 2, NT_T3 = 2, NT_R3 = 2, NT_T4 = 4, NT_R4 = 4;
+};
+// The 16-wave tiling's mid and tail as two 8-wave workgroups per CU (the
+// windows halved: 1,024 workgroups at B=32 T=500, two rounds as before), so
+// one workgroup's layer barriers overlap the other's MFMA chains
+// (M2_F32_MT, a measured A/B).
+struct CfgS1T8 {
+    static constexpr int M = 64, C = 128, TF = 28, W2 = 63, W3 = 250, WAVES = 8, MINW = 5;
+    static constexpr bool CP = false;
+    static constexpr int NT_IN = 2, NT_T1 = 2, NT_R1 = 4, NT_T2 = 4, NT_R2 = 4, NT_T3 = 4, NT_R3 = 4, NT_T4 = 4, NT_R4 = 4;
 };
 struct CfgS2W8 {
     static constexpr int M = 80, C = 256, TF = 12, W2 = 28, W3 = 120, WAVES = 8, MINW = 5;
@@ -466,11 +566,13 @@ __device__ __forceinline__ void voc_mid_body(int bx, int b, const float* __restr
     STAMP(1, 9);
 }
 
-template <class Cfg>
+// PAIR: ConvT4 and ResBlock4 in the two-phase forms (8-channel stages only).
+template <class Cfg, bool PAIR = false>
 __device__ __forceinline__ void voc_tail_body(int bx, int b, const float* __restrict__ U2, int L2, const VocW& w,
                                               float* __restrict__ audio) {
     constexpr int CI = Cfg::C / 4, W = Cfg::W3;
-    using Pl = TailPlan<CI, W>;
+    static_assert(!PAIR || CI / 4 == 8, "two-phase tail layers need 8 channels");
+    using Pl = TailPlan<CI, W, PAIR>;
     constexpr int C3 = Pl::C3, C4 = Pl::C4;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int p0 = bx * W;
@@ -504,15 +606,28 @@ __device__ __forceinline__ void voc_tail_body(int bx, int b, const float* __rest
     STAMP(2, 6);
     __syncthreads();
     STAMP(2, 7);
-    lconvT<C3, C4, 2, Cfg::NT_T4, Pl::P_U3>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, ctr + 3);
+    // (PAIR: half the column tiles per item, so the phase-merged layers keep
+    // every wave busy)
+    if constexpr (PAIR)
+        lconvT2p<C3, cmax(1, Cfg::NT_T4 / 2), Pl::P_U3>(w.wt4p, w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, ctr + 3);
+    else
+        lconvT<C3, C4, 2, Cfg::NT_T4, Pl::P_U3>(w.wt[3], w.bt[3], u3, u4, 2 * p0 - 2, Pl::NQ4, L4, ctr + 3);
     STAMP(2, 8);
     __syncthreads();
     STAMP(2, 9);
-    lconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::P_U4>(w.w1[3], w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4, ctr + 4);
+    if constexpr (PAIR)
+        lconv3_2p<cmax(1, Cfg::NT_R4 / 2), ACT_LEAKY, false, Pl::P_U4>(w.w1p, w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4, ctr + 4);
+    else
+        lconv3<C4, C4, Cfg::NT_R4, ACT_LEAKY, false, Pl::P_U4>(w.w1[3], w.b1[3], u4, h4, 4 * p0 - 2, Pl::H4_N, L4,
+                                                                ctr + 4);
     STAMP(2, 10);
     __syncthreads();
     STAMP(2, 11);
-    lconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::P_H4>(w.w2[3], w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4, ctr + 5);
+    if constexpr (PAIR)
+        lconv3_2p<cmax(1, Cfg::NT_R4 / 2), ACT_NONE, true, Pl::P_H4>(w.w2p, w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4, ctr + 5);
+    else
+        lconv3<C4, C4, Cfg::NT_R4, ACT_NONE, true, Pl::P_H4>(w.w2[3], w.b2[3], h4, u4, 4 * p0 - 1, Pl::O4_N, L4,
+                                                              ctr + 5);
     STAMP(2, 12);
     __syncthreads();
     STAMP(2, 13);
@@ -546,10 +661,10 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(con
                                                                             VocW w, float* __restrict__ U2) {
     voc_mid_body<Cfg>(blockIdx.x, blockIdx.y, U1, L1, w, U2);
 }
-template <class Cfg>
+template <class Cfg, bool PAIR = false>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_tail_kernel(const float* __restrict__ U2, int L2,
                                                                              VocW w, float* __restrict__ audio) {
-    voc_tail_body<Cfg>(blockIdx.x, blockIdx.y, U2, L2, w, audio);
+    voc_tail_body<Cfg, PAIR>(blockIdx.x, blockIdx.y, U2, L2, w, audio);
 }
 
 // The range policy's on-device redo (m2_set_range_policy "fallback"): ONE
@@ -579,7 +694,7 @@ __device__ __forceinline__ void redo_wait(unsigned* c, unsigned n) {
 // bodies in one loop need more registers than each kernel's own occupancy
 // target leaves (at MINW they spilled 52-73 VGPRs), and the redo's speed
 // matters less than the split kernels' (it runs only for out-of-range calls).
-template <class Cfg, bool TRANS>
+template <class Cfg, bool TRANS, bool PAIR = false>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::WAVES / 4) void voc_redo_kernel(const float* __restrict__ mel, int B,
                                                                              int T, VocW w, float* __restrict__ U1,
                                                                              float* __restrict__ U2,
@@ -604,7 +719,7 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::WAVES / 4) void voc_redo_kern
             redo_publish(q + 2);
         } else {
             redo_wait(q + 2, (unsigned)nm);
-            voc_tail_body<Cfg>((i - nh - nm) % tx, (i - nh - nm) / tx, U2, 16 * T, w, audio);
+            voc_tail_body<Cfg, PAIR>((i - nh - nm) % tx, (i - nh - nm) / tx, U2, 16 * T, w, audio);
         }
     }
 }
@@ -619,21 +734,21 @@ int32_t set_lds(K kernel, size_t bytes) {
     return M2_OK;
 }
 
-template <class Cfg>
+template <class Cfg, bool PAIR = false>
 int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                  hipStream_t st) {
     using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
     using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
-    using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
+    using TP = TailPlan<Cfg::C / 4, Cfg::W3, PAIR>;
     constexpr int threads = Cfg::WAVES * 64;
     constexpr size_t lds = 4 * (size_t)std::max(std::max(HP::LDS_FLOATS, MP::LDS_FLOATS), TP::LDS_FLOATS);
     static int full = 0, cus = 0;
     if (!full) {
         int32_t rc;
-        if ((rc = set_lds(voc_redo_kernel<Cfg, false>, lds))) return rc;
-        if ((rc = set_lds(voc_redo_kernel<Cfg, true>, lds))) return rc;
+        if ((rc = set_lds(voc_redo_kernel<Cfg, false, PAIR>, lds))) return rc;
+        if ((rc = set_lds(voc_redo_kernel<Cfg, true, PAIR>, lds))) return rc;
         int occ = 0, dev = 0;
-        M2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, voc_redo_kernel<Cfg, false>, threads, lds));
+        M2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, voc_redo_kernel<Cfg, false, PAIR>, threads, lds));
         M2_HIP(hipGetDevice(&dev));
         M2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         cus = std::max(1, cus);
@@ -645,10 +760,10 @@ int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, floa
     const int grid = sw().redo_grid < 0 ? cus : (sw().redo_grid == 0 ? full : sw().redo_grid);
     unsigned* q = const_cast<unsigned*>(reinterpret_cast<const unsigned*>(w.guard_queue));
     if (trans)
-        hipLaunchKernelGGL((voc_redo_kernel<Cfg, true>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2, audio,
+        hipLaunchKernelGGL((voc_redo_kernel<Cfg, true, PAIR>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2, audio,
                            q);
     else
-        hipLaunchKernelGGL((voc_redo_kernel<Cfg, false>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2,
+        hipLaunchKernelGGL((voc_redo_kernel<Cfg, false, PAIR>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2,
                            audio, q);
     M2_LAUNCHED("voc_redo_kernel");
     return M2_OK;
@@ -661,21 +776,25 @@ template <class Cfg> struct RedoCfg { using type = Cfg; };
 template <> struct RedoCfg<CfgS1W16> { using type = CfgS1W8; };
 template <> struct RedoCfg<CfgS1W16s> { using type = CfgS1W8; };
 
-template <class Cfg>
+// MCfg / TCfg: the mid's / tail's tiling (windows W2 / W3, waves), by
+// default the head's.
+// PAIR: the tail's 8-channel layers in the two-phase forms (lconvT2p /
+// lconv3_2p), in the guarded redo as well.
+template <class Cfg, class MCfg = Cfg, class TCfg = Cfg, bool PAIR = false>
 int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                   hipStream_t st, const std::function<void(int, bool)>& mark) {
-    if (w.guard) return voc_redo<typename RedoCfg<Cfg>::type>(mel, trans, B, T, w, U1, U2, audio, st);
+    if (w.guard) return voc_redo<typename RedoCfg<Cfg>::type, PAIR>(mel, trans, B, T, w, U1, U2, audio, st);
     using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
-    using MP = MidPlan<Cfg::C / 2, Cfg::W2>;
-    using TP = TailPlan<Cfg::C / 4, Cfg::W3>;
+    using MP = MidPlan<MCfg::C / 2, MCfg::W2>;
+    using TP = TailPlan<TCfg::C / 4, TCfg::W3, PAIR>;
     constexpr int threads = Cfg::WAVES * 64;
     static bool attr = false;
     if (!attr) {
         int32_t rc;
         if ((rc = set_lds(voc_head_kernel<Cfg, false>, HP::LDS_FLOATS * 4))) return rc;
         if ((rc = set_lds(voc_head_kernel<Cfg, true>, HP::LDS_FLOATS * 4))) return rc;
-        if ((rc = set_lds(voc_mid_kernel<Cfg>, MP::LDS_FLOATS * 4))) return rc;
-        if ((rc = set_lds(voc_tail_kernel<Cfg>, TP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_mid_kernel<MCfg>, MP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_tail_kernel<TCfg, PAIR>, TP::LDS_FLOATS * 4))) return rc;
         attr = true;
     }
     mark(0, true);
@@ -688,16 +807,31 @@ int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, flo
     mark(0, false);
     M2_LAUNCHED("voc_head_kernel");
     mark(1, true);
-    hipLaunchKernelGGL((voc_mid_kernel<Cfg>), dim3(cdiv(4 * T, Cfg::W2), B), dim3(threads), MP::LDS_FLOATS * 4, st, U1,
-                       4 * T, w, U2);
+    hipLaunchKernelGGL((voc_mid_kernel<MCfg>), dim3(cdiv(4 * T, MCfg::W2), B), dim3(MCfg::WAVES * 64), MP::LDS_FLOATS * 4,
+                       st, U1, 4 * T, w, U2);
     mark(1, false);
     M2_LAUNCHED("voc_mid_kernel");
     mark(2, true);
-    hipLaunchKernelGGL((voc_tail_kernel<Cfg>), dim3(cdiv(16 * T, Cfg::W3), B), dim3(threads), TP::LDS_FLOATS * 4, st,
-                       U2, 16 * T, w, audio);
+    hipLaunchKernelGGL((voc_tail_kernel<TCfg, PAIR>), dim3(cdiv(16 * T, TCfg::W3), B), dim3(TCfg::WAVES * 64),
+                       TP::LDS_FLOATS * 4, st, U2, 16 * T, w, audio);
     mark(2, false);
     M2_LAUNCHED("voc_tail_kernel");
     return M2_OK;
+}
+
+template <bool PAIR>
+int32_t s1_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
+                 hipStream_t st, const std::function<void(int, bool)>& mark, bool w16, int plan) {
+    if (plan == 3) return voc_fused<CfgS1W16s, CfgS1W16s, CfgS1W16s, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (w16) {
+        switch (sw().f32_mt) {
+            case 1: return voc_fused<CfgS1W16, CfgS1T8, CfgS1W16, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            case 2: return voc_fused<CfgS1W16, CfgS1W16, CfgS1T8, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            case 3: return voc_fused<CfgS1W16, CfgS1T8, CfgS1T8, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            default: return voc_fused<CfgS1W16, CfgS1W16, CfgS1W16, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+        }
+    }
+    return voc_fused<CfgS1W8, CfgS1W8, CfgS1W8, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
 }
 }  // namespace
 
@@ -716,9 +850,8 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
         const int n16 = B * cdiv(T, CfgS1W16::TF), n8 = B * cdiv(T, CfgS1W8::TF);
         const double waste16 = (double)cdiv(n16, 256) * 256 / n16, waste8 = (double)cdiv(n8, 512) * 512 / n8;
         const bool w16 = plan == 2 || (plan < 0 && waste16 <= waste8);
-        if (plan == 3) return voc_fused<CfgS1W16s>(mel, trans, B, T, w, U1, U2, audio, st, mark);
-        if (w16) return voc_fused<CfgS1W16>(mel, trans, B, T, w, U1, U2, audio, st, mark);
-        return voc_fused<CfgS1W8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+        return sw().f32_pair && w.wt4p ? s1_fused<true>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan)
+                                       : s1_fused<false>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
     }
     if (M == 80 && C == 256) return voc_fused<CfgS2W8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     if (M == 32 && C == 64) return voc_fused<CfgTinyW8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
@@ -752,6 +885,37 @@ std::vector<float> pack_conv3(const float* W, int Cout, int Cin) {
                 const int k = kk / Cin, ci = kk % Cin;
                 if (co < Cout) out[apack_index(mb, s, lane, KSP)] = W[((size_t)co * Cin + ci) * 3 + k];
             }
+    return out;
+}
+
+// Two-phase ConvT4 (lconvT2p): ConvTranspose1d(k=4, s=2, p=1), W [Cin][8][4],
+// as a k3 conv over input positions with rows (phase, co): tap d = k - 1,
+// out[2q] = x[q] W1 + x[q-1] W3, out[2q+1] = x[q+1] W0 + x[q] W2.
+std::vector<float> pack_convT2_paired(const float* W, int Cin) {
+    std::vector<float> d((size_t)16 * Cin * 3, 0.f);  // [row][ci][k] as pack_conv3 reads it
+    for (int co = 0; co < 8; ++co)
+        for (int ci = 0; ci < Cin; ++ci) {
+            const float* w = W + ((size_t)ci * 8 + co) * 4;
+            d[((size_t)co * Cin + ci) * 3 + 0] = w[3];
+            d[((size_t)co * Cin + ci) * 3 + 1] = w[1];
+            d[((size_t)(8 + co) * Cin + ci) * 3 + 1] = w[2];
+            d[((size_t)(8 + co) * Cin + ci) * 3 + 2] = w[0];
+        }
+    return pack_conv3(d.data(), 16, Cin);
+}
+
+// Two-phase 8-channel k3 conv (lconv3_2p), W [8][8][3]: A[row = 8p + co]
+// [kk = 8 tap + ci] = W[co][ci][tap - p] for tap - p in 0..2 (tap t reads
+// position a0 + 2j + t - 1).
+std::vector<float> pack_conv3_2p(const float* W) {
+    const int KS = 8, KSP = 8;
+    std::vector<float> out((size_t)KSP * 64, 0.f);
+    for (int s = 0; s < KS; ++s)
+        for (int lane = 0; lane < 64; ++lane) {
+            const int row = lane & 15, p = row >> 3, co = row & 7, kk = 4 * s + (lane >> 4);
+            const int tap = kk / 8, ci = kk % 8, k = tap - p;
+            if (k >= 0 && k <= 2) out[apack_index(0, s, lane, KSP)] = W[((size_t)co * 8 + ci) * 3 + k];
+        }
     return out;
 }
 

@@ -1,0 +1,60 @@
+"""GPU: the stage1 exact-f32 vocoder's tail / mid forms (the strict-fp32
+path, M2_VOC_F32=1 / m2_vocoder_select(1)): the 8-channel ConvT4 and
+ResBlock4 in the two-phase forms (M2_F32_PAIR=1, vocoder_fused.hip
+lconvT2p / lconv3_2p) and the 8-wave half-window mid / tail tilings
+(M2_F32_MT), each against the CPU oracle (reference components.py:196-200,
+tts_model.py:243-297) at the waveform bound, at ragged lengths whose
+windows end inside a 16- / 32-column tile, and on both tilings the batch
+size picks (the 16-wave one-per-CU form and the 8-wave form)."""
+import pytest
+import torch
+
+import m2tts_oracle as orc
+from conftest import AUDIO_RMS_TOL, golden_state, maxabs, rms, stage_config
+
+pytestmark = pytest.mark.gpu
+
+
+def build_model(dev):
+    from models.tts_model import M2TTSModel
+    m = M2TTSModel(**stage_config("s1").as_dict())
+    m.load_state_dict(golden_state("s1"))
+    return m.to(dev).eval()
+
+
+@pytest.mark.parametrize("pair", ["0", "1"])
+@pytest.mark.parametrize("mt", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("B,T,plan", [(3, 137, "-1"), (2, 61, "-1"), (5, 250, "1"), (1, 9, "2")])
+def test_exact_f32_tail_forms(gpu, monkeypatch, pair, mt, B, T, plan):
+    from m2amd import _lib
+    lib = _lib.load()
+    monkeypatch.setenv("M2_VOC_F32", "1")
+    monkeypatch.setenv("M2_F32_PAIR", pair)
+    monkeypatch.setenv("M2_F32_MT", mt)
+    monkeypatch.setenv("M2_VOC_PLAN", plan)
+    mel = torch.randn(B, 64, T, generator=torch.Generator().manual_seed(100 + B + T))
+    ref = orc.vocoder(golden_state("s1"), mel)
+    m = build_model(gpu)
+    assert lib.m2_vocoder_path(m._hip(gpu).handle) == 1
+    out = m.vocoder(mel.to(gpu)).cpu()
+    assert out.shape == ref.shape
+    assert torch.isfinite(out).all()
+    assert rms(out, ref) <= AUDIO_RMS_TOL
+    assert maxabs(out, ref) <= 1e-4
+
+
+def test_exact_f32_forms_agree(gpu, monkeypatch):
+    """Every form computes each sample with its own fixed summation order:
+    the tilings (M2_F32_MT) agree bit for bit within one layer form, and the
+    two-phase form differs from the phase-split one by fp32 reordering only."""
+    monkeypatch.setenv("M2_VOC_F32", "1")
+    mel = torch.randn(4, 64, 300, generator=torch.Generator().manual_seed(3)).to(gpu)
+    outs = {}
+    for pair in ("0", "1"):
+        for mt in ("0", "3"):
+            monkeypatch.setenv("M2_F32_PAIR", pair)
+            monkeypatch.setenv("M2_F32_MT", mt)
+            outs[(pair, mt)] = build_model(gpu).vocoder(mel).cpu()
+    assert torch.equal(outs[("0", "0")], outs[("0", "3")])
+    assert torch.equal(outs[("1", "0")], outs[("1", "3")])
+    assert maxabs(outs[("0", "0")], outs[("1", "0")]) <= 1e-5
