@@ -76,8 +76,8 @@ void reload_switches() {
     s.voc_tail_x3 = env_set("M2_VOC_TAIL_X3");
     s.voc_mid_x3 = env_set("M2_VOC_MID_X3");
     s.voc_plan = env_int("M2_VOC_PLAN", -1);
-    s.f32_mt = env_int("M2_F32_MT", 0);
-    s.f32_pair = env_int("M2_F32_PAIR", 0) != 0;
+    s.f32_mt = env_int("M2_F32_MT", 2);
+    s.f32_pair = env_int("M2_F32_PAIR", 1) != 0;
     const int mn = env_int("M2_MIDP_NCH", 0);
     s.midp_nch = mn > 0 ? mn : 0;
     const int tn = env_int("M2_TAILP_NCH", 0);

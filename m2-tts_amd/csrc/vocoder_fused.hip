@@ -248,8 +248,12 @@ __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float
 }
 
 // Two-phase forms of the 8-channel layers (stage1's ConvT4 and ResBlock4,
-// M2_F32_PAIR): an 8-channel output fills half of a 16-row m-block, so two
-// output phases share one: row (p, co) = 8p + co.
+// the default; M2_F32_PAIR=0 runs them phase by phase): an 8-channel output
+// fills half of a 16-row m-block, so two output phases share one: row
+// (p, co) = 8p + co.  The tail's MFMAs per window 5,056 -> 4,300 (W3 = 500);
+// the exact-f32 vocoder at B=32 T=500 0.2089 -> 0.1983 ms per call, one
+// process alternated (profiles/r06/r06z3_pair.txt), within 5.9e-7 of the
+// phase-by-phase form and of the oracle's bound (test_gpu_f32_forms.py).
 // ConvT4 paired: leaky(ConvTranspose1d(k=4, stride 2, pad 1)) as a k3 conv
 // over its input positions q whose 16 output rows are (phase, channel),
 // output t = 2q + p: 12 k-steps per 16 columns instead of 2 x 8
@@ -445,8 +449,11 @@ struct CfgS1W16s {  // CfgS1W16 with ~2-3 smaller work items per wave for the dy
 };
 // The 16-wave tiling's mid and tail as two 8-wave workgroups per CU (the
 // windows halved: 1,024 workgroups at B=32 T=500, two rounds as before), so
-// one workgroup's layer barriers overlap the other's MFMA chains
-// (M2_F32_MT, a measured A/B).
+// one workgroup's layer barriers overlap the other's MFMA chains (M2_F32_MT).
+// Measured in one process, B=32 T=500 with the two-phase tail layers
+// (profiles/r06/r06z3_mt.txt): the tail 0.1986 -> 0.1948 ms per call (the
+// default, M2_F32_MT=2); the mid 0.228 (its 63-position windows re-read
+// twice the halo).
 struct CfgS1T8 {
     static constexpr int M = 64, C = 128, TF = 28, W2 = 63, W3 = 250, WAVES = 8, MINW = 5;
     static constexpr bool CP = false;
