@@ -78,6 +78,7 @@ void reload_switches() {
     s.voc_plan = env_int("M2_VOC_PLAN", -1);
     s.f32_mt = env_int("M2_F32_MT", 2);
     s.f32_pair = env_int("M2_F32_PAIR", 1) != 0;
+    s.f32_comp = env_int("M2_F32_COMP", 1) != 0;
     const int mn = env_int("M2_MIDP_NCH", 0);
     s.midp_nch = mn > 0 ? mn : 0;
     const int tn = env_int("M2_TAILP_NCH", 0);
@@ -930,6 +931,18 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 add(pack_convT2_paired(wt.data(), 2 * ch), &m->vw.wt4p);
                 add(pack_conv3_2p(w1.data()), &m->vw.w1p);
                 add(pack_conv3_2p(w2.data()), &m->vw.w2p);
+            }
+        }
+        if (M == 64 && C == 128) {  // stage1: the exact-f32 head's composed input conv o ConvT1
+            std::vector<uint16_t> hw_unused;
+            std::vector<float> hb, he;
+            bool hok = true;
+            const auto bi = fetch("vocoder.input_conv.bias"), wt0 = fetch("vocoder.upsamples.0.weight"),
+                       bt0 = fetch("vocoder.upsamples.0.bias");
+            if (pack_x3_head_comp(wi.data(), bi.data(), wt0.data(), bt0.data(), M, M, C, &hw_unused, &hb, &he, &hok)) {
+                add(pack_f32_head_comp(wi.data(), wt0.data(), M, C), &m->vw.hcw);
+                add(std::move(hb), &m->vw.hcb);
+                add(std::move(he), &m->vw.hce);
             }
         }
         size_t tot = 0;

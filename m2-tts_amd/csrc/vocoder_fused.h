@@ -20,6 +20,10 @@ struct VocW {
     // ConvT4 (pack_convT2_paired) and ResBlock4's convs (pack_conv3_2p);
     // null when the last stage does not have 8 channels
     const float *wt4p = nullptr, *w1p = nullptr, *w2p = nullptr;
+    // stage1's input conv composed into ConvT1 (M2_F32_COMP): packed weights
+    // (pack_f32_head_comp), per-phase bias [4][C/2] and edge tables
+    // (pack_x3_head_comp's, MP = M); null otherwise
+    const float *hcw = nullptr, *hcb = nullptr, *hce = nullptr;
     // device word; when set, the call is the range policy's on-device redo
     // of a split-path call whose audio came out non-finite: ONE persistent
     // launch (voc_redo_kernel) whose workgroups return at once unless it is
@@ -48,6 +52,7 @@ extern const char* const kVocX3KernelNames[kVocKernels];
 std::vector<float> pack_conv3(const float* W, int Cout, int Cin);
 std::vector<float> pack_convT(const float* W, int Cin, int Cout, int R);
 std::vector<float> pack_convT2_paired(const float* W, int Cin);  // Cout = 8, R = 2
+std::vector<float> pack_f32_head_comp(const float* Win, const float* WT, int M, int C);
 std::vector<float> pack_conv3_2p(const float* W);                 // 8 -> 8 channels
 
 // ---------------------------------------------------------------------------

@@ -247,6 +247,82 @@ __device__ __forceinline__ void lconvT(const float* __restrict__ Wp, const float
     }
 }
 
+// The head's input conv composed into ConvT1 (stage1 exact-f32, the default;
+// M2_F32_COMP=0 runs the input conv as its own layer; B=32 T=500 0.1959 ->
+// 0.1847 ms per call alternated in one process, within 1.3e-6 of the
+// two-layer form, profiles/r06/r06z7_comp.txt):
+// u = leaky(Wc * mel + bc[ph]) with Wc[ph] = W_T[ph] o W_in a 4-tap transposed
+// conv straight from the mel window (taps kk: mel frame q + d0 + 1 - kk), the
+// weights composed on the host in double (pack_f32_head_comp; the split head's
+// composition, vocoder_x3.hip).  The input conv's own zero padding (a0 = 0 at
+// frames -1 and T) is not what the composed form sees there, so the outputs
+// reading a0[-1] (q = 0, ph < 2) or a0[T] (q = T - 1, ph >= 2) subtract
+// corr[ph][co] (head_f32_corr) before the activation.  Per-phase bias
+// bc[ph * C1 + co].
+template <int M, int COUT, int NT, int PIN>
+__device__ __forceinline__ void lconvT1c(const float* __restrict__ Wp, const float* __restrict__ bias, LB in, LB out,
+                                         int q0, int nq, int T, const float* corr, int* ctr) {
+    constexpr int R = 4, KC = M / 4, KS = 4 * KC, MB = (COUT + 15) / 16, PAD = R / 2;
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int ntiles = (nq + 15) >> 4;
+    const int nch = (ntiles + NT - 1) / NT;
+    const int L = 4 * T;
+    for (int item = first_item(ctr); item < R * MB * nch; item = next_item(ctr, item)) {
+        const int ph = item % R, rest = item / R;
+        const int mb = rest % MB, tile0 = (rest / MB) * NT;
+        const int nt = min(NT, ntiles - tile0);
+        const int d0 = (ph + PAD < R) ? 0 : 1;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = bias[ph * COUT + mb * 16 + lk * 4 + r];
+        f32x4 acc[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma_run<KC, 4, NT, PIN, -1>(Wp + (size_t)(ph * MB + mb) * KPlan<KS>::KSP * 64 + lane * 4,
+                                    in.p + lk * PIN + (q0 + tile0 * 16 + li - in.start + d0 + 1), nt, acc);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            if (n < nt) {
+                const int j = (tile0 + n) * 16 + li;
+                const int q = q0 + j, t = q * R + ph;
+                if (j < nq) {
+                    const bool edge = corr && (ph < 2 ? q == 0 : q == T - 1);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int co = mb * 16 + lk * 4 + r;
+                        float v = acc[n][r] + bv[r];
+                        if (edge) v -= corr[ph * COUT + co];
+                        v = act_t<ACT_LEAKY>(v);
+                        out.p[co * out.P + (t - out.start)] = (t >= 0 && t < L) ? v : 0.f;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// corr[ph][co] = sum_m E[ph][co][m] mel[m][frame] + e[ph][co], frame 0 for
+// ph < 2 (left edge: a0[-1]) and T - 1 for ph >= 2 (right edge: a0[T]), the
+// terms the composed form adds where the reference's ConvT1 sees a0's zero
+// padding (E, e: pack_x3_head_comp's edge tables at MP = M).
+template <int M, int C1>
+__device__ __forceinline__ void head_f32_corr(const float* __restrict__ E, LB mel, int T, bool left, bool right,
+                                              float* corr) {
+    for (int i = threadIdx.x; i < 4 * C1; i += blockDim.x) {
+        const int ph = i / C1;
+        const bool use = ph < 2 ? left : right;
+        float v = 0.f;
+        if (use) {
+            const int f = ph < 2 ? 0 : T - 1;
+            const float* x = mel.p + (f - mel.start);
+            const float* e = E + (size_t)i * M;
+            v = E[(size_t)4 * C1 * M + i];
+            for (int m = 0; m < M; ++m) v = fmaf(e[m], x[m * mel.P], v);
+        }
+        corr[i] = v;
+    }
+}
+
 // Two-phase forms of the 8-channel layers (stage1's ConvT4 and ResBlock4,
 // the default; M2_F32_PAIR=0 runs them phase by phase): an 8-channel output
 // fills half of a 16-row m-block, so two output phases share one: row
@@ -491,7 +567,9 @@ __device__ unsigned long long g_stamps[3][4096][16][16];
 
 // The three kernels' bodies are device functions of the window (bx, b), so
 // the guarded redo below can run them from one persistent launch.
-template <class Cfg, bool TRANS>
+// COMP: the input conv composed into ConvT1 (lconvT1c), one layer and one
+// barrier fewer.
+template <class Cfg, bool TRANS, bool COMP = false>
 __device__ __forceinline__ void voc_head_body(int bx, int b, const float* __restrict__ mel, int T, const VocW& w,
                                               float* __restrict__ U1) {
     constexpr int M = Cfg::M, C = Cfg::C, TF = Cfg::TF;
@@ -514,11 +592,25 @@ __device__ __forceinline__ void voc_head_body(int bx, int b, const float* __rest
     STAMP(0, 1);
     __syncthreads();
     STAMP(0, 2);
-    lconv3<M, C, Cfg::NT_IN, ACT_NONE, false, Pl::P_MEL>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T, ctr + 0);
-    STAMP(0, 3);
-    __syncthreads();
-    STAMP(0, 4);
-    lconvT<C, C1, 4, Cfg::NT_T1, Pl::P_A0>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T, ctr + 1);
+    if constexpr (COMP) {
+        // the edge terms (workgroup-uniform: the windows holding frame 0 or T - 1)
+        const bool left = f0 == 0, right = T - 1 >= f0 - 1 && T - 1 <= f0 + TF;
+        float* corr = a0w.p;  // the a0 rows are not used by the composed form
+        if (left || right) {
+            head_f32_corr<M, C1>(w.hce, melw, T, left, right, corr);
+            __syncthreads();
+        }
+        STAMP(0, 3);
+        STAMP(0, 4);
+        lconvT1c<M, C1, Cfg::NT_T1, Pl::P_MEL>(w.hcw, w.hcb, melw, uw, f0 - 1, Pl::NQ, T, (left || right) ? corr : nullptr,
+                                              ctr + 1);
+    } else {
+        lconv3<M, C, Cfg::NT_IN, ACT_NONE, false, Pl::P_MEL>(w.wi, w.bi, melw, a0w, f0 - 2, Pl::A0_N, T, ctr + 0);
+        STAMP(0, 3);
+        __syncthreads();
+        STAMP(0, 4);
+        lconvT<C, C1, 4, Cfg::NT_T1, Pl::P_A0>(w.wt[0], w.bt[0], a0w, uw, f0 - 1, Pl::NQ, 4 * T, ctr + 1);
+    }
     STAMP(0, 5);
     __syncthreads();
     STAMP(0, 6);
@@ -658,10 +750,10 @@ __device__ __forceinline__ void voc_tail_body(int bx, int b, const float* __rest
     STAMP(2, 14);
 }
 
-template <class Cfg, bool TRANS>
+template <class Cfg, bool TRANS, bool COMP = false>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_head_kernel(const float* __restrict__ mel, int T,
                                                                              VocW w, float* __restrict__ U1) {
-    voc_head_body<Cfg, TRANS>(blockIdx.x, blockIdx.y, mel, T, w, U1);
+    voc_head_body<Cfg, TRANS, COMP>(blockIdx.x, blockIdx.y, mel, T, w, U1);
 }
 template <class Cfg>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::MINW) void voc_mid_kernel(const float* __restrict__ U1, int L1,
@@ -701,7 +793,7 @@ __device__ __forceinline__ void redo_wait(unsigned* c, unsigned n) {
 // bodies in one loop need more registers than each kernel's own occupancy
 // target leaves (at MINW they spilled 52-73 VGPRs), and the redo's speed
 // matters less than the split kernels' (it runs only for out-of-range calls).
-template <class Cfg, bool TRANS, bool PAIR = false>
+template <class Cfg, bool TRANS, bool PAIR = false, bool COMP = false>
 __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::WAVES / 4) void voc_redo_kernel(const float* __restrict__ mel, int B,
                                                                              int T, VocW w, float* __restrict__ U1,
                                                                              float* __restrict__ U2,
@@ -718,7 +810,7 @@ __global__ __launch_bounds__(Cfg::WAVES * 64, Cfg::WAVES / 4) void voc_redo_kern
         const int i = item;
         if (i >= nh + nm + nt) break;
         if (i < nh) {
-            voc_head_body<Cfg, TRANS>(i % hx, i / hx, mel, T, w, U1);
+            voc_head_body<Cfg, TRANS, COMP>(i % hx, i / hx, mel, T, w, U1);
             redo_publish(q + 1);
         } else if (i < nh + nm) {
             redo_wait(q + 1, (unsigned)nh);
@@ -741,7 +833,7 @@ int32_t set_lds(K kernel, size_t bytes) {
     return M2_OK;
 }
 
-template <class Cfg, bool PAIR = false>
+template <class Cfg, bool PAIR = false, bool COMP = false>
 int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                  hipStream_t st) {
     using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
@@ -752,10 +844,10 @@ int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, floa
     static int full = 0, cus = 0;
     if (!full) {
         int32_t rc;
-        if ((rc = set_lds(voc_redo_kernel<Cfg, false, PAIR>, lds))) return rc;
-        if ((rc = set_lds(voc_redo_kernel<Cfg, true, PAIR>, lds))) return rc;
+        if ((rc = set_lds(voc_redo_kernel<Cfg, false, PAIR, COMP>, lds))) return rc;
+        if ((rc = set_lds(voc_redo_kernel<Cfg, true, PAIR, COMP>, lds))) return rc;
         int occ = 0, dev = 0;
-        M2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, voc_redo_kernel<Cfg, false, PAIR>, threads, lds));
+        M2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, voc_redo_kernel<Cfg, false, PAIR, COMP>, threads, lds));
         M2_HIP(hipGetDevice(&dev));
         M2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         cus = std::max(1, cus);
@@ -767,10 +859,10 @@ int32_t voc_redo(const float* mel, bool trans, int B, int T, const VocW& w, floa
     const int grid = sw().redo_grid < 0 ? cus : (sw().redo_grid == 0 ? full : sw().redo_grid);
     unsigned* q = const_cast<unsigned*>(reinterpret_cast<const unsigned*>(w.guard_queue));
     if (trans)
-        hipLaunchKernelGGL((voc_redo_kernel<Cfg, true, PAIR>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2, audio,
+        hipLaunchKernelGGL((voc_redo_kernel<Cfg, true, PAIR, COMP>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2, audio,
                            q);
     else
-        hipLaunchKernelGGL((voc_redo_kernel<Cfg, false, PAIR>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2,
+        hipLaunchKernelGGL((voc_redo_kernel<Cfg, false, PAIR, COMP>), dim3(grid), dim3(threads), lds, st, mel, B, T, w, U1, U2,
                            audio, q);
     M2_LAUNCHED("voc_redo_kernel");
     return M2_OK;
@@ -787,10 +879,10 @@ template <> struct RedoCfg<CfgS1W16s> { using type = CfgS1W8; };
 // default the head's.
 // PAIR: the tail's 8-channel layers in the two-phase forms (lconvT2p /
 // lconv3_2p), in the guarded redo as well.
-template <class Cfg, class MCfg = Cfg, class TCfg = Cfg, bool PAIR = false>
+template <class Cfg, class MCfg = Cfg, class TCfg = Cfg, bool PAIR = false, bool COMP = false>
 int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                   hipStream_t st, const std::function<void(int, bool)>& mark) {
-    if (w.guard) return voc_redo<typename RedoCfg<Cfg>::type, PAIR>(mel, trans, B, T, w, U1, U2, audio, st);
+    if (w.guard) return voc_redo<typename RedoCfg<Cfg>::type, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st);
     using HP = HeadPlan<Cfg::M, Cfg::C, Cfg::TF, Cfg::CP>;
     using MP = MidPlan<MCfg::C / 2, MCfg::W2>;
     using TP = TailPlan<TCfg::C / 4, TCfg::W3, PAIR>;
@@ -798,18 +890,18 @@ int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, flo
     static bool attr = false;
     if (!attr) {
         int32_t rc;
-        if ((rc = set_lds(voc_head_kernel<Cfg, false>, HP::LDS_FLOATS * 4))) return rc;
-        if ((rc = set_lds(voc_head_kernel<Cfg, true>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_head_kernel<Cfg, false, COMP>, HP::LDS_FLOATS * 4))) return rc;
+        if ((rc = set_lds(voc_head_kernel<Cfg, true, COMP>, HP::LDS_FLOATS * 4))) return rc;
         if ((rc = set_lds(voc_mid_kernel<MCfg>, MP::LDS_FLOATS * 4))) return rc;
         if ((rc = set_lds(voc_tail_kernel<TCfg, PAIR>, TP::LDS_FLOATS * 4))) return rc;
         attr = true;
     }
     mark(0, true);
     if (trans)
-        hipLaunchKernelGGL((voc_head_kernel<Cfg, true>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_FLOATS * 4,
+        hipLaunchKernelGGL((voc_head_kernel<Cfg, true, COMP>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_FLOATS * 4,
                            st, mel, T, w, U1);
     else
-        hipLaunchKernelGGL((voc_head_kernel<Cfg, false>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_FLOATS * 4,
+        hipLaunchKernelGGL((voc_head_kernel<Cfg, false, COMP>), dim3(cdiv(T, Cfg::TF), B), dim3(threads), HP::LDS_FLOATS * 4,
                            st, mel, T, w, U1);
     mark(0, false);
     M2_LAUNCHED("voc_head_kernel");
@@ -826,19 +918,25 @@ int32_t voc_fused(const float* mel, bool trans, int B, int T, const VocW& w, flo
     return M2_OK;
 }
 
-template <bool PAIR>
+template <bool PAIR, bool COMP>
 int32_t s1_fused(const float* mel, bool trans, int B, int T, const VocW& w, float* U1, float* U2, float* audio,
                  hipStream_t st, const std::function<void(int, bool)>& mark, bool w16, int plan) {
-    if (plan == 3) return voc_fused<CfgS1W16s, CfgS1W16s, CfgS1W16s, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (plan == 3)
+        return voc_fused<CfgS1W16s, CfgS1W16s, CfgS1W16s, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     if (w16) {
         switch (sw().f32_mt) {
-            case 1: return voc_fused<CfgS1W16, CfgS1T8, CfgS1W16, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
-            case 2: return voc_fused<CfgS1W16, CfgS1W16, CfgS1T8, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
-            case 3: return voc_fused<CfgS1W16, CfgS1T8, CfgS1T8, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
-            default: return voc_fused<CfgS1W16, CfgS1W16, CfgS1W16, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            case 1:
+                return voc_fused<CfgS1W16, CfgS1T8, CfgS1W16, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            case 2:
+                return voc_fused<CfgS1W16, CfgS1W16, CfgS1T8, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            case 3:
+                return voc_fused<CfgS1W16, CfgS1T8, CfgS1T8, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            default:
+                return voc_fused<CfgS1W16, CfgS1W16, CfgS1W16, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st,
+                                                                           mark);
         }
     }
-    return voc_fused<CfgS1W8, CfgS1W8, CfgS1W8, PAIR>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    return voc_fused<CfgS1W8, CfgS1W8, CfgS1W8, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
 }
 }  // namespace
 
@@ -857,8 +955,11 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
         const int n16 = B * cdiv(T, CfgS1W16::TF), n8 = B * cdiv(T, CfgS1W8::TF);
         const double waste16 = (double)cdiv(n16, 256) * 256 / n16, waste8 = (double)cdiv(n8, 512) * 512 / n8;
         const bool w16 = plan == 2 || (plan < 0 && waste16 <= waste8);
-        return sw().f32_pair && w.wt4p ? s1_fused<true>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan)
-                                       : s1_fused<false>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
+        const bool pair = sw().f32_pair && w.wt4p, comp = sw().f32_comp && w.hcw;
+        if (pair && comp) return s1_fused<true, true>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
+        if (pair) return s1_fused<true, false>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
+        if (comp) return s1_fused<false, true>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
+        return s1_fused<false, false>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
     }
     if (M == 80 && C == 256) return voc_fused<CfgS2W8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     if (M == 32 && C == 64) return voc_fused<CfgTinyW8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
@@ -892,6 +993,40 @@ std::vector<float> pack_conv3(const float* W, int Cout, int Cin) {
                 const int k = kk / Cin, ci = kk % Cin;
                 if (co < Cout) out[apack_index(mb, s, lane, KSP)] = W[((size_t)co * Cin + ci) * 3 + k];
             }
+    return out;
+}
+
+// input_conv o ConvT1 for the exact-f32 head (lconvT1c), composed in double:
+// Wc(ph, co, m, kk) as pack_x3_head_comp, packed [ph][mb][s][lane][s % 4] with
+// K index kk * M + m (4 taps x M mel channels).
+std::vector<float> pack_f32_head_comp(const float* Win, const float* WT, int M, int C) {
+    const int C1 = C / 2, R = 4, P = R / 2, MB = (C1 + 15) / 16, KS = M, KSP = (KS + 3) / 4 * 4;
+    auto kj = [&](int ph, int j) {
+        const int k0 = (ph + P < R) ? ph + P : ph + P - R, k1 = (ph + P < R) ? ph + P + R : ph + P;
+        return j ? k1 : k0;
+    };
+    std::vector<double> wc((size_t)R * C1 * M * 4, 0.0);  // [ph][co][m][kk]
+    for (int ph = 0; ph < R; ++ph)
+        for (int co = 0; co < C1; ++co)
+            for (int j = 0; j < 2; ++j) {
+                const int k = kj(ph, j);
+                for (int ci = 0; ci < C; ++ci) {
+                    const double a = WT[((size_t)ci * C1 + co) * 2 * R + k];
+                    for (int tin = 0; tin < 3; ++tin) {
+                        const int kk = j + 2 - tin;
+                        for (int m = 0; m < M; ++m)
+                            wc[(((size_t)ph * C1 + co) * M + m) * 4 + kk] += a * (double)Win[((size_t)ci * M + m) * 3 + tin];
+                    }
+                }
+            }
+    std::vector<float> out((size_t)R * MB * KSP * 64, 0.f);
+    for (int ph = 0; ph < R; ++ph)
+        for (int mb = 0; mb < MB; ++mb)
+            for (int s = 0; s < KS; ++s)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int co = mb * 16 + (lane & 15), k = 4 * s + (lane >> 4), kk = k / M, m = k % M;
+                    if (co < C1) out[apack_index(ph * MB + mb, s, lane, KSP)] = (float)wc[(((size_t)ph * C1 + co) * M + m) * 4 + kk];
+                }
     return out;
 }
 
