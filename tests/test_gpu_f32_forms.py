@@ -27,7 +27,8 @@ def build_model(dev):
 @pytest.mark.parametrize("comp", ["0", "1"])
 @pytest.mark.parametrize("pair", ["0", "1"])
 @pytest.mark.parametrize("mt", ["0", "1", "2", "3"])
-@pytest.mark.parametrize("B,T,plan", [(3, 137, "-1"), (2, 61, "-1"), (5, 250, "1"), (1, 9, "2"), (2, 127, "2")])
+@pytest.mark.parametrize("B,T,plan", [(3, 137, "-1"), (2, 61, "-1"), (5, 250, "1"), (1, 9, "2"), (2, 127, "2"),
+                                       (1, 1, "-1"), (2, 2, "2"), (1, 64, "2")])
 def test_exact_f32_tail_forms(gpu, monkeypatch, comp, pair, mt, B, T, plan):
     from m2amd import _lib
     lib = _lib.load()
