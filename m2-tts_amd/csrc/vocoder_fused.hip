@@ -62,8 +62,10 @@ constexpr int stride_for(int cols, bool compact) { return compact ? cstride(cols
 // is a ds_read with an immediate offset off one per-item base address).  Register double buffer over k-blocks of
 // KB steps: block i+1's loads are in flight while block i's KB*NT MFMAs run
 // (KB = 8: 2 KiB of weights per wave in flight - the weight stream from L2 is
-// latency-bound, so bytes in flight set its rate).  Loads of tiles past `nt`
-// re-read the last live tile (no branch; nothing is stored from them).
+// latency-bound, so bytes in flight set its rate; measured on the round-6
+// stage1 tree as a separate build, processes alternated: 1.5 % slower than
+// KB = 4, profiles/r06/r06z10_kb8.txt).  Loads of tiles past `nt` re-read the
+// last live tile (no branch; nothing is stored from them).
 #ifndef M2_KB8
 #define M2_KB8 0
 #endif
