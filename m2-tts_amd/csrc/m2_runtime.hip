@@ -1850,8 +1850,9 @@ struct CountFuse {
 // work behind every other workgroup: at stage2 B=8 S=100 the step is 1.9 %
 // shorter fused (duration 13.3 -> 15.7 us, the 5 us count launch gone), at
 // stage1 B=32 and stage2 B=64 S=100 it measured +0.3 / +0.7 % (in-process
-// A/B, profiles/r03/r03aa_ab.txt).  M2_DUR_COUNT=1 fuses up to the kernel's
-// limit (8192), =0 never.
+// A/B, profiles/r03/r03aa_ab.txt; again on the round-6 tree, stage1 B=32
+// S=100: 0.1455 -> 0.1469 ms fused, profiles/r06/r06z12_count_ab.txt).
+// M2_DUR_COUNT=1 fuses up to the kernel's limit (8192), =0 never.
 bool fuse_count(int B, int S) {
     if (sw().dur_count >= 0) return sw().dur_count != 0 && duration_count_fusable(B, S);
     return (long)B * S <= 2048 && duration_count_fusable(B, S);
