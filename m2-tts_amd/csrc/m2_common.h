@@ -43,7 +43,7 @@ struct Switches {
     bool voc_mid_x3 = false;    // M2_VOC_MID_X3 (handle creation)
     int voc_plan = -1;          // M2_VOC_PLAN
     int f32_mt = 2;             // M2_F32_MT=0|1|2|3: the stage1 exact-f32 16-wave tiling's mid / tail / both as 8-wave
-                                // half windows (default 2: the tail, r06z3_mt.txt)
+                                // half windows (default 2: the tail, r06z3_mt.txt); 4: 2 + the mid's items halved
     bool f32_pair = true;       // M2_F32_PAIR=0: the stage1 exact-f32 tail's 8-channel layers phase by phase
     bool f32_comp = true;       // M2_F32_COMP=0: the stage1 exact-f32 head's input conv as its own layer
     int midp_nch = 0;           // M2_MIDP_NCH: the stage1 mid's strip length in 16-column chunks (0: by grid)

@@ -933,6 +933,9 @@ int32_t s1_fused(const float* mel, bool trans, int B, int T, const VocW& w, floa
                 return voc_fused<CfgS1W16, CfgS1W16, CfgS1T8, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
             case 3:
                 return voc_fused<CfgS1W16, CfgS1T8, CfgS1T8, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+            case 4:  // the mid's items halved (two per wave), the tail on half windows: 0.1843 ->
+                     // 0.1894 ms alternated (profiles/r06/r06z14_mid_items.txt), a switch only
+                return voc_fused<CfgS1W16, CfgS1W16s, CfgS1T8, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st, mark);
             default:
                 return voc_fused<CfgS1W16, CfgS1W16, CfgS1W16, PAIR, COMP>(mel, trans, B, T, w, U1, U2, audio, st,
                                                                            mark);
