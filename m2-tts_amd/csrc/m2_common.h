@@ -45,6 +45,7 @@ struct Switches {
     int f32_mt = 2;             // M2_F32_MT=0|1|2|3: the stage1 exact-f32 16-wave tiling's mid / tail / both as 8-wave
                                 // half windows (default 2: the tail, r06z3_mt.txt); 4: 2 + the mid's items halved
     bool f32_pair = true;       // M2_F32_PAIR=0: the stage1 exact-f32 tail's 8-channel layers phase by phase
+    int x3_head_prio = 0;       // M2_X3_HEAD_PRIO=1: the split head's younger waves at higher issue priority
     bool f32_comp = true;       // M2_F32_COMP=0: the stage1 exact-f32 head's input conv as its own layer
     int midp_nch = 0;           // M2_MIDP_NCH: the stage1 mid's strip length in 16-column chunks (0: by grid)
     int tailp_nch = 0;          // M2_TAILP_NCH: strip length in 16-column chunks (0: by grid)

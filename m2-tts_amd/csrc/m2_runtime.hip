@@ -79,6 +79,7 @@ void reload_switches() {
     s.f32_mt = env_int("M2_F32_MT", 2);
     s.f32_pair = env_int("M2_F32_PAIR", 1) != 0;
     s.f32_comp = env_int("M2_F32_COMP", 1) != 0;
+    s.x3_head_prio = env_int("M2_X3_HEAD_PRIO", 0);
     const int mn = env_int("M2_MIDP_NCH", 0);
     s.midp_nch = mn > 0 ? mn : 0;
     const int tn = env_int("M2_TAILP_NCH", 0);
@@ -1697,6 +1698,7 @@ int32_t vocoder_run(const m2_model* m, const float* mel, int32_t mel_layout, int
         VocX vx = m->vx;
         VocW vw = m->vw;
         vx.dT = vw.dT = dT;
+        vx.head_prio = sw().x3_head_prio;
         if (x3 && redo >= 0) {
             vx.rflag = m->rflag_dev + redo;
             vx.rclear = m->rflag_dev + (redo ^ 1);

@@ -142,6 +142,10 @@ struct VocX {
     // the redo's four work-queue words (VocW::guard_queue), zeroed with rclear:
     // a redo launch that stopped early cannot leave them claimed for the next
     unsigned* rqueue = nullptr;
+    // x3 head: issue priority by wave age (M2_X3_HEAD_PRIO=1: the younger
+    // waves of each SIMD higher; measured level at stage1 B=32 in both
+    // orders, profiles/r06/r06z16_head_prio.txt: an A/B switch only)
+    int head_prio = 0;
     // device frame count (dev_frames): when set, the T passed to the launches
     // is the capacity their grids cover
     const int32_t* dT = nullptr;

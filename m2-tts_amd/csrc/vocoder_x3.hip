@@ -1067,6 +1067,12 @@ __global__ __launch_bounds__(Cfg::HW * 64, Cfg::HMIN) void x3_head_kernel(const 
         if (threadIdx.x == 0) *reinterpret_cast<volatile int*>(w.rclear) = 0;
         else if (w.rqueue) reinterpret_cast<volatile unsigned*>(w.rqueue)[threadIdx.x - 1] = 0u;
     }
+    if (w.head_prio == 1) {  // waves w, w + 4, ... share a SIMD; age favours the older ones
+        const int pr = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >> 2;
+        if (pr == 1) __builtin_amdgcn_s_setprio(1);
+        else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+        else if (pr >= 3) __builtin_amdgcn_s_setprio(3);
+    }
     constexpr int M = Cfg::M, MP = Cfg::MP, C = Cfg::C, TF = Cfg::TF;
     int wx, wy;
     head_tile(wx, wy);

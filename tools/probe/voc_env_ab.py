@@ -46,8 +46,11 @@ def main():
             ref = a.clone()
         print(f"{var}={v}: bit-equal to {vals[0]}: {torch.equal(a, ref)}  max-abs {(a - ref).abs().max().item():.3g}",
               flush=True)
-    for _ in range(20):
+    import time
+    t_end = time.perf_counter() + 0.6  # clock settling (bench.py settle_ms)
+    while time.perf_counter() < t_end:
         m.vocoder(mel)
+        torch.cuda.synchronize()
     for _ in range(rounds):
         for v in vals:
             setv(v)
