@@ -934,7 +934,7 @@ int32_t m2_model_create(const m2_config* cfg, const void* const* weights, int32_
                 add(pack_conv3_2p(w2.data()), &m->vw.w2p);
             }
         }
-        if (M == 64 && C == 128) {  // stage1: the exact-f32 head's composed input conv o ConvT1
+        if ((M == 64 && C == 128) || (M == 80 && C == 256)) {  // the exact-f32 head's composed input conv o ConvT1
             std::vector<uint16_t> hw_unused;
             std::vector<float> hb, he;
             bool hok = true;

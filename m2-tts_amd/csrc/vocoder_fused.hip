@@ -966,7 +966,11 @@ int32_t launch_vocoder_fused(const float* mel, bool trans, int M, int C, int B, 
         if (comp) return s1_fused<false, true>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
         return s1_fused<false, false>(mel, trans, B, T, w, U1, U2, audio, st, mark, w16, plan);
     }
-    if (M == 80 && C == 256) return voc_fused<CfgS2W8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    if (M == 80 && C == 256) {
+        if (sw().f32_comp && w.hcw)
+            return voc_fused<CfgS2W8, CfgS2W8, CfgS2W8, false, true>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+        return voc_fused<CfgS2W8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
+    }
     if (M == 32 && C == 64) return voc_fused<CfgTinyW8>(mel, trans, B, T, w, U1, U2, audio, st, mark);
     return fail(M2_E_SHAPE, "fused vocoder: unsupported (mel_channels, vocoder_channels)");
 }

@@ -81,3 +81,27 @@ def test_exact_f32_composed_head_guarded_redo(gpu, monkeypatch):
     out = m.vocoder(mel.to(gpu))
     m.set_vocoder_precision("f32")
     assert torch.equal(out, m.vocoder(mel.to(gpu)))
+
+
+@pytest.mark.parametrize("comp", ["0", "1"])
+@pytest.mark.parametrize("B,T", [(2, 61), (1, 1), (3, 25), (2, 12), (1, 13)])
+def test_exact_f32_composed_head_stage2(gpu, monkeypatch, comp, B, T):
+    """stage2's exact-f32 head (M = 80, C = 256, 12-frame windows) with the
+    input conv composed into ConvT1 (M2_F32_COMP=1, the default) or as its own
+    layer: against the oracle at lengths that put both utterance edges in one
+    window, end a window exactly, or leave one frame in the last window."""
+    from m2amd import _lib
+    from models.tts_model import M2TTSModel
+    lib = _lib.load()
+    monkeypatch.setenv("M2_VOC_F32", "1")
+    monkeypatch.setenv("M2_F32_COMP", comp)
+    mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(200 + B + T))
+    ref = orc.vocoder(golden_state("s2"), mel)
+    m = M2TTSModel(**stage_config("s2").as_dict())
+    m.load_state_dict(golden_state("s2"))
+    m = m.to(gpu).eval()
+    assert lib.m2_vocoder_path(m._hip(gpu).handle) == 1
+    out = m.vocoder(mel.to(gpu)).cpu()
+    assert out.shape == ref.shape and torch.isfinite(out).all()
+    assert rms(out, ref) <= AUDIO_RMS_TOL
+    assert maxabs(out, ref) <= 1e-4
